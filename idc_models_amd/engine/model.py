@@ -1,0 +1,293 @@
+"""Keras-style training API: ``compile / fit / evaluate / predict / get_weights / ...``.
+
+Mirrors what the reference scripts call on ``tf.keras`` models:
+``compile`` (``dist_model_tf_vgg.py:130-132``), ``evaluate(steps=20)`` (``:134``),
+``fit(epochs, validation_data, initial_epoch)`` (``:136-160``), ``trainable`` / ``layers[:k]``
+(``:141-151``), ``get_weights/set_weights`` (``secure_fed_model.py:138,149``),
+``load_weights`` / ``ModelCheckpoint`` (``fed_model.py:103-105,138``).
+
+Execution is delegated to a *step backend*:
+
+* ``eager`` — the PyTorch reference modules with autograd (CPU, or fp32 on GPU).  This is the
+  ``world_size=1`` CPU plumbing config and the numerics oracle.
+* ``fused`` — the MI355X program (``idc_models_amd.runtime``): static NHWC bf16 arenas,
+  hand-written HIP/MFMA kernels, explicit backward, HIP-graph replay.  Chosen automatically on a
+  GPU for supported models (``backend='auto'``).
+
+Distribution is delegated to a strategy (``idc_models_amd.parallel``): one process per GPU,
+gradient all-reduce over RCCL in buckets, metric / BN-statistic reductions per epoch.
+"""
+from __future__ import annotations
+
+import contextlib
+import math
+from typing import Dict, Iterable, List, Optional, Sequence
+
+import numpy as np
+import torch
+
+from . import losses as losses_mod
+from . import metrics as metrics_mod
+from . import optimizers as optim_mod
+from .arena import ParamArena
+from .callbacks import CallbackList, History
+from ..data.dataset import to_float_images
+
+_STRATEGY_STACK: List = []
+
+
+def current_strategy():
+    if _STRATEGY_STACK:
+        return _STRATEGY_STACK[-1]
+    from ..parallel.strategy import default_strategy
+    return default_strategy()
+
+
+@contextlib.contextmanager
+def strategy_scope(strategy):
+    _STRATEGY_STACK.append(strategy)
+    try:
+        yield strategy
+    finally:
+        _STRATEGY_STACK.pop()
+
+
+class EagerStep:
+    """Reference step: autograd through the Keras-semantics modules."""
+
+    name = "eager"
+
+    def __init__(self, model: "Model"):
+        self.m = model
+
+    def _forward(self, x, training: bool):
+        net = self.m.net
+        net.train(training)
+        x = to_float_images(x.to(self.m.device, non_blocking=True))
+        return net(x)
+
+    def train_step(self, x, y):
+        m = self.m
+        y = y.to(m.device, non_blocking=True)
+        logits = self._forward(x, True)
+        loss = m.loss(logits, y)
+        m.arena.zero_grad()
+        if m.arena.params:
+            m.strategy.bucketer(m.arena)  # installs overlap hooks once (no-op single device)
+            loss.backward()
+            m.strategy.apply_gradients(m.optimizer, m.arena)
+        return loss.detach(), logits.detach()
+
+    @torch.no_grad()
+    def eval_step(self, x, y):
+        logits = self._forward(x, False)
+        y = y.to(self.m.device, non_blocking=True)
+        return self.m.loss(logits, y), logits
+
+    def sync_from_module(self):
+        pass
+
+    def sync_to_module(self):
+        pass
+
+
+class Model:
+    """Wraps a Keras-semantics network (``idc_models_amd.models``) with the Keras training API."""
+
+    def __init__(self, net, strategy=None, device=None):
+        self.net = net
+        self.strategy = strategy or current_strategy()
+        self.device = torch.device(device) if device is not None else self.strategy.device
+        self.net.to(self.device)
+        self.optimizer = None
+        self.loss = None
+        self.metrics: List = []
+        self.arena: Optional[ParamArena] = None
+        self.impl = None
+        self.backend = "auto"
+        self.history = None
+        self.strategy.broadcast_module(self.net)
+
+    # ------------------------------------------------------------------ keras surface
+    @property
+    def layers(self):
+        return self.net.layers
+
+    @property
+    def trainable(self):
+        return self.net.trainable
+
+    @trainable.setter
+    def trainable(self, v):
+        self.net.trainable = v
+
+    @property
+    def trainable_weights(self):
+        return self.net.trainable_weights
+
+    @property
+    def non_trainable_weights(self):
+        return self.net.non_trainable_weights
+
+    @property
+    def weights(self):
+        return self.net.weights
+
+    def count_params(self):
+        return self.net.count_params()
+
+    def get_layer(self, name):
+        return self.net.get_layer(name)
+
+    # ------------------------------------------------------------------ compile
+    def compile(self, optimizer="rmsprop", loss="binary_crossentropy", metrics=("accuracy",),
+                keras_compat_accuracy: bool = False, backend: str = "auto", **backend_opts):
+        """(Re)compile: fresh optimizer state and a fresh arena over the current trainable set
+        (Keras recompile semantics after changing ``trainable``, ``dist_model_tf_vgg.py:148-154``)."""
+        self._release_impl()
+        self.optimizer = optim_mod.get(optimizer)
+        self.loss = losses_mod.get(loss)
+        self.keras_compat_accuracy = keras_compat_accuracy
+        self.metric_specs = list(metrics or [])
+        params = [p for p in self.net.trainable_weights if isinstance(p, torch.nn.Parameter)]
+        self.arena = ParamArena(params, device=self.device)
+        self.optimizer.bind(self.arena)
+        self.backend = backend
+        self.backend_opts = backend_opts
+        self.impl = self._make_impl(backend)
+        return self
+
+    def _release_impl(self):
+        if self.impl is not None and hasattr(self.impl, "close"):
+            self.impl.sync_to_module()
+            self.impl.close()
+        self.impl = None
+        if self.arena is not None:
+            self.arena.release()
+            self.arena = None
+
+    def _make_impl(self, backend):
+        if backend == "eager" or self.device.type != "cuda":
+            if backend == "fused":
+                raise RuntimeError("the fused MI355X backend needs a GPU device")
+            return EagerStep(self)
+        from ..runtime import fused_supported, FusedStep
+        if backend == "fused" or (backend == "auto" and fused_supported(self.net, self.loss)):
+            return FusedStep(self, **self.backend_opts)
+        return EagerStep(self)
+
+    def _new_metrics(self):
+        dev = self.device
+        ms = [metrics_mod.Mean("loss", dev)]
+        for spec in self.metric_specs:
+            ms.append(metrics_mod.get(spec, self.keras_compat_accuracy, dev))
+        return ms
+
+    # ------------------------------------------------------------------ loops
+    def _run_epoch(self, data, steps, train: bool, callbacks=None):
+        ms = self._new_metrics()
+        it = self.strategy.distribute(data)
+        for step, (x, y) in enumerate(it):
+            if steps is not None and step >= steps:
+                break
+            if train:
+                loss, logits = self.impl.train_step(x, y)
+            else:
+                loss, logits = self.impl.eval_step(x, y)
+            yd = y.to(self.device, non_blocking=True)
+            ms[0].update_value(loss, logits.shape[0])
+            for m in ms[1:]:
+                m.update(logits, yd)
+            if callbacks is not None:
+                callbacks.on_train_batch_end(step)
+        self.strategy.reduce_metrics(ms)
+        return {m.name: m.result() for m in ms}
+
+    def fit(self, x, epochs: int = 1, validation_data=None, initial_epoch: int = 0,
+            steps_per_epoch: Optional[int] = None, validation_steps: Optional[int] = None,
+            callbacks=None, verbose: int = 1):
+        assert self.impl is not None, "call compile() first"
+        history = History()
+        cbs = CallbackList([history] + list(callbacks or []), self)
+        cbs.on_train_begin()
+        for epoch in range(initial_epoch, epochs):
+            cbs.on_epoch_begin(epoch)
+            logs = self._run_epoch(x, steps_per_epoch, True, cbs)
+            self.strategy.sync_bn_stats(self)
+            if validation_data is not None:
+                vlogs = self.evaluate(validation_data, steps=validation_steps, verbose=0,
+                                      return_dict=True)
+                logs.update({"val_" + k: v for k, v in vlogs.items()})
+            if verbose and self.strategy.is_chief:
+                print(f"Epoch {epoch + 1}/{epochs} - " +
+                      " - ".join(f"{k}: {v:.4f}" for k, v in logs.items()))
+            cbs.on_epoch_end(epoch, logs)
+        cbs.on_train_end()
+        self.impl.sync_to_module()
+        self.history = history
+        return history
+
+    def evaluate(self, x, steps: Optional[int] = None, verbose: int = 0, return_dict=False):
+        assert self.impl is not None, "call compile() first"
+        logs = self._run_epoch(x, steps, False)
+        if verbose and self.strategy.is_chief:
+            print(" - ".join(f"{k}: {v:.4f}" for k, v in logs.items()))
+        if return_dict:
+            return logs
+        vals = list(logs.values())
+        return vals if len(vals) > 1 else vals[0]
+
+    @torch.no_grad()
+    def predict(self, x, steps=None):
+        outs = []
+        for i, (xb, yb) in enumerate(x):
+            if steps is not None and i >= steps:
+                break
+            _, logits = self.impl.eval_step(xb, yb) if self.impl else (None, self.net.eval()(to_float_images(xb.to(self.device))))
+            outs.append(logits.float().cpu())
+        return torch.cat(outs).numpy()
+
+    # ------------------------------------------------------------------ weights
+    def get_weights(self) -> List[np.ndarray]:
+        if self.impl is not None:
+            self.impl.sync_to_module()
+        return [t.detach().float().cpu().numpy().copy() for t in self.net.weights]
+
+    def set_weights(self, weights: Sequence[np.ndarray]) -> None:
+        ts = self.net.weights
+        if len(ts) != len(weights):
+            raise ValueError(f"expected {len(ts)} weight arrays, got {len(weights)}")
+        with torch.no_grad():
+            for t, w in zip(ts, weights):
+                w = torch.as_tensor(np.asarray(w, dtype=np.float32))
+                if tuple(w.shape) != tuple(t.shape):
+                    raise ValueError(f"shape mismatch {tuple(w.shape)} vs {tuple(t.shape)}")
+                t.copy_(w.to(t.device))
+        if self.impl is not None:
+            self.impl.sync_from_module()
+
+    def save_weights(self, path: str) -> None:
+        from ..ckpt import save_weights
+        if self.impl is not None:
+            self.impl.sync_to_module()
+        save_weights(self.net, path)
+
+    def load_weights(self, path: str) -> None:
+        from ..ckpt import load_weights
+        load_weights(self.net, path)
+        self.strategy.broadcast_module(self.net)
+        if self.impl is not None:
+            self.impl.sync_from_module()
+
+    def save_checkpoint(self, path: str, extra: Optional[dict] = None) -> None:
+        from ..ckpt import save_checkpoint
+        if self.impl is not None:
+            self.impl.sync_to_module()
+        save_checkpoint(self, path, extra)
+
+    def load_checkpoint(self, path: str) -> dict:
+        from ..ckpt import load_checkpoint
+        out = load_checkpoint(self, path)
+        if self.impl is not None:
+            self.impl.sync_from_module()
+        return out

@@ -1,0 +1,223 @@
+"""Distribution strategies (one process per device).
+
+Reference: ``tf.distribute.MirroredStrategy`` (``dist_model_tf_vgg.py:115-117``,
+``dist_model_tf_mobile.py:115``, ``dist_model_tf_dense.py:20-22``) and
+``CentralStorageStrategy`` (``dist_model_tf_dense.py:18,24``).  TF drives N GPUs from ONE process;
+on MI355X the idiomatic form is one process per GPU over RCCL:
+
+* ``OneDeviceStrategy`` — single device (CPU plumbing config or 1 GPU).
+* ``MirroredStrategy`` — rank-0 broadcast at model creation (C2), bucketed SUM all-reduce of the
+  flat gradient arena overlapped with backward (C1), 1/N folded into the optimizer, every rank
+  applies the same update; metrics reduced once per epoch (C3); BN moving statistics averaged at
+  epoch end (C4: sync-on-read MEAN).  ``global_batch`` semantics: each batch yielded by the
+  dataset is the GLOBAL batch and rank r takes rows [r*B/N, (r+1)*B/N) — the vgg/mobile
+  convention; the dense script's ``256 * num_replicas`` global batch is the same thing.
+* ``CentralStorageStrategy`` — variables and optimizer state are owned by rank 0: gradients are
+  ``reduce``-d to rank 0, rank 0 applies RMSprop, parameters are ``broadcast`` back (C5).
+"""
+from __future__ import annotations
+
+import contextlib
+from typing import List, Optional
+
+import torch
+import torch.distributed as dist
+
+from . import comm
+from .buckets import DEFAULT_BUCKET_BYTES, GradBucketer
+
+
+class Strategy:
+    def __init__(self, device=None):
+        self.rank, self.world, self.local_rank = 0, 1, 0
+        if device is None:
+            device = "cuda" if torch.cuda.is_available() else "cpu"
+        device = torch.device(device)
+        if device.type == "cuda" and device.index is None:
+            device = torch.device("cuda", torch.cuda.current_device())
+        self.device = device
+        self._bucketers = {}
+
+    @property
+    def num_replicas_in_sync(self) -> int:
+        return self.world
+
+    @property
+    def is_chief(self) -> bool:
+        return self.rank == 0
+
+    def scope(self):
+        from ..engine.model import strategy_scope
+        return strategy_scope(self)
+
+    # hooks used by engine.Model ------------------------------------------------------
+    def broadcast_module(self, net):
+        pass
+
+    def apply_gradients(self, optimizer, arena):
+        """Reduce gradients across replicas (if any) and apply the optimizer update."""
+        optimizer.step(arena)
+
+    def reduce_metrics(self, metrics):
+        pass
+
+    def sync_bn_stats(self, model):
+        pass
+
+    def distribute(self, data):
+        return data
+
+    def bucketer(self, arena):
+        return None
+
+
+class OneDeviceStrategy(Strategy):
+    pass
+
+
+_DEFAULT = None
+
+
+def default_strategy() -> Strategy:
+    global _DEFAULT
+    if _DEFAULT is None:
+        _DEFAULT = OneDeviceStrategy()
+    return _DEFAULT
+
+
+class MirroredStrategy(Strategy):
+    def __init__(self, devices=None, bucket_bytes: int = DEFAULT_BUCKET_BYTES, backend=None):
+        rank, world, local = comm.init_process_group(backend)
+        if torch.cuda.is_available() and (backend in (None, "nccl")):
+            torch.cuda.set_device(local)
+            dev = torch.device("cuda", local)
+        else:
+            dev = torch.device("cpu")
+        super().__init__(dev)
+        self.rank, self.world, self.local_rank = rank, world, local
+        self.bucket_bytes = bucket_bytes
+        self.devices = devices
+
+    def broadcast_module(self, net):
+        if self.world == 1:
+            return
+        with torch.no_grad():
+            for t in net.weight_tensors():
+                comm.broadcast_(t.data, 0)
+
+    def bucketer(self, arena):
+        key = id(arena)
+        b = self._bucketers.get(key)
+        if b is None or b.arena is not arena:
+            b = GradBucketer(arena, self.bucket_bytes)
+            b.install_hooks()
+            self._bucketers = {key: b}
+        return b
+
+    def apply_gradients(self, optimizer, arena):
+        if self.world == 1:
+            optimizer.step(arena)
+            return
+        self.bucketer(arena).finish()
+        optimizer.step(arena, grad_scale=1.0 / self.world)
+
+    def reduce_metrics(self, metrics):
+        if self.world == 1:
+            return
+        states, owners = [], []
+        for m in metrics:
+            st = m.state()
+            if st:
+                states.extend(st)
+                owners.append((m, len(st)))
+        red = comm.pack_all_reduce(states)
+        i = 0
+        for m, n in owners:
+            m.set_state(red[i:i + n])
+            i += n
+        # exact AUC needs all scores: gather them (small: one float per example)
+        from ..engine.metrics import AUC
+        for m in metrics:
+            if isinstance(m, AUC) and m.mode == "exact" and m.scores:
+                s, l = m.gather_arrays()
+                n = torch.tensor([s.numel()], device=self.device)
+                sizes = [torch.zeros_like(n) for _ in range(self.world)]
+                dist.all_gather(sizes, n)
+                mx = int(max(int(x) for x in sizes))
+                pad = torch.full((mx,), float("nan"), device=s.device)
+                pad[:s.numel()] = s
+                padl = torch.zeros(mx, device=s.device)
+                padl[:l.numel()] = l
+                gs = [torch.empty_like(pad) for _ in range(self.world)]
+                gl = [torch.empty_like(padl) for _ in range(self.world)]
+                dist.all_gather(gs, pad)
+                dist.all_gather(gl, padl)
+                ss = torch.cat([g[:int(k)] for g, k in zip(gs, sizes)])
+                ll = torch.cat([g[:int(k)] for g, k in zip(gl, sizes)])
+                m.scores, m.labels = [ss], [ll]
+
+    def sync_bn_stats(self, model):
+        if self.world == 1:
+            return
+        from ..models.layers import BatchNormalization
+        if model.impl is not None:
+            model.impl.sync_to_module()
+        bufs = []
+        for l in _all_layers(model.net):
+            if isinstance(l, BatchNormalization):
+                bufs += [l.moving_mean, l.moving_variance]
+        if not bufs:
+            return
+        red = comm.pack_all_reduce(bufs)
+        with torch.no_grad():
+            for b, r in zip(bufs, red):
+                b.copy_(r / self.world)
+        if model.impl is not None:
+            model.impl.sync_from_module()
+
+    def distribute(self, data):
+        if self.world == 1:
+            return data
+        return _ShardedBatches(data, self.rank, self.world)
+
+
+class CentralStorageStrategy(MirroredStrategy):
+    """Params + optimizer state owned by rank 0: reduce -> update on root -> broadcast."""
+
+    def bucketer(self, arena):
+        return None
+
+    def apply_gradients(self, optimizer, arena):
+        if self.world == 1:
+            optimizer.step(arena)
+            return
+        dist.reduce(arena.grad, 0, op=dist.ReduceOp.SUM)
+        if self.rank == 0:
+            optimizer.step(arena, grad_scale=1.0 / self.world)
+        dist.broadcast(arena.data, 0)
+
+
+class _ShardedBatches:
+    """Rank ``r`` takes its contiguous slice of every global batch."""
+
+    def __init__(self, data, rank, world):
+        self.data, self.rank, self.world = data, rank, world
+
+    def __len__(self):
+        return len(self.data)
+
+    def __iter__(self):
+        for x, y in self.data:
+            b = x.shape[0]
+            per = b // self.world
+            if per == 0:
+                raise ValueError(f"global batch {b} smaller than {self.world} replicas")
+            lo = self.rank * per
+            yield x[lo:lo + per], y[lo:lo + per]
+
+
+def _all_layers(net):
+    for l in getattr(net, "layers", []):
+        yield l
+        if hasattr(l, "layers") and l is not net:
+            yield from _all_layers(l)
