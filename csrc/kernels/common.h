@@ -1,0 +1,135 @@
+// Common device helpers for the idc_models_amd gfx950 (MI355X / CDNA4) kernel library.
+//
+// Conventions used by every kernel in csrc/kernels:
+//   * activations are NHWC bf16 with an explicit per-pixel stride `ld` (elements) so a kernel can
+//     read/write a channel SLICE of a wider buffer (DenseNet's concat-free stage buffers);
+//   * all reductions accumulate in fp32; per-channel statistics are fp32 [sum | sumsq] arrays;
+//   * wave = 64 lanes; every block size is a multiple of 64.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace idc {
+
+typedef uint16_t bf16_t;  // raw bf16 bits
+typedef short v8s __attribute__((ext_vector_type(8)));
+typedef __bf16 v8bf __attribute__((ext_vector_type(8)));
+typedef float v4f __attribute__((ext_vector_type(4)));
+typedef float v16f __attribute__((ext_vector_type(16)));
+
+__device__ __forceinline__ float bf2f(bf16_t h) {
+  return __uint_as_float(((uint32_t)h) << 16);
+}
+
+// round-to-nearest-even; NaN kept a NaN (hipcc emits v_cvt_pk_bf16_f32 for the cast form)
+__device__ __forceinline__ bf16_t f2bf(float f) {
+  __bf16 b = (__bf16)f;
+  return __builtin_bit_cast(bf16_t, b);
+}
+
+__device__ __forceinline__ uint32_t pack2bf(float a, float b) {
+  return (uint32_t)f2bf(a) | ((uint32_t)f2bf(b) << 16);
+}
+
+__device__ __forceinline__ void unpack8(const uint4& v, float* f) {
+  const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    f[2 * i] = __uint_as_float(w[i] << 16);
+    f[2 * i + 1] = __uint_as_float(w[i] & 0xffff0000u);
+  }
+}
+
+__device__ __forceinline__ uint4 pack8(const float* f) {
+  uint4 v;
+  v.x = pack2bf(f[0], f[1]);
+  v.y = pack2bf(f[2], f[3]);
+  v.z = pack2bf(f[4], f[5]);
+  v.w = pack2bf(f[6], f[7]);
+  return v;
+}
+
+enum Act : int { ACT_NONE = 0, ACT_RELU = 1, ACT_RELU6 = 2 };
+
+__device__ __forceinline__ float apply_act(float v, int act) {
+  if (act == ACT_RELU) return fmaxf(v, 0.f);
+  if (act == ACT_RELU6) return fminf(fmaxf(v, 0.f), 6.f);
+  return v;
+}
+
+// derivative mask of the activation evaluated at pre-activation value z
+__device__ __forceinline__ float act_mask(float z, int act) {
+  if (act == ACT_RELU) return z > 0.f ? 1.f : 0.f;
+  if (act == ACT_RELU6) return (z > 0.f && z < 6.f) ? 1.f : 0.f;
+  return 1.f;
+}
+
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+// Bijective XCD-aware remap of a linear block id: consecutive "logical" tiles land on the same
+// XCD (blocks b and b+8 share an XCD under round-robin dispatch), improving L2 reuse of shared
+// operand panels.  Placement only affects speed, never correctness (guide §5 T1).
+__device__ __forceinline__ int xcd_remap(int bid, int nblocks) {
+  const int nx = 8;
+  if (nblocks < 2 * nx) return bid;
+  int xcd = bid % nx;
+  int q = nblocks / nx, r = nblocks % nx;
+  int base = (xcd < r) ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q;
+  return base + bid / nx;
+}
+
+// BatchNorm descriptor shared by every kernel that applies a BN affine (+activation) to an
+// operand on the fly ("pending BN").  mode 1: batch statistics from `stats` ([sum|sumsq] over
+// `count` samples); mode 2: inference (moving statistics).  mode 0: identity (act only).
+struct BnArgs {
+  const float* stats;     // [2*C] sum, sumsq (mode 1)
+  const float* gamma;     // [C]
+  const float* beta;      // [C]
+  const float* mmean;     // [C] (mode 2)
+  const float* mvar;      // [C] (mode 2)
+  float inv_count;        // 1/count for mode 1
+  float eps;
+  int mode;
+  int act;
+  int C;                  // channels covered by stats/gamma (stats row length)
+};
+
+__device__ __forceinline__ void bn_coeffs(const BnArgs& b, int c, float& scale, float& shift) {
+  if (b.mode == 0) {
+    scale = 1.f;
+    shift = 0.f;
+    return;
+  }
+  float mean, var;
+  if (b.mode == 1) {
+    mean = b.stats[c] * b.inv_count;
+    var = fmaxf(b.stats[b.C + c] * b.inv_count - mean * mean, 0.f);
+  } else {
+    mean = b.mmean[c];
+    var = b.mvar[c];
+  }
+  float r = rsqrtf(var + b.eps);
+  float g = b.gamma ? b.gamma[c] : 1.f;
+  float be = b.beta ? b.beta[c] : 0.f;
+  scale = g * r;
+  shift = be - mean * scale;
+}
+
+// mean and 1/sigma of a channel (for x-hat in backward)
+__device__ __forceinline__ void bn_mean_rstd(const BnArgs& b, int c, float& mean, float& rstd) {
+  float var;
+  if (b.mode == 1) {
+    mean = b.stats[c] * b.inv_count;
+    var = fmaxf(b.stats[b.C + c] * b.inv_count - mean * mean, 0.f);
+  } else {
+    mean = b.mmean[c];
+    var = b.mvar[c];
+  }
+  rstd = rsqrtf(var + b.eps);
+}
+
+}  // namespace idc

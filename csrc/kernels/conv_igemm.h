@@ -1,0 +1,42 @@
+#pragma once
+#include "common.h"
+
+namespace idc {
+
+enum OutMode : int { OUT_BF16 = 0, OUT_F32 = 1, OUT_F32_ACC = 2 };
+enum Tile : int { TILE_128x128 = 0, TILE_128x64 = 1, TILE_256x32 = 2, TILE_64x64 = 3, TILE_64x32 = 4 };
+
+struct ConvArgs {
+  // input operand (A): NHWC, pointer already offset to the channel slice; element type bf16 or
+  // fp32 (fp32 is converted while staging; used for fp32 gradient buffers)
+  const void* x;
+  int N, H, W, Cin, ldx;
+  // output
+  int Ho, Wo, Cout;
+  void* y;
+  int ldy;
+  // weights [Cout][KH][KW][Cin] bf16 (k-contiguous)
+  const bf16_t* w;
+  int KH, KW, SH, SW, PT, PL;
+  // prologue: pending BN (+act) applied to A (per input channel)
+  BnArgs pro;
+  // epilogue
+  int epi_mode;       // 0: bias/act/store/stats   1: backward through forward-input BN+act
+  const float* bias;  // [Cout] or null
+  int epi_act;
+  int out_mode;       // OutMode (epi 0)
+  float* stats_out;   // [2*stats_ld] sum|sumsq of stored values, channel c at stats_off + c
+  int stats_ld;
+  int stats_off;
+  // epi 1
+  const bf16_t* mx;   // forward input x at output positions [M, ldmx]
+  int ldmx;
+  BnArgs mbn;         // the forward BN(+act) that was applied to mx
+  float* gsum;        // [Cout] += sum(dZ)
+  float* gsumx;       // [Cout] += sum(dZ * xhat)
+};
+
+hipError_t conv_igemm(const ConvArgs& a, int tile, bool a_f32, hipStream_t st);
+int conv_pick_tile(int M, int Cout);
+
+}  // namespace idc

@@ -1,0 +1,23 @@
+#pragma once
+#include "common.h"
+
+namespace idc {
+
+struct WgradArgs {
+  const bf16_t* x;  // forward input (raw; BN+act re-applied via `pro`), channel slice, ld = ldx
+  int N, H, W, Cin, ldx;
+  const void* g;    // dY [M, ldg] (bf16 or fp32), channel slice
+  int ldg;
+  int Ho, Wo, Cout;
+  int KH, KW, SH, SW, PT, PL;
+  BnArgs pro;
+  float* dw;        // [K][Cout] fp32 (Keras HWIO), accumulated atomically
+  float scale;      // multiplies the contribution (1.0 normally)
+  int cin_real;     // Keras Cin when the staged input is channel-padded (0: == Cin)
+  int pix_per_split;
+};
+
+hipError_t conv_wgrad(WgradArgs a, int splits, bool g_f32, hipStream_t st);
+int wgrad_pick_splits(int M, int K, int Cout);
+
+}  // namespace idc

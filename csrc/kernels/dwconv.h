@@ -1,0 +1,28 @@
+#pragma once
+#include "common.h"
+
+namespace idc {
+
+// Depthwise KxK conv (depth multiplier 1), NHWC bf16, Keras kernel layout (KH,KW,C,1) fp32.
+struct DwArgs {
+  const bf16_t* x; int ldx;     // forward input (raw; pending BN+act via `pro`)
+  int N, H, W, C;
+  BnArgs pro;
+  const float* w;               // (KH,KW,C) fp32 master
+  int KH, KW, S, PT, PL, Ho, Wo;
+  // fwd: y raw output + stats
+  bf16_t* y; int ldy;
+  float* stats; int stats_ld;
+  // bwd data: dy -> dx (dZ through the pending BN+act; sums into gsum/gsumx)
+  const bf16_t* dy; int lddy;
+  bf16_t* dx; int lddx;
+  float* gsum; float* gsumx;
+  // wgrad
+  float* dw;
+};
+
+hipError_t dwconv_fwd(const DwArgs& a, hipStream_t st);
+hipError_t dwconv_bwd_data(const DwArgs& a, hipStream_t st);
+hipError_t dwconv_wgrad(const DwArgs& a, hipStream_t st);
+
+}  // namespace idc

@@ -1,0 +1,107 @@
+#pragma once
+#include "common.h"
+
+namespace idc {
+
+// dst = A_c*dz + B_c*x + C_c  (BatchNorm backward, coefficients from the saved statistics and the
+// reductions sum(dZ), sum(dZ*xhat) accumulated by the producer of dz)
+struct BnBwdApplyArgs {
+  const bf16_t* dz; int lddz;
+  const bf16_t* x; int ldx;
+  BnArgs bn;
+  const float* gsum; const float* gsumx;
+  float inv_n;
+  void* dst; int lddst;
+  int dst_f32, accumulate;
+  int M, C;
+};
+
+// dZ = dy * act'(bn(x)); sums of dZ and dZ*xhat per channel; optional dZ store
+struct BnBwdReduceArgs {
+  const void* dy; int lddy; int dy_f32;
+  const bf16_t* x; int ldx;
+  BnArgs bn;
+  bf16_t* dz; int lddz;   // may be null
+  float* gsum; float* gsumx;
+  int M, C;
+};
+
+struct PoolArgs {
+  const bf16_t* x; int ldx;
+  int N, H, W, C;
+  BnArgs pro;          // pending BN + act applied to inputs (mode 0 & act 0: identity)
+  int k, s, pt, pl;
+  int Ho, Wo;
+  bf16_t* y; int ldy;  // output slice
+  uint8_t* argmax;     // [N*Ho*Wo*C] (max pool)
+  float* stats; int stats_ld; int stats_off;  // output statistics (optional)
+};
+
+struct PoolBwdArgs {
+  const void* dy; int lddy; int dy_f32;   // grad wrt pool output
+  const uint8_t* argmax;
+  int N, H, W, C, k, s, pt, pl, Ho, Wo;
+  // epilogue: backward through the pending BN+act of the forward input (mode/act 0: plain)
+  const bf16_t* x; int ldx;
+  BnArgs bn;
+  bf16_t* dx; int lddx;    // output (dZ if bn active, else plain grad)
+  float* gsum; float* gsumx;
+  int is_avg;
+};
+
+struct BnMovingDesc {
+  const float* stats; int C; float inv_count; float unbias;  // unbias = n/(n-1)
+  float* mmean; float* mvar; float momentum;
+  int ld;  // statistics row length (sumsq of channel c at stats[ld + c])
+};
+
+struct HeadArgs {
+  const bf16_t* x; int ldx;  // [N*HW, C]
+  int N, HW, C, U;
+  BnArgs pro;
+  const float* w;   // [C][U] fp32 master
+  const float* b;   // [U]
+  const float* labels;  // [N] (U==1) or [N][U]
+  float* logits;    // [N][U]
+  float* feats;     // [N][C]
+  float* dlogits;   // [N][U]
+  float* loss;      // scalar, += mean loss
+  float loss_scale; // 1/N_global-batch-mean factor (1/N local)
+  int training;
+};
+
+struct HeadBwdArgs {
+  const float* feats; const float* dlogits; const float* w;
+  int N, HW, C, U;
+  float* dw; float* db;   // grads (accumulate)
+  float* dA; int ldda;    // [N*HW, C] fp32 output: dfeat/HW broadcast
+};
+
+struct CastEntry {
+  const float* src;  // Keras HWIO fp32
+  bf16_t* fwd;       // [Cout][KH][KW][Cpad]
+  bf16_t* dgrad;     // [Cin][KH][KW][Cout] flipped (may be null)
+  int KH, KW, Cin, Cout, Cpad;
+  int dw;            // 1: depthwise kernel (KH,KW,C,1) -> [C][KH][KW] (fwd only)
+  long long begin;   // prefix offset in the flat thread space
+};
+
+hipError_t bn_bwd_apply(const BnBwdApplyArgs& a, hipStream_t st);
+hipError_t bn_bwd_reduce(const BnBwdReduceArgs& a, hipStream_t st);
+hipError_t maxpool_fwd(const PoolArgs& a, hipStream_t st);
+hipError_t avgpool_fwd(const PoolArgs& a, hipStream_t st);
+hipError_t pool_bwd(const PoolBwdArgs& a, hipStream_t st);
+hipError_t bn_update_moving(const BnMovingDesc* d_descs, int n, int maxC, hipStream_t st);
+hipError_t head_fwd(const HeadArgs& a, hipStream_t st);
+hipError_t head_bwd(const HeadBwdArgs& a, hipStream_t st);
+hipError_t rmsprop(float* w, const float* g, float* ms, long long n, float lr, float rho,
+                   float eps, float grad_scale, hipStream_t st);
+hipError_t cast_weights(const CastEntry* d_entries, int n, long long total, hipStream_t st);
+hipError_t input_stage(const void* x, int x_u8, int N, int H, int W, int C, bf16_t* y, int Cpad,
+                       hipStream_t st);
+hipError_t bn_stats(const bf16_t* x, int ldx, int M, int C, float* stats, int stats_ld,
+                    int stats_off, hipStream_t st);
+hipError_t bn_apply(const bf16_t* x, int ldx, BnArgs bn, const bf16_t* res, int ldres,
+                    bf16_t* y, int ldy, int M, int C, float* stats, int stats_ld, hipStream_t st);
+
+}  // namespace idc

@@ -1,0 +1,684 @@
+// Memory-bound kernels of the idc_models_amd runtime (gfx950).
+//
+// Every kernel here streams NHWC bf16 (or fp32 gradient) rows with 16-byte vectors: a thread owns
+// one 8-channel chunk of a row (guide Guideline 13), a block covers R = 256/(C/8) rows per sweep
+// and per-channel reductions go lane -> LDS float atomics -> ONE global atomic per channel per
+// block.  Per-channel BN coefficients are computed once per block into LDS.
+//
+//   bn_bwd_apply   dst (=|+=) A*dZ + B*x + C      BatchNorm backward (DenseNet concat grads += )
+//   bn_bwd_reduce  dZ = dy*act'(bn(x)), sum dZ, sum dZ*xhat   (BN backward pass 1)
+//   maxpool_fwd    pending BN+act -> max pool (+argmax, +output stats)   (DenseNet stem, VGG)
+//   avgpool_fwd    pending BN+act -> avg pool (DenseNet transition: pool BEFORE the 1x1 conv,
+//                  exact because a 1x1 conv commutes with 2x2 average pooling; 4x fewer FLOPs)
+//   pool_bwd       max/avg pool backward as a GATHER (no atomics) + BN-backward epilogue
+//   bn_update_moving  all BN layers' moving mean/var in ONE launch per step
+//   head_fwd/bwd   fused [BN+act ->] GAP -> Dense -> BCE / softmax-CE (+ grads)
+//   rmsprop        fused Keras RMSprop over the flat fp32 arena (1/world folded in)
+//   cast_weights   fp32 Keras HWIO master -> bf16 kernel layouts (fwd + flipped dgrad), one launch
+//   input_stage    uint8/fp32 NHWC images -> bf16 NHWC padded to 8 channels
+#include "common.h"
+#include "nn_kernels.h"
+
+namespace idc {
+
+namespace {
+
+struct ChunkMap {
+  int C8, R, tx, ty;
+  __device__ ChunkMap(int C) {
+    C8 = C / 8;
+    R = 256 / C8;
+    if (R < 1) R = 1;
+    tx = threadIdx.x % C8;
+    ty = threadIdx.x / C8;
+  }
+  __device__ bool active() const { return ty < R; }
+};
+
+__device__ __forceinline__ void load8(const void* base, int f32, size_t off, float* v) {
+  if (f32) {
+    const float* p = reinterpret_cast<const float*>(base) + off;
+    float4 a = *reinterpret_cast<const float4*>(p);
+    float4 b = *reinterpret_cast<const float4*>(p + 4);
+    v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w;
+    v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
+  } else {
+    uint4 u = *reinterpret_cast<const uint4*>(reinterpret_cast<const bf16_t*>(base) + off);
+    unpack8(u, v);
+  }
+}
+
+__device__ __forceinline__ void store8(void* base, int f32, size_t off, const float* v, int acc) {
+  if (f32) {
+    float* p = reinterpret_cast<float*>(base) + off;
+    float w[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) w[j] = v[j];
+    if (acc) {
+      float4 a = *reinterpret_cast<const float4*>(p);
+      float4 b = *reinterpret_cast<const float4*>(p + 4);
+      w[0] += a.x; w[1] += a.y; w[2] += a.z; w[3] += a.w;
+      w[4] += b.x; w[5] += b.y; w[6] += b.z; w[7] += b.w;
+    }
+    *reinterpret_cast<float4*>(p) = make_float4(w[0], w[1], w[2], w[3]);
+    *reinterpret_cast<float4*>(p + 4) = make_float4(w[4], w[5], w[6], w[7]);
+  } else {
+    bf16_t* p = reinterpret_cast<bf16_t*>(base) + off;
+    float w[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) w[j] = v[j];
+    if (acc) {
+      float o[8];
+      unpack8(*reinterpret_cast<const uint4*>(p), o);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) w[j] += o[j];
+    }
+    *reinterpret_cast<uint4*>(p) = pack8(w);
+  }
+}
+
+inline int grid_rows(int M, int C, int per_thread_rows = 4) {
+  int C8 = C / 8;
+  int R = 256 / C8;
+  if (R < 1) R = 1;
+  long long blocks = ((long long)M + (long long)R * per_thread_rows - 1) / ((long long)R * per_thread_rows);
+  if (blocks > 4096) blocks = 4096;
+  if (blocks < 1) blocks = 1;
+  return (int)blocks;
+}
+
+// block-level: s_a/s_b partial sums -> global atomics
+__device__ __forceinline__ void flush_sums(float* s_a, float* s_b, int C, float* ga, float* gb) {
+  __syncthreads();
+  for (int c = threadIdx.x; c < C; c += blockDim.x) {
+    if (ga) atomicAdd(&ga[c], s_a[c]);
+    if (gb) atomicAdd(&gb[c], s_b[c]);
+  }
+}
+
+}  // namespace
+
+// ------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void bn_bwd_apply_kernel(BnBwdApplyArgs a) {
+  extern __shared__ float sh[];
+  float* sA = sh;
+  float* sB = sh + a.C;
+  float* sC = sh + 2 * a.C;
+  for (int c = threadIdx.x; c < a.C; c += blockDim.x) {
+    float mean, rstd;
+    bn_mean_rstd(a.bn, c, mean, rstd);
+    float g = a.bn.gamma ? a.bn.gamma[c] : 1.f;
+    if (a.bn.mode == 1) {
+      float sd = a.gsum[c] * a.inv_n, sdx = a.gsumx[c] * a.inv_n;
+      sA[c] = g * rstd;
+      sB[c] = -g * rstd * rstd * sdx;
+      sC[c] = -g * rstd * sd + g * rstd * rstd * mean * sdx;
+    } else {
+      sA[c] = g * rstd;
+      sB[c] = 0.f;
+      sC[c] = 0.f;
+    }
+  }
+  __syncthreads();
+  ChunkMap cm(a.C);
+  if (!cm.active()) return;
+  const int c = cm.tx * 8;
+  for (int row = blockIdx.x * cm.R + cm.ty; row < a.M; row += gridDim.x * cm.R) {
+    float d[8], x[8], o[8];
+    unpack8(*reinterpret_cast<const uint4*>(a.dz + (size_t)row * a.lddz + c), d);
+    unpack8(*reinterpret_cast<const uint4*>(a.x + (size_t)row * a.ldx + c), x);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) o[j] = sA[c + j] * d[j] + sB[c + j] * x[j] + sC[c + j];
+    store8(a.dst, a.dst_f32, (size_t)row * a.lddst + c, o, a.accumulate);
+  }
+}
+
+hipError_t bn_bwd_apply(const BnBwdApplyArgs& a, hipStream_t st) {
+  if (a.M == 0) return hipSuccess;
+  hipLaunchKernelGGL(bn_bwd_apply_kernel, dim3(grid_rows(a.M, a.C)), dim3(256), 3 * a.C * 4, st, a);
+  return hipGetLastError();
+}
+
+// ------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(BnBwdReduceArgs a) {
+  extern __shared__ float sh[];
+  float* s_sc = sh;
+  float* s_sh = sh + a.C;
+  float* s_mu = sh + 2 * a.C;
+  float* s_rs = sh + 3 * a.C;
+  float* s_a = sh + 4 * a.C;
+  float* s_b = sh + 5 * a.C;
+  for (int c = threadIdx.x; c < a.C; c += blockDim.x) {
+    bn_coeffs(a.bn, c, s_sc[c], s_sh[c]);
+    float mean = 0.f, rstd = 1.f;
+    if (a.bn.mode) bn_mean_rstd(a.bn, c, mean, rstd);
+    s_mu[c] = mean;
+    s_rs[c] = rstd;
+    s_a[c] = 0.f;
+    s_b[c] = 0.f;
+  }
+  __syncthreads();
+  ChunkMap cm(a.C);
+  float ps[8] = {0}, px[8] = {0};
+  if (cm.active()) {
+    const int c = cm.tx * 8;
+    for (int row = blockIdx.x * cm.R + cm.ty; row < a.M; row += gridDim.x * cm.R) {
+      float dy[8], x[8], d[8];
+      load8(a.dy, a.dy_f32, (size_t)row * a.lddy + c, dy);
+      unpack8(*reinterpret_cast<const uint4*>(a.x + (size_t)row * a.ldx + c), x);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) d[j] = dy[j] * act_mask(x[j] * s_sc[c + j] + s_sh[c + j], a.bn.act);
+      if (a.dz) {
+        uint4 p = pack8(d);
+        *reinterpret_cast<uint4*>(a.dz + (size_t)row * a.lddz + c) = p;
+        unpack8(p, d);  // reduce exactly what was stored
+      }
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        ps[j] += d[j];
+        px[j] += d[j] * (x[j] - s_mu[c + j]) * s_rs[c + j];
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      atomicAdd(&s_a[c + j], ps[j]);
+      atomicAdd(&s_b[c + j], px[j]);
+    }
+  }
+  flush_sums(s_a, s_b, a.C, a.gsum, a.gsumx);
+}
+
+hipError_t bn_bwd_reduce(const BnBwdReduceArgs& a, hipStream_t st) {
+  if (a.M == 0) return hipSuccess;
+  hipLaunchKernelGGL(bn_bwd_reduce_kernel, dim3(grid_rows(a.M, a.C, 16)), dim3(256), 6 * a.C * 4, st, a);
+  return hipGetLastError();
+}
+
+// ------------------------------------------------------------------------------------------
+template <bool IS_MAX>
+__global__ __launch_bounds__(256) void pool_fwd_kernel(PoolArgs a) {
+  extern __shared__ float sh[];
+  float* s_sc = sh;
+  float* s_sh = sh + a.C;
+  float* s_a = sh + 2 * a.C;
+  float* s_b = sh + 3 * a.C;
+  for (int c = threadIdx.x; c < a.C; c += blockDim.x) {
+    bn_coeffs(a.pro, c, s_sc[c], s_sh[c]);
+    s_a[c] = 0.f;
+    s_b[c] = 0.f;
+  }
+  __syncthreads();
+  ChunkMap cm(a.C);
+  const int Mo = a.N * a.Ho * a.Wo;
+  float ps[8] = {0}, pq[8] = {0};
+  const bool ident = (a.pro.mode == 0 && a.pro.act == ACT_NONE);
+  if (cm.active()) {
+    const int c = cm.tx * 8;
+    for (int o = blockIdx.x * cm.R + cm.ty; o < Mo; o += gridDim.x * cm.R) {
+      int wo = o % a.Wo, t = o / a.Wo, ho = t % a.Ho, n = t / a.Ho;
+      float best[8], sum[8];
+      uint8_t arg[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) { best[j] = -3.4e38f; sum[j] = 0.f; arg[j] = 0; }
+      for (int r = 0; r < a.k; ++r)
+        for (int s2 = 0; s2 < a.k; ++s2) {
+          int h = ho * a.s - a.pt + r, w = wo * a.s - a.pl + s2;
+          float v[8];
+          if ((unsigned)h < (unsigned)a.H && (unsigned)w < (unsigned)a.W) {
+            unpack8(*reinterpret_cast<const uint4*>(a.x + ((size_t)(n * a.H + h) * a.W + w) * a.ldx + c), v);
+            if (!ident) {
+#pragma unroll
+              for (int j = 0; j < 8; ++j) v[j] = apply_act(v[j] * s_sc[c + j] + s_sh[c + j], a.pro.act);
+            }
+          } else {
+#pragma unroll
+            for (int j = 0; j < 8; ++j) v[j] = 0.f;  // Keras ZeroPadding before the pool
+          }
+#pragma unroll
+          for (int j = 0; j < 8; ++j) {
+            if (IS_MAX) {
+              if (v[j] > best[j]) { best[j] = v[j]; arg[j] = (uint8_t)(r * a.k + s2); }
+            } else {
+              sum[j] += v[j];
+            }
+          }
+        }
+      float out[8];
+      const float inv = 1.f / (float)(a.k * a.k);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) out[j] = IS_MAX ? best[j] : sum[j] * inv;
+      uint4 p = pack8(out);
+      *reinterpret_cast<uint4*>(a.y + (size_t)o * a.ldy + c) = p;
+      if (IS_MAX && a.argmax) {
+        uint2 ar;
+        ar.x = arg[0] | (arg[1] << 8) | (arg[2] << 16) | ((uint32_t)arg[3] << 24);
+        ar.y = arg[4] | (arg[5] << 8) | (arg[6] << 16) | ((uint32_t)arg[7] << 24);
+        *reinterpret_cast<uint2*>(a.argmax + (size_t)o * a.C + c) = ar;
+      }
+      if (a.stats) {
+        unpack8(p, out);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) { ps[j] += out[j]; pq[j] += out[j] * out[j]; }
+      }
+    }
+    if (a.stats) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) { atomicAdd(&s_a[c + j], ps[j]); atomicAdd(&s_b[c + j], pq[j]); }
+    }
+  }
+  if (a.stats)
+    flush_sums(s_a, s_b, a.C, a.stats + a.stats_off, a.stats + a.stats_ld + a.stats_off);
+}
+
+hipError_t maxpool_fwd(const PoolArgs& a, hipStream_t st) {
+  hipLaunchKernelGGL(pool_fwd_kernel<true>, dim3(grid_rows(a.N * a.Ho * a.Wo, a.C)), dim3(256),
+                     4 * a.C * 4, st, a);
+  return hipGetLastError();
+}
+
+hipError_t avgpool_fwd(const PoolArgs& a, hipStream_t st) {
+  hipLaunchKernelGGL(pool_fwd_kernel<false>, dim3(grid_rows(a.N * a.Ho * a.Wo, a.C)), dim3(256),
+                     4 * a.C * 4, st, a);
+  return hipGetLastError();
+}
+
+// gather-form pool backward: each input element collects from the windows that contain it
+__global__ __launch_bounds__(256) void pool_bwd_kernel(PoolBwdArgs a) {
+  extern __shared__ float sh[];
+  float* s_sc = sh;
+  float* s_sh = sh + a.C;
+  float* s_mu = sh + 2 * a.C;
+  float* s_rs = sh + 3 * a.C;
+  float* s_a = sh + 4 * a.C;
+  float* s_b = sh + 5 * a.C;
+  const bool epi = (a.bn.mode != 0 || a.bn.act != ACT_NONE);
+  for (int c = threadIdx.x; c < a.C; c += blockDim.x) {
+    bn_coeffs(a.bn, c, s_sc[c], s_sh[c]);
+    float mean = 0.f, rstd = 1.f;
+    if (a.bn.mode) bn_mean_rstd(a.bn, c, mean, rstd);
+    s_mu[c] = mean; s_rs[c] = rstd; s_a[c] = 0.f; s_b[c] = 0.f;
+  }
+  __syncthreads();
+  ChunkMap cm(a.C);
+  const int Mi = a.N * a.H * a.W;
+  float ps[8] = {0}, px[8] = {0};
+  if (cm.active()) {
+    const int c = cm.tx * 8;
+    const float inv = 1.f / (float)(a.k * a.k);
+    for (int i = blockIdx.x * cm.R + cm.ty; i < Mi; i += gridDim.x * cm.R) {
+      int w = i % a.W, t = i / a.W, h = t % a.H, n = t / a.H;
+      float g[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+      // windows oh with oh*s - pt <= h <= oh*s - pt + k - 1
+      int oh_lo = (h + a.pt - a.k + 1 + a.s - 1);
+      oh_lo = oh_lo < 0 ? 0 : oh_lo / a.s;
+      int oh_hi = (h + a.pt) / a.s;
+      int ow_lo = (w + a.pl - a.k + 1 + a.s - 1);
+      ow_lo = ow_lo < 0 ? 0 : ow_lo / a.s;
+      int ow_hi = (w + a.pl) / a.s;
+      if (oh_hi >= a.Ho) oh_hi = a.Ho - 1;
+      if (ow_hi >= a.Wo) ow_hi = a.Wo - 1;
+      for (int oh = oh_lo; oh <= oh_hi; ++oh)
+        for (int ow = ow_lo; ow <= ow_hi; ++ow) {
+          size_t o = (size_t)(n * a.Ho + oh) * a.Wo + ow;
+          float d[8];
+          load8(a.dy, a.dy_f32, o * a.lddy + c, d);
+          if (a.is_avg) {
+#pragma unroll
+            for (int j = 0; j < 8; ++j) g[j] += d[j] * inv;
+          } else {
+            int rr = h - (oh * a.s - a.pt), ss = w - (ow * a.s - a.pl);
+            uint8_t mine = (uint8_t)(rr * a.k + ss);
+            uint2 ar = *reinterpret_cast<const uint2*>(a.argmax + o * a.C + c);
+            uint8_t am[8] = {(uint8_t)(ar.x), (uint8_t)(ar.x >> 8), (uint8_t)(ar.x >> 16), (uint8_t)(ar.x >> 24),
+                             (uint8_t)(ar.y), (uint8_t)(ar.y >> 8), (uint8_t)(ar.y >> 16), (uint8_t)(ar.y >> 24)};
+#pragma unroll
+            for (int j = 0; j < 8; ++j) g[j] += (am[j] == mine) ? d[j] : 0.f;
+          }
+        }
+      if (epi) {
+        float x[8];
+        unpack8(*reinterpret_cast<const uint4*>(a.x + (size_t)i * a.ldx + c), x);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) g[j] *= act_mask(x[j] * s_sc[c + j] + s_sh[c + j], a.bn.act);
+        uint4 p = pack8(g);
+        *reinterpret_cast<uint4*>(a.dx + (size_t)i * a.lddx + c) = p;
+        unpack8(p, g);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          ps[j] += g[j];
+          px[j] += g[j] * (x[j] - s_mu[c + j]) * s_rs[c + j];
+        }
+      } else {
+        *reinterpret_cast<uint4*>(a.dx + (size_t)i * a.lddx + c) = pack8(g);
+      }
+    }
+    if (epi && (a.gsum || a.gsumx)) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) { atomicAdd(&s_a[c + j], ps[j]); atomicAdd(&s_b[c + j], px[j]); }
+    }
+  }
+  if (epi && (a.gsum || a.gsumx)) flush_sums(s_a, s_b, a.C, a.gsum, a.gsumx);
+}
+
+hipError_t pool_bwd(const PoolBwdArgs& a, hipStream_t st) {
+  hipLaunchKernelGGL(pool_bwd_kernel, dim3(grid_rows(a.N * a.H * a.W, a.C)), dim3(256),
+                     6 * a.C * 4, st, a);
+  return hipGetLastError();
+}
+
+// ------------------------------------------------------------------------------------------
+__global__ void bn_update_moving_kernel(const BnMovingDesc* d, int n) {
+  const BnMovingDesc& b = d[blockIdx.y];
+  for (int c = blockIdx.x * blockDim.x + threadIdx.x; c < b.C; c += gridDim.x * blockDim.x) {
+    float mean = b.stats[c] * b.inv_count;
+    float var = fmaxf(b.stats[b.ld + c] * b.inv_count - mean * mean, 0.f) * b.unbias;
+    b.mmean[c] = b.momentum * b.mmean[c] + (1.f - b.momentum) * mean;
+    b.mvar[c] = b.momentum * b.mvar[c] + (1.f - b.momentum) * var;
+  }
+}
+
+hipError_t bn_update_moving(const BnMovingDesc* d, int n, int maxC, hipStream_t st) {
+  if (n == 0) return hipSuccess;
+  dim3 grid((maxC + 255) / 256, n);
+  hipLaunchKernelGGL(bn_update_moving_kernel, grid, dim3(256), 0, st, d, n);
+  return hipGetLastError();
+}
+
+// ------------------------------------------------------------------------------------------
+// head forward: one block per sample
+__global__ __launch_bounds__(256) void head_fwd_kernel(HeadArgs a) {
+  extern __shared__ float sh[];
+  float* s_feat = sh;            // [C]
+  float* s_red = sh + a.C;       // [U][4 waves]
+  const int n = blockIdx.x;
+  const bool ident = (a.pro.mode == 0 && a.pro.act == ACT_NONE);
+  const float inv_hw = 1.f / (float)a.HW;
+  for (int c = threadIdx.x; c < a.C; c += blockDim.x) {
+    float sc = 1.f, sf = 0.f;
+    if (!ident) bn_coeffs(a.pro, c, sc, sf);
+    float acc = 0.f;
+    for (int p = 0; p < a.HW; ++p) {
+      float v = bf2f(a.x[((size_t)n * a.HW + p) * a.ldx + c]);
+      if (!ident) v = apply_act(v * sc + sf, a.pro.act);
+      acc += v;
+    }
+    acc *= inv_hw;
+    s_feat[c] = acc;
+    a.feats[(size_t)n * a.C + c] = acc;
+  }
+  __syncthreads();
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  for (int u = 0; u < a.U; ++u) {
+    float p = 0.f;
+    for (int c = threadIdx.x; c < a.C; c += blockDim.x) p += s_feat[c] * a.w[(size_t)c * a.U + u];
+    p = wave_sum(p);
+    if (lane == 0) s_red[u * 4 + wid] = p;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    float lg[32];
+    for (int u = 0; u < a.U; ++u) {
+      lg[u] = s_red[u * 4] + s_red[u * 4 + 1] + s_red[u * 4 + 2] + s_red[u * 4 + 3] + (a.b ? a.b[u] : 0.f);
+      a.logits[n * a.U + u] = lg[u];
+    }
+    if (a.training || a.loss) {
+      float loss = 0.f;
+      if (a.U == 1) {
+        float x = lg[0], z = a.labels[n];
+        loss = fmaxf(x, 0.f) - x * z + log1pf(expf(-fabsf(x)));
+        float sig = 1.f / (1.f + expf(-x));
+        if (a.dlogits) a.dlogits[n] = (sig - z) * a.loss_scale;
+      } else {
+        float mx = lg[0];
+        for (int u = 1; u < a.U; ++u) mx = fmaxf(mx, lg[u]);
+        float se = 0.f;
+        for (int u = 0; u < a.U; ++u) se += expf(lg[u] - mx);
+        float lse = mx + logf(se);
+        float tsum = 0.f;
+        for (int u = 0; u < a.U; ++u) tsum += a.labels[n * a.U + u];
+        for (int u = 0; u < a.U; ++u) {
+          float y = a.labels[n * a.U + u];
+          loss += -y * (lg[u] - lse);
+          if (a.dlogits) a.dlogits[n * a.U + u] = (expf(lg[u] - lse) * tsum - y) * a.loss_scale;
+        }
+      }
+      if (a.loss) atomicAdd(a.loss, loss * a.loss_scale);
+    }
+  }
+}
+
+hipError_t head_fwd(const HeadArgs& a, hipStream_t st) {
+  hipLaunchKernelGGL(head_fwd_kernel, dim3(a.N), dim3(256), (a.C + 4 * a.U) * 4, st, a);
+  return hipGetLastError();
+}
+
+// head backward: block per 64-channel slice; reduces over the batch for dW, writes dA
+__global__ __launch_bounds__(256) void head_bwd_kernel(HeadBwdArgs a) {
+  __shared__ float s_dw[64][17];
+  const int c0 = blockIdx.x * 64;
+  const int cl = threadIdx.x & 63, grp = threadIdx.x >> 6;  // 4 sample groups
+  const int c = c0 + cl;
+  float acc[16];
+  for (int u = 0; u < 16; ++u) acc[u] = 0.f;
+  const float inv_hw = 1.f / (float)a.HW;
+  for (int n = grp; n < a.N; n += 4) {
+    float f = (c < a.C) ? a.feats[(size_t)n * a.C + c] : 0.f;
+    float df = 0.f;
+    for (int u = 0; u < a.U; ++u) {
+      float dl = a.dlogits[n * a.U + u];
+      acc[u] += f * dl;
+      if (c < a.C) df += dl * a.w[(size_t)c * a.U + u];
+    }
+    if (c < a.C) {
+      float v = df * inv_hw;
+      for (int p = 0; p < a.HW; ++p) a.dA[((size_t)n * a.HW + p) * a.ldda + c] = v;
+    }
+  }
+  for (int u = 0; u < a.U; ++u) {
+    if (grp == 0) s_dw[cl][u] = 0.f;
+  }
+  __syncthreads();
+  for (int u = 0; u < a.U; ++u) atomicAdd(&s_dw[cl][u], acc[u]);
+  __syncthreads();
+  if (grp == 0 && c < a.C)
+    for (int u = 0; u < a.U; ++u) atomicAdd(&a.dw[(size_t)c * a.U + u], s_dw[cl][u]);
+  if (blockIdx.x == 0 && threadIdx.x < a.U && a.db) {
+    float s = 0.f;
+    for (int n = 0; n < a.N; ++n) s += a.dlogits[n * a.U + threadIdx.x];
+    atomicAdd(&a.db[threadIdx.x], s);
+  }
+}
+
+hipError_t head_bwd(const HeadBwdArgs& a, hipStream_t st) {
+  if (a.U > 16) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(head_bwd_kernel, dim3((a.C + 63) / 64), dim3(256), 0, st, a);
+  return hipGetLastError();
+}
+
+// ------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void rmsprop_kernel(float* __restrict__ w, const float* __restrict__ g,
+                                                      float* __restrict__ ms, long long n4, float lr,
+                                                      float rho, float eps, float gs) {
+  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n4;
+       i += (long long)gridDim.x * blockDim.x) {
+    float4 gv = reinterpret_cast<const float4*>(g)[i];
+    float4 mv = reinterpret_cast<float4*>(ms)[i];
+    float4 wv = reinterpret_cast<float4*>(w)[i];
+    float gg[4] = {gv.x * gs, gv.y * gs, gv.z * gs, gv.w * gs};
+    float mm[4] = {mv.x, mv.y, mv.z, mv.w};
+    float ww[4] = {wv.x, wv.y, wv.z, wv.w};
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      mm[j] = rho * mm[j] + (1.f - rho) * gg[j] * gg[j];
+      ww[j] -= lr * gg[j] / (sqrtf(mm[j]) + eps);
+    }
+    reinterpret_cast<float4*>(ms)[i] = make_float4(mm[0], mm[1], mm[2], mm[3]);
+    reinterpret_cast<float4*>(w)[i] = make_float4(ww[0], ww[1], ww[2], ww[3]);
+  }
+}
+
+hipError_t rmsprop(float* w, const float* g, float* ms, long long n, float lr, float rho, float eps,
+                   float grad_scale, hipStream_t st) {
+  long long n4 = n / 4;  // arena sizes are multiples of 64 elements
+  long long blocks = (n4 + 255) / 256;
+  if (blocks > 8192) blocks = 8192;
+  if (blocks < 1) blocks = 1;
+  hipLaunchKernelGGL(rmsprop_kernel, dim3((int)blocks), dim3(256), 0, st, w, g, ms, n4, lr, rho, eps,
+                     grad_scale);
+  return hipGetLastError();
+}
+
+// ------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void cast_weights_kernel(const CastEntry* __restrict__ es, int n,
+                                                           long long total) {
+  for (long long t = blockIdx.x * (long long)blockDim.x + threadIdx.x; t < total;
+       t += (long long)gridDim.x * blockDim.x) {
+    int lo = 0, hi = n - 1;
+    while (lo < hi) {
+      int mid = (lo + hi + 1) >> 1;
+      if (es[mid].begin <= t) lo = mid; else hi = mid - 1;
+    }
+    const CastEntry& e = es[lo];
+    long long i = t - e.begin;
+    if (e.dw) {
+      // depthwise (KH,KW,C,1) -> [C][KH][KW]
+      int rs = (int)(i % (e.KH * e.KW));
+      int c = (int)(i / (e.KH * e.KW));
+      e.fwd[i] = f2bf(e.src[(size_t)rs * e.Cin + c]);
+      continue;
+    }
+    // destination index i over [Cout][KH][KW][Cpad]
+    int c = (int)(i % e.Cpad);
+    long long t2 = i / e.Cpad;
+    int s = (int)(t2 % e.KW);
+    t2 /= e.KW;
+    int r = (int)(t2 % e.KH);
+    int co = (int)(t2 / e.KH);
+    float v = 0.f;
+    if (c < e.Cin) v = e.src[(((size_t)r * e.KW + s) * e.Cin + c) * e.Cout + co];
+    e.fwd[i] = f2bf(v);
+    if (e.dgrad && c < e.Cin) {
+      // Wf[c][KH-1-r][KW-1-s][co]
+      e.dgrad[(((size_t)c * e.KH + (e.KH - 1 - r)) * e.KW + (e.KW - 1 - s)) * e.Cout + co] = f2bf(v);
+    }
+  }
+}
+
+hipError_t cast_weights(const CastEntry* d_entries, int n, long long total, hipStream_t st) {
+  if (n == 0 || total == 0) return hipSuccess;
+  long long blocks = (total + 255) / 256;
+  if (blocks > 4096) blocks = 4096;
+  hipLaunchKernelGGL(cast_weights_kernel, dim3((int)blocks), dim3(256), 0, st, d_entries, n, total);
+  return hipGetLastError();
+}
+
+// ------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void input_stage_kernel(const void* x, int u8, long long npix, int C,
+                                                          bf16_t* y, int Cpad) {
+  for (long long p = blockIdx.x * (long long)blockDim.x + threadIdx.x; p < npix;
+       p += (long long)gridDim.x * blockDim.x) {
+    float v[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    for (int c = 0; c < C && c < 8; ++c) {
+      v[c] = u8 ? (float)reinterpret_cast<const uint8_t*>(x)[p * C + c] * (1.f / 255.f)
+                : reinterpret_cast<const float*>(x)[p * C + c];
+    }
+    for (int c0 = 0; c0 < Cpad; c0 += 8) {
+      uint4 q = c0 == 0 ? pack8(v) : make_uint4(0, 0, 0, 0);
+      *reinterpret_cast<uint4*>(y + p * Cpad + c0) = q;
+    }
+  }
+}
+
+hipError_t input_stage(const void* x, int x_u8, int N, int H, int W, int C, bf16_t* y, int Cpad,
+                       hipStream_t st) {
+  long long npix = (long long)N * H * W;
+  long long blocks = (npix + 255) / 256;
+  if (blocks > 4096) blocks = 4096;
+  hipLaunchKernelGGL(input_stage_kernel, dim3((int)blocks), dim3(256), 0, st, x, x_u8, npix, C, y, Cpad);
+  return hipGetLastError();
+}
+
+// ------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void bn_stats_kernel(const bf16_t* x, int ldx, int M, int C,
+                                                       float* stats, int stats_ld, int stats_off) {
+  extern __shared__ float sh[];
+  float* s_a = sh;
+  float* s_b = sh + C;
+  for (int c = threadIdx.x; c < C; c += blockDim.x) { s_a[c] = 0.f; s_b[c] = 0.f; }
+  __syncthreads();
+  ChunkMap cm(C);
+  if (cm.active()) {
+    const int c = cm.tx * 8;
+    float ps[8] = {0}, pq[8] = {0};
+    for (int row = blockIdx.x * cm.R + cm.ty; row < M; row += gridDim.x * cm.R) {
+      float v[8];
+      unpack8(*reinterpret_cast<const uint4*>(x + (size_t)row * ldx + c), v);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) { ps[j] += v[j]; pq[j] += v[j] * v[j]; }
+    }
+#pragma unroll
+    for (int j = 0; j < 8; ++j) { atomicAdd(&s_a[c + j], ps[j]); atomicAdd(&s_b[c + j], pq[j]); }
+  }
+  flush_sums(s_a, s_b, C, stats + stats_off, stats + stats_ld + stats_off);
+}
+
+hipError_t bn_stats(const bf16_t* x, int ldx, int M, int C, float* stats, int stats_ld, int stats_off,
+                    hipStream_t st) {
+  hipLaunchKernelGGL(bn_stats_kernel, dim3(grid_rows(M, C, 16)), dim3(256), 2 * C * 4, st, x, ldx, M, C,
+                     stats, stats_ld, stats_off);
+  return hipGetLastError();
+}
+
+// y = act(bn(x)) [+ res]; optional stats of y  (MobileNetV2 block outputs, eval paths)
+__global__ __launch_bounds__(256) void bn_apply_kernel(const bf16_t* x, int ldx, BnArgs bn, const bf16_t* res,
+                                                       int ldres, bf16_t* y, int ldy, int M, int C,
+                                                       float* stats, int stats_ld) {
+  extern __shared__ float sh[];
+  float* s_sc = sh;
+  float* s_sh = sh + C;
+  float* s_a = sh + 2 * C;
+  float* s_b = sh + 3 * C;
+  for (int c = threadIdx.x; c < C; c += blockDim.x) {
+    bn_coeffs(bn, c, s_sc[c], s_sh[c]);
+    s_a[c] = 0.f; s_b[c] = 0.f;
+  }
+  __syncthreads();
+  ChunkMap cm(C);
+  if (cm.active()) {
+    const int c = cm.tx * 8;
+    float ps[8] = {0}, pq[8] = {0};
+    for (int row = blockIdx.x * cm.R + cm.ty; row < M; row += gridDim.x * cm.R) {
+      float v[8];
+      unpack8(*reinterpret_cast<const uint4*>(x + (size_t)row * ldx + c), v);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[j] = apply_act(v[j] * s_sc[c + j] + s_sh[c + j], bn.act);
+      if (res) {
+        float r[8];
+        unpack8(*reinterpret_cast<const uint4*>(res + (size_t)row * ldres + c), r);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) v[j] += r[j];
+      }
+      uint4 p = pack8(v);
+      *reinterpret_cast<uint4*>(y + (size_t)row * ldy + c) = p;
+      if (stats) {
+        unpack8(p, v);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) { ps[j] += v[j]; pq[j] += v[j] * v[j]; }
+      }
+    }
+    if (stats) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) { atomicAdd(&s_a[c + j], ps[j]); atomicAdd(&s_b[c + j], pq[j]); }
+    }
+  }
+  if (stats) flush_sums(s_a, s_b, C, stats, stats + stats_ld);
+}
+
+hipError_t bn_apply(const bf16_t* x, int ldx, BnArgs bn, const bf16_t* res, int ldres, bf16_t* y, int ldy,
+                    int M, int C, float* stats, int stats_ld, hipStream_t st) {
+  hipLaunchKernelGGL(bn_apply_kernel, dim3(grid_rows(M, C)), dim3(256), 4 * C * 4, st, x, ldx, bn, res, ldres,
+                     y, ldy, M, C, stats, stats_ld);
+  return hipGetLastError();
+}
+
+}  // namespace idc

@@ -1,0 +1,302 @@
+// Native execution plan for the idc_models_amd MI355X runtime.
+//
+// The Python lowering (idc_models_amd/runtime) turns a model + batch shape into a STATIC list of
+// kernel launches over preallocated arenas (activations, statistics, gradients, weights).  This
+// file owns that list: ops are appended once (argument structs copied in as raw bytes whose
+// layout is mirrored by ctypes on the Python side and checked via `struct_sizes()`), then
+//
+//   * run(begin, end, stream)        issues ops[begin:end] back-to-back from C++ (no Python per
+//                                     kernel), used for eager steps and for segment replays;
+//   * capture(begin, end, stream)    records ops[begin:end] into a hipGraph (thread-local capture
+//                                     mode) and instantiates it -> graph id;
+//   * launch(graph, stream)          replays a captured segment: one host call per segment.
+//
+// A training step is typically 3 graphs (forward, backward, optimizer) or, under data
+// parallelism, backward split into bucket-aligned segments so RCCL all-reduces (issued by
+// torch.distributed on its own stream) overlap the remaining backward segments.
+#include <hip/hip_runtime.h>
+#include <pybind11/pybind11.h>
+#include <pybind11/stl.h>
+
+#include <cstring>
+#include <stdexcept>
+#include <string>
+#include <vector>
+
+#include "../kernels/conv_igemm.h"
+#include "../kernels/conv_wgrad.h"
+#include "../kernels/dwconv.h"
+#include "../kernels/nn_kernels.h"
+#include "../kernels/secagg.h"
+
+namespace py = pybind11;
+using namespace idc;
+
+namespace {
+
+enum OpKind : int {
+  OP_CONV = 0,
+  OP_WGRAD = 1,
+  OP_BN_BWD_APPLY = 2,
+  OP_BN_BWD_REDUCE = 3,
+  OP_MAXPOOL = 4,
+  OP_AVGPOOL = 5,
+  OP_POOL_BWD = 6,
+  OP_BN_MOVING = 7,
+  OP_HEAD_FWD = 8,
+  OP_HEAD_BWD = 9,
+  OP_RMSPROP = 10,
+  OP_CAST = 11,
+  OP_INPUT = 12,
+  OP_MEMSET = 13,
+  OP_BN_STATS = 14,
+  OP_BN_APPLY = 15,
+  OP_DW_FWD = 16,
+  OP_DW_BWD_DATA = 17,
+  OP_DW_WGRAD = 18,
+  OP_COPY = 19,
+};
+
+struct Op {
+  int kind;
+  int i[8];
+  float f[8];
+  long long l[4];
+  uintptr_t p[8];
+  std::vector<unsigned char> blob;
+};
+
+inline void check(hipError_t e, const char* what) {
+  if (e != hipSuccess) throw std::runtime_error(std::string(what) + ": " + hipGetErrorString(e));
+}
+
+template <typename T>
+const T& as(const Op& op) {
+  if (op.blob.size() != sizeof(T)) throw std::runtime_error("bad op payload size");
+  return *reinterpret_cast<const T*>(op.blob.data());
+}
+
+class Plan {
+ public:
+  ~Plan() { clear_graphs(); }
+
+  int add(int kind, py::bytes payload, std::vector<int> ints, std::vector<float> floats,
+          std::vector<long long> longs, std::vector<uintptr_t> ptrs) {
+    Op op;
+    op.kind = kind;
+    std::memset(op.i, 0, sizeof(op.i));
+    std::memset(op.f, 0, sizeof(op.f));
+    std::memset(op.l, 0, sizeof(op.l));
+    std::memset(op.p, 0, sizeof(op.p));
+    std::string s = payload;
+    op.blob.assign(s.begin(), s.end());
+    for (size_t k = 0; k < ints.size() && k < 8; ++k) op.i[k] = ints[k];
+    for (size_t k = 0; k < floats.size() && k < 8; ++k) op.f[k] = floats[k];
+    for (size_t k = 0; k < longs.size() && k < 4; ++k) op.l[k] = longs[k];
+    for (size_t k = 0; k < ptrs.size() && k < 8; ++k) op.p[k] = ptrs[k];
+    ops_.push_back(std::move(op));
+    return (int)ops_.size() - 1;
+  }
+
+  void set_float(int idx, int slot, float v) { ops_.at(idx).f[slot] = v; }
+
+  int size() const { return (int)ops_.size(); }
+
+  void run(int begin, int end, uintptr_t stream) {
+    hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+    if (end < 0 || end > (int)ops_.size()) end = (int)ops_.size();
+    for (int k = begin; k < end; ++k) exec(ops_[k], st);
+  }
+
+  int capture(int begin, int end, uintptr_t stream) {
+    hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+    if (end < 0 || end > (int)ops_.size()) end = (int)ops_.size();
+    check(hipStreamBeginCapture(st, hipStreamCaptureModeThreadLocal), "hipStreamBeginCapture");
+    try {
+      for (int k = begin; k < end; ++k) exec(ops_[k], st);
+    } catch (...) {
+      hipGraph_t g;
+      hipStreamEndCapture(st, &g);
+      if (g) hipGraphDestroy(g);
+      throw;
+    }
+    hipGraph_t g = nullptr;
+    check(hipStreamEndCapture(st, &g), "hipStreamEndCapture");
+    hipGraphExec_t ex = nullptr;
+    check(hipGraphInstantiate(&ex, g, nullptr, nullptr, 0), "hipGraphInstantiate");
+    graphs_.push_back(g);
+    execs_.push_back(ex);
+    return (int)execs_.size() - 1;
+  }
+
+  void launch(int gid, uintptr_t stream) {
+    check(hipGraphLaunch(execs_.at(gid), reinterpret_cast<hipStream_t>(stream)), "hipGraphLaunch");
+  }
+
+  void clear_graphs() {
+    for (auto e : execs_) hipGraphExecDestroy(e);
+    for (auto g : graphs_) hipGraphDestroy(g);
+    execs_.clear();
+    graphs_.clear();
+  }
+
+  std::string describe(int idx) const {
+    static const char* names[] = {"conv", "wgrad", "bn_bwd_apply", "bn_bwd_reduce", "maxpool", "avgpool",
+                                  "pool_bwd", "bn_moving", "head_fwd", "head_bwd", "rmsprop", "cast",
+                                  "input", "memset", "bn_stats", "bn_apply", "dw_fwd", "dw_bwd_data",
+                                  "dw_wgrad", "copy"};
+    int k = ops_.at(idx).kind;
+    return (k >= 0 && k < 20) ? names[k] : "?";
+  }
+
+ private:
+  void exec(const Op& op, hipStream_t st) {
+    switch (op.kind) {
+      case OP_CONV: check(conv_igemm(as<ConvArgs>(op), op.i[0], op.i[1] != 0, st), "conv_igemm"); break;
+      case OP_WGRAD: check(conv_wgrad(as<WgradArgs>(op), op.i[0], op.i[1] != 0, st), "conv_wgrad"); break;
+      case OP_BN_BWD_APPLY: check(bn_bwd_apply(as<BnBwdApplyArgs>(op), st), "bn_bwd_apply"); break;
+      case OP_BN_BWD_REDUCE: check(bn_bwd_reduce(as<BnBwdReduceArgs>(op), st), "bn_bwd_reduce"); break;
+      case OP_MAXPOOL: check(maxpool_fwd(as<PoolArgs>(op), st), "maxpool_fwd"); break;
+      case OP_AVGPOOL: check(avgpool_fwd(as<PoolArgs>(op), st), "avgpool_fwd"); break;
+      case OP_POOL_BWD: check(pool_bwd(as<PoolBwdArgs>(op), st), "pool_bwd"); break;
+      case OP_BN_MOVING:
+        check(bn_update_moving(reinterpret_cast<const BnMovingDesc*>(op.p[0]), op.i[0], op.i[1], st),
+              "bn_update_moving");
+        break;
+      case OP_HEAD_FWD: check(head_fwd(as<HeadArgs>(op), st), "head_fwd"); break;
+      case OP_HEAD_BWD: check(head_bwd(as<HeadBwdArgs>(op), st), "head_bwd"); break;
+      case OP_RMSPROP:
+        check(rmsprop(reinterpret_cast<float*>(op.p[0]), reinterpret_cast<const float*>(op.p[1]),
+                      reinterpret_cast<float*>(op.p[2]), op.l[0], op.f[0], op.f[1], op.f[2], op.f[3], st),
+              "rmsprop");
+        break;
+      case OP_CAST:
+        check(cast_weights(reinterpret_cast<const CastEntry*>(op.p[0]), op.i[0], op.l[0], st), "cast_weights");
+        break;
+      case OP_INPUT:
+        check(input_stage(reinterpret_cast<const void*>(op.p[0]), op.i[0], op.i[1], op.i[2], op.i[3], op.i[4],
+                          reinterpret_cast<bf16_t*>(op.p[1]), op.i[5], st),
+              "input_stage");
+        break;
+      case OP_MEMSET:
+        check(hipMemsetAsync(reinterpret_cast<void*>(op.p[0]), 0, (size_t)op.l[0], st), "memset");
+        break;
+      case OP_BN_STATS:
+        check(bn_stats(reinterpret_cast<const bf16_t*>(op.p[0]), op.i[0], op.i[1], op.i[2],
+                       reinterpret_cast<float*>(op.p[1]), op.i[3], op.i[4], st),
+              "bn_stats");
+        break;
+      case OP_BN_APPLY: {
+        const BnArgs& bn = as<BnArgs>(op);
+        check(bn_apply(reinterpret_cast<const bf16_t*>(op.p[0]), op.i[0], bn,
+                       reinterpret_cast<const bf16_t*>(op.p[1]), op.i[1], reinterpret_cast<bf16_t*>(op.p[2]),
+                       op.i[2], op.i[3], op.i[4], reinterpret_cast<float*>(op.p[3]), op.i[5], st),
+              "bn_apply");
+        break;
+      }
+      case OP_DW_FWD: check(dwconv_fwd(as<DwArgs>(op), st), "dwconv_fwd"); break;
+      case OP_DW_BWD_DATA: check(dwconv_bwd_data(as<DwArgs>(op), st), "dwconv_bwd_data"); break;
+      case OP_DW_WGRAD: check(dwconv_wgrad(as<DwArgs>(op), st), "dwconv_wgrad"); break;
+      case OP_COPY:
+        check(hipMemcpyAsync(reinterpret_cast<void*>(op.p[0]), reinterpret_cast<const void*>(op.p[1]),
+                             (size_t)op.l[0], hipMemcpyDeviceToDevice, st),
+              "copy");
+        break;
+      default: throw std::runtime_error("unknown op kind");
+    }
+  }
+
+  std::vector<Op> ops_;
+  std::vector<hipGraph_t> graphs_;
+  std::vector<hipGraphExec_t> execs_;
+};
+
+// direct (non-plan) entry points, used by the op-level python API and tests
+void py_conv(py::bytes payload, int tile, int a_f32, uintptr_t stream) {
+  std::string s = payload;
+  if (s.size() != sizeof(ConvArgs)) throw std::runtime_error("ConvArgs size mismatch");
+  ConvArgs a;
+  std::memcpy(&a, s.data(), sizeof(a));
+  if (tile < 0) tile = conv_pick_tile(a.N * a.Ho * a.Wo, a.Cout);
+  check(conv_igemm(a, tile, a_f32 != 0, reinterpret_cast<hipStream_t>(stream)), "conv_igemm");
+}
+
+void py_wgrad(py::bytes payload, int splits, int g_f32, uintptr_t stream) {
+  std::string s = payload;
+  if (s.size() != sizeof(WgradArgs)) throw std::runtime_error("WgradArgs size mismatch");
+  WgradArgs a;
+  std::memcpy(&a, s.data(), sizeof(a));
+  if (splits <= 0) splits = wgrad_pick_splits(a.N * a.Ho * a.Wo, a.KH * a.KW * a.Cin, a.Cout);
+  check(conv_wgrad(a, splits, g_f32 != 0, reinterpret_cast<hipStream_t>(stream)), "conv_wgrad");
+}
+
+py::dict struct_sizes() {
+  py::dict d;
+  d["BnArgs"] = sizeof(BnArgs);
+  d["ConvArgs"] = sizeof(ConvArgs);
+  d["WgradArgs"] = sizeof(WgradArgs);
+  d["BnBwdApplyArgs"] = sizeof(BnBwdApplyArgs);
+  d["BnBwdReduceArgs"] = sizeof(BnBwdReduceArgs);
+  d["PoolArgs"] = sizeof(PoolArgs);
+  d["PoolBwdArgs"] = sizeof(PoolBwdArgs);
+  d["BnMovingDesc"] = sizeof(BnMovingDesc);
+  d["HeadArgs"] = sizeof(HeadArgs);
+  d["HeadBwdArgs"] = sizeof(HeadBwdArgs);
+  d["CastEntry"] = sizeof(CastEntry);
+  d["DwArgs"] = sizeof(DwArgs);
+  d["ConvArgs.mbn"] = offsetof(ConvArgs, mbn);
+  d["ConvArgs.gsumx"] = offsetof(ConvArgs, gsumx);
+  d["WgradArgs.pix_per_split"] = offsetof(WgradArgs, pix_per_split);
+  d["HeadArgs.training"] = offsetof(HeadArgs, training);
+  d["PoolBwdArgs.is_avg"] = offsetof(PoolBwdArgs, is_avg);
+  return d;
+}
+
+int py_pick_tile(int M, int Cout) { return conv_pick_tile(M, Cout); }
+int py_pick_splits(int M, int K, int Cout) { return wgrad_pick_splits(M, K, Cout); }
+
+void py_secagg_mask(uintptr_t x, uintptr_t out, long long n, float scale, float clip, int nclients,
+                    int rank, unsigned long long seed, unsigned long long round_, uintptr_t stream) {
+  check(secagg_quantize_mask(reinterpret_cast<const float*>(x), reinterpret_cast<uint32_t*>(out), n, scale, clip,
+                             nclients, rank, seed, round_, reinterpret_cast<hipStream_t>(stream)),
+        "secagg_quantize_mask");
+}
+
+void py_secagg_unmask(uintptr_t sum, uintptr_t out, long long n, float scale, int nclients, float divisor,
+                      uintptr_t stream) {
+  check(secagg_dequantize(reinterpret_cast<const uint32_t*>(sum), reinterpret_cast<float*>(out), n, scale,
+                          nclients, divisor, reinterpret_cast<hipStream_t>(stream)),
+        "secagg_dequantize");
+}
+
+void py_rmsprop(uintptr_t w, uintptr_t g, uintptr_t ms, long long n, float lr, float rho, float eps, float gs,
+                uintptr_t stream) {
+  check(rmsprop(reinterpret_cast<float*>(w), reinterpret_cast<const float*>(g), reinterpret_cast<float*>(ms), n,
+                lr, rho, eps, gs, reinterpret_cast<hipStream_t>(stream)),
+        "rmsprop");
+}
+
+}  // namespace
+
+PYBIND11_MODULE(_idc_native, m) {
+  m.doc() = "idc_models_amd native MI355X (gfx950) kernels and plan executor";
+  py::class_<Plan>(m, "Plan")
+      .def(py::init<>())
+      .def("add", &Plan::add)
+      .def("set_float", &Plan::set_float)
+      .def("size", &Plan::size)
+      .def("run", &Plan::run)
+      .def("capture", &Plan::capture)
+      .def("launch", &Plan::launch)
+      .def("clear_graphs", &Plan::clear_graphs)
+      .def("describe", &Plan::describe);
+  m.def("conv", &py_conv);
+  m.def("wgrad", &py_wgrad);
+  m.def("struct_sizes", &struct_sizes);
+  m.def("pick_tile", &py_pick_tile);
+  m.def("pick_splits", &py_pick_splits);
+  m.def("rmsprop", &py_rmsprop);
+  m.def("secagg_mask", &py_secagg_mask);
+  m.def("secagg_unmask", &py_secagg_unmask);
+  m.attr("OP_CONV") = (int)OP_CONV;
+}

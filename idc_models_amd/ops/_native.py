@@ -1,0 +1,198 @@
+"""Loader for the native MI355X extension + ctypes mirrors of its argument structs.
+
+The kernels take plain C structs (``csrc/kernels/*.h``).  Python fills the identical layout with
+``ctypes`` and hands the raw bytes to the C++ plan (``csrc/runtime/plan.cpp``); sizes and a few
+field offsets are verified against ``sizeof/offsetof`` reported by the extension at import time,
+so a layout drift fails loudly instead of corrupting a launch.
+
+On a machine with a GPU the extension MUST load (there is no silent eager fallback for the fused
+runtime); on a CPU-only machine ``available()`` is False and only the reference path runs.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import importlib
+import os
+
+import torch
+
+_ext = None
+_err = None
+
+vp = C.c_void_p
+ci = C.c_int
+cf = C.c_float
+cll = C.c_longlong
+
+
+class BnArgs(C.Structure):
+    _fields_ = [("stats", vp), ("gamma", vp), ("beta", vp), ("mmean", vp), ("mvar", vp),
+                ("inv_count", cf), ("eps", cf), ("mode", ci), ("act", ci), ("C", ci)]
+
+
+class ConvArgs(C.Structure):
+    _fields_ = [("x", vp), ("N", ci), ("H", ci), ("W", ci), ("Cin", ci), ("ldx", ci),
+                ("Ho", ci), ("Wo", ci), ("Cout", ci), ("y", vp), ("ldy", ci),
+                ("w", vp), ("KH", ci), ("KW", ci), ("SH", ci), ("SW", ci), ("PT", ci), ("PL", ci),
+                ("pro", BnArgs), ("epi_mode", ci), ("bias", vp), ("epi_act", ci), ("out_mode", ci),
+                ("stats_out", vp), ("stats_ld", ci), ("stats_off", ci),
+                ("mx", vp), ("ldmx", ci), ("mbn", BnArgs), ("gsum", vp), ("gsumx", vp)]
+
+
+class WgradArgs(C.Structure):
+    _fields_ = [("x", vp), ("N", ci), ("H", ci), ("W", ci), ("Cin", ci), ("ldx", ci),
+                ("g", vp), ("ldg", ci), ("Ho", ci), ("Wo", ci), ("Cout", ci),
+                ("KH", ci), ("KW", ci), ("SH", ci), ("SW", ci), ("PT", ci), ("PL", ci),
+                ("pro", BnArgs), ("dw", vp), ("scale", cf), ("cin_real", ci), ("pix_per_split", ci)]
+
+
+class BnBwdApplyArgs(C.Structure):
+    _fields_ = [("dz", vp), ("lddz", ci), ("x", vp), ("ldx", ci), ("bn", BnArgs),
+                ("gsum", vp), ("gsumx", vp), ("inv_n", cf), ("dst", vp), ("lddst", ci),
+                ("dst_f32", ci), ("accumulate", ci), ("M", ci), ("C", ci)]
+
+
+class BnBwdReduceArgs(C.Structure):
+    _fields_ = [("dy", vp), ("lddy", ci), ("dy_f32", ci), ("x", vp), ("ldx", ci), ("bn", BnArgs),
+                ("dz", vp), ("lddz", ci), ("gsum", vp), ("gsumx", vp), ("M", ci), ("C", ci)]
+
+
+class PoolArgs(C.Structure):
+    _fields_ = [("x", vp), ("ldx", ci), ("N", ci), ("H", ci), ("W", ci), ("C", ci),
+                ("pro", BnArgs), ("k", ci), ("s", ci), ("pt", ci), ("pl", ci), ("Ho", ci),
+                ("Wo", ci), ("y", vp), ("ldy", ci), ("argmax", vp), ("stats", vp),
+                ("stats_ld", ci), ("stats_off", ci)]
+
+
+class PoolBwdArgs(C.Structure):
+    _fields_ = [("dy", vp), ("lddy", ci), ("dy_f32", ci), ("argmax", vp), ("N", ci), ("H", ci),
+                ("W", ci), ("C", ci), ("k", ci), ("s", ci), ("pt", ci), ("pl", ci), ("Ho", ci),
+                ("Wo", ci), ("x", vp), ("ldx", ci), ("bn", BnArgs), ("dx", vp), ("lddx", ci),
+                ("gsum", vp), ("gsumx", vp), ("is_avg", ci)]
+
+
+class BnMovingDesc(C.Structure):
+    _fields_ = [("stats", vp), ("C", ci), ("inv_count", cf), ("unbias", cf), ("mmean", vp),
+                ("mvar", vp), ("momentum", cf), ("ld", ci)]
+
+
+class HeadArgs(C.Structure):
+    _fields_ = [("x", vp), ("ldx", ci), ("N", ci), ("HW", ci), ("C", ci), ("U", ci),
+                ("pro", BnArgs), ("w", vp), ("b", vp), ("labels", vp), ("logits", vp),
+                ("feats", vp), ("dlogits", vp), ("loss", vp), ("loss_scale", cf), ("training", ci)]
+
+
+class HeadBwdArgs(C.Structure):
+    _fields_ = [("feats", vp), ("dlogits", vp), ("w", vp), ("N", ci), ("HW", ci), ("C", ci),
+                ("U", ci), ("dw", vp), ("db", vp), ("dA", vp), ("ldda", ci)]
+
+
+class CastEntry(C.Structure):
+    _fields_ = [("src", vp), ("fwd", vp), ("dgrad", vp), ("KH", ci), ("KW", ci), ("Cin", ci),
+                ("Cout", ci), ("Cpad", ci), ("dw", ci), ("begin", cll)]
+
+
+class DwArgs(C.Structure):
+    _fields_ = [("x", vp), ("ldx", ci), ("N", ci), ("H", ci), ("W", ci), ("C", ci),
+                ("pro", BnArgs), ("w", vp), ("KH", ci), ("KW", ci), ("S", ci), ("PT", ci),
+                ("PL", ci), ("Ho", ci), ("Wo", ci), ("y", vp), ("ldy", ci), ("stats", vp),
+                ("stats_ld", ci), ("dy", vp), ("lddy", ci), ("dx", vp), ("lddx", ci),
+                ("gsum", vp), ("gsumx", vp), ("dw", vp)]
+
+
+_STRUCTS = {"BnArgs": BnArgs, "ConvArgs": ConvArgs, "WgradArgs": WgradArgs,
+            "BnBwdApplyArgs": BnBwdApplyArgs, "BnBwdReduceArgs": BnBwdReduceArgs,
+            "PoolArgs": PoolArgs, "PoolBwdArgs": PoolBwdArgs, "BnMovingDesc": BnMovingDesc,
+            "HeadArgs": HeadArgs, "HeadBwdArgs": HeadBwdArgs, "CastEntry": CastEntry,
+            "DwArgs": DwArgs}
+
+# op kinds (csrc/runtime/plan.cpp)
+OP_CONV, OP_WGRAD, OP_BN_BWD_APPLY, OP_BN_BWD_REDUCE, OP_MAXPOOL, OP_AVGPOOL, OP_POOL_BWD = range(7)
+OP_BN_MOVING, OP_HEAD_FWD, OP_HEAD_BWD, OP_RMSPROP, OP_CAST, OP_INPUT, OP_MEMSET = range(7, 14)
+OP_BN_STATS, OP_BN_APPLY, OP_DW_FWD, OP_DW_BWD_DATA, OP_DW_WGRAD, OP_COPY = range(14, 20)
+
+ACT = {None: 0, "none": 0, "linear": 0, "relu": 1, "relu6": 2}
+OUT_BF16, OUT_F32, OUT_F32_ACC = 0, 1, 2
+
+
+def _verify(ext):
+    sizes = ext.struct_sizes()
+    for name, cls in _STRUCTS.items():
+        if C.sizeof(cls) != sizes[name]:
+            raise RuntimeError(f"native struct {name}: ctypes {C.sizeof(cls)} != C++ {sizes[name]}")
+    checks = {"ConvArgs.mbn": ConvArgs.mbn.offset, "ConvArgs.gsumx": ConvArgs.gsumx.offset,
+              "WgradArgs.pix_per_split": WgradArgs.pix_per_split.offset,
+              "HeadArgs.training": HeadArgs.training.offset,
+              "PoolBwdArgs.is_avg": PoolBwdArgs.is_avg.offset}
+    for k, v in checks.items():
+        if sizes[k] != v:
+            raise RuntimeError(f"native struct field {k}: ctypes offset {v} != C++ {sizes[k]}")
+
+
+def load(build_if_missing: bool = True):
+    """Import the extension (building it first if the .so is absent and hipcc exists)."""
+    global _ext, _err
+    if _ext is not None:
+        return _ext
+    try:
+        _ext = importlib.import_module("idc_models_amd._idc_native")
+    except ImportError as e:  # pragma: no cover - exercised on fresh checkouts
+        _err = e
+        if build_if_missing and os.path.exists("/opt/rocm/bin/hipcc"):
+            import sys
+            root = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+            sys.path.insert(0, root)
+            from tools.build_native import build
+            build(verbose=False)
+            _ext = importlib.import_module("idc_models_amd._idc_native")
+        else:
+            raise
+    _verify(_ext)
+    return _ext
+
+
+def available() -> bool:
+    try:
+        load(build_if_missing=False)
+        return True
+    except Exception:
+        return False
+
+
+def require():
+    """The GPU path must run native code: raise loudly if it cannot."""
+    try:
+        return load()
+    except Exception as e:
+        raise RuntimeError("idc_models_amd native extension (gfx950 HIP kernels) is not available; "
+                           "run `python tools/build_native.py`") from e
+
+
+def ptr(t) -> int:
+    if t is None:
+        return 0
+    if isinstance(t, int):
+        return t
+    return t.data_ptr()
+
+
+def stream_handle(stream=None) -> int:
+    s = stream if stream is not None else torch.cuda.current_stream()
+    return int(s.cuda_stream)
+
+
+def raw(struct) -> bytes:
+    return C.string_at(C.addressof(struct), C.sizeof(struct))
+
+
+def bn_args(stats=None, gamma=None, beta=None, mmean=None, mvar=None, count=1, eps=1e-3,
+            mode=0, act=0, C_=0) -> BnArgs:
+    b = BnArgs()
+    b.stats, b.gamma, b.beta = ptr(stats), ptr(gamma), ptr(beta)
+    b.mmean, b.mvar = ptr(mmean), ptr(mvar)
+    b.inv_count = 1.0 / float(max(count, 1))
+    b.eps = float(eps)
+    b.mode = int(mode)
+    b.act = int(act)
+    b.C = int(C_)
+    return b

@@ -1,0 +1,283 @@
+"""Functional NHWC ops on MI355X kernels (``torch.Tensor`` in / out, one launch each).
+
+These are thin wrappers that fill the kernel argument structs and launch on the current stream.
+They are what the numerics tests compare against PyTorch fp32 references, and a usable
+standalone API (``torch.nn.functional``-style, but NHWC bf16 with fused BN/activation).
+
+BN prologue/epilogue descriptors are passed as ``BN(...)`` objects:
+    BN(stats=[2C] sum|sumsq, gamma, beta, count)               batch statistics (mode 1)
+    BN(mean=..., var=..., gamma, beta, mode=2)                 inference statistics
+    BN(act=RELU)                                               activation only
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass
+from typing import Optional, Tuple
+
+import torch
+
+from . import _native as nat
+
+RELU, RELU6 = 1, 2
+
+
+@dataclass
+class BN:
+    stats: Optional[torch.Tensor] = None
+    gamma: Optional[torch.Tensor] = None
+    beta: Optional[torch.Tensor] = None
+    mean: Optional[torch.Tensor] = None
+    var: Optional[torch.Tensor] = None
+    count: int = 1
+    eps: float = 1e-3
+    mode: int = 1
+    act: int = 0
+    ld: Optional[int] = None
+
+    def args(self) -> nat.BnArgs:
+        if self.stats is None and self.mean is None:
+            return nat.bn_args(mode=0, act=self.act)
+        C = self.ld or (self.stats.numel() // 2 if self.stats is not None else self.mean.numel())
+        return nat.bn_args(stats=self.stats, gamma=self.gamma, beta=self.beta, mmean=self.mean,
+                           mvar=self.var, count=self.count, eps=self.eps,
+                           mode=self.mode if self.stats is not None or self.mode == 2 else 2,
+                           act=self.act, C_=C)
+
+
+def _ident():
+    return nat.bn_args(mode=0, act=0)
+
+
+def weight_fwd_layout(kernel_hwio: torch.Tensor, cpad: Optional[int] = None) -> torch.Tensor:
+    """Keras HWIO fp32 -> bf16 [Cout][KH][KW][Cpad]."""
+    kh, kw, cin, cout = kernel_hwio.shape
+    w = kernel_hwio.permute(3, 0, 1, 2)
+    if cpad and cpad > cin:
+        w = torch.nn.functional.pad(w, (0, cpad - cin))
+    return w.contiguous().to(torch.bfloat16)
+
+
+def weight_dgrad_layout(kernel_hwio: torch.Tensor) -> torch.Tensor:
+    """Keras HWIO -> bf16 flipped [Cin][KH][KW][Cout]."""
+    return kernel_hwio.flip(0, 1).permute(2, 0, 1, 3).contiguous().to(torch.bfloat16)
+
+
+def conv2d(x: torch.Tensor, kernel_hwio: torch.Tensor, stride=(1, 1), pads=(0, 0),
+           out_hw: Optional[Tuple[int, int]] = None, pro: Optional[BN] = None,
+           bias: Optional[torch.Tensor] = None, act: int = 0, out_f32: bool = False,
+           stats: Optional[torch.Tensor] = None, tile: int = -1,
+           w_layout: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """y = act(conv(pro(x)) + bias); x NHWC (bf16 or fp32), Cin % 8 == 0.  Optional output
+    statistics [sum|sumsq] accumulated into ``stats``."""
+    N, H, W, Cin = x.shape
+    kh, kw, kcin, cout = kernel_hwio.shape
+    if out_hw is None:
+        out_hw = ((H + 2 * pads[0] - kh) // stride[0] + 1, (W + 2 * pads[1] - kw) // stride[1] + 1)
+    Ho, Wo = out_hw
+    y = torch.empty((N, Ho, Wo, cout), dtype=torch.float32 if out_f32 else torch.bfloat16,
+                    device=x.device)
+    wl = w_layout if w_layout is not None else weight_fwd_layout(kernel_hwio, Cin)
+    a = nat.ConvArgs()
+    a.x = x.data_ptr()
+    a.N, a.H, a.W, a.Cin, a.ldx = N, H, W, Cin, Cin
+    a.Ho, a.Wo, a.Cout = Ho, Wo, cout
+    a.y, a.ldy = y.data_ptr(), cout
+    a.w = wl.data_ptr()
+    a.KH, a.KW, a.SH, a.SW = kh, kw, stride[0], stride[1]
+    a.PT, a.PL = pads
+    a.pro = pro.args() if pro is not None else _ident()
+    a.epi_mode = 0
+    a.bias = nat.ptr(bias)
+    a.epi_act = act
+    a.out_mode = nat.OUT_F32 if out_f32 else nat.OUT_BF16
+    if stats is not None:
+        a.stats_out, a.stats_ld, a.stats_off = stats.data_ptr(), cout, 0
+    a.mbn = _ident()
+    nat.require().conv(nat.raw(a), tile, 1 if x.dtype == torch.float32 else 0, nat.stream_handle())
+    return y
+
+
+def conv2d_dgrad(dy: torch.Tensor, kernel_hwio: torch.Tensor, in_hw: Tuple[int, int], pads=(0, 0),
+                 mx: Optional[torch.Tensor] = None, mbn: Optional[BN] = None,
+                 gsum: Optional[torch.Tensor] = None, gsumx: Optional[torch.Tensor] = None,
+                 out_f32: bool = False) -> torch.Tensor:
+    """Stride-1 data gradient.  With ``mx``/``mbn``: returns dZ = dX * act'(bn(mx)) and
+    accumulates sum(dZ) into gsum, sum(dZ*xhat) into gsumx."""
+    N, Ho, Wo, Cout = dy.shape
+    kh, kw, cin, _ = kernel_hwio.shape
+    H, W = in_hw
+    dx = torch.empty((N, H, W, cin), dtype=torch.float32 if out_f32 else torch.bfloat16,
+                     device=dy.device)
+    wl = weight_dgrad_layout(kernel_hwio)
+    a = nat.ConvArgs()
+    a.x = dy.data_ptr()
+    a.N, a.H, a.W, a.Cin, a.ldx = N, Ho, Wo, Cout, Cout
+    a.Ho, a.Wo, a.Cout = H, W, cin
+    a.y, a.ldy = dx.data_ptr(), cin
+    a.w = wl.data_ptr()
+    a.KH, a.KW, a.SH, a.SW = kh, kw, 1, 1
+    a.PT, a.PL = kh - 1 - pads[0], kw - 1 - pads[1]
+    a.pro = _ident()
+    a.mbn = _ident()
+    if mx is not None:
+        a.epi_mode = 1
+        a.mx, a.ldmx = mx.data_ptr(), cin
+        a.mbn = mbn.args()
+        a.gsum, a.gsumx = nat.ptr(gsum), nat.ptr(gsumx)
+    else:
+        a.out_mode = nat.OUT_F32 if out_f32 else nat.OUT_BF16
+    nat.require().conv(nat.raw(a), -1, 1 if dy.dtype == torch.float32 else 0, nat.stream_handle())
+    return dx
+
+
+def conv2d_wgrad(x: torch.Tensor, dy: torch.Tensor, kernel_shape, stride=(1, 1), pads=(0, 0),
+                 pro: Optional[BN] = None, cin_real: int = 0, splits: int = -1,
+                 out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """dW (Keras HWIO fp32) accumulated into ``out`` (zeros if not given)."""
+    N, H, W, Cin = x.shape
+    _, Ho, Wo, Cout = dy.shape
+    kh, kw = kernel_shape[0], kernel_shape[1]
+    creal = cin_real or Cin
+    if out is None:
+        out = torch.zeros((kh, kw, creal, Cout), dtype=torch.float32, device=x.device)
+    a = nat.WgradArgs()
+    a.x = x.data_ptr()
+    a.N, a.H, a.W, a.Cin, a.ldx = N, H, W, Cin, Cin
+    a.g, a.ldg = dy.data_ptr(), Cout
+    a.Ho, a.Wo, a.Cout = Ho, Wo, Cout
+    a.KH, a.KW, a.SH, a.SW = kh, kw, stride[0], stride[1]
+    a.PT, a.PL = pads
+    a.pro = pro.args() if pro is not None else _ident()
+    a.dw = out.data_ptr()
+    a.scale = 1.0
+    a.cin_real = cin_real
+    nat.require().wgrad(nat.raw(a), splits, 1 if dy.dtype == torch.float32 else 0, nat.stream_handle())
+    return out
+
+
+def _plan1(kind, payload=None, ints=(), floats=(), longs=(), ptrs=()):
+    p = nat.require().Plan()
+    p.add(kind, nat.raw(payload) if payload is not None else b"", list(ints), list(floats),
+          list(longs), [int(q) for q in ptrs])
+    p.run(0, -1, nat.stream_handle())
+
+
+def pool2d(x: torch.Tensor, k: int, s: int, pads=(0, 0), is_max=True, pro: Optional[BN] = None,
+           stats: Optional[torch.Tensor] = None, out_hw=None):
+    N, H, W, C = x.shape
+    if out_hw is None:
+        out_hw = ((H + 2 * pads[0] - k) // s + 1, (W + 2 * pads[1] - k) // s + 1)
+    Ho, Wo = out_hw
+    y = torch.empty((N, Ho, Wo, C), dtype=torch.bfloat16, device=x.device)
+    am = torch.empty((N * Ho * Wo * C,), dtype=torch.uint8, device=x.device) if is_max else None
+    a = nat.PoolArgs()
+    a.x, a.ldx = x.data_ptr(), C
+    a.N, a.H, a.W, a.C = N, H, W, C
+    a.pro = pro.args() if pro is not None else _ident()
+    a.k, a.s, a.pt, a.pl, a.Ho, a.Wo = k, s, pads[0], pads[1], Ho, Wo
+    a.y, a.ldy = y.data_ptr(), C
+    a.argmax = nat.ptr(am)
+    if stats is not None:
+        a.stats, a.stats_ld, a.stats_off = stats.data_ptr(), C, 0
+    _plan1(nat.OP_MAXPOOL if is_max else nat.OP_AVGPOOL, a)
+    return y, am
+
+
+def pool2d_bwd(dy: torch.Tensor, in_shape, k: int, s: int, pads=(0, 0), is_max=True, argmax=None,
+               x: Optional[torch.Tensor] = None, bn: Optional[BN] = None, gsum=None, gsumx=None):
+    N, H, W, C = in_shape
+    _, Ho, Wo, _ = dy.shape
+    dx = torch.empty((N, H, W, C), dtype=torch.bfloat16, device=dy.device)
+    a = nat.PoolBwdArgs()
+    a.dy, a.lddy, a.dy_f32 = dy.data_ptr(), C, 1 if dy.dtype == torch.float32 else 0
+    a.argmax = nat.ptr(argmax)
+    a.N, a.H, a.W, a.C, a.k, a.s, a.pt, a.pl, a.Ho, a.Wo = N, H, W, C, k, s, pads[0], pads[1], Ho, Wo
+    if x is not None:
+        a.x, a.ldx = x.data_ptr(), C
+        a.bn = bn.args()
+        a.gsum, a.gsumx = nat.ptr(gsum), nat.ptr(gsumx)
+    else:
+        a.bn = _ident()
+    a.dx, a.lddx = dx.data_ptr(), C
+    a.is_avg = 0 if is_max else 1
+    _plan1(nat.OP_POOL_BWD, a)
+    return dx
+
+
+def bn_bwd_apply(dz, x, bn: BN, gsum, gsumx, out_f32=False, dst=None, accumulate=False):
+    M, C = x.reshape(-1, x.shape[-1]).shape
+    if dst is None:
+        dst = torch.zeros(x.shape, dtype=torch.float32 if out_f32 else torch.bfloat16, device=x.device)
+    a = nat.BnBwdApplyArgs()
+    a.dz, a.lddz, a.x, a.ldx = dz.data_ptr(), C, x.data_ptr(), C
+    a.bn = bn.args()
+    a.gsum, a.gsumx = nat.ptr(gsum), nat.ptr(gsumx)
+    a.inv_n = 1.0 / M
+    a.dst, a.lddst = dst.data_ptr(), C
+    a.dst_f32 = 1 if dst.dtype == torch.float32 else 0
+    a.accumulate = 1 if accumulate else 0
+    a.M, a.C = M, C
+    _plan1(nat.OP_BN_BWD_APPLY, a)
+    return dst
+
+
+def bn_bwd_reduce(dy, x, bn: BN, gsum, gsumx, store_dz=True):
+    M, C = x.reshape(-1, x.shape[-1]).shape
+    dz = torch.empty(x.shape, dtype=torch.bfloat16, device=x.device) if store_dz else None
+    a = nat.BnBwdReduceArgs()
+    a.dy, a.lddy, a.dy_f32 = dy.data_ptr(), C, 1 if dy.dtype == torch.float32 else 0
+    a.x, a.ldx = x.data_ptr(), C
+    a.bn = bn.args()
+    a.dz, a.lddz = nat.ptr(dz), C
+    a.gsum, a.gsumx = nat.ptr(gsum), nat.ptr(gsumx)
+    a.M, a.C = M, C
+    _plan1(nat.OP_BN_BWD_REDUCE, a)
+    return dz
+
+
+def bn_stats(x: torch.Tensor) -> torch.Tensor:
+    M, C = x.reshape(-1, x.shape[-1]).shape
+    st = torch.zeros(2 * C, dtype=torch.float32, device=x.device)
+    _plan1(nat.OP_BN_STATS, ints=(C, M, C, C, 0), ptrs=(x.data_ptr(), st.data_ptr()))
+    return st
+
+
+def dwconv(x, kernel, stride=1, pads=(1, 1), out_hw=None, pro: Optional[BN] = None, stats=None):
+    N, H, W, C = x.shape
+    kh, kw = kernel.shape[0], kernel.shape[1]
+    if out_hw is None:
+        out_hw = ((H + 2 * pads[0] - kh) // stride + 1, (W + 2 * pads[1] - kw) // stride + 1)
+    Ho, Wo = out_hw
+    y = torch.empty((N, Ho, Wo, C), dtype=torch.bfloat16, device=x.device)
+    a = _dw_args(x, kernel, stride, pads, Ho, Wo, pro)
+    a.y, a.ldy = y.data_ptr(), C
+    if stats is not None:
+        a.stats, a.stats_ld = stats.data_ptr(), C
+    _plan1(nat.OP_DW_FWD, a)
+    return y
+
+
+def _dw_args(x, kernel, stride, pads, Ho, Wo, pro):
+    N, H, W, C = x.shape
+    a = nat.DwArgs()
+    a.x, a.ldx = x.data_ptr(), C
+    a.N, a.H, a.W, a.C = N, H, W, C
+    a.pro = pro.args() if pro is not None else _ident()
+    a.w = kernel.contiguous().data_ptr()
+    a.KH, a.KW, a.S, a.PT, a.PL, a.Ho, a.Wo = kernel.shape[0], kernel.shape[1], stride, pads[0], pads[1], Ho, Wo
+    return a
+
+
+def dwconv_bwd(x, kernel, dy, stride=1, pads=(1, 1), pro: Optional[BN] = None, gsum=None, gsumx=None):
+    N, H, W, C = x.shape
+    _, Ho, Wo, _ = dy.shape
+    a = _dw_args(x, kernel, stride, pads, Ho, Wo, pro)
+    dx = torch.empty_like(x)
+    dw = torch.zeros(kernel.shape, dtype=torch.float32, device=x.device)
+    a.dy, a.lddy = dy.data_ptr(), C
+    a.dx, a.lddx = dx.data_ptr(), C
+    a.gsum, a.gsumx = nat.ptr(gsum), nat.ptr(gsumx)
+    a.dw = dw.data_ptr()
+    _plan1(nat.OP_DW_BWD_DATA, a)
+    _plan1(nat.OP_DW_WGRAD, a)
+    return dx, dw

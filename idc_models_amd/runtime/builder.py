@@ -1,0 +1,373 @@
+"""Program builder: lowers a model into a static launch plan over preallocated device arenas.
+
+Design (MI355X-first):
+
+* shapes are static per (batch, training) — every buffer is allocated once, every kernel argument
+  struct is built once, and the whole step is replayed as HIP graphs by the native ``Plan``;
+* activations are NHWC bf16; "pending BN" — tensors are stored RAW (pre-BN) together with their
+  per-channel [sum|sumsq] batch statistics produced in the producer's epilogue, and every consumer
+  applies its own BN affine + activation while staging its operand (no BN/ReLU kernels);
+* all batch statistics of a step live in ONE stats arena (one memset per step), all gradients in
+  the flat fp32 gradient arena (one memset per step), all BN moving-average updates are ONE launch;
+* bf16 weight copies in kernel layouts (forward ``[Cout][KH][KW][Cin]``, flipped dgrad
+  ``[Cin][KH][KW][Cout]``) are produced from the fp32 Keras-layout masters by ONE cast launch
+  after each optimizer step.
+"""
+from __future__ import annotations
+
+import ctypes as C
+from dataclasses import dataclass
+from typing import Dict, List, Optional, Tuple
+
+import torch
+
+from ..ops import _native as nat
+
+BF16 = torch.bfloat16
+F32 = torch.float32
+
+
+@dataclass
+class Tensor4:
+    """A (possibly channel-sliced) NHWC tensor view: base tensor + channel offset + pixel stride."""
+    t: torch.Tensor
+    N: int
+    H: int
+    W: int
+    C: int          # channels of this view
+    ld: int         # pixel stride (elements)
+    coff: int = 0   # channel offset into base
+
+    @property
+    def ptr(self) -> int:
+        return self.t.data_ptr() + self.coff * self.t.element_size()
+
+    @property
+    def M(self) -> int:
+        return self.N * self.H * self.W
+
+    @property
+    def is_f32(self) -> bool:
+        return self.t.dtype == F32
+
+    def slice(self, c0: int, c: int) -> "Tensor4":
+        return Tensor4(self.t, self.N, self.H, self.W, c, self.ld, self.coff + c0)
+
+
+@dataclass
+class Stats:
+    """[sum | sumsq] statistics of a tensor: row length ``ld`` channels, ``count`` samples."""
+    t: torch.Tensor   # view into the stats arena, 2*ld floats
+    ld: int
+    count: int
+
+    @property
+    def ptr(self):
+        return self.t.data_ptr()
+
+
+class BNRef:
+    """A Keras BatchNormalization layer resolved for one program."""
+
+    def __init__(self, layer, builder: "Builder", stats: Optional[Stats], act: int):
+        self.layer = layer
+        self.training = builder.training and layer.trainable
+        self.mode = 1 if self.training else 2
+        self.stats = stats
+        self.act = act
+        self.C = layer.channels
+        self.b = builder
+        arena = builder.arena
+        self.gamma = layer.gamma
+        self.beta = layer.beta
+        self.trainable = builder.training and layer.trainable and layer.gamma.requires_grad
+        self.dgamma = arena.grad_of(layer.gamma) if self.trainable else None
+        self.dbeta = arena.grad_of(layer.beta) if self.trainable else None
+
+    def args(self) -> nat.BnArgs:
+        st = self.stats
+        return nat.bn_args(stats=st.t if (st is not None and self.mode == 1) else None,
+                           gamma=self.gamma, beta=self.beta,
+                           mmean=self.layer.moving_mean, mvar=self.layer.moving_variance,
+                           count=st.count if st is not None else 1, eps=self.layer.epsilon,
+                           mode=self.mode, act=self.act, C_=st.ld if st is not None else self.C)
+
+
+def act_only(act: int) -> nat.BnArgs:
+    return nat.bn_args(mode=0, act=act)
+
+
+IDENT = None
+
+
+class Builder:
+    def __init__(self, net, arena, device, batch: int, training: bool):
+        self.net = net
+        self.arena = arena
+        self.device = device
+        self.B = batch
+        self.training = training
+        self.ops: List[tuple] = []          # (segment, kind, payload bytes, ints, floats, longs, ptrs)
+        self.keep: List[torch.Tensor] = []  # keep allocations alive
+        self._stats_chunks: List[Tuple[int, int]] = []
+        self._stats_size = 0
+        self.stats_arena: Optional[torch.Tensor] = None
+        self.cast_all: List[nat.CastEntry] = []
+        self.cast_trainable: List[nat.CastEntry] = []
+        self.moving: List[nat.BnMovingDesc] = []
+        self.conv_weights: Dict[int, dict] = {}
+        self.segment = "fwd"
+        self.bwd_marks: List[Tuple[int, int]] = []  # (op index, lowest arena param index ready)
+        # stats arena is allocated lazily with a generous capacity; views are handed out in order
+        self._stats_cap = 1 << 20
+        self.stats_arena = torch.zeros(self._stats_cap, dtype=F32, device=device)
+
+    # ------------------------------------------------------------------ allocation
+    def alloc(self, shape, dtype=BF16) -> torch.Tensor:
+        t = torch.zeros(shape, dtype=dtype, device=self.device)
+        self.keep.append(t)
+        return t
+
+    def nhwc(self, N, H, W, C, dtype=BF16) -> Tensor4:
+        return Tensor4(self.alloc((N, H, W, C), dtype), N, H, W, C, C)
+
+    def stats(self, ld: int, count: int) -> Stats:
+        n = 2 * ((ld + 3) // 4 * 4)
+        if self._stats_size + n > self._stats_cap:
+            raise RuntimeError("stats arena capacity exceeded")
+        v = self.stats_arena[self._stats_size:self._stats_size + n]
+        self._stats_size += n
+        return Stats(v, ld, count)
+
+    # ------------------------------------------------------------------ op emission
+    def emit(self, kind, payload=None, ints=(), floats=(), longs=(), ptrs=()):
+        raw = nat.raw(payload) if payload is not None else b""
+        self.ops.append((self.segment, kind, raw, list(ints), list(floats), list(longs),
+                         [int(p) for p in ptrs]))
+
+    def mark_grads_ready(self, params):
+        """Backward has finished producing the grads of ``params`` (for DP bucket overlap)."""
+        idx = [i for i, p in enumerate(self.arena.params) if any(p is q for q in params)]
+        if idx:
+            self.bwd_marks.append((len(self.ops), min(idx)))
+
+    # ------------------------------------------------------------------ weights
+    def conv_weight(self, layer, cin_pad: Optional[int] = None, need_dgrad: bool = False):
+        """bf16 kernel-layout copies of a Conv2D kernel (cast from the fp32 Keras master)."""
+        key = id(layer)
+        ent = self.conv_weights.get(key)
+        kh, kw = layer.kernel_size
+        cin, cout = layer.in_ch, layer.filters
+        cpad = cin_pad or cin
+        if ent is None:
+            fwd = self.alloc((cout * kh * kw * cpad,), BF16)
+            ent = {"fwd": fwd, "dgrad": None, "cpad": cpad, "layer": layer}
+            self.conv_weights[key] = ent
+        if need_dgrad and ent["dgrad"] is None:
+            ent["dgrad"] = self.alloc((cin * kh * kw * cout,), BF16)
+        return ent
+
+    def finalize_casts(self):
+        trainable_ids = {id(p) for p in self.arena.params}
+        entries_all, entries_tr = [], []
+        for ent in self.conv_weights.values():
+            layer = ent["layer"]
+            kh, kw = layer.kernel_size
+            e = nat.CastEntry()
+            e.src = layer.kernel.data_ptr()
+            e.fwd = ent["fwd"].data_ptr()
+            e.dgrad = ent["dgrad"].data_ptr() if ent["dgrad"] is not None else 0
+            e.KH, e.KW, e.Cin, e.Cout, e.Cpad, e.dw = kh, kw, layer.in_ch, layer.filters, ent["cpad"], 0
+            entries_all.append(e)
+            if id(layer.kernel) in trainable_ids:
+                entries_tr.append(e)
+        self.cast_all_dev, self.cast_all_total, self.cast_all_n = self._upload_cast(entries_all)
+        self.cast_tr_dev, self.cast_tr_total, self.cast_tr_n = self._upload_cast(entries_tr)
+
+    def _upload_cast(self, entries):
+        total = 0
+        for e in entries:
+            e.begin = total
+            total += e.Cout * e.KH * e.KW * e.Cpad
+        if not entries:
+            return None, 0, 0
+        arr = (nat.CastEntry * len(entries))(*entries)
+        host = torch.frombuffer(bytearray(C.string_at(C.addressof(arr), C.sizeof(arr))),
+                                dtype=torch.uint8)
+        dev = host.to(self.device)
+        self.keep.append(dev)
+        return dev, total, len(entries)
+
+    def finalize_moving(self):
+        if not self.moving:
+            self.moving_dev = None
+            return
+        arr = (nat.BnMovingDesc * len(self.moving))(*self.moving)
+        host = torch.frombuffer(bytearray(C.string_at(C.addressof(arr), C.sizeof(arr))),
+                                dtype=torch.uint8)
+        self.moving_dev = host.to(self.device)
+        self.keep.append(self.moving_dev)
+        self.moving_maxc = max(d.C for d in self.moving)
+
+    def add_moving(self, bn: BNRef):
+        if bn.mode != 1:
+            return
+        st = bn.stats
+        d = nat.BnMovingDesc()
+        d.stats = st.ptr
+        d.C = bn.C
+        d.ld = st.ld
+        d.inv_count = 1.0 / st.count
+        d.unbias = st.count / max(st.count - 1, 1)
+        d.mmean = bn.layer.moving_mean.data_ptr()
+        d.mvar = bn.layer.moving_variance.data_ptr()
+        d.momentum = bn.layer.momentum
+        self.moving.append(d)
+
+    # ------------------------------------------------------------------ kernels
+    def conv(self, x: Tensor4, layer, y: Tensor4, *, stride=(1, 1), pads=(0, 0), pro=None,
+             bias=None, epi_act=0, out_mode=nat.OUT_BF16, stats: Optional[Stats] = None,
+             stats_off=0, w=None, cin_override=None, tile=-1):
+        """Forward conv (or, with ``w`` given, a generic conv such as a dgrad)."""
+        a = nat.ConvArgs()
+        a.x = x.ptr
+        a.N, a.H, a.W = x.N, x.H, x.W
+        a.Cin = cin_override or x.C
+        a.ldx = x.ld
+        a.Ho, a.Wo, a.Cout = y.H, y.W, y.C
+        a.y, a.ldy = y.ptr, y.ld
+        kh, kw = layer.kernel_size if layer is not None else w["k"]
+        a.KH, a.KW = kh, kw
+        a.SH, a.SW = stride
+        a.PT, a.PL = pads
+        if w is None:
+            ent = self.conv_weight(layer, cin_pad=a.Cin)
+            ent["layer"] = layer
+            a.w = ent["fwd"].data_ptr()
+        else:
+            a.w = w["ptr"]
+        a.pro = pro if pro is not None else act_only(0)
+        a.epi_mode = 0
+        a.bias = nat.ptr(bias)
+        a.epi_act = epi_act
+        a.out_mode = out_mode
+        if stats is not None:
+            a.stats_out, a.stats_ld, a.stats_off = stats.ptr, stats.ld, stats_off
+        a.mbn = act_only(0)
+        M = x.N * y.H * y.W
+        if tile < 0:
+            tile = nat.load().pick_tile(M, y.C)
+        self.emit(nat.OP_CONV, a, ints=(tile, 1 if x.is_f32 else 0))
+
+    def dgrad(self, dy: Tensor4, layer, dx: Tensor4, *, pads=(0, 0), mx: Optional[Tensor4] = None,
+              mbn: Optional[nat.BnArgs] = None, gsum=None, gsumx=None, out_mode=nat.OUT_BF16):
+        """Stride-1 data gradient: conv of dy with the flipped kernel; optional BN-backward
+        epilogue through the BN+act that produced the forward input ``mx``."""
+        kh, kw = layer.kernel_size
+        ent = self.conv_weight(layer, need_dgrad=True)
+        ent["layer"] = layer
+        a = nat.ConvArgs()
+        a.x = dy.ptr
+        a.N, a.H, a.W, a.Cin, a.ldx = dy.N, dy.H, dy.W, dy.C, dy.ld
+        a.Ho, a.Wo, a.Cout = dx.H, dx.W, dx.C
+        a.y, a.ldy = dx.ptr, dx.ld
+        a.w = ent["dgrad"].data_ptr()
+        a.KH, a.KW, a.SH, a.SW = kh, kw, 1, 1
+        a.PT, a.PL = kh - 1 - pads[0], kw - 1 - pads[1]
+        a.pro = act_only(0)
+        a.mbn = act_only(0)
+        if mx is not None:
+            a.epi_mode = 1
+            a.mx, a.ldmx = mx.ptr, mx.ld
+            a.mbn = mbn
+            a.gsum, a.gsumx = nat.ptr(gsum), nat.ptr(gsumx)
+        else:
+            a.epi_mode = 0
+            a.out_mode = out_mode
+        tile = nat.load().pick_tile(dx.M, dx.C)
+        self.emit(nat.OP_CONV, a, ints=(tile, 1 if dy.is_f32 else 0))
+
+    def wgrad(self, x: Tensor4, layer, g: Tensor4, dw: torch.Tensor, *, stride=(1, 1), pads=(0, 0),
+              pro=None, cin_real=0, splits=-1):
+        kh, kw = layer.kernel_size
+        a = nat.WgradArgs()
+        a.x = x.ptr
+        a.N, a.H, a.W, a.Cin, a.ldx = x.N, x.H, x.W, x.C, x.ld
+        a.g, a.ldg = g.ptr, g.ld
+        a.Ho, a.Wo, a.Cout = g.H, g.W, g.C
+        a.KH, a.KW = kh, kw
+        a.SH, a.SW = stride
+        a.PT, a.PL = pads
+        a.pro = pro if pro is not None else act_only(0)
+        a.dw = dw.data_ptr()
+        a.scale = 1.0
+        if not cin_real and x.C != layer.in_ch:
+            cin_real = layer.in_ch  # channel-padded staged input (first conv): Keras rows only
+        if dw.numel() != kh * kw * layer.in_ch * layer.filters:
+            raise RuntimeError(f"wgrad target of {layer.name} has {dw.numel()} elements")
+        a.cin_real = cin_real
+        if splits < 0:
+            splits = nat.load().pick_splits(g.M, kh * kw * x.C, g.C)
+        self.emit(nat.OP_WGRAD, a, ints=(splits, 1 if g.is_f32 else 0))
+
+    def bn_bwd_apply(self, dz: Tensor4, x: Tensor4, bn: BNRef, dst: Tensor4, accumulate: bool):
+        a = nat.BnBwdApplyArgs()
+        a.dz, a.lddz = dz.ptr, dz.ld
+        a.x, a.ldx = x.ptr, x.ld
+        a.bn = bn.args()
+        a.gsum, a.gsumx = nat.ptr(bn.dbeta), nat.ptr(bn.dgamma)
+        a.inv_n = 1.0 / float(x.M)
+        a.dst, a.lddst = dst.ptr, dst.ld
+        a.dst_f32 = 1 if dst.is_f32 else 0
+        a.accumulate = 1 if accumulate else 0
+        a.M, a.C = x.M, x.C
+        if bn.mode == 1 and (bn.dbeta is None):
+            raise RuntimeError("batch-mode BN backward needs gradient workspaces")
+        self.emit(nat.OP_BN_BWD_APPLY, a)
+
+    def bn_bwd_reduce(self, dy: Tensor4, x: Tensor4, bn: BNRef, dz: Tensor4):
+        a = nat.BnBwdReduceArgs()
+        a.dy, a.lddy, a.dy_f32 = dy.ptr, dy.ld, 1 if dy.is_f32 else 0
+        a.x, a.ldx = x.ptr, x.ld
+        a.bn = bn.args()
+        a.dz, a.lddz = dz.ptr, dz.ld
+        a.gsum, a.gsumx = nat.ptr(bn.dbeta), nat.ptr(bn.dgamma)
+        a.M, a.C = x.M, x.C
+        self.emit(nat.OP_BN_BWD_REDUCE, a)
+
+    def pool(self, x: Tensor4, y: Tensor4, *, k, s, pt=0, pl=0, pro=None, is_max=True,
+             argmax: Optional[torch.Tensor] = None, stats: Optional[Stats] = None, stats_off=0):
+        a = nat.PoolArgs()
+        a.x, a.ldx = x.ptr, x.ld
+        a.N, a.H, a.W, a.C = x.N, x.H, x.W, x.C
+        a.pro = pro if pro is not None else act_only(0)
+        a.k, a.s, a.pt, a.pl = k, s, pt, pl
+        a.Ho, a.Wo = y.H, y.W
+        a.y, a.ldy = y.ptr, y.ld
+        a.argmax = nat.ptr(argmax)
+        if stats is not None:
+            a.stats, a.stats_ld, a.stats_off = stats.ptr, stats.ld, stats_off
+        self.emit(nat.OP_MAXPOOL if is_max else nat.OP_AVGPOOL, a)
+
+    def pool_bwd(self, dy: Tensor4, dx: Tensor4, *, k, s, pt=0, pl=0, is_max=True, argmax=None,
+                 x: Optional[Tensor4] = None, bn: Optional[BNRef] = None, act=0):
+        a = nat.PoolBwdArgs()
+        a.dy, a.lddy, a.dy_f32 = dy.ptr, dy.ld, 1 if dy.is_f32 else 0
+        a.argmax = nat.ptr(argmax)
+        a.N, a.H, a.W, a.C = dx.N, dx.H, dx.W, dx.C
+        a.k, a.s, a.pt, a.pl = k, s, pt, pl
+        a.Ho, a.Wo = dy.H, dy.W
+        if x is not None:
+            a.x, a.ldx = x.ptr, x.ld
+            a.bn = bn.args() if bn is not None else act_only(act)
+            if bn is not None:
+                a.gsum, a.gsumx = nat.ptr(bn.dbeta), nat.ptr(bn.dgamma)
+        else:
+            a.bn = act_only(0)
+        a.dx, a.lddx = dx.ptr, dx.ld
+        a.is_avg = 0 if is_max else 1
+        self.emit(nat.OP_POOL_BWD, a)
+
+    def memset(self, t: torch.Tensor, nbytes: Optional[int] = None):
+        self.emit(nat.OP_MEMSET, longs=(nbytes if nbytes is not None else t.numel() * t.element_size(),),
+                  ptrs=(t.data_ptr(),))

@@ -1,0 +1,190 @@
+"""DenseNet-121/169/201 lowering (the north-star benchmark model).
+
+MI355X-specific structure:
+
+* **concat-free stage buffers** — each dense stage owns ONE NHWC buffer holding all of its
+  channels; every 3x3 conv writes its 32 new channels into its slice in place,
+  every 1x1 conv reads the ``[0:Cin)`` prefix with the buffer's pixel stride;
+* **statistics computed once per channel** — a channel's batch mean/var is identical for every
+  later ``_0_bn`` that normalises it (SURVEY §2.4.3 "exact shortcut"), so the producer's epilogue
+  reduces [sum|sumsq] ONCE into the stage's stats row and each consumer applies its own gamma/beta
+  in its operand prologue;
+* **transition = pool first** — ``BN->ReLU->conv1x1->avgpool`` is computed as
+  ``BN->ReLU->avgpool->conv1x1`` (a 1x1 conv commutes with 2x2 averaging): 4x fewer MFMA FLOPs;
+* **gradient of the concat buffer** — one fp32 gradient buffer per stage; the transition (or the
+  head) STORES it, every dense layer's BN1 backward ACCUMULATES into its channel prefix, so the
+  slice a layer reads is complete when backward reaches it and no zeroing pass is needed.
+"""
+from __future__ import annotations
+
+import torch
+
+from ..ops import _native as nat
+from .builder import BF16, F32, BNRef, Builder, Tensor4
+from .lower_common import RELU, FreezeInfo, HeadIO, emit_head, emit_head_bwd, emit_input
+
+
+def lower_densenet(b: Builder, net, U: int, input_dtype):
+    base, dense = net.base, net.head
+    B = b.B
+    training = b.training
+    fz = FreezeInfo(base, training)
+    L = {l.name: l for l in base.layers}
+    H, W, Cimg = base.input_shape
+    io = HeadIO(b, U)
+
+    # ---------------------------------------------------------------- forward
+    b.segment = "fwd"
+    if training:
+        b.memset(b.stats_arena)  # size patched at finalize
+    xin, x8 = emit_input(b, H, W, Cimg, input_dtype)
+    conv1, bn1l = L["conv1/conv"], L["conv1/bn"]
+    H1, W1 = (H + 6 - 7) // 2 + 1, (W + 6 - 7) // 2 + 1
+    ys = b.nhwc(B, H1, W1, 64)
+    ss = b.stats(64, B * H1 * W1) if training else None
+    b.conv(x8, conv1, ys, stride=(2, 2), pads=(3, 3), stats=ss)
+    bn_stem = BNRef(bn1l, b, ss, RELU)
+    b.add_moving(bn_stem)
+    Hs, Ws = (H1 + 2 - 3) // 2 + 1, (W1 + 2 - 3) // 2 + 1
+
+    stages = []
+    c0 = 64
+    nblocks = base.blocks
+    ctot = c0 + 32 * nblocks[0]
+    buf = b.nhwc(B, Hs, Ws, ctot)
+    sbuf = b.stats(ctot, B * Hs * Ws) if training else None
+    argmax = b.alloc((B * Hs * Ws * 64,), torch.uint8)
+    b.pool(ys, buf.slice(0, 64), k=3, s=2, pt=1, pl=1, pro=bn_stem.args(), is_max=True,
+           argmax=argmax, stats=sbuf, stats_off=0)
+
+    for si, nb in enumerate(nblocks):
+        st = {"buf": buf, "stats": sbuf, "c0": c0, "ctot": ctot, "H": Hs, "W": Ws, "layers": []}
+        M = B * Hs * Ws
+        for li in range(nb):
+            name = f"conv{si + 2}_block{li + 1}"
+            cin = c0 + 32 * li
+            bn1 = BNRef(L[name + "_0_bn"], b, sbuf, RELU)
+            cv1, bn2l, cv2 = L[name + "_1_conv"], L[name + "_1_bn"], L[name + "_2_conv"]
+            t = b.nhwc(B, Hs, Ws, 128)
+            stt = b.stats(128, M) if training else None
+            b.conv(buf.slice(0, cin), cv1, t, pro=bn1.args(), stats=stt)
+            bn2 = BNRef(bn2l, b, stt, RELU)
+            b.conv(t, cv2, buf.slice(cin, 32), pads=(1, 1), pro=bn2.args(), stats=sbuf, stats_off=cin)
+            b.add_moving(bn1)
+            b.add_moving(bn2)
+            st["layers"].append({"cin": cin, "bn1": bn1, "cv1": cv1, "bn2": bn2, "cv2": cv2, "t": t})
+        if si < len(nblocks) - 1:
+            bnt = BNRef(L[f"pool{si + 2}_bn"], b, sbuf, RELU)
+            cvt = L[f"pool{si + 2}_conv"]
+            Hn, Wn = Hs // 2, Ws // 2
+            p = b.nhwc(B, Hn, Wn, ctot)
+            b.pool(buf, p, k=2, s=2, pro=bnt.args(), is_max=False)
+            c0n = ctot // 2
+            ctotn = c0n + 32 * nblocks[si + 1]
+            bufn = b.nhwc(B, Hn, Wn, ctotn)
+            sbufn = b.stats(ctotn, B * Hn * Wn) if training else None
+            b.conv(p, cvt, bufn.slice(0, c0n), stats=sbufn, stats_off=0)
+            b.add_moving(bnt)
+            st["trans"] = {"bn": bnt, "conv": cvt, "p": p}
+            stages.append(st)
+            buf, sbuf, c0, ctot, Hs, Ws = bufn, sbufn, c0n, ctotn, Hn, Wn
+        else:
+            stages.append(st)
+
+    bnf = BNRef(L["bn"], b, sbuf, RELU)
+    b.add_moving(bnf)
+    emit_head(b, buf, bnf.args(), dense, U, io, training)
+    if training:
+        b.emit("MOVING")
+
+    b.xin, b.io = xin, io
+    b.debug = {"ys": ys, "ss": ss, "stages": stages, "x8": x8}
+    if not training:
+        return
+
+    # ---------------------------------------------------------------- backward
+    b.segment = "bwd"
+    b.memset(b.arena.grad)
+    last = stages[-1]
+    need_base = fz.at_or_before(L["bn"])
+    dA = emit_head_bwd(b, last["buf"], dense, U, io, need_dA=need_base)
+    if not need_base:
+        return
+    M4 = last["buf"].M
+    zf = b.nhwc(last["buf"].N, last["buf"].H, last["buf"].W, last["ctot"])
+    b.bn_bwd_reduce(dA, last["buf"], bnf, zf)
+    b.mark_grads_ready([bnf.gamma, bnf.beta])
+    if not fz.before(L["bn"]):
+        return
+    dbuf = b.nhwc(last["buf"].N, last["H"], last["W"], last["ctot"], F32)
+    b.bn_bwd_apply(zf, last["buf"], bnf, dbuf, accumulate=False)
+
+    for si in range(len(stages) - 1, -1, -1):
+        st = stages[si]
+        buf = st["buf"]
+        N, Hs, Ws, ctot = buf.N, st["H"], st["W"], st["ctot"]
+        z1 = b.nhwc(N, Hs, Ws, ctot)
+        z2 = b.nhwc(N, Hs, Ws, 128)
+        dt = b.nhwc(N, Hs, Ws, 128)
+        stop = False
+        for lay in reversed(st["layers"]):
+            cin, bn1, cv1, bn2, cv2, t = lay["cin"], lay["bn1"], lay["cv1"], lay["bn2"], lay["cv2"], lay["t"]
+            dO = dbuf.slice(cin, 32)
+            if fz.trainable(cv2):
+                b.wgrad(t, cv2, dO, b.arena.grad_of(cv2.kernel), pads=(1, 1), pro=bn2.args())
+            if not fz.before(cv2):
+                stop = True
+                break
+            b.dgrad(dO, cv2, z2, pads=(1, 1), mx=t, mbn=bn2.args(), gsum=bn2.dbeta, gsumx=bn2.dgamma)
+            if not fz.before(bn2.layer):
+                stop = True
+                break
+            b.bn_bwd_apply(z2, t, bn2, dt, accumulate=False)
+            if fz.trainable(cv1):
+                b.wgrad(buf.slice(0, cin), cv1, dt, b.arena.grad_of(cv1.kernel), pro=bn1.args())
+            if not fz.before(cv1):
+                stop = True
+                break
+            z1v = Tensor4(z1.t, N, Hs, Ws, cin, cin)
+            b.dgrad(dt, cv1, z1v, mx=buf.slice(0, cin), mbn=bn1.args(), gsum=bn1.dbeta, gsumx=bn1.dgamma)
+            b.mark_grads_ready([cv2.kernel, cv1.kernel, bn2.gamma, bn2.beta, bn1.gamma, bn1.beta])
+            if not fz.before(bn1.layer):
+                stop = True
+                break
+            b.bn_bwd_apply(z1v, buf.slice(0, cin), bn1, dbuf.slice(0, cin), accumulate=True)
+        if stop:
+            return
+        if si == 0:
+            break
+        # transition of the previous stage (writes this stage's channels [0:c0))
+        prev = stages[si - 1]
+        tr = prev["trans"]
+        bnt, cvt, p = tr["bn"], tr["conv"], tr["p"]
+        dO = dbuf.slice(0, st["c0"])
+        if fz.trainable(cvt):
+            b.wgrad(p, cvt, dO, b.arena.grad_of(cvt.kernel))
+        if not fz.before(cvt):
+            return
+        dp = b.nhwc(p.N, p.H, p.W, p.C)
+        b.dgrad(dO, cvt, dp)
+        pbuf = prev["buf"]
+        zt = b.nhwc(pbuf.N, prev["H"], prev["W"], prev["ctot"])
+        b.pool_bwd(dp, zt, k=2, s=2, is_max=False, x=pbuf, bn=bnt)
+        b.mark_grads_ready([cvt.kernel, bnt.gamma, bnt.beta])
+        if not fz.before(bnt.layer):
+            return
+        dbuf = b.nhwc(pbuf.N, prev["H"], prev["W"], prev["ctot"], F32)
+        b.bn_bwd_apply(zt, pbuf, bnt, dbuf, accumulate=False)
+
+    # stem: maxpool backward through BN+ReLU of conv1, then conv1 wgrad
+    if not fz.at_or_before(bn1l):
+        return
+    zs = b.nhwc(B, H1, W1, 64)
+    b.pool_bwd(dbuf.slice(0, 64), zs, k=3, s=2, pt=1, pl=1, is_max=True, argmax=argmax, x=ys,
+               bn=bn_stem)
+    if fz.trainable(conv1):
+        dys = b.nhwc(B, H1, W1, 64)
+        b.bn_bwd_apply(zs, ys, bn_stem, dys, accumulate=False)
+        b.wgrad(x8, conv1, dys, b.arena.grad_of(conv1.kernel), stride=(2, 2), pads=(3, 3),
+                cin_real=Cimg)
+    b.mark_grads_ready([conv1.kernel, bn_stem.gamma, bn_stem.beta])

@@ -1,0 +1,260 @@
+"""A lowered, executable training/eval program and the ``fused`` Model backend.
+
+``FusedProgram`` = one static plan for (model, batch, training, input dtype):
+  segment ``fwd``  input staging -> convs/pools (fused BN/act) -> head loss -> BN moving update
+  segment ``bwd``  grad-arena memset -> head bwd -> dgrad/wgrad/BN-bwd in reverse order
+  segment ``opt``  fused RMSprop over the flat arena -> bf16 weight re-cast (ONE launch each)
+Each segment is captured into a HIP graph on first use and replayed afterwards.  Under data
+parallelism the backward segment is split at bucket boundaries so each bucket's RCCL all-reduce
+is launched while the remaining backward segments run.
+"""
+from __future__ import annotations
+
+import os
+from typing import Dict, List, Optional, Tuple
+
+import torch
+
+from ..engine.losses import BinaryCrossentropy, CategoricalCrossentropy, SparseCategoricalCrossentropy
+from ..engine.optimizers import RMSprop
+from ..ops import _native as nat
+from .builder import Builder
+
+
+def _lowering_for(net):
+    from ..models import Sequential
+    from ..models.densenet import DenseNet
+    from ..models.mobilenet_v2 import MobileNetV2
+    from ..models.vgg import VGG16
+
+    if not isinstance(net, Sequential):
+        return None
+    base = net.base
+    if isinstance(base, DenseNet):
+        from .lower_densenet import lower_densenet
+        return lower_densenet
+    if isinstance(base, VGG16):
+        from .lower_vgg import lower_vgg
+        return lower_vgg
+    if isinstance(base, MobileNetV2):
+        from .lower_mobilenet import lower_mobilenet
+        return lower_mobilenet
+    return None
+
+
+def fused_supported(net, loss) -> bool:
+    if _lowering_for(net) is None:
+        return False
+    if not isinstance(loss, (BinaryCrossentropy, CategoricalCrossentropy, SparseCategoricalCrossentropy)):
+        return False
+    if not getattr(loss, "from_logits", True):
+        return False
+    if net.num_outputs > 16:
+        return False
+    return nat.available()
+
+
+class FusedProgram:
+    def __init__(self, model, batch: int, training: bool, input_dtype, grad_scale: float = 1.0,
+                 use_graphs: bool = True):
+        nat.require()
+        self.model = model
+        self.training = training
+        self.batch = batch
+        net = model.net
+        self.U = net.num_outputs
+        b = Builder(net, model.arena, model.device, batch, training)
+        _lowering_for(net)(b, net, self.U, input_dtype)
+        self.b = b
+        self.xin = b.xin
+        self.io = b.io
+        b.finalize_casts()
+        b.finalize_moving()
+        # optimizer segment
+        if training and model.arena.params:
+            b.segment = "opt"
+            opt = model.optimizer
+            if not isinstance(opt, RMSprop) or opt.momentum or opt.centered:
+                self.host_optimizer = True
+            else:
+                self.host_optimizer = False
+                ms = opt.ms
+                b.emit(nat.OP_RMSPROP, floats=(opt.learning_rate, opt.rho, opt.epsilon, grad_scale),
+                       longs=(model.arena.numel,),
+                       ptrs=(model.arena.data.data_ptr(), model.arena.grad.data_ptr(), ms.data_ptr()))
+            if b.cast_tr_n:
+                b.emit(nat.OP_CAST, ints=(b.cast_tr_n,), longs=(b.cast_tr_total,),
+                       ptrs=(b.cast_tr_dev.data_ptr(),))
+        else:
+            self.host_optimizer = False
+        self.plan = nat.load().Plan()
+        self.seg: Dict[str, Tuple[int, int]] = {}
+        self.rms_index = None
+        cur, start = None, 0
+        op_index = 0
+        self.bwd_marks = []
+        mark_at = {}
+        for pos, lo in b.bwd_marks:
+            mark_at.setdefault(pos, []).append(lo)
+        for i, (seg, kind, raw, ints, floats, longs, ptrs) in enumerate(b.ops):
+            if seg != cur:
+                if cur is not None:
+                    self.seg[cur] = (start, op_index)
+                cur, start = seg, op_index
+            if i in mark_at:
+                self.bwd_marks.append((op_index, min(mark_at[i])))
+            if kind == "MOVING":
+                if b.moving_dev is None:
+                    continue
+                kind, ints, ptrs = nat.OP_BN_MOVING, [len(b.moving), b.moving_maxc], [b.moving_dev.data_ptr()]
+            if kind == nat.OP_MEMSET and ptrs[0] == b.stats_arena.data_ptr():
+                longs = [max(b._stats_size, 4) * 4]
+            if kind == nat.OP_RMSPROP:
+                self.rms_index = op_index
+            self.plan.add(kind, raw, ints, floats, longs, ptrs)
+            op_index += 1
+        if cur is not None:
+            self.seg[cur] = (start, op_index)
+        self.use_graphs = use_graphs and os.environ.get("IDC_NO_GRAPHS", "0") != "1"
+        self.graphs: Dict[Tuple[int, int], int] = {}
+        self.grad_scale = grad_scale
+        self.stream = torch.cuda.Stream(device=model.device)
+        # initial bf16 weight casts (all convs, frozen ones included)
+        if b.cast_all_n:
+            cast = nat.load().Plan()
+            cast.add(nat.OP_CAST, b"", [b.cast_all_n], [], [b.cast_all_total], [b.cast_all_dev.data_ptr()])
+            self._cast_all_plan = cast
+        else:
+            self._cast_all_plan = None
+        self.recast_all()
+
+    # ------------------------------------------------------------------ execution
+    def _sh(self):
+        return self.stream.cuda_stream
+
+    def recast_all(self):
+        if self._cast_all_plan is not None:
+            with torch.cuda.stream(self.stream):
+                self._cast_all_plan.run(0, -1, self._sh())
+
+    def run_range(self, lo: int, hi: int):
+        if hi <= lo:
+            return
+        if self.use_graphs:
+            g = self.graphs.get((lo, hi))
+            if g is None:
+                g = self.plan.capture(lo, hi, self._sh())
+                self.graphs[(lo, hi)] = g
+            self.plan.launch(g, self._sh())
+        else:
+            self.plan.run(lo, hi, self._sh())
+
+    def run_segment(self, name: str):
+        if name in self.seg:
+            self.run_range(*self.seg[name])
+
+    def set_lr(self, lr: float):
+        if self.rms_index is not None:
+            self.plan.set_float(self.rms_index, 0, float(lr))
+            self.plan.clear_graphs()
+            self.graphs = {}
+
+    def close(self):
+        self.plan.clear_graphs()
+
+
+def _labels_to(io_labels: torch.Tensor, y: torch.Tensor, U: int):
+    y = y.to(io_labels.device, non_blocking=True)
+    if U == 1:
+        io_labels.copy_(y.reshape(-1).float())
+    elif y.dim() == 2 and y.shape[1] == U:
+        io_labels.copy_(y.float())
+    else:
+        io_labels.zero_()
+        io_labels.scatter_(1, y.reshape(-1, 1).long(), 1.0)
+
+
+class FusedStep:
+    """``engine.Model`` backend that runs the lowered MI355X program."""
+
+    name = "fused"
+
+    def __init__(self, model, use_graphs: bool = True):
+        self.m = model
+        self.use_graphs = use_graphs
+        self.progs: Dict[tuple, FusedProgram] = {}
+        self._lr = model.optimizer.learning_rate if model.optimizer else None
+
+    def _prog(self, batch: int, training: bool, dtype) -> FusedProgram:
+        key = (batch, training, dtype)
+        p = self.progs.get(key)
+        if p is None:
+            gs = 1.0 / self.m.strategy.num_replicas_in_sync
+            p = FusedProgram(self.m, batch, training, dtype, grad_scale=gs, use_graphs=self.use_graphs)
+            self.progs[key] = p
+        return p
+
+    def _stage_inputs(self, p: FusedProgram, x, y):
+        cur = torch.cuda.current_stream(self.m.device)
+        p.stream.wait_stream(cur)
+        with torch.cuda.stream(p.stream):
+            p.xin.copy_(x.to(p.xin.device, non_blocking=True).to(p.xin.dtype))
+            if y is not None:
+                _labels_to(p.io.labels, y, p.U)
+
+    def train_step(self, x, y):
+        m = self.m
+        dtype = torch.uint8 if x.dtype == torch.uint8 else torch.float32
+        p = self._prog(x.shape[0], True, dtype)
+        self._stage_inputs(p, x, y)
+        p.run_segment("fwd")
+        strategy = m.strategy
+        if "bwd" in p.seg:
+            lo, hi = p.seg["bwd"]
+            bucketer = strategy.bucketer(m.arena) if strategy.num_replicas_in_sync > 1 else None
+            if bucketer is not None and p.bwd_marks:
+                # backward in bucket-aligned segments: launch each bucket's all-reduce as soon
+                # as its gradients are final, while the remaining backward keeps the GPU busy
+                pos = lo
+                for mark, low_param in p.bwd_marks:
+                    if mark <= pos:
+                        continue
+                    p.run_range(pos, mark)
+                    pos = mark
+                    with torch.cuda.stream(p.stream):
+                        bucketer.launch_range(low_param, None)
+                p.run_range(pos, hi)
+                with torch.cuda.stream(p.stream):
+                    bucketer.finish()
+            else:
+                p.run_range(lo, hi)
+                if bucketer is not None:
+                    with torch.cuda.stream(p.stream):
+                        bucketer.finish()
+        if p.host_optimizer:
+            with torch.cuda.stream(p.stream):
+                m.optimizer.step(m.arena, grad_scale=1.0 / strategy.num_replicas_in_sync)
+        p.run_segment("opt")
+        torch.cuda.current_stream(m.device).wait_stream(p.stream)
+        return p.io.loss.reshape(()).clone(), p.io.logits.clone()
+
+    def eval_step(self, x, y):
+        dtype = torch.uint8 if x.dtype == torch.uint8 else torch.float32
+        p = self._prog(x.shape[0], False, dtype)
+        self._stage_inputs(p, x, y)
+        p.run_segment("fwd")
+        torch.cuda.current_stream(self.m.device).wait_stream(p.stream)
+        return p.io.loss.reshape(()).clone(), p.io.logits.clone()
+
+    def sync_from_module(self):
+        # weights were overwritten on the module side (set_weights / load_weights): re-cast
+        for p in self.progs.values():
+            p.recast_all()
+
+    def sync_to_module(self):
+        torch.cuda.synchronize(self.m.device)
+
+    def close(self):
+        for p in self.progs.values():
+            p.close()
+        self.progs = {}

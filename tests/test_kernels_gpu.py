@@ -1,0 +1,320 @@
+"""Numerics of every HIP kernel vs a plain PyTorch fp32 reference of the same op.
+
+Shapes are the shape classes of SURVEY §2.4: 1x1 with K-tails (Cin = 64+32k), 3x3 s1 'same'
+with N=32 outputs, the 7x7 s2 stem on a channel-padded image, 3x3 s2 with Keras' asymmetric
+correct_pad, M tails, fp32 gradient operands, pending-BN prologues and BN-backward epilogues.
+bf16 tolerances: inputs are rounded to bf16 before the reference so only accumulation differs.
+"""
+import pytest
+import torch
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+
+DEV = "cuda"
+
+
+def bf(x):
+    return x.to(torch.bfloat16).float()
+
+
+def relerr(a, b):
+    a, b = a.float(), b.float()
+    return ((a - b).norm() / (b.norm() + 1e-12)).item()
+
+
+def ref_conv(x_nhwc, w_hwio, stride, pads_tblr, bias=None, act=0):
+    x = x_nhwc.permute(0, 3, 1, 2)
+    t, bo, l, r = pads_tblr
+    x = F.pad(x, (l, r, t, bo))
+    y = F.conv2d(x, w_hwio.permute(3, 2, 0, 1), bias, stride=stride)
+    if act == 1:
+        y = F.relu(y)
+    return y.permute(0, 2, 3, 1)
+
+
+def bn_ref(x, stats, gamma, beta, count, eps, act):
+    C = x.shape[-1]
+    mean = stats[:C] / count
+    var = (stats[C:] / count - mean * mean).clamp_min(0)
+    z = (x - mean) * torch.rsqrt(var + eps) * gamma + beta
+    if act == 1:
+        z = F.relu(z)
+    elif act == 2:
+        z = z.clamp(0, 6)
+    return z
+
+
+@pytest.fixture(scope="module")
+def fn():
+    from idc_models_amd.ops import functional as fn
+    fn.nat.require()
+    return fn
+
+
+@pytest.mark.parametrize("N,H,Cin,Cout,k,s,pads,outhw", [
+    (2, 13, 96, 128, 1, 1, (0, 0, 0, 0), None),     # DenseNet 1x1, K tail (96 = 64+32)
+    (2, 13, 128, 32, 3, 1, (1, 1, 1, 1), None),     # DenseNet 3x3 growth conv
+    (3, 7, 224, 128, 1, 1, (0, 0, 0, 0), None),     # M tail
+    (2, 50, 8, 64, 7, 2, (3, 3, 3, 3), None),       # stem 7x7 s2 on padded image
+    (2, 50, 8, 32, 3, 2, (0, 1, 0, 1), (25, 25)),   # MobileNetV2 Conv1 correct_pad
+    (2, 25, 64, 128, 3, 1, (1, 1, 1, 1), None),     # VGG block2_conv1
+    (1, 3, 512, 512, 3, 1, (1, 1, 1, 1), None),     # VGG block5 tiny M
+])
+def test_conv_fwd(fn, N, H, Cin, Cout, k, s, pads, outhw):
+    x = bf(torch.randn(N, H, H, Cin, device=DEV))
+    w = bf(torch.randn(k, k, Cin, Cout, device=DEV) * (2.0 / (k * k * Cin)) ** 0.5)
+    bias = torch.randn(Cout, device=DEV) * 0.1
+    ho = outhw or ((H + pads[0] + pads[1] - k) // s + 1,) * 2
+    y = fn.conv2d(x.to(torch.bfloat16), w, stride=(s, s), pads=(pads[0], pads[2]), out_hw=ho,
+                  bias=bias, act=1, out_f32=True)
+    ref = ref_conv(x, w, s, pads, bias, act=1)
+    assert y.shape == ref.shape
+    assert relerr(y, ref) < 1e-2
+
+
+def test_conv_fwd_asymmetric_B(fn):
+    """A = identity-like input, asymmetric B: catches a transposed C write (guide §3)."""
+    N, H, C = 1, 4, 16
+    x = torch.zeros(N, H, H, C, device=DEV)
+    for i in range(16):
+        x[0, i // 4, i % 4, i] = 1.0
+    w = torch.arange(C * 32, device=DEV, dtype=torch.float32).reshape(1, 1, C, 32) / 64.0
+    y = fn.conv2d(x.to(torch.bfloat16), w, out_f32=True)
+    ref = ref_conv(x, bf(w), 1, (0, 0, 0, 0))
+    assert torch.allclose(y, ref, atol=1e-2)
+
+
+def test_conv_prologue_bn_relu_and_stats(fn):
+    N, H, Cin, Cout = 4, 13, 160, 128
+    x = bf(torch.randn(N, H, H, Cin, device=DEV) * 2 + 0.5)
+    st = torch.cat([x.sum((0, 1, 2)), (x * x).sum((0, 1, 2))])
+    gamma = torch.rand(Cin, device=DEV) + 0.5
+    beta = torch.randn(Cin, device=DEV) * 0.1
+    w = bf(torch.randn(1, 1, Cin, Cout, device=DEV) * 0.1)
+    stats_out = torch.zeros(2 * Cout, device=DEV)
+    cnt = N * H * H
+    y = fn.conv2d(x.to(torch.bfloat16), w, pro=fn.BN(stats=st, gamma=gamma, beta=beta, count=cnt,
+                  eps=1.001e-5, act=1), stats=stats_out)
+    a = bn_ref(x, st, gamma, beta, cnt, 1.001e-5, 1)
+    ref = ref_conv(bf(a), w, 1, (0, 0, 0, 0))
+    assert relerr(y, ref) < 1e-2
+    yf = y.float()
+    assert relerr(stats_out[:Cout], yf.sum((0, 1, 2))) < 1e-3
+    assert relerr(stats_out[Cout:], (yf * yf).sum((0, 1, 2))) < 1e-3
+
+
+def test_conv_fp32_operand(fn):
+    N, H, Cin, Cout = 2, 13, 32, 128
+    x = torch.randn(N, H, H, Cin, device=DEV)
+    w = bf(torch.randn(3, 3, Cin, Cout, device=DEV) * 0.1)
+    y = fn.conv2d(x, w, pads=(1, 1), out_f32=True)
+    ref = ref_conv(bf(x), w, 1, (1, 1, 1, 1))
+    assert relerr(y, ref) < 1e-2
+
+
+@pytest.mark.parametrize("N,H,Cin,Cout,k", [(2, 13, 128, 32, 3), (2, 13, 96, 128, 1), (3, 6, 64, 64, 3)])
+def test_conv_dgrad(fn, N, H, Cin, Cout, k):
+    p = k // 2
+    dy = bf(torch.randn(N, H, H, Cout, device=DEV))
+    w = bf(torch.randn(k, k, Cin, Cout, device=DEV) * 0.1)
+    dx = fn.conv2d_dgrad(dy.to(torch.bfloat16), w, (H, H), pads=(p, p), out_f32=True)
+    ref = torch.nn.grad.conv2d_input((N, Cin, H, H), w.permute(3, 2, 0, 1), dy.permute(0, 3, 1, 2),
+                                     padding=p).permute(0, 2, 3, 1)
+    assert relerr(dx, ref) < 1e-2
+
+
+def test_conv_dgrad_bn_epilogue(fn):
+    N, H, Cin, Cout = 4, 6, 128, 32
+    mx = bf(torch.randn(N, H, H, Cin, device=DEV))
+    st = torch.cat([mx.sum((0, 1, 2)), (mx * mx).sum((0, 1, 2))])
+    gamma = torch.rand(Cin, device=DEV) + 0.5
+    beta = torch.randn(Cin, device=DEV) * 0.1
+    cnt = N * H * H
+    dy = bf(torch.randn(N, H, H, Cout, device=DEV))
+    w = bf(torch.randn(3, 3, Cin, Cout, device=DEV) * 0.1)
+    gsum = torch.zeros(Cin, device=DEV)
+    gsumx = torch.zeros(Cin, device=DEV)
+    dz = fn.conv2d_dgrad(dy.to(torch.bfloat16), w, (H, H), pads=(1, 1), mx=mx.to(torch.bfloat16),
+                         mbn=fn.BN(stats=st, gamma=gamma, beta=beta, count=cnt, eps=1e-3, act=1),
+                         gsum=gsum, gsumx=gsumx)
+    dA = torch.nn.grad.conv2d_input((N, Cin, H, H), w.permute(3, 2, 0, 1), dy.permute(0, 3, 1, 2),
+                                    padding=1).permute(0, 2, 3, 1)
+    mean = st[:Cin] / cnt
+    var = st[Cin:] / cnt - mean ** 2
+    xhat = (mx - mean) * torch.rsqrt(var + 1e-3)
+    z = xhat * gamma + beta
+    dZ = dA * (z > 0).float()
+    assert relerr(dz, dZ) < 1e-2
+    assert relerr(gsum, dZ.sum((0, 1, 2))) < 2e-2
+    assert relerr(gsumx, (dZ * xhat).sum((0, 1, 2))) < 2e-2
+
+
+@pytest.mark.parametrize("N,H,Cin,Cout,k,s,pads,gf32", [
+    (4, 13, 128, 32, 3, 1, (1, 1), True),     # DenseNet 3x3 (fp32 concat grads)
+    (4, 13, 96, 128, 1, 1, (0, 0), False),    # DenseNet 1x1
+    (2, 25, 64, 128, 3, 1, (1, 1), False),    # VGG
+    (2, 50, 8, 64, 7, 2, (3, 3), False),      # stem (padded channels)
+])
+def test_conv_wgrad(fn, N, H, Cin, Cout, k, s, pads, gf32):
+    x = bf(torch.randn(N, H, H, Cin, device=DEV))
+    Ho = (H + 2 * pads[0] - k) // s + 1
+    dy = torch.randn(N, Ho, Ho, Cout, device=DEV)
+    dyb = dy if gf32 else dy.to(torch.bfloat16)
+    dw = fn.conv2d_wgrad(x.to(torch.bfloat16), dyb, (k, k), stride=(s, s), pads=pads)
+    ref = torch.nn.grad.conv2d_weight(x.permute(0, 3, 1, 2), (Cout, Cin, k, k), bf(dy).permute(0, 3, 1, 2),
+                                      stride=s, padding=pads[0]).permute(2, 3, 1, 0)
+    assert relerr(dw, ref) < 1e-2
+
+
+def test_conv_wgrad_prologue_and_cin_real(fn):
+    N, H, Cin, Cout = 2, 50, 8, 64
+    x = torch.zeros(N, H, H, Cin, device=DEV)
+    x[..., :3] = torch.rand(N, H, H, 3, device=DEV)
+    x = bf(x)
+    dy = bf(torch.randn(N, 25, 25, Cout, device=DEV))
+    dw = fn.conv2d_wgrad(x.to(torch.bfloat16), dy.to(torch.bfloat16), (7, 7), stride=(2, 2), pads=(3, 3),
+                         cin_real=3)
+    ref = torch.nn.grad.conv2d_weight(x[..., :3].permute(0, 3, 1, 2), (Cout, 3, 7, 7), dy.permute(0, 3, 1, 2),
+                                      stride=2, padding=3).permute(2, 3, 1, 0)
+    assert dw.shape == (7, 7, 3, 64)
+    assert relerr(dw, ref) < 1e-2
+
+
+def test_wgrad_with_bn_prologue(fn):
+    N, H, Cin, Cout = 4, 13, 128, 32
+    t = bf(torch.randn(N, H, H, Cin, device=DEV))
+    st = torch.cat([t.sum((0, 1, 2)), (t * t).sum((0, 1, 2))])
+    g, b = torch.rand(Cin, device=DEV) + 0.5, torch.randn(Cin, device=DEV) * 0.1
+    dy = bf(torch.randn(N, H, H, Cout, device=DEV))
+    cnt = N * H * H
+    dw = fn.conv2d_wgrad(t.to(torch.bfloat16), dy.to(torch.bfloat16), (3, 3), pads=(1, 1),
+                         pro=fn.BN(stats=st, gamma=g, beta=b, count=cnt, eps=1e-3, act=1))
+    a = bf(bn_ref(t, st, g, b, cnt, 1e-3, 1))
+    ref = torch.nn.grad.conv2d_weight(a.permute(0, 3, 1, 2), (Cout, Cin, 3, 3), dy.permute(0, 3, 1, 2),
+                                      padding=1).permute(2, 3, 1, 0)
+    assert relerr(dw, ref) < 1.5e-2
+
+
+def test_maxpool_fwd_bwd_stem(fn):
+    N, H, C = 2, 25, 64
+    y = bf(torch.randn(N, H, H, C, device=DEV))
+    st = torch.cat([y.sum((0, 1, 2)), (y * y).sum((0, 1, 2))])
+    g, b = torch.rand(C, device=DEV) + 0.5, torch.randn(C, device=DEV) * 0.1
+    cnt = N * H * H
+    bn = fn.BN(stats=st, gamma=g, beta=b, count=cnt, eps=1.001e-5, act=1)
+    out_stats = torch.zeros(2 * C, device=DEV)
+    p, am = fn.pool2d(y.to(torch.bfloat16), 3, 2, pads=(1, 1), is_max=True, pro=bn, stats=out_stats)
+    a = bn_ref(y, st, g, b, cnt, 1.001e-5, 1).requires_grad_(True)
+    ap = F.pad(a.permute(0, 3, 1, 2), (1, 1, 1, 1))
+    ref = F.max_pool2d(ap, 3, 2).permute(0, 2, 3, 1)
+    assert relerr(p, ref) < 1e-2
+    assert relerr(out_stats[:C], p.float().sum((0, 1, 2))) < 1e-3
+    dp = torch.randn_like(ref)
+    ref.backward(dp)
+    gsum = torch.zeros(C, device=DEV)
+    gsumx = torch.zeros(C, device=DEV)
+    dz = fn.pool2d_bwd(dp.contiguous(), (N, H, H, C), 3, 2, pads=(1, 1), is_max=True, argmax=am,
+                       x=y.to(torch.bfloat16), bn=bn, gsum=gsum, gsumx=gsumx)
+    # reference dZ (grad wrt BN pre-activation)
+    z = bn_ref(y, st, g, b, cnt, 1.001e-5, 0)
+    dZ = a.grad * (z > 0).float()
+    assert relerr(dz, dZ) < 2e-2
+
+
+def test_avgpool_fwd_bwd(fn):
+    N, H, C = 2, 13, 256
+    x = bf(torch.randn(N, H, H, C, device=DEV))
+    p, _ = fn.pool2d(x.to(torch.bfloat16), 2, 2, is_max=False)
+    ref = F.avg_pool2d(x.permute(0, 3, 1, 2), 2, 2).permute(0, 2, 3, 1)
+    assert p.shape == ref.shape == (N, 6, 6, C)
+    assert relerr(p, ref) < 1e-2
+    dp = torch.randn(N, 6, 6, C, device=DEV)
+    dx = fn.pool2d_bwd(dp.to(torch.bfloat16), (N, H, H, C), 2, 2, is_max=False)
+    xr = x.clone().requires_grad_(True)
+    F.avg_pool2d(xr.permute(0, 3, 1, 2), 2, 2).permute(0, 2, 3, 1).backward(bf(dp))
+    assert relerr(dx, xr.grad) < 1e-2
+
+
+def test_bn_backward_pair_matches_autograd(fn):
+    N, H, C = 4, 6, 64
+    x = bf(torch.randn(N, H, H, C, device=DEV) * 3 + 1)
+    st = torch.cat([x.sum((0, 1, 2)), (x * x).sum((0, 1, 2))])
+    g, b = torch.rand(C, device=DEV) + 0.5, torch.randn(C, device=DEV) * 0.1
+    cnt = N * H * H
+    xr = x.clone().requires_grad_(True)
+    mean = xr.mean((0, 1, 2))
+    var = xr.var((0, 1, 2), unbiased=False)
+    gr, br = g.clone().requires_grad_(True), b.clone().requires_grad_(True)
+    y = F.relu((xr - mean) * torch.rsqrt(var + 1e-3) * gr + br)
+    dy = torch.randn_like(y)
+    y.backward(dy)
+    bn = fn.BN(stats=st, gamma=g, beta=b, count=cnt, eps=1e-3, act=1)
+    gsum = torch.zeros(C, device=DEV)
+    gsumx = torch.zeros(C, device=DEV)
+    dz = fn.bn_bwd_reduce(dy, x.to(torch.bfloat16), bn, gsum, gsumx)
+    dx = fn.bn_bwd_apply(dz, x.to(torch.bfloat16), bn, gsum, gsumx, out_f32=True)
+    assert relerr(gsum, br.grad) < 2e-2
+    assert relerr(gsumx, gr.grad) < 2e-2
+    assert relerr(dx, xr.grad) < 3e-2
+
+
+def test_bn_stats(fn):
+    x = bf(torch.randn(3, 7, 7, 96, device=DEV))
+    st = fn.bn_stats(x.to(torch.bfloat16))
+    assert relerr(st[:96], x.sum((0, 1, 2))) < 1e-4
+    assert relerr(st[96:], (x * x).sum((0, 1, 2))) < 1e-4
+
+
+@pytest.mark.parametrize("s,H,pads,ho", [(1, 13, (1, 1), 13), (2, 26, (0, 0), 13), (2, 13, (1, 1), 7)])
+def test_dwconv(fn, s, H, pads, ho):
+    N, C = 2, 96
+    x = bf(torch.randn(N, H, H, C, device=DEV))
+    k = torch.randn(3, 3, C, 1, device=DEV) * 0.3
+    y = fn.dwconv(x.to(torch.bfloat16), k, stride=s, pads=pads, out_hw=(ho, ho))
+    # Keras: stride-2 uses explicit correct_pad (top/left pads[0], bottom/right enough for ho)
+    xr = x.clone().requires_grad_(True)
+    xp = F.pad(xr.permute(0, 3, 1, 2), (pads[1], 2, pads[0], 2))
+    kr = k.clone().requires_grad_(True)
+    ref = F.conv2d(xp, kr.permute(2, 3, 0, 1), stride=s, groups=C)[:, :, :ho, :ho].permute(0, 2, 3, 1)
+    assert relerr(y, ref) < 1e-2
+    dy = bf(torch.randn_like(ref))
+    ref.backward(dy)
+    dx, dw = fn.dwconv_bwd(x.to(torch.bfloat16), k, dy.to(torch.bfloat16), stride=s, pads=pads)
+    assert relerr(dx, xr.grad) < 1e-2
+    assert relerr(dw, kr.grad) < 1e-2
+
+
+def test_rmsprop_kernel_matches_keras_formula():
+    from idc_models_amd.ops.optim import rmsprop_
+    n = 4096
+    w = torch.randn(n, device=DEV)
+    g = torch.randn(n, device=DEV)
+    ms = torch.rand(n, device=DEV)
+    w0, ms0 = w.clone(), ms.clone()
+    rmsprop_(w, g, ms, 1e-3, 0.9, 1e-7, 0.5)
+    gs = g * 0.5
+    ms_ref = 0.9 * ms0 + 0.1 * gs * gs
+    w_ref = w0 - 1e-3 * gs / (ms_ref.sqrt() + 1e-7)
+    assert torch.allclose(ms, ms_ref, rtol=1e-5, atol=1e-7)
+    assert torch.allclose(w, w_ref, rtol=1e-5, atol=1e-6)
+
+
+def test_secagg_masks_cancel_exactly():
+    from idc_models_amd.fed.secagg import mask_quantize, unmask_mean
+    K, n = 5, 10007
+    xs = [torch.randn(n, device=DEV) for _ in range(K)]
+    scale = 2.0 ** 16
+    masked = [mask_quantize(x, scale, K, r, seed=1234, round_=7) for r, x in enumerate(xs)]
+    total = torch.zeros(n, dtype=torch.int64, device=DEV)
+    for m in masked:
+        total = (total + m.to(torch.int64)) % (1 << 32)
+    s32 = total.to(torch.int64)
+    s32 = torch.where(s32 >= (1 << 31), s32 - (1 << 32), s32).to(torch.int32)
+    plain = sum(torch.round(x * scale).to(torch.int64) for x in xs)
+    assert torch.equal(s32.to(torch.int64), plain)
+    mean = unmask_mean(s32, scale, K, K)
+    assert torch.allclose(mean, sum(xs) / K, atol=K / scale)
+    # CPU numpy Philox produces the same bits as the GPU kernel
+    cpu = mask_quantize(xs[1].cpu(), scale, K, 1, seed=1234, round_=7)
+    assert torch.equal(cpu, masked[1].cpu())

@@ -1,0 +1,91 @@
+"""Build the native MI355X extension ``idc_models_amd/_idc_native*.so`` with hipcc (gfx950 only).
+
+No torch.utils.cpp_extension / hipify: the kernels are plain HIP C++ written for CDNA4, the
+bindings are pybind11, and the module has no libtorch dependency (tensors cross the boundary as
+device pointers + the HIP stream handle), so it builds in seconds and loads in any process.
+
+    python tools/build_native.py            # incremental
+    python tools/build_native.py --clean
+"""
+from __future__ import annotations
+
+import argparse
+import concurrent.futures as cf
+import os
+import shutil
+import subprocess
+import sys
+import sysconfig
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+CSRC = os.path.join(ROOT, "csrc")
+BUILD = os.path.join(ROOT, "build", "native")
+PKG = os.path.join(ROOT, "idc_models_amd")
+ARCH = os.environ.get("IDC_OFFLOAD_ARCH", "gfx950")
+HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
+
+SOURCES = [
+    "kernels/conv_igemm.hip",
+    "kernels/conv_wgrad.hip",
+    "kernels/nn_kernels.hip",
+    "kernels/dwconv.hip",
+    "kernels/secagg.hip",
+    "runtime/plan.cpp",
+]
+
+
+def ext_path() -> str:
+    return os.path.join(PKG, "_idc_native" + sysconfig.get_config_var("EXT_SUFFIX"))
+
+
+def _headers():
+    hs = []
+    for d, _, fs in os.walk(CSRC):
+        hs += [os.path.join(d, f) for f in fs if f.endswith(".h")]
+    return hs
+
+
+def _compile(src: str, extra) -> str:
+    import pybind11
+
+    s = os.path.join(CSRC, src)
+    o = os.path.join(BUILD, src.replace("/", "_") + ".o")
+    newest_dep = max([os.path.getmtime(s)] + [os.path.getmtime(h) for h in _headers()])
+    if os.path.exists(o) and os.path.getmtime(o) >= newest_dep and not extra.get("force"):
+        return o
+    cmd = [HIPCC, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-c", s, "-o", o,
+           f"-I{pybind11.get_include()}", f"-I{sysconfig.get_paths()['include']}",
+           "-Wno-unused-result", "-Wno-unused-variable"]
+    if src.endswith(".cpp"):
+        cmd += ["-x", "hip"]
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    if r.returncode != 0:
+        raise RuntimeError(f"hipcc failed for {src}:\n{r.stderr[-6000:]}")
+    return o
+
+
+def build(clean: bool = False, jobs: int = 8, verbose: bool = True) -> str:
+    if clean and os.path.isdir(BUILD):
+        shutil.rmtree(BUILD)
+    os.makedirs(BUILD, exist_ok=True)
+    with cf.ThreadPoolExecutor(max_workers=jobs) as ex:
+        objs = list(ex.map(lambda s: _compile(s, {}), SOURCES))
+    out = ext_path()
+    if not os.path.exists(out) or os.path.getmtime(out) < max(os.path.getmtime(o) for o in objs):
+        tmp = out + ".tmp"
+        cmd = [HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", tmp] + objs
+        r = subprocess.run(cmd, capture_output=True, text=True)
+        if r.returncode != 0:
+            raise RuntimeError(f"link failed:\n{r.stderr[-4000:]}")
+        os.replace(tmp, out)
+    if verbose:
+        print(f"[build_native] {out}")
+    return out
+
+
+if __name__ == "__main__":
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--clean", action="store_true")
+    ap.add_argument("-j", type=int, default=min(8, os.cpu_count() or 4))
+    a = ap.parse_args()
+    build(a.clean, a.j)
