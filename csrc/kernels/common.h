@@ -51,17 +51,33 @@ __device__ __forceinline__ uint4 pack8(const float* f) {
 
 enum Act : int { ACT_NONE = 0, ACT_RELU = 1, ACT_RELU6 = 2 };
 
+// Activations are evaluated branch-free as a clamp to [lo, hi] (ReLU: [0,inf), ReLU6: [0,6],
+// linear: (-inf,inf)); with `act` a kernel argument the bounds are loop-invariant selects, so the
+// hot loops carry no per-element branches (a switch here compiled to per-element s_cbranch).
+__device__ __forceinline__ float act_lo(int act) { return act ? 0.f : -INFINITY; }
+__device__ __forceinline__ float act_hi(int act) { return act == ACT_RELU6 ? 6.f : INFINITY; }
+
 __device__ __forceinline__ float apply_act(float v, int act) {
-  if (act == ACT_RELU) return fmaxf(v, 0.f);
-  if (act == ACT_RELU6) return fminf(fmaxf(v, 0.f), 6.f);
-  return v;
+  return fminf(fmaxf(v, act_lo(act)), act_hi(act));
 }
 
-// derivative mask of the activation evaluated at pre-activation value z
+// derivative mask of the activation evaluated at pre-activation value z (TF: relu' = z > 0,
+// relu6' = 0 < z < 6)
 __device__ __forceinline__ float act_mask(float z, int act) {
-  if (act == ACT_RELU) return z > 0.f ? 1.f : 0.f;
-  if (act == ACT_RELU6) return (z > 0.f && z < 6.f) ? 1.f : 0.f;
-  return 1.f;
+  return (z > act_lo(act) && z < act_hi(act)) ? 1.f : 0.f;
+}
+
+// y[j] = act(x[j]*sc[j] + sh[j]) for 8 channels; sc/sh 32-B aligned LDS tables
+__device__ __forceinline__ void affine_act8(float* v, const float* sc, const float* sh, float lo,
+                                            float hi) {
+  const float4 s0 = *reinterpret_cast<const float4*>(sc);
+  const float4 s1 = *reinterpret_cast<const float4*>(sc + 4);
+  const float4 h0 = *reinterpret_cast<const float4*>(sh);
+  const float4 h1 = *reinterpret_cast<const float4*>(sh + 4);
+  const float s[8] = {s0.x, s0.y, s0.z, s0.w, s1.x, s1.y, s1.z, s1.w};
+  const float h[8] = {h0.x, h0.y, h0.z, h0.w, h1.x, h1.y, h1.z, h1.w};
+#pragma unroll
+  for (int j = 0; j < 8; ++j) v[j] = fminf(fmaxf(fmaf(v[j], s[j], h[j]), lo), hi);
 }
 
 __device__ __forceinline__ float wave_sum(float v) {

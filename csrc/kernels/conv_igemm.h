@@ -38,5 +38,8 @@ struct ConvArgs {
 
 hipError_t conv_igemm(const ConvArgs& a, int tile, bool a_f32, hipStream_t st);
 int conv_pick_tile(int M, int Cout);
+int conv_num_tiles();
+int conv_tile_bm(int t);
+int conv_tile_bn(int t);
 
 }  // namespace idc

@@ -144,13 +144,28 @@ __global__ __launch_bounds__(256) void conv_igemm_kernel(ConvArgs a) {
 
   const TA* __restrict__ X = reinterpret_cast<const TA*>(a.x);
   const bf16_t* __restrict__ Wt = a.w;
+  const float pro_lo = act_lo(a.pro.act), pro_hi = act_hi(a.pro.act);
+  const float epi_lo = act_lo(a.epi_act), epi_hi = act_hi(a.epi_act);
+  const float msk_lo = act_lo(a.mbn.act), msk_hi = act_hi(a.mbn.act);
 
-  uint4 ra[NA];
-  bool rvalid[NA];
-  float rpre[sizeof(TA) == 4 ? NA : 1][8];
-  uint4 rb[NB];
+  // two staging register sets: tile t+2 is loaded while tile t is computed and tile t+1 (already
+  // in registers) waits to be written to LDS, so each global load has two compute phases to land
+  struct Stage {
+    uint4 ra[NA];
+    bool rvalid[NA];
+    float rpre[sizeof(TA) == 4 ? NA : 1][8];
+    uint4 rb[NB];
+    bool bvalid[NB];
+    int kc;
+  };
+  Stage st0, st1;
 
-  auto load_tile = [&]() {
+  auto load_tile = [&](Stage& S) {
+    uint4* ra = S.ra;
+    bool* rvalid = S.rvalid;
+    auto& rpre = S.rpre;
+    uint4* rb = S.rb;
+    S.kc = kc;
 #pragma unroll
     for (int i = 0; i < NA; ++i) {
       bool ok = a_ok[i] && (kglob < K);
@@ -162,16 +177,17 @@ __global__ __launch_bounds__(256) void conv_igemm_kernel(ConvArgs a) {
         ok = ok && (unsigned)h < (unsigned)a.H && (unsigned)w < (unsigned)a.W;
         off = ((size_t)(a_img[i] * a.H + h) * a.W + w) * a.ldx + kc;
       }
+      // unconditional loads from a clamped address: a guarded "ok ? load : 0" makes hipcc branch
+      // around each load and drain vmcnt(0), which destroys the two-deep prefetch
       rvalid[i] = ok;
+      off = ok ? off : 0;
       if constexpr (sizeof(TA) == 2) {
-        ra[i] = ok ? *reinterpret_cast<const uint4*>(X + off) : make_uint4(0, 0, 0, 0);
+        ra[i] = *reinterpret_cast<const uint4*>(X + off);
       } else {
-        if (ok) {
-          float4 u = *reinterpret_cast<const float4*>(X + off);
-          float4 v = *reinterpret_cast<const float4*>(X + off + 4);
-          rpre[i][0] = u.x; rpre[i][1] = u.y; rpre[i][2] = u.z; rpre[i][3] = u.w;
-          rpre[i][4] = v.x; rpre[i][5] = v.y; rpre[i][6] = v.z; rpre[i][7] = v.w;
-        }
+        float4 u = *reinterpret_cast<const float4*>(X + off);
+        float4 v = *reinterpret_cast<const float4*>(X + off + 4);
+        rpre[i][0] = u.x; rpre[i][1] = u.y; rpre[i][2] = u.z; rpre[i][3] = u.w;
+        rpre[i][4] = v.x; rpre[i][5] = v.y; rpre[i][6] = v.z; rpre[i][7] = v.w;
       }
     }
     const int k0 = kglob - my_chunk * 8;
@@ -182,13 +198,19 @@ __global__ __launch_bounds__(256) void conv_igemm_kernel(ConvArgs a) {
       int n = n0 + row;
       int k = k0 + ch * 8;
       bool ok = (idx < BN * CPR) && (n < a.Cout) && (k < K);
-      rb[i] = ok ? *reinterpret_cast<const uint4*>(Wt + (size_t)n * K + k) : make_uint4(0, 0, 0, 0);
+      S.bvalid[i] = ok;
+      rb[i] = *reinterpret_cast<const uint4*>(Wt + (ok ? (size_t)n * K + k : 0));
     }
   };
 
-  auto store_tile = [&](int buf) {
+  auto store_tile = [&](Stage& S, int buf) {
     bf16_t* as = As + buf * A_ELEMS;
     bf16_t* bs = Bs + buf * B_ELEMS;
+    const uint4* ra = S.ra;
+    const bool* rvalid = S.rvalid;
+    const auto& rpre = S.rpre;
+    const uint4* rb = S.rb;
+    const int kc = S.kc;
 #pragma unroll
     for (int i = 0; i < NA; ++i) {
       int idx = tid + i * NT;
@@ -200,9 +222,7 @@ __global__ __launch_bounds__(256) void conv_igemm_kernel(ConvArgs a) {
           if constexpr (PRO) {
             float f[8];
             unpack8(ra[i], f);
-#pragma unroll
-            for (int j = 0; j < 8; ++j)
-              f[j] = apply_act(f[j] * s_scale[kc + j] + s_shift[kc + j], a.pro.act);
+            affine_act8(f, s_scale + kc, s_shift + kc, pro_lo, pro_hi);
             v = pack8(f);
           } else {
             v = ra[i];
@@ -210,10 +230,8 @@ __global__ __launch_bounds__(256) void conv_igemm_kernel(ConvArgs a) {
         } else {
           float f[8];
 #pragma unroll
-          for (int j = 0; j < 8; ++j) {
-            f[j] = rpre[i][j];
-            if constexpr (PRO) f[j] = apply_act(f[j] * s_scale[kc + j] + s_shift[kc + j], a.pro.act);
-          }
+          for (int j = 0; j < 8; ++j) f[j] = rpre[i][j];
+          if constexpr (PRO) affine_act8(f, s_scale + kc, s_shift + kc, pro_lo, pro_hi);
           v = pack8(f);
         }
       }
@@ -224,7 +242,8 @@ __global__ __launch_bounds__(256) void conv_igemm_kernel(ConvArgs a) {
       int idx = tid + i * NT;
       if (idx >= BN * CPR) break;
       int row = idx / CPR, ch = idx % CPR;
-      *reinterpret_cast<uint4*>(bs + row * BK + swz_chunk<BK>(row, ch) * 8) = rb[i];
+      *reinterpret_cast<uint4*>(bs + row * BK + swz_chunk<BK>(row, ch) * 8) =
+          S.bvalid[i] ? rb[i] : make_uint4(0, 0, 0, 0);
     }
   };
 
@@ -244,22 +263,18 @@ __global__ __launch_bounds__(256) void conv_igemm_kernel(ConvArgs a) {
 
   const int nk = (K + BK - 1) / BK;
   __syncthreads();  // prologue tables visible
-  load_tile();
-  store_tile(0);
+  load_tile(st0);
+  advance_k();
+  load_tile(st1);
+  store_tile(st0, 0);
   __syncthreads();
 
   const int frow = lane & 15;
   const int fk = lane >> 4;
 
-  for (int kt = 0; kt < nk; ++kt) {
-    const int cur = kt & 1;
-    const bool more = (kt + 1) < nk;
-    if (more) {
-      advance_k();
-      load_tile();
-    }
-    const bf16_t* as = As + cur * A_ELEMS;
-    const bf16_t* bs = Bs + cur * B_ELEMS;
+  auto compute = [&](int buf) {
+    const bf16_t* as = As + buf * A_ELEMS;
+    const bf16_t* bs = Bs + buf * B_ELEMS;
 #pragma unroll
     for (int q = 0; q < BK / 32; ++q) {
       v8bf af[TM], bfr[TN];
@@ -279,8 +294,31 @@ __global__ __launch_bounds__(256) void conv_igemm_kernel(ConvArgs a) {
         for (int j = 0; j < TN; ++j)
           acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
     }
-    if (more) store_tile(cur ^ 1);
+  };
+
+  // iteration kt: LDS[kt&1] holds tile kt, registers hold tile kt+1 (set (kt+1)&1);
+  // tile kt+2 is issued into the set that was written to LDS last iteration.
+  // Loads/stores are unconditional: tiles past the end are clamped + zero-filled (their LDS
+  // writes land in a buffer that is never read again).  Conditional load/store pairs made the
+  // waitcnt pass drain vmcnt(0) at the loop back-edge, serialising the prefetch.
+  int kt = 0;
+  for (; kt + 2 <= nk; kt += 2) {
+    // even step: compute LDS0 (tile kt), st1 holds kt+1, reload st0 with kt+2
+    advance_k();
+    load_tile(st0);
+    compute(0);
+    store_tile(st1, 1);
     __syncthreads();
+    // odd step: compute LDS1 (tile kt+1), st0 holds kt+2, reload st1 with kt+3
+    advance_k();
+    load_tile(st1);
+    compute(1);
+    store_tile(st0, 0);
+    __syncthreads();
+  }
+  if (kt < nk) {
+    compute(0);  // odd tile count: the last tile sits in LDS0
+    __syncthreads();  // the epilogue's fp32 staging tile aliases LDS0
   }
 
   // ---- epilogue: WM passes, each stages one wave-row (WTM x BN) of fp32 results in LDS ------
@@ -318,7 +356,7 @@ __global__ __launch_bounds__(256) void conv_igemm_kernel(ConvArgs a) {
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
           float t = v[j] + (a.bias ? a.bias[n + j] : 0.f);
-          v[j] = apply_act(t, a.epi_act);
+          v[j] = fminf(fmaxf(t, epi_lo), epi_hi);
         }
         if (a.out_mode == OUT_BF16) {
           uint4 p = pack8(v);
@@ -352,7 +390,7 @@ __global__ __launch_bounds__(256) void conv_igemm_kernel(ConvArgs a) {
         for (int j = 0; j < 8; ++j) {
           int cj = c8 * 8 + j;
           float z = xf[j] * s_e0[cj] + s_e1[cj];
-          d[j] = v[j] * act_mask(z, a.mbn.act);
+          d[j] = (z > msk_lo && z < msk_hi) ? v[j] : 0.f;
         }
         uint4 p = pack8(d);
         *reinterpret_cast<uint4*>(reinterpret_cast<bf16_t*>(a.y) + (size_t)m * a.ldy + n) = p;
@@ -406,41 +444,59 @@ static hipError_t launch_cfg(const ConvArgs& a, bool is1x1, bool a_f32, int pro,
 #define IDC_E(IS1, TA, P)      \
   if (epi == 0) IDC_L(IS1, TA, P, 0); \
   else IDC_L(IS1, TA, P, 1);
-#define IDC_P(IS1, TA)   \
-  if (pro) { IDC_E(IS1, TA, 1) } \
-  else { IDC_E(IS1, TA, 0) }
+  // fp32 operands (gradient buffers) never carry a pending-BN prologue
   if (a_f32) {
-    if (is1x1) { IDC_P(true, float) } else { IDC_P(false, float) }
+    if (pro) return hipErrorInvalidValue;
+    if (is1x1) { IDC_E(true, float, 0) } else { IDC_E(false, float, 0) }
+  } else if (pro) {
+    if (is1x1) { IDC_E(true, bf16_t, 1) } else { IDC_E(false, bf16_t, 1) }
   } else {
-    if (is1x1) { IDC_P(true, bf16_t) } else { IDC_P(false, bf16_t) }
+    if (is1x1) { IDC_E(true, bf16_t, 0) } else { IDC_E(false, bf16_t, 0) }
   }
-#undef IDC_P
 #undef IDC_E
 #undef IDC_L
   return hipGetLastError();
 }
 
+struct TileInfo { int bm, bn; };
+static const TileInfo kTiles[] = {
+    {128, 128}, {128, 64}, {256, 32}, {64, 64}, {64, 32},   // BK 32
+    {128, 128}, {128, 64}, {128, 32}, {64, 64}, {64, 32},   // BK 64
+    {256, 32}, {64, 128}};                                 // BK 64
+
+int conv_num_tiles() { return (int)(sizeof(kTiles) / sizeof(kTiles[0])); }
+int conv_tile_bm(int t) { return kTiles[t].bm; }
+int conv_tile_bn(int t) { return kTiles[t].bn; }
+
 hipError_t conv_igemm(const ConvArgs& a, int tile, bool a_f32, hipStream_t st) {
   const bool is1x1 = a.KH == 1 && a.KW == 1 && a.SH == 1 && a.SW == 1 && a.PT == 0 && a.PL == 0;
   const int pro = (a.pro.mode != 0 || a.pro.act != ACT_NONE) ? 1 : 0;
   const int epi = a.epi_mode;
+  if ((a.Cin % 8) || (a.Cout % 8) || (a.ldx % 8) || (a.ldy % 8)) return hipErrorInvalidValue;
   switch (tile) {
-    case TILE_128x128: return launch_cfg<128, 128, 32, 2, 2>(a, is1x1, a_f32, pro, epi, st);
-    case TILE_128x64: return launch_cfg<128, 64, 32, 2, 2>(a, is1x1, a_f32, pro, epi, st);
-    case TILE_256x32: return launch_cfg<256, 32, 32, 4, 1>(a, is1x1, a_f32, pro, epi, st);
-    case TILE_64x64: return launch_cfg<64, 64, 32, 2, 2>(a, is1x1, a_f32, pro, epi, st);
-    case TILE_64x32: return launch_cfg<64, 32, 32, 2, 2>(a, is1x1, a_f32, pro, epi, st);
+    case 0: return launch_cfg<128, 128, 32, 2, 2>(a, is1x1, a_f32, pro, epi, st);
+    case 1: return launch_cfg<128, 64, 32, 2, 2>(a, is1x1, a_f32, pro, epi, st);
+    case 2: return launch_cfg<256, 32, 32, 4, 1>(a, is1x1, a_f32, pro, epi, st);
+    case 3: return launch_cfg<64, 64, 32, 2, 2>(a, is1x1, a_f32, pro, epi, st);
+    case 4: return launch_cfg<64, 32, 32, 2, 2>(a, is1x1, a_f32, pro, epi, st);
+    case 5: return launch_cfg<128, 128, 64, 2, 2>(a, is1x1, a_f32, pro, epi, st);
+    case 6: return launch_cfg<128, 64, 64, 2, 2>(a, is1x1, a_f32, pro, epi, st);
+    case 7: return launch_cfg<128, 32, 64, 4, 1>(a, is1x1, a_f32, pro, epi, st);
+    case 8: return launch_cfg<64, 64, 64, 2, 2>(a, is1x1, a_f32, pro, epi, st);
+    case 9: return launch_cfg<64, 32, 64, 2, 2>(a, is1x1, a_f32, pro, epi, st);
+    case 10: return launch_cfg<256, 32, 64, 4, 1>(a, is1x1, a_f32, pro, epi, st);
+    case 11: return launch_cfg<64, 128, 64, 2, 2>(a, is1x1, a_f32, pro, epi, st);
     default: return hipErrorInvalidValue;
   }
 }
 
 int conv_pick_tile(int M, int Cout) {
   auto blocks = [&](int bm, int bn) { return ((M + bm - 1) / bm) * ((Cout + bn - 1) / bn); };
-  if (Cout <= 32) return blocks(256, 32) >= 256 ? TILE_256x32 : TILE_64x32;
-  if (Cout <= 64) return blocks(128, 64) >= 256 ? TILE_128x64 : TILE_64x64;
-  if (blocks(128, 128) >= 256) return TILE_128x128;
-  if (blocks(128, 64) >= 256) return TILE_128x64;
-  return TILE_64x64;
+  if (Cout <= 32) return blocks(128, 32) >= 256 ? 7 : 9;
+  if (Cout <= 64) return blocks(128, 64) >= 256 ? 6 : 8;
+  if (blocks(128, 128) >= 256) return 5;
+  if (blocks(64, 128) >= 256) return 11;
+  return 8;
 }
 
 }  // namespace idc

@@ -140,6 +140,7 @@ __global__ __launch_bounds__(256) void conv_wgrad_kernel(WgradArgs a) {
   uint4 ra[NA];
   bool rv[NA];
   uint4 rg[NG];
+  bool gv[NG];
   float rgf[sizeof(TG) == 4 ? NG : 1][8];
 
   auto load = [&](int mbase) {
@@ -157,7 +158,7 @@ __global__ __launch_bounds__(256) void conv_wgrad_kernel(WgradArgs a) {
         off = ((size_t)(p_img[i] * a.H + h) * a.W + w) * a.ldx + kc;
       }
       rv[i] = ok;
-      ra[i] = ok ? *reinterpret_cast<const uint4*>(X + off) : make_uint4(0, 0, 0, 0);
+      ra[i] = *reinterpret_cast<const uint4*>(X + (ok ? off : 0));  // unconditional (no drain)
     }
 #pragma unroll
     for (int i = 0; i < NG; ++i) {
@@ -166,18 +167,15 @@ __global__ __launch_bounds__(256) void conv_wgrad_kernel(WgradArgs a) {
       int m = mbase + row;
       int co = c0 + ch * 8;
       bool ok = (idx < BP * GCH) && (m < pend) && (co < a.Cout);
+      const size_t goff = ok ? (size_t)m * a.ldg + co : 0;
+      gv[i] = ok;
       if constexpr (sizeof(TG) == 2) {
-        rg[i] = ok ? *reinterpret_cast<const uint4*>(G + (size_t)m * a.ldg + co) : make_uint4(0, 0, 0, 0);
+        rg[i] = *reinterpret_cast<const uint4*>(G + goff);
       } else {
-        if (ok) {
-          float4 u = *reinterpret_cast<const float4*>(G + (size_t)m * a.ldg + co);
-          float4 v = *reinterpret_cast<const float4*>(G + (size_t)m * a.ldg + co + 4);
-          rgf[i][0] = u.x; rgf[i][1] = u.y; rgf[i][2] = u.z; rgf[i][3] = u.w;
-          rgf[i][4] = v.x; rgf[i][5] = v.y; rgf[i][6] = v.z; rgf[i][7] = v.w;
-        } else {
-#pragma unroll
-          for (int j = 0; j < 8; ++j) rgf[i][j] = 0.f;
-        }
+        float4 u = *reinterpret_cast<const float4*>(G + goff);
+        float4 v = *reinterpret_cast<const float4*>(G + goff + 4);
+        rgf[i][0] = u.x; rgf[i][1] = u.y; rgf[i][2] = u.z; rgf[i][3] = u.w;
+        rgf[i][4] = v.x; rgf[i][5] = v.y; rgf[i][6] = v.z; rgf[i][7] = v.w;
       }
     }
   };
@@ -194,8 +192,7 @@ __global__ __launch_bounds__(256) void conv_wgrad_kernel(WgradArgs a) {
         if constexpr (PRO) {
           float f[8];
           unpack8(ra[i], f);
-#pragma unroll
-          for (int j = 0; j < 8; ++j) f[j] = apply_act(f[j] * s_scale[kc + j] + s_shift[kc + j], a.pro.act);
+          affine_act8(f, s_scale + kc, s_shift + kc, act_lo(a.pro.act), act_hi(a.pro.act));
           v = pack8(f);
         } else {
           v = ra[i];
@@ -211,6 +208,7 @@ __global__ __launch_bounds__(256) void conv_wgrad_kernel(WgradArgs a) {
       uint4 v;
       if constexpr (sizeof(TG) == 2) v = rg[i];
       else v = pack8(rgf[i]);
+      if (!gv[i]) v = make_uint4(0, 0, 0, 0);
       *reinterpret_cast<uint4*>(gs + row * BC + wswz<GROWB>(row, ch) * 8) = v;
     }
   };
@@ -228,11 +226,9 @@ __global__ __launch_bounds__(256) void conv_wgrad_kernel(WgradArgs a) {
   __syncthreads();
   for (int it = 0; it < nsteps; ++it) {
     const int cur = it & 1;
-    const bool more = it + 1 < nsteps;
-    if (more) {
-      if constexpr (!IS1X1) step_pixels();
-      load(pbeg + (it + 1) * BP);
-    }
+    // unconditional prefetch (rows past `pend` are masked): no back-edge vmcnt(0) drain
+    if constexpr (!IS1X1) step_pixels();
+    load(pbeg + (it + 1) * BP);
     const bf16_t* as = As + cur * C::A_ELEMS;
     const bf16_t* gs = Gs + cur * C::G_ELEMS;
     v8bf af[TM], gf[TN];
@@ -245,7 +241,7 @@ __global__ __launch_bounds__(256) void conv_wgrad_kernel(WgradArgs a) {
 #pragma unroll
       for (int j = 0; j < TN; ++j)
         acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], gf[j], acc[i][j], 0, 0, 0);
-    if (more) store(cur ^ 1);
+    store(cur ^ 1);
     __syncthreads();
   }
 

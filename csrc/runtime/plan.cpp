@@ -99,6 +99,13 @@ class Plan {
   }
 
   void set_float(int idx, int slot, float v) { ops_.at(idx).f[slot] = v; }
+  void set_int(int idx, int slot, int v) { ops_.at(idx).i[slot] = v; }
+  int get_int(int idx, int slot) const { return ops_.at(idx).i[slot]; }
+  int kind(int idx) const { return ops_.at(idx).kind; }
+  py::bytes payload(int idx) const {
+    const auto& b = ops_.at(idx).blob;
+    return py::bytes(reinterpret_cast<const char*>(b.data()), b.size());
+  }
 
   int size() const { return (int)ops_.size(); }
 
@@ -284,6 +291,10 @@ PYBIND11_MODULE(_idc_native, m) {
       .def(py::init<>())
       .def("add", &Plan::add)
       .def("set_float", &Plan::set_float)
+      .def("set_int", &Plan::set_int)
+      .def("get_int", &Plan::get_int)
+      .def("kind", &Plan::kind)
+      .def("payload", &Plan::payload)
       .def("size", &Plan::size)
       .def("run", &Plan::run)
       .def("capture", &Plan::capture)
@@ -295,6 +306,9 @@ PYBIND11_MODULE(_idc_native, m) {
   m.def("struct_sizes", &struct_sizes);
   m.def("pick_tile", &py_pick_tile);
   m.def("pick_splits", &py_pick_splits);
+  m.def("num_tiles", &conv_num_tiles);
+  m.def("tile_bm", &conv_tile_bm);
+  m.def("tile_bn", &conv_tile_bn);
   m.def("rmsprop", &py_rmsprop);
   m.def("secagg_mask", &py_secagg_mask);
   m.def("secagg_unmask", &py_secagg_unmask);

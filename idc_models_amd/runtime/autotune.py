@@ -1,0 +1,121 @@
+"""Plan-build-time autotuning of conv tile shapes and wgrad split factors.
+
+The conv GEMMs of these CNNs are skinny and irregular (N = 32..512, K = 27..4608, M = 256..640k;
+SURVEY §2.4), so no single tile wins: each conv / wgrad op of a freshly built plan is timed on
+its real shape with every applicable tile (or split factor) and the fastest is written back into
+the op before the plan is captured into a HIP graph.  Results are cached per shape signature for
+the process (and optionally persisted as JSON via IDC_TUNE_CACHE).
+
+Side effects of the trial launches only touch buffers that every step re-initialises (the
+statistics arena and the gradient arena are memset at the start of their segments; activations
+are overwritten), so tuning is safe before the first real step.
+"""
+from __future__ import annotations
+
+import json
+import os
+from typing import Dict, Tuple
+
+import torch
+
+from ..ops import _native as nat
+
+_CACHE: Dict[Tuple, int] = {}
+_LOADED = False
+
+
+def _load_cache():
+    global _LOADED
+    if _LOADED:
+        return
+    _LOADED = True
+    p = os.environ.get("IDC_TUNE_CACHE")
+    if p and os.path.exists(p):
+        with open(p) as f:
+            for k, v in json.load(f).items():
+                _CACHE[tuple(json.loads(k))] = v
+
+
+def _save_cache():
+    p = os.environ.get("IDC_TUNE_CACHE")
+    if p:
+        with open(p, "w") as f:
+            json.dump({json.dumps(list(k)): v for k, v in _CACHE.items()}, f)
+
+
+def _time_op(plan, i, stream, reps=4) -> float:
+    sh = stream.cuda_stream
+    plan.run(i, i + 1, sh)  # warm-up
+    e0 = torch.cuda.Event(enable_timing=True)
+    e1 = torch.cuda.Event(enable_timing=True)
+    with torch.cuda.stream(stream):
+        e0.record()
+        for _ in range(reps):
+            plan.run(i, i + 1, sh)
+        e1.record()
+    e1.synchronize()
+    return e0.elapsed_time(e1) / reps
+
+
+def _conv_candidates(ext, M: int, cout: int):
+    ntile = ext.num_tiles()
+    cap = 32 if cout <= 32 else (64 if cout <= 64 else 128)
+    out = []
+    for t in range(ntile):
+        bm, bn = ext.tile_bm(t), ext.tile_bn(t)
+        if bn > cap:
+            continue
+        if bm > 64 and M <= 2 * 64:
+            continue
+        out.append(t)
+    return out
+
+
+def autotune_plan(plan, stream, verbose: bool = False) -> int:
+    """Tune every conv / wgrad op of ``plan`` in place.  Returns the number of ops tuned."""
+    _load_cache()
+    ext = nat.load()
+    n = 0
+    for i in range(plan.size()):
+        kind = plan.kind(i)
+        if kind == nat.OP_CONV:
+            a = nat.ConvArgs.from_buffer_copy(plan.payload(i))
+            f32 = plan.get_int(i, 1)
+            M = a.N * a.Ho * a.Wo
+            pro = int(a.pro.mode != 0 or a.pro.act != 0)
+            key = ("conv", M, a.Cout, a.Cin, a.KH, a.KW, a.SH, a.PT, a.ldx, f32, pro, a.epi_mode)
+            best = _CACHE.get(key)
+            if best is None:
+                times = {}
+                for t in _conv_candidates(ext, M, a.Cout) or [ext.pick_tile(M, a.Cout)]:
+                    plan.set_int(i, 0, t)
+                    times[t] = _time_op(plan, i, stream)
+                best = min(times, key=times.get)
+                _CACHE[key] = best
+                if verbose:
+                    print("tune conv", key, {k: round(v * 1e3, 1) for k, v in times.items()}, "->", best)
+            plan.set_int(i, 0, best)
+            n += 1
+        elif kind == nat.OP_WGRAD:
+            a = nat.WgradArgs.from_buffer_copy(plan.payload(i))
+            f32 = plan.get_int(i, 1)
+            s0 = max(plan.get_int(i, 0), 1)
+            M = a.N * a.Ho * a.Wo
+            key = ("wgrad", M, a.Cout, a.Cin, a.KH, a.KW, a.SH, f32, int(a.pro.mode != 0 or a.pro.act != 0))
+            best = _CACHE.get(key)
+            if best is None:
+                cands = sorted({max(1, s0 // 4), max(1, s0 // 2), s0, s0 * 2, s0 * 4})
+                cands = [s for s in cands if (M + s - 1) // s >= 32] or [1]
+                times = {}
+                for s in cands:
+                    plan.set_int(i, 0, s)
+                    times[s] = _time_op(plan, i, stream)
+                best = min(times, key=times.get)
+                _CACHE[key] = best
+                if verbose:
+                    print("tune wgrad", key, {k: round(v * 1e3, 1) for k, v in times.items()}, "->", best)
+            plan.set_int(i, 0, best)
+            n += 1
+    _save_cache()
+    torch.cuda.synchronize()
+    return n

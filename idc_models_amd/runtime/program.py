@@ -127,6 +127,9 @@ class FusedProgram:
         else:
             self._cast_all_plan = None
         self.recast_all()
+        if os.environ.get("IDC_AUTOTUNE", "1") != "0":
+            from .autotune import autotune_plan
+            autotune_plan(self.plan, self.stream, verbose=os.environ.get("IDC_TUNE_VERBOSE") == "1")
 
     # ------------------------------------------------------------------ execution
     def _sh(self):

@@ -58,9 +58,10 @@ def _check(m, ref, x, y, slack=0.02):
     p.run_segment("bwd")
     torch.cuda.synchronize()
     loss_ref, logits_ref, grads_ref = _ref_grads(ref, x, y)
-    _, logits16, grads16 = _ref_grads(ref16, x, y, bf16=True)
+    loss16, logits16, grads16 = _ref_grads(ref16, x, y, bf16=True)
     loss = p.io.loss.item()
-    assert abs(loss - loss_ref.item()) < 5e-2 * max(1.0, abs(loss_ref.item())), (loss, loss_ref.item())
+    assert abs(loss - loss_ref.item()) < 2 * abs(loss16.item() - loss_ref.item()) + 0.02, \
+        (loss, loss_ref.item(), loss16.item())
     lg = p.io.logits.reshape(-1)
     dev_fused = (lg - logits_ref.reshape(-1)).abs().max().item()
     dev_auto = (logits16.reshape(-1) - logits_ref.reshape(-1)).abs().max().item()
@@ -80,7 +81,9 @@ def test_densenet121_fused_matches_eager():
 
 
 def test_densenet121_moving_stats_and_step():
-    m, ref, x, y = _setup("densenet121", 8)
+    m, ref, x, y = _setup("densenet121", 16)
+    from idc_models_amd.engine import RMSprop
+    m.compile(RMSprop(1e-4), "binary_crossentropy", ["accuracy"], backend="fused")  # dense script lr
     loss0, _ = m.impl.train_step(x, y)
     torch.cuda.synchronize()
     bn = m.net.base.get_layer("conv2_block1_1_bn")
@@ -108,7 +111,9 @@ def test_densenet_fine_tune_at_150():
 
 
 def test_densenet201_cifar_shape():
-    m, ref, x, y = _setup("densenet201", 4, shape=(32, 32, 3))
+    # batch 32: at batch 8 random-init DenseNet-201 is chaotic in bf16 (autocast's own gradient
+    # cosine vs fp32 drops to ~0.4), which makes any comparison meaningless
+    m, ref, x, y = _setup("densenet201", 32, shape=(32, 32, 3))
     _check(m, ref, x, y)
 
 

@@ -73,6 +73,20 @@ def test_conv_fwd(fn, N, H, Cin, Cout, k, s, pads, outhw):
     assert relerr(y, ref) < 1e-2
 
 
+@pytest.mark.parametrize("tile", list(range(12)))
+def test_conv_every_tile_large_m_odd_ktiles(fn, tile):
+    """Every tile config at scale: M = 40000 with an odd K-tile count (K = 392 -> 7 / 13 tiles)
+    exercises the pipeline tail + epilogue LDS aliasing (a missing barrier once raced here)."""
+    N, H, Cin, Cout = 64, 50, 8, 64
+    x = bf(torch.randn(N, H, H, Cin, device=DEV))
+    w = bf(torch.randn(7, 7, Cin, Cout, device=DEV) * 0.05)
+    st = torch.zeros(2 * Cout, device=DEV)
+    y = fn.conv2d(x.to(torch.bfloat16), w, stride=(2, 2), pads=(3, 3), out_f32=True, tile=tile, stats=st)
+    ref = ref_conv(x, w, 2, (3, 3, 3, 3))
+    assert relerr(y, ref) < 1e-2
+    assert relerr(st[:Cout], ref.sum((0, 1, 2))) < 1e-2
+
+
 def test_conv_fwd_asymmetric_B(fn):
     """A = identity-like input, asymmetric B: catches a transposed C write (guide §3)."""
     N, H, C = 1, 4, 16

@@ -29,13 +29,14 @@ def main():
     arch = sys.argv[1] if len(sys.argv) > 1 else "vgg16"
     B = int(sys.argv[2]) if len(sys.argv) > 2 else 16
     dev = torch.device("cuda", 0)
-    net = build_model(arch, num_outputs=1, seed=0)
+    shape = tuple(int(v) for v in sys.argv[3].split(",")) if len(sys.argv) > 3 else (50, 50, 3)
+    net = build_model(arch, shape, num_outputs=1, seed=0)
     ref = copy.deepcopy(net).to(dev)
     ref16 = copy.deepcopy(net).to(dev)
     m = Model(net, device=dev)
     m.compile(RMSprop(1e-3), "binary_crossentropy", [], backend="fused")
     g = torch.Generator().manual_seed(1)
-    x = torch.randint(0, 256, (B, 50, 50, 3), generator=g, dtype=torch.uint8).to(dev)
+    x = torch.randint(0, 256, (B,) + shape, generator=g, dtype=torch.uint8).to(dev)
     y = torch.randint(0, 2, (B,), generator=g).to(dev)
     p = m.impl._prog(B, True, torch.uint8)
     m.impl._stage_inputs(p, x, y)
