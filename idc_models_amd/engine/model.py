@@ -157,6 +157,12 @@ class Model:
         self.impl = self._make_impl(backend)
         return self
 
+    def reset_optimizer(self):
+        """Fresh optimizer slot state without re-lowering (TFF re-creates the client optimizer
+        every round, ``fed_model.py:208``)."""
+        if self.optimizer is not None and self.arena is not None:
+            self.optimizer.reset_state()  # in place: captured graphs keep their slot pointers
+
     def _release_impl(self):
         if self.impl is not None and hasattr(self.impl, "close"):
             self.impl.sync_to_module()

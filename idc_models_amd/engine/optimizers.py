@@ -40,6 +40,14 @@ class Optimizer:
     def state_tensors(self):
         return {}
 
+    def reset_state(self) -> None:
+        """Zero every slot IN PLACE (pointers captured by HIP graphs stay valid)."""
+        with torch.no_grad():
+            for t in self.state_tensors().values():
+                if t is not None:
+                    t.zero_()
+        self.iterations = 0
+
 
 class RMSprop(Optimizer):
     name = "RMSprop"

@@ -64,7 +64,41 @@ def _compile(src: str, extra) -> str:
     return o
 
 
+H5_PREFIX = os.environ.get("IDC_HDF5_PREFIX", "/opt/conda")
+
+
+def h5_ext_path() -> str:
+    return os.path.join(PKG, "_idc_h5" + sysconfig.get_config_var("EXT_SUFFIX"))
+
+
+def build_h5(verbose: bool = True):
+    """Host-only pybind11 module over libhdf5 (Keras-layout weight files)."""
+    import pybind11
+
+    src = os.path.join(CSRC, "ckpt", "h5io.cpp")
+    out = h5_ext_path()
+    hdr = os.path.join(H5_PREFIX, "include", "hdf5.h")
+    if not os.path.exists(hdr):
+        if verbose:
+            print(f"[build_native] libhdf5 not found under {H5_PREFIX}; HDF5 checkpoints disabled")
+        return None
+    if os.path.exists(out) and os.path.getmtime(out) >= os.path.getmtime(src):
+        return out
+    cmd = ["g++", "-O2", "-std=c++17", "-shared", "-fPIC", src, "-o", out,
+           f"-I{pybind11.get_include()}", f"-I{sysconfig.get_paths()['include']}",
+           f"-I{H5_PREFIX}/include", f"-L{H5_PREFIX}/lib", "-lhdf5", f"-Wl,-rpath,{H5_PREFIX}/lib",
+           # the rpath also exposes an older libstdc++ in that prefix: link ours statically
+           "-static-libstdc++", "-static-libgcc"]
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    if r.returncode != 0:
+        raise RuntimeError(f"h5io build failed:\n{r.stderr[-4000:]}")
+    if verbose:
+        print(f"[build_native] {out}")
+    return out
+
+
 def build(clean: bool = False, jobs: int = 8, verbose: bool = True) -> str:
+    build_h5(verbose)
     if clean and os.path.isdir(BUILD):
         shutil.rmtree(BUILD)
     os.makedirs(BUILD, exist_ok=True)
