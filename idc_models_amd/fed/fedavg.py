@@ -131,12 +131,12 @@ class FedAvgProcess:
             for i, name in enumerate(self.metric_names):
                 met[1 + i] += n_k * logs.get(name if name in logs else "accuracy", 0.0)
         # one packed all-reduce of [delta sums | bn sums | n | metrics]
-        parts = [delta_sum, n_sum.float(), met.float()] + ([ntr_sum] if ntr_sum is not None else [])
+        parts = [delta_sum, n_sum, met] + ([ntr_sum] if ntr_sum is not None else [])
         if world > 1:
             flatp = torch.cat([p.reshape(-1).float() for p in parts])
             comm.all_reduce_(flatp)
             off = 0
-            for p in parts:
+            for p in parts:  # copy back IN PLACE (n_sum/met are float64 accumulators)
                 p.copy_(flatp[off:off + p.numel()].view(p.shape).to(p.dtype))
                 off += p.numel()
         total = float(n_sum.item())

@@ -120,7 +120,7 @@ class SecureFederatedProcess:
         if n_prot:
             with Timer("Encryption/aggregation", self.printer if self.verbose else None):
                 if self.mode == "mask":
-                    prot_mean = self._masked_mean(n_prot, dev)
+                    prot_mean = self._masked_mean(n_prot, sum(prot_sizes), dev)
                 elif self.mode == "paillier":
                     prot_mean = self._paillier_mean(n_prot, dev)
                 else:
@@ -137,12 +137,11 @@ class SecureFederatedProcess:
             off += n
         return out
 
-    def _masked_mean(self, n_prot: int, dev) -> torch.Tensor:
+    def _masked_mean(self, n_prot: int, n: int, dev) -> torch.Tensor:
         vecs = {k: torch.cat([w.reshape(-1).to(dev) for w in self.states[k].weights[:n_prot]]) for k in self.mine}
         mx = max([float(v.abs().max()) for v in vecs.values()] or [0.0])
         mx = comm.all_reduce_max(mx, dev) if self.world > 1 else mx
         scale = secagg.choose_scale(mx, self.K)
-        n = next(iter(vecs.values())).numel() if vecs else 0
         total = torch.zeros(n, dtype=torch.int64, device=dev)
         for k, v in vecs.items():
             masked = secagg.mask_quantize(v, scale, self.K, k, seed=self.seed + 7919, round_=self.round)
