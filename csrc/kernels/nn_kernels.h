@@ -94,6 +94,7 @@ hipError_t pool_bwd(const PoolBwdArgs& a, hipStream_t st);
 hipError_t bn_update_moving(const BnMovingDesc* d_descs, int n, int maxC, hipStream_t st);
 hipError_t head_fwd(const HeadArgs& a, hipStream_t st);
 hipError_t head_bwd(const HeadBwdArgs& a, hipStream_t st);
+hipError_t zero_fill(void* p, long long nbytes, hipStream_t st);
 hipError_t rmsprop(float* w, const float* g, float* ms, long long n, float lr, float rho,
                    float eps, float grad_scale, hipStream_t st);
 hipError_t cast_weights(const CastEntry* d_entries, int n, long long total, hipStream_t st);

@@ -517,6 +517,29 @@ __global__ __launch_bounds__(256) void rmsprop_kernel(float* __restrict__ w, con
   }
 }
 
+// zero fill as a plain kernel: keeps graph segments free of memset nodes and lets the fill
+// overlap with nothing but its own stream order (16-B stores for the aligned body)
+__global__ __launch_bounds__(256) void zero_fill_kernel(unsigned char* __restrict__ p, long long nbytes) {
+  const long long n16 = nbytes >> 4;
+  uint4* q = reinterpret_cast<uint4*>(p);
+  const long long stride = (long long)gridDim.x * blockDim.x;
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n16; i += stride)
+    q[i] = make_uint4(0u, 0u, 0u, 0u);
+  const long long t = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t < (nbytes & 15)) p[(n16 << 4) + t] = 0;
+}
+
+hipError_t zero_fill(void* p, long long nbytes, hipStream_t st) {
+  if (nbytes <= 0) return hipSuccess;
+  if (reinterpret_cast<uintptr_t>(p) & 15) return hipErrorInvalidValue;
+  long long blocks = ((nbytes >> 4) + 255) / 256;
+  if (blocks > 4096) blocks = 4096;
+  if (blocks < 1) blocks = 1;
+  hipLaunchKernelGGL(zero_fill_kernel, dim3((int)blocks), dim3(256), 0, st,
+                     reinterpret_cast<unsigned char*>(p), nbytes);
+  return hipGetLastError();
+}
+
 hipError_t rmsprop(float* w, const float* g, float* ms, long long n, float lr, float rho, float eps,
                    float grad_scale, hipStream_t st) {
   long long n4 = n / 4;  // arena sizes are multiples of 64 elements

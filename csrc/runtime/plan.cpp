@@ -14,10 +14,18 @@
 // A training step is typically 3 graphs (forward, backward, optimizer) or, under data
 // parallelism, backward split into bucket-aligned segments so RCCL all-reduces (issued by
 // torch.distributed on its own stream) overlap the remaining backward segments.
+//
+// Lanes: an op tagged lane 1 runs on the plan's SIDE stream, forked from the main stream at its
+// position (event record + wait, which become graph edges under capture) and joined back at the
+// end of every run/capture range.  Weight-gradient kernels are off the backward critical path
+// (nothing but the optimizer consumes them), so the lowering puts them on lane 1 where they fill
+// the CUs the small, latency-bound dgrad chain leaves idle.  The lowering guarantees that a
+// side-lane op only reads buffers no later main-lane op of the same range overwrites.
 #include <hip/hip_runtime.h>
 #include <pybind11/pybind11.h>
 #include <pybind11/stl.h>
 
+#include <cstdlib>
 #include <cstring>
 #include <stdexcept>
 #include <string>
@@ -59,6 +67,7 @@ enum OpKind : int {
 
 struct Op {
   int kind;
+  int lane = 0;
   int i[8];
   float f[8];
   long long l[4];
@@ -78,12 +87,19 @@ const T& as(const Op& op) {
 
 class Plan {
  public:
-  ~Plan() { clear_graphs(); }
+  ~Plan() {
+    if (std::getenv("IDC_PLAN_LEAK")) return;  // debugging aid: never release HIP objects
+    clear_graphs();
+    if (fork_) hipEventDestroy(fork_);
+    if (join_) hipEventDestroy(join_);
+    if (side_) hipStreamDestroy(side_);
+  }
 
   int add(int kind, py::bytes payload, std::vector<int> ints, std::vector<float> floats,
-          std::vector<long long> longs, std::vector<uintptr_t> ptrs) {
+          std::vector<long long> longs, std::vector<uintptr_t> ptrs, int lane) {
     Op op;
     op.kind = kind;
+    op.lane = lane;
     std::memset(op.i, 0, sizeof(op.i));
     std::memset(op.f, 0, sizeof(op.f));
     std::memset(op.l, 0, sizeof(op.l));
@@ -112,15 +128,17 @@ class Plan {
   void run(int begin, int end, uintptr_t stream) {
     hipStream_t st = reinterpret_cast<hipStream_t>(stream);
     if (end < 0 || end > (int)ops_.size()) end = (int)ops_.size();
-    for (int k = begin; k < end; ++k) exec(ops_[k], st);
+    issue(begin, end, st);
   }
+
+  int lane(int idx) const { return ops_.at(idx).lane; }
 
   int capture(int begin, int end, uintptr_t stream) {
     hipStream_t st = reinterpret_cast<hipStream_t>(stream);
     if (end < 0 || end > (int)ops_.size()) end = (int)ops_.size();
     check(hipStreamBeginCapture(st, hipStreamCaptureModeThreadLocal), "hipStreamBeginCapture");
     try {
-      for (int k = begin; k < end; ++k) exec(ops_[k], st);
+      issue(begin, end, st);
     } catch (...) {
       hipGraph_t g;
       hipStreamEndCapture(st, &g);
@@ -157,6 +175,39 @@ class Plan {
   }
 
  private:
+  void ensure_side() {
+    if (side_) return;
+    check(hipStreamCreateWithFlags(&side_, hipStreamNonBlocking), "hipStreamCreate(side)");
+    check(hipEventCreateWithFlags(&fork_, hipEventDisableTiming), "hipEventCreate(fork)");
+    check(hipEventCreateWithFlags(&join_, hipEventDisableTiming), "hipEventCreate(join)");
+  }
+
+  // issue ops[begin:end): lane-0 ops on `st`, lane-1 ops on the side stream forked at their
+  // position; one fork per run of side ops that follows main work, one join at the end.
+  void issue(int begin, int end, hipStream_t st) {
+    bool side_used = false, main_since_fork = true;
+    for (int k = begin; k < end; ++k) {
+      const Op& op = ops_[k];
+      if (op.lane == 1) {
+        ensure_side();
+        if (main_since_fork) {
+          check(hipEventRecord(fork_, st), "hipEventRecord(fork)");
+          check(hipStreamWaitEvent(side_, fork_, 0), "hipStreamWaitEvent(fork)");
+          main_since_fork = false;
+        }
+        exec(op, side_);
+        side_used = true;
+      } else {
+        exec(op, st);
+        main_since_fork = true;
+      }
+    }
+    if (side_used) {
+      check(hipEventRecord(join_, side_), "hipEventRecord(join)");
+      check(hipStreamWaitEvent(st, join_, 0), "hipStreamWaitEvent(join)");
+    }
+  }
+
   void exec(const Op& op, hipStream_t st) {
     switch (op.kind) {
       case OP_CONV: check(conv_igemm(as<ConvArgs>(op), op.i[0], op.i[1] != 0, st), "conv_igemm"); break;
@@ -186,7 +237,7 @@ class Plan {
               "input_stage");
         break;
       case OP_MEMSET:
-        check(hipMemsetAsync(reinterpret_cast<void*>(op.p[0]), 0, (size_t)op.l[0], st), "memset");
+        check(zero_fill(reinterpret_cast<void*>(op.p[0]), op.l[0], st), "zero_fill");
         break;
       case OP_BN_STATS:
         check(bn_stats(reinterpret_cast<const bf16_t*>(op.p[0]), op.i[0], op.i[1], op.i[2],
@@ -214,6 +265,8 @@ class Plan {
   }
 
   std::vector<Op> ops_;
+  hipStream_t side_ = nullptr;
+  hipEvent_t fork_ = nullptr, join_ = nullptr;
   std::vector<hipGraph_t> graphs_;
   std::vector<hipGraphExec_t> execs_;
 };
@@ -289,7 +342,9 @@ PYBIND11_MODULE(_idc_native, m) {
   m.doc() = "idc_models_amd native MI355X (gfx950) kernels and plan executor";
   py::class_<Plan>(m, "Plan")
       .def(py::init<>())
-      .def("add", &Plan::add)
+      .def("add", &Plan::add, py::arg("kind"), py::arg("payload"), py::arg("ints"), py::arg("floats"),
+           py::arg("longs"), py::arg("ptrs"), py::arg("lane") = 0)
+      .def("lane", &Plan::lane)
       .def("set_float", &Plan::set_float)
       .def("set_int", &Plan::set_int)
       .def("get_int", &Plan::get_int)

@@ -16,6 +16,7 @@ Design (MI355X-first):
 from __future__ import annotations
 
 import ctypes as C
+import os
 from dataclasses import dataclass
 from typing import Dict, List, Optional, Tuple
 
@@ -107,7 +108,7 @@ class Builder:
         self.device = device
         self.B = batch
         self.training = training
-        self.ops: List[tuple] = []          # (segment, kind, payload bytes, ints, floats, longs, ptrs)
+        self.ops: List[tuple] = []  # (segment, kind, payload bytes, ints, floats, longs, ptrs, lane)
         self.keep: List[torch.Tensor] = []  # keep allocations alive
         self._stats_chunks: List[Tuple[int, int]] = []
         self._stats_size = 0
@@ -117,6 +118,9 @@ class Builder:
         self.moving: List[nat.BnMovingDesc] = []
         self.conv_weights: Dict[int, dict] = {}
         self.segment = "fwd"
+        self.side_lane = os.environ.get("IDC_SIDE_LANE", "1") != "0"
+        self.guard = os.environ.get("IDC_GUARD") == "1"
+        self.guards: List[tuple] = []
         self.bwd_marks: List[Tuple[int, int]] = []  # (op index, lowest arena param index ready)
         # stats arena is allocated lazily with a generous capacity; views are handed out in order
         self._stats_cap = 1 << 20
@@ -124,9 +128,28 @@ class Builder:
 
     # ------------------------------------------------------------------ allocation
     def alloc(self, shape, dtype=BF16) -> torch.Tensor:
+        if self.guard:
+            return self._alloc_guarded(shape, dtype)
         t = torch.zeros(shape, dtype=dtype, device=self.device)
         self.keep.append(t)
         return t
+
+    GUARD = 1 << 14  # elements on each side (IDC_GUARD=1 debugging aid)
+
+    def _alloc_guarded(self, shape, dtype) -> torch.Tensor:
+        """Buffer flanked by NaN guards: out-of-bounds reads poison results, out-of-bounds
+        writes are found by ``guards_intact`` (see tools/guard_check.py)."""
+        n = 1
+        for d in (shape if isinstance(shape, (tuple, list)) else (shape,)):
+            n *= int(d)
+        g = self.GUARD
+        base = torch.empty(n + 2 * g, dtype=dtype, device=self.device)
+        fill = float("nan") if dtype.is_floating_point else 0
+        base.fill_(fill)
+        base[g:g + n].zero_()
+        self.keep.append(base)
+        self.guards.append((base, g, n))
+        return base[g:g + n].view(shape)
 
     def nhwc(self, N, H, W, C, dtype=BF16) -> Tensor4:
         return Tensor4(self.alloc((N, H, W, C), dtype), N, H, W, C, C)
@@ -140,10 +163,12 @@ class Builder:
         return Stats(v, ld, count)
 
     # ------------------------------------------------------------------ op emission
-    def emit(self, kind, payload=None, ints=(), floats=(), longs=(), ptrs=()):
+    def emit(self, kind, payload=None, ints=(), floats=(), longs=(), ptrs=(), lane=0):
+        """Append one op.  ``lane=1`` puts it on the plan's side stream (see plan.cpp): only for
+        ops whose inputs no later main-lane op of the segment overwrites (weight gradients)."""
         raw = nat.raw(payload) if payload is not None else b""
         self.ops.append((self.segment, kind, raw, list(ints), list(floats), list(longs),
-                         [int(p) for p in ptrs]))
+                         [int(p) for p in ptrs], lane if self.side_lane else 0))
 
     def mark_grads_ready(self, params):
         """Backward has finished producing the grads of ``params`` (for DP bucket overlap)."""
@@ -288,7 +313,7 @@ class Builder:
         self.emit(nat.OP_CONV, a, ints=(tile, 1 if dy.is_f32 else 0))
 
     def wgrad(self, x: Tensor4, layer, g: Tensor4, dw: torch.Tensor, *, stride=(1, 1), pads=(0, 0),
-              pro=None, cin_real=0, splits=-1):
+              pro=None, cin_real=0, splits=-1, lane=0):
         kh, kw = layer.kernel_size
         a = nat.WgradArgs()
         a.x = x.ptr
@@ -308,7 +333,7 @@ class Builder:
         a.cin_real = cin_real
         if splits < 0:
             splits = nat.load().pick_splits(g.M, kh * kw * x.C, g.C)
-        self.emit(nat.OP_WGRAD, a, ints=(splits, 1 if g.is_f32 else 0))
+        self.emit(nat.OP_WGRAD, a, ints=(splits, 1 if g.is_f32 else 0), lane=lane)
 
     def bn_bwd_apply(self, dz: Tensor4, x: Tensor4, bn: BNRef, dst: Tensor4, accumulate: bool):
         a = nat.BnBwdApplyArgs()

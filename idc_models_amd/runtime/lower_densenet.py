@@ -125,13 +125,14 @@ def lower_densenet(b: Builder, net, U: int, input_dtype):
         N, Hs, Ws, ctot = buf.N, st["H"], st["W"], st["ctot"]
         z1 = b.nhwc(N, Hs, Ws, ctot)
         z2 = b.nhwc(N, Hs, Ws, 128)
-        dt = b.nhwc(N, Hs, Ws, 128)
         stop = False
         for lay in reversed(st["layers"]):
             cin, bn1, cv1, bn2, cv2, t = lay["cin"], lay["bn1"], lay["cv1"], lay["bn2"], lay["cv2"], lay["t"]
             dO = dbuf.slice(cin, 32)
+            # weight gradients run on the side lane: their inputs (t, this layer's dO slice, the
+            # per-layer dt, the stage buffer) are never overwritten later in the backward
             if fz.trainable(cv2):
-                b.wgrad(t, cv2, dO, b.arena.grad_of(cv2.kernel), pads=(1, 1), pro=bn2.args())
+                b.wgrad(t, cv2, dO, b.arena.grad_of(cv2.kernel), pads=(1, 1), pro=bn2.args(), lane=1)
             if not fz.before(cv2):
                 stop = True
                 break
@@ -139,9 +140,10 @@ def lower_densenet(b: Builder, net, U: int, input_dtype):
             if not fz.before(bn2.layer):
                 stop = True
                 break
+            dt = b.nhwc(N, Hs, Ws, 128)  # per layer: read later by the side-lane wgrad
             b.bn_bwd_apply(z2, t, bn2, dt, accumulate=False)
             if fz.trainable(cv1):
-                b.wgrad(buf.slice(0, cin), cv1, dt, b.arena.grad_of(cv1.kernel), pro=bn1.args())
+                b.wgrad(buf.slice(0, cin), cv1, dt, b.arena.grad_of(cv1.kernel), pro=bn1.args(), lane=1)
             if not fz.before(cv1):
                 stop = True
                 break
@@ -162,7 +164,7 @@ def lower_densenet(b: Builder, net, U: int, input_dtype):
         bnt, cvt, p = tr["bn"], tr["conv"], tr["p"]
         dO = dbuf.slice(0, st["c0"])
         if fz.trainable(cvt):
-            b.wgrad(p, cvt, dO, b.arena.grad_of(cvt.kernel))
+            b.wgrad(p, cvt, dO, b.arena.grad_of(cvt.kernel), lane=1)
         if not fz.before(cvt):
             return
         dp = b.nhwc(p.N, p.H, p.W, p.C)
@@ -186,5 +188,5 @@ def lower_densenet(b: Builder, net, U: int, input_dtype):
         dys = b.nhwc(B, H1, W1, 64)
         b.bn_bwd_apply(zs, ys, bn_stem, dys, accumulate=False)
         b.wgrad(x8, conv1, dys, b.arena.grad_of(conv1.kernel), stride=(2, 2), pads=(3, 3),
-                cin_real=Cimg)
+                cin_real=Cimg, lane=1)
     b.mark_grads_ready([conv1.kernel, bn_stem.gamma, bn_stem.beta])

@@ -72,7 +72,7 @@ def lower_vgg(b: Builder, net, U: int, input_dtype):
             g, masked = dx, True
         else:
             if fz.trainable(l):
-                b.wgrad(x, l, g, ar.grad_of(l.kernel), pads=(1, 1))
+                b.wgrad(x, l, g, ar.grad_of(l.kernel), pads=(1, 1), lane=1)  # inputs never reused
                 b.mark_grads_ready([l.kernel, l.bias])
             if not fz.before(l):
                 return
