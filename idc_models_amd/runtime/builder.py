@@ -393,6 +393,53 @@ class Builder:
         a.is_avg = 0 if is_max else 1
         self.emit(nat.OP_POOL_BWD, a)
 
+    def bn_apply(self, x: Tensor4, bn: "BNRef", y: Tensor4, *, act: Optional[int] = None,
+                 res: Optional[Tensor4] = None, stats: Optional[Stats] = None):
+        """Materialise y = act(BN(x)) [+ res] (bf16), optionally reducing y's statistics."""
+        args = bn.args()
+        if act is not None:
+            args.act = act
+        self.emit(nat.OP_BN_APPLY, args,
+                  ints=(x.ld, res.ld if res is not None else 0, y.ld, x.M, x.C,
+                        stats.ld if stats is not None else 0),
+                  ptrs=(x.ptr, res.ptr if res is not None else 0, y.ptr,
+                        stats.ptr if stats is not None else 0))
+
+    def _dw_args(self, x: Tensor4, layer, Ho: int, Wo: int, stride: int, pads, pro) -> nat.DwArgs:
+        kh, kw = layer.kernel_size
+        a = nat.DwArgs()
+        a.x, a.ldx = x.ptr, x.ld
+        a.N, a.H, a.W, a.C = x.N, x.H, x.W, x.C
+        a.pro = pro if pro is not None else act_only(0)
+        a.w = layer.depthwise_kernel.data_ptr()  # fp32 master (KH, KW, C, 1), read directly
+        a.KH, a.KW, a.S, a.PT, a.PL, a.Ho, a.Wo = kh, kw, stride, pads[0], pads[1], Ho, Wo
+        return a
+
+    def dwconv(self, x: Tensor4, layer, y: Tensor4, *, stride=1, pads=(1, 1), pro=None,
+               stats: Optional[Stats] = None):
+        a = self._dw_args(x, layer, y.H, y.W, stride, pads, pro)
+        a.y, a.ldy = y.ptr, y.ld
+        if stats is not None:
+            a.stats, a.stats_ld = stats.ptr, stats.ld
+        self.emit(nat.OP_DW_FWD, a)
+
+    def dw_bwd_data(self, x: Tensor4, layer, dy: Tensor4, dz: Tensor4, *, stride=1, pads=(1, 1),
+                    bn: Optional["BNRef"] = None):
+        """dz = (dy conv^T w) * act'(BN(x)), sums into bn's dbeta/dgamma (x = raw dw input)."""
+        a = self._dw_args(x, layer, dy.H, dy.W, stride, pads, bn.args() if bn is not None else None)
+        a.dy, a.lddy = dy.ptr, dy.ld
+        a.dx, a.lddx = dz.ptr, dz.ld
+        if bn is not None:
+            a.gsum, a.gsumx = nat.ptr(bn.dbeta), nat.ptr(bn.dgamma)
+        self.emit(nat.OP_DW_BWD_DATA, a)
+
+    def dw_wgrad(self, x: Tensor4, layer, dy: Tensor4, dw: torch.Tensor, *, stride=1, pads=(1, 1),
+                 pro=None, lane=0):
+        a = self._dw_args(x, layer, dy.H, dy.W, stride, pads, pro)
+        a.dy, a.lddy = dy.ptr, dy.ld
+        a.dw = dw.data_ptr()
+        self.emit(nat.OP_DW_WGRAD, a, lane=lane)
+
     def memset(self, t: torch.Tensor, nbytes: Optional[int] = None):
         self.emit(nat.OP_MEMSET, longs=(nbytes if nbytes is not None else t.numel() * t.element_size(),),
                   ptrs=(t.data_ptr(),))

@@ -1,0 +1,194 @@
+"""MobileNetV2 lowering (``dist_model_tf_mobile.py`` backbone; SURVEY §2.4.2, north-star FL model).
+
+MI355X structure:
+
+* pointwise (1x1) convs are MFMA implicit GEMMs whose operand prologue applies the producer's
+  pending BN + ReLU6 (expand -> depthwise BN and depthwise -> project BN never materialise);
+* depthwise 3x3 convs are bandwidth kernels (``dwconv.hip``) that read the fp32 master kernel,
+  apply the pending expand-BN + ReLU6 on load and reduce their own output statistics;
+* each block output ``BN_project(p) [+ residual]`` is materialised ONCE by ``bn_apply`` (it is the
+  next block's expand input AND, for identity blocks, its residual);
+* backward mirrors it: BN backward of the project BN (reduce + apply), project dgrad with the
+  BN-backward epilogue through depthwise-BN + ReLU6, depthwise backward-data with the same
+  epilogue through expand-BN + ReLU6, expand dgrad ACCUMULATED into the residual gradient in
+  place (fp32), weight gradients on the side lane.
+Keras ``correct_pad`` asymmetric padding of stride-2 layers = top/left pad + implicit bottom/right.
+"""
+from __future__ import annotations
+
+import torch
+
+from ..models.layers import correct_pad
+from ..ops import _native as nat
+from .builder import F32, BNRef, Builder, Tensor4
+from .lower_common import RELU6, FreezeInfo, HeadIO, emit_head, emit_head_bwd, emit_input
+
+
+def _dw_geometry(h, w, stride):
+    if stride == 1:
+        return (1, 1), h, w
+    pad = correct_pad(h, w, 3)
+    ho = (h + pad[0][0] + pad[0][1] - 3) // 2 + 1
+    wo = (w + pad[1][0] + pad[1][1] - 3) // 2 + 1
+    return (pad[0][0], pad[1][0]), ho, wo
+
+
+def lower_mobilenet(b: Builder, net, U: int, input_dtype):
+    from ..models.mobilenet_v2 import MBV2_BLOCKS
+    base, dense = net.base, net.head
+    B, training = b.B, b.training
+    fz = FreezeInfo(base, training)
+    L = {l.name: l for l in base.layers}
+    H, W, Cimg = base.input_shape
+    io = HeadIO(b, U)
+
+    # ------------------------------------------------------------------ forward
+    b.segment = "fwd"
+    if training:
+        b.memset(b.stats_arena)
+    xin, x8 = emit_input(b, H, W, Cimg, input_dtype)
+    conv1, bnl0 = L["Conv1"], L["bn_Conv1"]
+    pad = correct_pad(H, W, 3)
+    H1 = (H + pad[0][0] + pad[0][1] - 3) // 2 + 1
+    W1 = (W + pad[1][0] + pad[1][1] - 3) // 2 + 1
+    stem_pads = (pad[0][0], pad[1][0])
+    y0 = b.nhwc(B, H1, W1, conv1.filters)
+    s0 = b.stats(conv1.filters, B * H1 * W1) if training else None
+    b.conv(x8, conv1, y0, stride=(2, 2), pads=stem_pads, stats=s0)
+    bn0 = BNRef(bnl0, b, s0, RELU6)
+    b.add_moving(bn0)
+
+    blocks = []
+    h_in = None                 # materialised block input (None for block 0: pending y0/bn0)
+    cin, h, w = conv1.filters, H1, W1
+    for bid, (filters, stride, t) in enumerate(MBV2_BLOCKS):
+        pre = f"block_{bid}_" if bid else "expanded_conv_"
+        blk = {"bid": bid, "stride": stride, "h_in": h_in}
+        if bid:
+            ex, exbn = L[pre + "expand"], L[pre + "expand_BN"]
+            e = b.nhwc(B, h, w, ex.filters)
+            se = b.stats(ex.filters, B * h * w) if training else None
+            b.conv(h_in, ex, e, stats=se)
+            bn_e = BNRef(exbn, b, se, RELU6)
+            b.add_moving(bn_e)
+            blk.update(ex=ex, e=e, bn_in=bn_e)
+            dw_in, bn_in = e, bn_e
+        else:
+            dw_in, bn_in = y0, bn0
+            blk.update(ex=None, e=y0, bn_in=bn0)
+        dwl, dwbn = L[pre + "depthwise"], L[pre + "depthwise_BN"]
+        pads, ho, wo = _dw_geometry(h, w, stride)
+        ch = dw_in.C
+        d = b.nhwc(B, ho, wo, ch)
+        sd = b.stats(ch, B * ho * wo) if training else None
+        b.dwconv(dw_in, dwl, d, stride=stride, pads=pads, pro=bn_in.args(), stats=sd)
+        bn_d = BNRef(dwbn, b, sd, RELU6)
+        b.add_moving(bn_d)
+        prj, prjbn = L[pre + "project"], L[pre + "project_BN"]
+        pw = prj.filters
+        p = b.nhwc(B, ho, wo, pw)
+        sp = b.stats(pw, B * ho * wo) if training else None
+        b.conv(d, prj, p, pro=bn_d.args(), stats=sp)
+        bn_p = BNRef(prjbn, b, sp, 0)
+        b.add_moving(bn_p)
+        residual = (cin == pw and stride == 1)
+        hout = b.nhwc(B, ho, wo, pw)
+        b.bn_apply(p, bn_p, hout, res=h_in if residual else None)
+        blk.update(dwl=dwl, pads=pads, d=d, bn_d=bn_d, prj=prj, p=p, bn_p=bn_p, residual=residual,
+                   h_out=hout)
+        blocks.append(blk)
+        h_in, cin, h, w = hout, pw, ho, wo
+
+    c1l, c1bnl = L["Conv_1"], L["Conv_1_bn"]
+    c1 = b.nhwc(B, h, w, c1l.filters)
+    sc1 = b.stats(c1l.filters, B * h * w) if training else None
+    b.conv(h_in, c1l, c1, stats=sc1)
+    bn_c1 = BNRef(c1bnl, b, sc1, RELU6)
+    b.add_moving(bn_c1)
+    emit_head(b, c1, bn_c1.args(), dense, U, io, training)
+    if training:
+        b.emit("MOVING")
+    b.xin, b.io = xin, io
+    b.debug = {"y0": y0, "blocks": blocks, "c1": c1}
+    if not training:
+        return
+
+    # ------------------------------------------------------------------ backward
+    b.segment = "bwd"
+    b.memset(b.arena.grad)
+    need_base = fz.at_or_before(c1bnl)
+    dA = emit_head_bwd(b, c1, dense, U, io, need_dA=need_base)
+    if not need_base:
+        return
+    zc = b.nhwc(c1.N, c1.H, c1.W, c1.C)
+    b.bn_bwd_reduce(dA, c1, bn_c1, zc)
+    b.mark_grads_ready([bn_c1.gamma, bn_c1.beta])
+    if not fz.before(c1bnl):
+        return
+    dc1 = b.nhwc(c1.N, c1.H, c1.W, c1.C)
+    b.bn_bwd_apply(zc, c1, bn_c1, dc1, accumulate=False)
+    h_last = blocks[-1]["h_out"]
+    if fz.trainable(c1l):
+        b.wgrad(h_last, c1l, dc1, b.arena.grad_of(c1l.kernel), lane=1)
+    b.mark_grads_ready([c1l.kernel])
+    if not fz.before(c1l):
+        return
+    G = b.nhwc(h_last.N, h_last.H, h_last.W, h_last.C, F32)
+    b.dgrad(dc1, c1l, G, out_mode=nat.OUT_F32)
+
+    for blk in reversed(blocks):
+        p, bn_p, d, bn_d = blk["p"], blk["bn_p"], blk["d"], blk["bn_d"]
+        prj, dwl = blk["prj"], blk["dwl"]
+        # project BN (no activation): G is the gradient of BN_p(p) (+ residual passthrough)
+        zp = b.nhwc(p.N, p.H, p.W, p.C)
+        b.bn_bwd_reduce(G, p, bn_p, zp)
+        b.mark_grads_ready([bn_p.gamma, bn_p.beta])
+        if not fz.before(bn_p.layer):
+            return
+        dp = b.nhwc(p.N, p.H, p.W, p.C)
+        b.bn_bwd_apply(zp, p, bn_p, dp, accumulate=False)
+        if fz.trainable(prj):
+            b.wgrad(d, prj, dp, b.arena.grad_of(prj.kernel), pro=bn_d.args(), lane=1)
+        b.mark_grads_ready([prj.kernel])
+        if not fz.before(prj):
+            return
+        zd = b.nhwc(d.N, d.H, d.W, d.C)
+        b.dgrad(dp, prj, zd, mx=d, mbn=bn_d.args(), gsum=bn_d.dbeta, gsumx=bn_d.dgamma)
+        b.mark_grads_ready([bn_d.gamma, bn_d.beta])
+        if not fz.before(bn_d.layer):
+            return
+        dd = b.nhwc(d.N, d.H, d.W, d.C)
+        b.bn_bwd_apply(zd, d, bn_d, dd, accumulate=False)
+        e, bn_in = blk["e"], blk["bn_in"]
+        if fz.trainable(dwl):
+            b.dw_wgrad(e, dwl, dd, b.arena.grad_of(dwl.depthwise_kernel), stride=blk["stride"],
+                       pads=blk["pads"], pro=bn_in.args(), lane=1)
+        b.mark_grads_ready([dwl.depthwise_kernel])
+        if not fz.before(dwl):
+            return
+        ze = b.nhwc(e.N, e.H, e.W, e.C)
+        b.dw_bwd_data(e, dwl, dd, ze, stride=blk["stride"], pads=blk["pads"], bn=bn_in)
+        b.mark_grads_ready([bn_in.gamma, bn_in.beta])
+        if not fz.before(bn_in.layer):
+            return
+        de = b.nhwc(e.N, e.H, e.W, e.C)
+        b.bn_bwd_apply(ze, e, bn_in, de, accumulate=False)
+        ex = blk["ex"]
+        if ex is None:  # block 0: de is the gradient of the raw stem conv output
+            if fz.trainable(conv1):
+                b.wgrad(x8, conv1, de, b.arena.grad_of(conv1.kernel), stride=(2, 2), pads=stem_pads,
+                        cin_real=Cimg, lane=1)
+            b.mark_grads_ready([conv1.kernel])
+            return
+        h_prev = blk["h_in"]
+        if fz.trainable(ex):
+            b.wgrad(h_prev, ex, de, b.arena.grad_of(ex.kernel), lane=1)
+        b.mark_grads_ready([ex.kernel])
+        if not fz.before(ex):
+            return
+        if blk["residual"]:
+            # dL/dh_prev = G (identity shortcut) + expand^T de: accumulate into G in place
+            b.dgrad(de, ex, G, out_mode=nat.OUT_F32_ACC)
+        else:
+            G = b.nhwc(h_prev.N, h_prev.H, h_prev.W, h_prev.C, F32)
+            b.dgrad(de, ex, G, out_mode=nat.OUT_F32)

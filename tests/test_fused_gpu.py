@@ -127,8 +127,28 @@ def test_vgg16_fused_matches_eager():
 
 
 def test_mobilenetv2_fused_matches_eager():
-    m, ref, x, y = _setup("mobilenetv2", 8)
+    m, ref, x, y = _setup("mobilenetv2", 16)
     _check(m, ref, x, y)
+
+
+def test_mobilenetv2_fine_tune_at_100():
+    m, ref, x, y = _setup("mobilenetv2", 16, fine_tune_at=100)
+    _check(m, ref, x, y)
+
+
+def test_mobilenetv2_phase1_frozen_base():
+    m, ref, x, y = _setup("mobilenetv2", 16, freeze_base=True)
+    assert len(m.arena.params) == 2
+    _check(m, ref, x, y)
+
+
+def test_mobilenetv2_steps_reduce_loss_and_update_moving_stats():
+    m, ref, x, y = _setup("mobilenetv2", 32)
+    bn = m.net.base.get_layer("block_5_project_BN")
+    mm0 = bn.moving_mean.clone()
+    losses = [m.impl.train_step(x, y)[0].item() for _ in range(8)]
+    assert all(l == l for l in losses) and losses[-1] < losses[0], losses
+    assert not torch.equal(bn.moving_mean, mm0)
 
 
 def test_fused_fit_and_evaluate_api():

@@ -1,0 +1,103 @@
+"""Lowering dry-runs on the CPU: every model family x freeze mode lowers to a plan whose every raw
+device pointer lies inside a live tensor (no dangling or out-of-range argument), whose ctypes
+argument structs match the native layouts, and whose backward stops where Keras freezing says."""
+import ctypes as C
+
+import pytest
+import torch
+
+from idc_models_amd.ops import _native as nat
+
+pytestmark = pytest.mark.skipif(not nat.available(), reason="native extension not built")
+
+CASES = [("densenet121", None), ("densenet121", 150), ("densenet121", "frozen"), ("vgg16", None),
+         ("vgg16", 15), ("mobilenetv2", None), ("mobilenetv2", 100), ("mobilenetv2", "frozen")]
+
+
+def _lower(arch, ft, training, B=4):
+    from idc_models_amd.engine import Model, RMSprop
+    from idc_models_amd.models import build_model
+    from idc_models_amd.parallel import OneDeviceStrategy
+    from idc_models_amd.runtime.builder import Builder
+    from idc_models_amd.runtime.program import _lowering_for
+    net = build_model(arch, None, 1, seed=0)
+    if ft == "frozen":
+        net.base.trainable = False
+    elif ft:
+        for l in net.base.layers[:ft]:
+            l.trainable = False
+    m = Model(net, OneDeviceStrategy("cpu"))
+    m.compile(RMSprop(1e-4), "binary_crossentropy", [], backend="eager")
+    b = Builder(net, m.arena, torch.device("cpu"), B, training)
+    _lowering_for(net)(b, net, 1, torch.uint8)
+    b.finalize_casts()
+    b.finalize_moving()
+    return m, net, b
+
+
+STRUCTS = {nat.OP_CONV: nat.ConvArgs, nat.OP_WGRAD: nat.WgradArgs, nat.OP_BN_BWD_APPLY: nat.BnBwdApplyArgs,
+           nat.OP_BN_BWD_REDUCE: nat.BnBwdReduceArgs, nat.OP_MAXPOOL: nat.PoolArgs,
+           nat.OP_AVGPOOL: nat.PoolArgs, nat.OP_POOL_BWD: nat.PoolBwdArgs, nat.OP_HEAD_FWD: nat.HeadArgs,
+           nat.OP_HEAD_BWD: nat.HeadBwdArgs, nat.OP_DW_FWD: nat.DwArgs, nat.OP_DW_BWD_DATA: nat.DwArgs,
+           nat.OP_DW_WGRAD: nat.DwArgs, nat.OP_BN_APPLY: nat.BnArgs}
+
+
+def _pointers(obj, out):
+    for f in obj._fields_:
+        v = getattr(obj, f[0])
+        if isinstance(v, C.Structure):
+            _pointers(v, out)
+        elif f[1] is C.c_void_p and v:
+            out.append((f[0], v))
+
+
+@pytest.mark.parametrize("arch,ft", CASES)
+def test_plan_pointers_are_live(arch, ft):
+    m, net, b = _lower(arch, ft, True)
+    ranges = [(t.data_ptr(), t.data_ptr() + t.numel() * t.element_size()) for t in
+              b.keep + [b.stats_arena, m.arena.data, m.arena.grad] + list(net.parameters()) +
+              list(net.buffers())]
+    bad = []
+    for i, (seg, kind, raw, ints, floats, longs, ptrs, lane) in enumerate(b.ops):
+        vals = [("ptr", p) for p in ptrs if p]
+        if kind in STRUCTS:
+            assert len(raw) == C.sizeof(STRUCTS[kind]), (i, kind)
+            _pointers(STRUCTS[kind].from_buffer_copy(raw), vals)
+        for name, v in vals:
+            if not any(lo <= v < hi for lo, hi in ranges):
+                bad.append((i, kind, name))
+    assert not bad, bad[:10]
+
+
+@pytest.mark.parametrize("arch,ft", CASES)
+def test_forward_only_plan_has_no_backward(arch, ft):
+    _, _, b = _lower(arch, ft, False)
+    assert {op[0] for op in b.ops} == {"fwd"}
+    assert not b.moving  # inference never updates moving statistics
+
+
+def test_frozen_base_backward_is_head_only():
+    _, _, b = _lower("mobilenetv2", "frozen", True)
+    bwd = [op[1] for op in b.ops if op[0] == "bwd"]
+    assert nat.OP_HEAD_BWD in bwd
+    assert not any(k in (nat.OP_WGRAD, nat.OP_DW_WGRAD, nat.OP_CONV) for k in bwd)
+
+
+def test_fine_tune_backward_stops_at_first_trainable_layer():
+    m, net, b = _lower("mobilenetv2", 100, True)
+    n_wgrad = sum(1 for op in b.ops if op[1] in (nat.OP_WGRAD, nat.OP_DW_WGRAD))
+    trainable_convs = [l for l in net.base.layers[100:] if l.keras_class in ("Conv2D", "DepthwiseConv2D")]
+    assert n_wgrad == len(trainable_convs)
+
+
+def test_weight_gradients_are_on_the_side_lane():
+    _, _, b = _lower("densenet121", None, True)
+    lanes = {op[7] for op in b.ops if op[1] == nat.OP_WGRAD}
+    assert lanes == ({1} if b.side_lane else {0})
+    assert all(op[7] == 0 for op in b.ops if op[1] != nat.OP_WGRAD)
+
+
+def test_struct_layouts_match_native():
+    sizes = nat.load().struct_sizes()
+    for name, st in nat._STRUCTS.items():
+        assert C.sizeof(st) == sizes[name], name
