@@ -36,7 +36,11 @@ struct ConvArgs {
   float* gsumx;       // [Cout] += sum(dZ * xhat)
 };
 
+// tile TILE_HALO selects the one-image-per-workgroup direct 3x3 kernel (conv3x3_halo.hip)
+constexpr int TILE_HALO = 100;
 hipError_t conv_igemm(const ConvArgs& a, int tile, bool a_f32, hipStream_t st);
+bool conv3x3_halo_ok(const ConvArgs& a);
+hipError_t conv3x3_halo(const ConvArgs& a, bool a_f32, hipStream_t st);
 int conv_pick_tile(int M, int Cout);
 int conv_num_tiles();
 int conv_tile_bm(int t);

@@ -473,6 +473,7 @@ hipError_t conv_igemm(const ConvArgs& a, int tile, bool a_f32, hipStream_t st) {
   const int pro = (a.pro.mode != 0 || a.pro.act != ACT_NONE) ? 1 : 0;
   const int epi = a.epi_mode;
   if ((a.Cin % 8) || (a.Cout % 8) || (a.ldx % 8) || (a.ldy % 8)) return hipErrorInvalidValue;
+  if (tile == TILE_HALO) return conv3x3_halo(a, a_f32, st);
   switch (tile) {
     case 0: return launch_cfg<128, 128, 32, 2, 2>(a, is1x1, a_f32, pro, epi, st);
     case 1: return launch_cfg<128, 64, 32, 2, 2>(a, is1x1, a_f32, pro, epi, st);

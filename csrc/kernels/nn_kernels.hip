@@ -99,7 +99,12 @@ __device__ __forceinline__ void flush_sums(float* s_a, float* s_b, int C, float*
 }  // namespace
 
 // ------------------------------------------------------------------------------------------
+// Bandwidth kernel: every thread owns one 8-channel chunk of RU rows per iteration and issues
+// all of its loads before any arithmetic (RU independent 16-B loads in flight per operand), with
+// the destination type / accumulate mode as template parameters so the loop is branch-free.
+template <bool F32, bool ACC>
 __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(BnBwdApplyArgs a) {
+  constexpr int RU = 4;
   extern __shared__ float sh[];
   float* sA = sh;
   float* sB = sh + a.C;
@@ -123,19 +128,68 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(BnBwdApplyArgs a) {
   ChunkMap cm(a.C);
   if (!cm.active()) return;
   const int c = cm.tx * 8;
-  for (int row = blockIdx.x * cm.R + cm.ty; row < a.M; row += gridDim.x * cm.R) {
-    float d[8], x[8], o[8];
-    unpack8(*reinterpret_cast<const uint4*>(a.dz + (size_t)row * a.lddz + c), d);
-    unpack8(*reinterpret_cast<const uint4*>(a.x + (size_t)row * a.ldx + c), x);
+  float ka[8], kb[8], kc[8];
 #pragma unroll
-    for (int j = 0; j < 8; ++j) o[j] = sA[c + j] * d[j] + sB[c + j] * x[j] + sC[c + j];
-    store8(a.dst, a.dst_f32, (size_t)row * a.lddst + c, o, a.accumulate);
+  for (int j = 0; j < 8; ++j) { ka[j] = sA[c + j]; kb[j] = sB[c + j]; kc[j] = sC[c + j]; }
+  const int step = gridDim.x * cm.R;
+  for (int row0 = blockIdx.x * cm.R + cm.ty; row0 < a.M; row0 += step * RU) {
+    uint4 dz[RU], xx[RU];
+    float4 o0[RU], o1[RU];
+    int rows[RU];
+#pragma unroll
+    for (int u = 0; u < RU; ++u) {
+      int r = row0 + u * step;
+      rows[u] = r < a.M ? r : a.M - 1;  // clamped: loads stay unconditional
+      dz[u] = *reinterpret_cast<const uint4*>(a.dz + (size_t)rows[u] * a.lddz + c);
+      xx[u] = *reinterpret_cast<const uint4*>(a.x + (size_t)rows[u] * a.ldx + c);
+      if constexpr (F32 && ACC) {
+        const float* q = reinterpret_cast<const float*>(a.dst) + (size_t)rows[u] * a.lddst + c;
+        o0[u] = *reinterpret_cast<const float4*>(q);
+        o1[u] = *reinterpret_cast<const float4*>(q + 4);
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < RU; ++u) {
+      if (row0 + u * step >= a.M) break;
+      float d[8], x[8], o[8];
+      unpack8(dz[u], d);
+      unpack8(xx[u], x);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) o[j] = ka[j] * d[j] + kb[j] * x[j] + kc[j];
+      if constexpr (F32) {
+        float* q = reinterpret_cast<float*>(a.dst) + (size_t)rows[u] * a.lddst + c;
+        if constexpr (ACC) {
+          o[0] += o0[u].x; o[1] += o0[u].y; o[2] += o0[u].z; o[3] += o0[u].w;
+          o[4] += o1[u].x; o[5] += o1[u].y; o[6] += o1[u].z; o[7] += o1[u].w;
+        }
+        *reinterpret_cast<float4*>(q) = make_float4(o[0], o[1], o[2], o[3]);
+        *reinterpret_cast<float4*>(q + 4) = make_float4(o[4], o[5], o[6], o[7]);
+      } else {
+        bf16_t* q = reinterpret_cast<bf16_t*>(a.dst) + (size_t)rows[u] * a.lddst + c;
+        if constexpr (ACC) {
+          float p[8];
+          unpack8(*reinterpret_cast<const uint4*>(q), p);
+#pragma unroll
+          for (int j = 0; j < 8; ++j) o[j] += p[j];
+        }
+        *reinterpret_cast<uint4*>(q) = pack8(o);
+      }
+    }
   }
 }
 
 hipError_t bn_bwd_apply(const BnBwdApplyArgs& a, hipStream_t st) {
   if (a.M == 0) return hipSuccess;
-  hipLaunchKernelGGL(bn_bwd_apply_kernel, dim3(grid_rows(a.M, a.C)), dim3(256), 3 * a.C * 4, st, a);
+  // ~1 iteration of RU rows per thread: enough blocks to fill all 256 CUs several times over
+  dim3 grid(grid_rows(a.M, a.C, 4)), block(256);
+  size_t shm = 3 * a.C * 4;
+  if (a.dst_f32) {
+    if (a.accumulate) hipLaunchKernelGGL((bn_bwd_apply_kernel<true, true>), grid, block, shm, st, a);
+    else hipLaunchKernelGGL((bn_bwd_apply_kernel<true, false>), grid, block, shm, st, a);
+  } else {
+    if (a.accumulate) hipLaunchKernelGGL((bn_bwd_apply_kernel<false, true>), grid, block, shm, st, a);
+    else hipLaunchKernelGGL((bn_bwd_apply_kernel<false, false>), grid, block, shm, st, a);
+  }
   return hipGetLastError();
 }
 

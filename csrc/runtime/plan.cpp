@@ -132,6 +132,7 @@ class Plan {
   }
 
   int lane(int idx) const { return ops_.at(idx).lane; }
+  void set_side_flush(int n) { side_flush_ = n < 1 ? 1 : n; }
 
   int capture(int begin, int end, uintptr_t stream) {
     hipStream_t st = reinterpret_cast<hipStream_t>(stream);
@@ -182,26 +183,36 @@ class Plan {
     check(hipEventCreateWithFlags(&join_, hipEventDisableTiming), "hipEventCreate(join)");
   }
 
-  // issue ops[begin:end): lane-0 ops on `st`, lane-1 ops on the side stream forked at their
-  // position; one fork per run of side ops that follows main work, one join at the end.
+  // issue ops[begin:end): lane-0 ops on `st`; lane-1 ops are queued and issued on the side
+  // stream in batches — one fork (event record + wait) per batch, placed after the main op that
+  // completes `side_flush_` main ops past the batch's first member (every queued op's producers
+  // precede the fork, and the lowering guarantees no later main op overwrites a side op's
+  // inputs, so deferring is safe) — and one join at the end.  Batching keeps the host API calls
+  // per step low: with direct (non-graph) issue the backward is otherwise host-bound.
   void issue(int begin, int end, hipStream_t st) {
-    bool side_used = false, main_since_fork = true;
+    bool side_used = false;
+    std::vector<int> pending;
+    int main_since = 0;
+    auto flush = [&]() {
+      if (pending.empty()) return;
+      ensure_side();
+      check(hipEventRecord(fork_, st), "hipEventRecord(fork)");
+      check(hipStreamWaitEvent(side_, fork_, 0), "hipStreamWaitEvent(fork)");
+      for (int k : pending) exec(ops_[k], side_);
+      pending.clear();
+      side_used = true;
+    };
     for (int k = begin; k < end; ++k) {
       const Op& op = ops_[k];
       if (op.lane == 1) {
-        ensure_side();
-        if (main_since_fork) {
-          check(hipEventRecord(fork_, st), "hipEventRecord(fork)");
-          check(hipStreamWaitEvent(side_, fork_, 0), "hipStreamWaitEvent(fork)");
-          main_since_fork = false;
-        }
-        exec(op, side_);
-        side_used = true;
+        if (pending.empty()) main_since = 0;
+        pending.push_back(k);
       } else {
         exec(op, st);
-        main_since_fork = true;
+        if (!pending.empty() && ++main_since >= side_flush_) flush();
       }
     }
+    flush();
     if (side_used) {
       check(hipEventRecord(join_, side_), "hipEventRecord(join)");
       check(hipStreamWaitEvent(st, join_, 0), "hipStreamWaitEvent(join)");
@@ -266,6 +277,7 @@ class Plan {
 
   std::vector<Op> ops_;
   hipStream_t side_ = nullptr;
+  int side_flush_ = 1;
   hipEvent_t fork_ = nullptr, join_ = nullptr;
   std::vector<hipGraph_t> graphs_;
   std::vector<hipGraphExec_t> execs_;
@@ -313,6 +325,14 @@ py::dict struct_sizes() {
 }
 
 int py_pick_tile(int M, int Cout) { return conv_pick_tile(M, Cout); }
+
+bool py_halo_ok(py::bytes payload) {
+  std::string s = payload;
+  if (s.size() != sizeof(ConvArgs)) throw std::runtime_error("ConvArgs size mismatch");
+  ConvArgs a;
+  std::memcpy(&a, s.data(), sizeof(a));
+  return conv3x3_halo_ok(a);
+}
 int py_pick_splits(int M, int K, int Cout) { return wgrad_pick_splits(M, K, Cout); }
 
 void py_secagg_mask(uintptr_t x, uintptr_t out, long long n, float scale, float clip, int nclients,
@@ -345,6 +365,7 @@ PYBIND11_MODULE(_idc_native, m) {
       .def("add", &Plan::add, py::arg("kind"), py::arg("payload"), py::arg("ints"), py::arg("floats"),
            py::arg("longs"), py::arg("ptrs"), py::arg("lane") = 0)
       .def("lane", &Plan::lane)
+      .def("set_side_flush", &Plan::set_side_flush)
       .def("set_float", &Plan::set_float)
       .def("set_int", &Plan::set_int)
       .def("get_int", &Plan::get_int)
@@ -360,6 +381,8 @@ PYBIND11_MODULE(_idc_native, m) {
   m.def("wgrad", &py_wgrad);
   m.def("struct_sizes", &struct_sizes);
   m.def("pick_tile", &py_pick_tile);
+  m.def("halo_ok", &py_halo_ok);
+  m.attr("TILE_HALO") = TILE_HALO;
   m.def("pick_splits", &py_pick_splits);
   m.def("num_tiles", &conv_num_tiles);
   m.def("tile_bm", &conv_tile_bm);

@@ -100,7 +100,7 @@ def conv2d(x: torch.Tensor, kernel_hwio: torch.Tensor, stride=(1, 1), pads=(0, 0
 def conv2d_dgrad(dy: torch.Tensor, kernel_hwio: torch.Tensor, in_hw: Tuple[int, int], pads=(0, 0),
                  mx: Optional[torch.Tensor] = None, mbn: Optional[BN] = None,
                  gsum: Optional[torch.Tensor] = None, gsumx: Optional[torch.Tensor] = None,
-                 out_f32: bool = False) -> torch.Tensor:
+                 out_f32: bool = False, tile: int = -1) -> torch.Tensor:
     """Stride-1 data gradient.  With ``mx``/``mbn``: returns dZ = dX * act'(bn(mx)) and
     accumulates sum(dZ) into gsum, sum(dZ*xhat) into gsumx."""
     N, Ho, Wo, Cout = dy.shape
@@ -126,7 +126,7 @@ def conv2d_dgrad(dy: torch.Tensor, kernel_hwio: torch.Tensor, in_hw: Tuple[int, 
         a.gsum, a.gsumx = nat.ptr(gsum), nat.ptr(gsumx)
     else:
         a.out_mode = nat.OUT_F32 if out_f32 else nat.OUT_BF16
-    nat.require().conv(nat.raw(a), -1, 1 if dy.dtype == torch.float32 else 0, nat.stream_handle())
+    nat.require().conv(nat.raw(a), tile, 1 if dy.dtype == torch.float32 else 0, nat.stream_handle())
     return dx
 
 

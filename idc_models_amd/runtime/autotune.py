@@ -57,7 +57,7 @@ def _time_op(plan, i, stream, reps=4) -> float:
     return e0.elapsed_time(e1) / reps
 
 
-def _conv_candidates(ext, M: int, cout: int):
+def _conv_candidates(ext, M: int, cout: int, payload: bytes = None):
     ntile = ext.num_tiles()
     cap = 32 if cout <= 32 else (64 if cout <= 64 else 128)
     out = []
@@ -68,6 +68,8 @@ def _conv_candidates(ext, M: int, cout: int):
         if bm > 64 and M <= 2 * 64:
             continue
         out.append(t)
+    if payload is not None and os.environ.get("IDC_HALO", "0") == "1" and ext.halo_ok(payload):
+        out.append(ext.TILE_HALO)
     return out
 
 
@@ -83,11 +85,12 @@ def autotune_plan(plan, stream, verbose: bool = False) -> int:
             f32 = plan.get_int(i, 1)
             M = a.N * a.Ho * a.Wo
             pro = int(a.pro.mode != 0 or a.pro.act != 0)
-            key = ("conv", M, a.Cout, a.Cin, a.KH, a.KW, a.SH, a.PT, a.ldx, f32, pro, a.epi_mode)
+            key = ("conv", M, a.Cout, a.Cin, a.KH, a.KW, a.SH, a.PT, a.ldx, f32, pro, a.epi_mode,
+                   a.out_mode, int(bool(a.bias)), a.H, a.W)
             best = _CACHE.get(key)
             if best is None:
                 times = {}
-                for t in _conv_candidates(ext, M, a.Cout) or [ext.pick_tile(M, a.Cout)]:
+                for t in _conv_candidates(ext, M, a.Cout, plan.payload(i)) or [ext.pick_tile(M, a.Cout)]:
                     plan.set_int(i, 0, t)
                     times[t] = _time_op(plan, i, stream)
                 best = min(times, key=times.get)

@@ -120,6 +120,9 @@ class Builder:
         self.segment = "fwd"
         self.side_lane = os.environ.get("IDC_SIDE_LANE", "1") != "0"
         self.guard = os.environ.get("IDC_GUARD") == "1"
+        # direct 3x3 kernel (conv3x3_halo.hip): opt-in — ~25% faster per kernel in isolation, but
+        # its 90-150 KB LDS footprint blocks the side-lane wgrads from sharing CUs (net loss)
+        self.use_halo = os.environ.get("IDC_HALO", "0") == "1"
         self.guards: List[tuple] = []
         self.bwd_marks: List[Tuple[int, int]] = []  # (op index, lowest arena param index ready)
         # stats arena is allocated lazily with a generous capacity; views are handed out in order
@@ -177,20 +180,28 @@ class Builder:
             self.bwd_marks.append((len(self.ops), min(idx)))
 
     # ------------------------------------------------------------------ weights
-    def conv_weight(self, layer, cin_pad: Optional[int] = None, need_dgrad: bool = False):
-        """bf16 kernel-layout copies of a Conv2D kernel (cast from the fp32 Keras master)."""
-        key = id(layer)
+    def conv_weight(self, layer, cin_pad: Optional[int] = None, need_dgrad: bool = False,
+                    center: bool = False):
+        """bf16 kernel-layout copies of a Conv2D kernel (cast from the fp32 Keras master).
+        ``center``: only the centre tap of a 3x3 kernel (a 'same' 3x3 conv on a 1x1 image is a 1x1
+        conv with W[1,1] — the other 8 taps only ever multiply zero padding)."""
+        key = (id(layer), center)
         ent = self.conv_weights.get(key)
-        kh, kw = layer.kernel_size
+        kh, kw = (1, 1) if center else layer.kernel_size
         cin, cout = layer.in_ch, layer.filters
         cpad = cin_pad or cin
         if ent is None:
             fwd = self.alloc((cout * kh * kw * cpad,), BF16)
-            ent = {"fwd": fwd, "dgrad": None, "cpad": cpad, "layer": layer}
+            ent = {"fwd": fwd, "dgrad": None, "cpad": cpad, "layer": layer, "center": center}
             self.conv_weights[key] = ent
         if need_dgrad and ent["dgrad"] is None:
             ent["dgrad"] = self.alloc((cin * kh * kw * cout,), BF16)
         return ent
+
+    @staticmethod
+    def is_center_only(layer, H: int, W: int, stride, pads) -> bool:
+        return (tuple(layer.kernel_size) == (3, 3) and H == 1 and W == 1 and tuple(stride) == (1, 1)
+                and tuple(pads) == (1, 1))
 
     def finalize_casts(self):
         trainable_ids = {id(p) for p in self.arena.params}
@@ -200,6 +211,9 @@ class Builder:
             kh, kw = layer.kernel_size
             e = nat.CastEntry()
             e.src = layer.kernel.data_ptr()
+            if ent["center"]:  # HWIO[1][1] is a contiguous (Cin, Cout) block = a 1x1 HWIO kernel
+                e.src += (kw + 1) * layer.in_ch * layer.filters * layer.kernel.element_size()
+                kh, kw = 1, 1
             e.fwd = ent["fwd"].data_ptr()
             e.dgrad = ent["dgrad"].data_ptr() if ent["dgrad"] is not None else 0
             e.KH, e.KW, e.Cin, e.Cout, e.Cpad, e.dw = kh, kw, layer.in_ch, layer.filters, ent["cpad"], 0
@@ -262,12 +276,14 @@ class Builder:
         a.Ho, a.Wo, a.Cout = y.H, y.W, y.C
         a.y, a.ldy = y.ptr, y.ld
         kh, kw = layer.kernel_size if layer is not None else w["k"]
+        center = w is None and self.is_center_only(layer, x.H, x.W, stride, pads)
+        if center:
+            kh, kw, pads = 1, 1, (0, 0)
         a.KH, a.KW = kh, kw
         a.SH, a.SW = stride
         a.PT, a.PL = pads
         if w is None:
-            ent = self.conv_weight(layer, cin_pad=a.Cin)
-            ent["layer"] = layer
+            ent = self.conv_weight(layer, cin_pad=a.Cin, center=center)
             a.w = ent["fwd"].data_ptr()
         else:
             a.w = w["ptr"]
@@ -281,16 +297,24 @@ class Builder:
         a.mbn = act_only(0)
         M = x.N * y.H * y.W
         if tile < 0:
-            tile = nat.load().pick_tile(M, y.C)
+            tile = self._default_tile(a, M, y.C)
         self.emit(nat.OP_CONV, a, ints=(tile, 1 if x.is_f32 else 0))
+
+    def _default_tile(self, a, M: int, cout: int) -> int:
+        ext = nat.load()
+        if self.use_halo and ext.halo_ok(nat.raw(a)):
+            return ext.TILE_HALO
+        return ext.pick_tile(M, cout)
 
     def dgrad(self, dy: Tensor4, layer, dx: Tensor4, *, pads=(0, 0), mx: Optional[Tensor4] = None,
               mbn: Optional[nat.BnArgs] = None, gsum=None, gsumx=None, out_mode=nat.OUT_BF16):
         """Stride-1 data gradient: conv of dy with the flipped kernel; optional BN-backward
         epilogue through the BN+act that produced the forward input ``mx``."""
         kh, kw = layer.kernel_size
-        ent = self.conv_weight(layer, need_dgrad=True)
-        ent["layer"] = layer
+        center = self.is_center_only(layer, dx.H, dx.W, (1, 1), pads)
+        if center:
+            kh, kw, pads = 1, 1, (0, 0)
+        ent = self.conv_weight(layer, need_dgrad=True, center=center)
         a = nat.ConvArgs()
         a.x = dy.ptr
         a.N, a.H, a.W, a.Cin, a.ldx = dy.N, dy.H, dy.W, dy.C, dy.ld
@@ -309,12 +333,19 @@ class Builder:
         else:
             a.epi_mode = 0
             a.out_mode = out_mode
-        tile = nat.load().pick_tile(dx.M, dx.C)
+        tile = self._default_tile(a, dx.M, dx.C)
         self.emit(nat.OP_CONV, a, ints=(tile, 1 if dy.is_f32 else 0))
 
     def wgrad(self, x: Tensor4, layer, g: Tensor4, dw: torch.Tensor, *, stride=(1, 1), pads=(0, 0),
               pro=None, cin_real=0, splits=-1, lane=0):
         kh, kw = layer.kernel_size
+        if self.is_center_only(layer, x.H, x.W, stride, pads):
+            # only the centre tap sees data: its gradient is the 1x1 wgrad; the other taps keep
+            # the zero the gradient arena was cleared to
+            if dw.numel() != kh * kw * layer.in_ch * layer.filters:
+                raise RuntimeError(f"wgrad target of {layer.name} has {dw.numel()} elements")
+            dw = dw.view(kh, kw, layer.in_ch, layer.filters)[1, 1]
+            kh, kw, pads = 1, 1, (0, 0)
         a = nat.WgradArgs()
         a.x = x.ptr
         a.N, a.H, a.W, a.Cin, a.ldx = x.N, x.H, x.W, x.C, x.ld
@@ -330,6 +361,8 @@ class Builder:
             cin_real = layer.in_ch  # channel-padded staged input (first conv): Keras rows only
         if dw.numel() != kh * kw * layer.in_ch * layer.filters:
             raise RuntimeError(f"wgrad target of {layer.name} has {dw.numel()} elements")
+        if not dw.is_contiguous():
+            raise RuntimeError(f"wgrad target of {layer.name} is not contiguous")
         a.cin_real = cin_real
         if splits < 0:
             splits = nat.load().pick_splits(g.M, kh * kw * x.C, g.C)

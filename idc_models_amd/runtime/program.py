@@ -93,6 +93,8 @@ class FusedProgram:
         else:
             self.host_optimizer = False
         self.plan = nat.load().Plan()
+        # side-lane ops are issued in batches every IDC_SIDE_FLUSH main ops (plan.cpp: issue)
+        self.plan.set_side_flush(int(os.environ.get("IDC_SIDE_FLUSH", "8")))
         self.seg: Dict[str, Tuple[int, int]] = {}
         self.rms_index = None
         cur, start = None, 0

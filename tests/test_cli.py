@@ -44,3 +44,31 @@ def test_secure_round(tmp_path, capsys, mode):
     out = capsys.readouterr().out.strip().splitlines()
     assert any("Secure fed model took" in l for l in out)
     assert len([l for l in out if len(l.split()) == 3]) >= 2  # "loss acc auc" per round
+
+
+@pytest.mark.parametrize("name,kind", [("mobilenetv2_cpu", "dist"), ("vgg16_dp8", "dist"),
+                                       ("densenet121_dp8", "dist"), ("fedavg_mobilenetv2_8", "fed"),
+                                       ("secure_densenet121_8", "secure")])
+def test_north_star_configs_are_valid(name, kind):
+    """Every configs/*.yaml key is a field of its recipe's config dataclass."""
+    import dataclasses
+    import os
+    from idc_models_amd.recipes import FedConfig, SecureConfig, TransferConfig
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    with open(os.path.join(root, "configs", name + ".yaml")) as f:
+        cfg = yaml.safe_load(f)
+    cls = {"dist": TransferConfig, "fed": FedConfig, "secure": SecureConfig}[kind]
+    fields = {f.name for f in dataclasses.fields(cls)}
+    assert set(cfg) <= fields, set(cfg) - fields
+    if "input_shape" in cfg:
+        cfg["input_shape"] = tuple(cfg["input_shape"])
+    cls(**cfg)
+
+
+def test_mobilenetv2_cpu_config_runs(tmp_path, capsys):
+    """North-star config 1 end to end on the CPU (shortened: 1 step per phase, synthetic data)."""
+    import os
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    assert main(["dist", "mobile", str(tmp_path), "--synthetic", "--epochs", "1", "--steps-per-epoch", "1",
+                 "--config", os.path.join(root, "configs", "mobilenetv2_cpu.yaml")]) == 0
+    assert "Fine-tuning with 1 devices took" in capsys.readouterr().out

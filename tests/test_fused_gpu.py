@@ -110,7 +110,9 @@ def test_densenet_phase1_frozen_base():
 
 
 def test_densenet_fine_tune_at_150():
-    m, ref, x, y = _setup("densenet121", 8, fine_tune_at=150)
+    # batch 32: at batch 8 the bf16 forward of this random-init net is chaotic (autocast's own
+    # logit deviation from fp32 reaches 0.16), so the comparison would only measure noise
+    m, ref, x, y = _setup("densenet121", 32, fine_tune_at=150)
     _check(m, ref, x, y)
 
 

@@ -118,6 +118,55 @@ def test_conv_prologue_bn_relu_and_stats(fn):
     assert relerr(stats_out[Cout:], (yf * yf).sum((0, 1, 2))) < 1e-3
 
 
+@pytest.mark.parametrize("H", [13, 6, 3, 1])
+def test_conv3x3_halo_fwd_bn_prologue_stats(fn, H):
+    """One-image-per-workgroup direct 3x3 kernel (DenseNet growth conv) == reference conv."""
+    N, Cin, Cout = 5, 128, 32
+    ext = fn.nat.require()
+    x = bf(torch.randn(N, H, H, Cin, device=DEV) * 2 + 0.5)
+    st = torch.cat([x.sum((0, 1, 2)), (x * x).sum((0, 1, 2))])
+    gamma = torch.rand(Cin, device=DEV) + 0.5
+    beta = torch.randn(Cin, device=DEV) * 0.1
+    w = bf(torch.randn(3, 3, Cin, Cout, device=DEV) * 0.05)
+    stats_out = torch.zeros(2 * Cout, device=DEV)
+    cnt = N * H * H
+    y = fn.conv2d(x.to(torch.bfloat16), w, pads=(1, 1), tile=ext.TILE_HALO, stats=stats_out,
+                  pro=fn.BN(stats=st, gamma=gamma, beta=beta, count=cnt, eps=1.001e-5, act=1))
+    ref = ref_conv(bf(bn_ref(x, st, gamma, beta, cnt, 1.001e-5, 1)), w, 1, (1, 1, 1, 1))
+    assert relerr(y, ref) < 1e-2
+    yf = y.float()
+    assert relerr(stats_out[:Cout], yf.sum((0, 1, 2))) < 1e-3
+    assert relerr(stats_out[Cout:], (yf * yf).sum((0, 1, 2))) < 1e-3
+
+
+@pytest.mark.parametrize("H", [13, 6, 3])
+def test_conv3x3_halo_dgrad_fp32_bn_epilogue(fn, H):
+    """dgrad of the growth conv from the fp32 concat gradient, BN-backward epilogue."""
+    N, Cin, Cout = 3, 128, 32
+    ext = fn.nat.require()
+    mx = bf(torch.randn(N, H, H, Cin, device=DEV))
+    st = torch.cat([mx.sum((0, 1, 2)), (mx * mx).sum((0, 1, 2))])
+    gamma = torch.rand(Cin, device=DEV) + 0.5
+    beta = torch.randn(Cin, device=DEV) * 0.1
+    cnt = N * H * H
+    dy = torch.randn(N, H, H, Cout, device=DEV)
+    w = bf(torch.randn(3, 3, Cin, Cout, device=DEV) * 0.1)
+    gsum = torch.zeros(Cin, device=DEV)
+    gsumx = torch.zeros(Cin, device=DEV)
+    dz = fn.conv2d_dgrad(dy, w, (H, H), pads=(1, 1), mx=mx.to(torch.bfloat16), tile=ext.TILE_HALO,
+                         mbn=fn.BN(stats=st, gamma=gamma, beta=beta, count=cnt, eps=1e-3, act=1),
+                         gsum=gsum, gsumx=gsumx)
+    dA = torch.nn.grad.conv2d_input((N, Cin, H, H), w.permute(3, 2, 0, 1), bf(dy).permute(0, 3, 1, 2),
+                                    padding=1).permute(0, 2, 3, 1)
+    mean = st[:Cin] / cnt
+    var = st[Cin:] / cnt - mean ** 2
+    xhat = (mx - mean) * torch.rsqrt(var + 1e-3)
+    dZ = dA * ((xhat * gamma + beta) > 0).float()
+    assert relerr(dz, dZ) < 1e-2
+    assert relerr(gsum, dZ.sum((0, 1, 2))) < 2e-2
+    assert relerr(gsumx, (dZ * xhat).sum((0, 1, 2))) < 2e-2
+
+
 def test_conv_fp32_operand(fn):
     N, H, Cin, Cout = 2, 13, 32, 128
     x = torch.randn(N, H, H, Cin, device=DEV)

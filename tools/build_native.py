@@ -26,6 +26,7 @@ HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 
 SOURCES = [
     "kernels/conv_igemm.hip",
+    "kernels/conv3x3_halo.hip",
     "kernels/conv_wgrad.hip",
     "kernels/nn_kernels.hip",
     "kernels/dwconv.hip",
