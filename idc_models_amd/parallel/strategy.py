@@ -86,9 +86,16 @@ def default_strategy() -> Strategy:
 
 
 class MirroredStrategy(Strategy):
-    def __init__(self, devices=None, bucket_bytes: int = DEFAULT_BUCKET_BYTES, backend=None):
+    def __init__(self, devices=None, bucket_bytes: int = DEFAULT_BUCKET_BYTES, backend=None,
+                 device=None):
+        """``device`` overrides the per-rank device (e.g. several gloo ranks sharing one GPU to
+        rehearse the data-parallel path on a single-GPU machine)."""
         rank, world, local = comm.init_process_group(backend)
-        if torch.cuda.is_available() and (backend in (None, "nccl")):
+        if device is not None:
+            dev = torch.device(device)
+            if dev.type == "cuda":
+                torch.cuda.set_device(dev)
+        elif torch.cuda.is_available() and (backend in (None, "nccl")):
             torch.cuda.set_device(local)
             dev = torch.device("cuda", local)
         else:
@@ -183,6 +190,8 @@ class MirroredStrategy(Strategy):
 
 class CentralStorageStrategy(MirroredStrategy):
     """Params + optimizer state owned by rank 0: reduce -> update on root -> broadcast."""
+
+    central_storage = True
 
     def bucketer(self, arena):
         return None

@@ -254,9 +254,12 @@ class FusedStep:
         if validate:
             self._validate(p, "after fwd")
         strategy = m.strategy
+        world = strategy.num_replicas_in_sync
+        if world > 1 and getattr(strategy, "central_storage", False):
+            return self._central_storage_step(p, validate)
         if "bwd" in p.seg:
             lo, hi = p.seg["bwd"]
-            bucketer = strategy.bucketer(m.arena) if strategy.num_replicas_in_sync > 1 else None
+            bucketer = strategy.bucketer(m.arena) if world > 1 else None
             if bucketer is not None and p.bwd_marks:
                 # backward in bucket-aligned segments: launch each bucket's all-reduce as soon
                 # as its gradients are final, while the remaining backward keeps the GPU busy
@@ -284,6 +287,33 @@ class FusedStep:
         p.run_segment("opt")
         if validate:
             self._validate(p, "after opt")
+        torch.cuda.current_stream(m.device).wait_stream(p.stream)
+        return p.io.loss.reshape(()).clone(), p.io.logits.clone()
+
+    def _central_storage_step(self, p: FusedProgram, validate: bool):
+        """CentralStorageStrategy (``dist_model_tf_dense.py:24``): gradients are reduced to rank 0,
+        only rank 0 owns optimizer state and applies RMSprop, the updated fp32 parameters are
+        broadcast and every rank re-casts its bf16 kernel copies."""
+        import torch.distributed as dist
+        m = self.m
+        st = m.strategy
+        p.run_segment("bwd")
+        with torch.cuda.stream(p.stream):
+            dist.reduce(m.arena.grad, 0, op=dist.ReduceOp.SUM)
+        if "opt" in p.seg:
+            lo, hi = p.seg["opt"]
+            if p.host_optimizer:
+                if st.rank == 0:
+                    with torch.cuda.stream(p.stream):
+                        m.optimizer.step(m.arena, grad_scale=1.0 / st.world)
+                cast_lo = lo
+            else:
+                if st.rank == 0:
+                    p.run_range(lo, p.rms_index + 1, graph=False)
+                cast_lo = p.rms_index + 1
+            with torch.cuda.stream(p.stream):
+                dist.broadcast(m.arena.data, 0)
+            p.run_range(cast_lo, hi, graph=False)
         torch.cuda.current_stream(m.device).wait_stream(p.stream)
         return p.io.loss.reshape(()).clone(), p.io.logits.clone()
 
