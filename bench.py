@@ -24,7 +24,7 @@ import time
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
-STOCK_PYTORCH_IMG_S_PER_GPU = {"densenet121": 9379.3, "vgg16": 58586.2}
+STOCK_PYTORCH_IMG_S_PER_GPU = {"densenet121": 9379.3, "vgg16": 58586.2, "mobilenetv2": 19653.8}
 
 
 def main():

@@ -1,4 +1,4 @@
-"""In-situ comparison point: stock PyTorch-ROCm DenseNet-121 / VGG16 training step.
+"""In-situ comparison point: stock PyTorch-ROCm DenseNet-121 / VGG16 / MobileNetV2 training step.
 
 BASELINE.md: the reference publishes no numbers, so the point to beat is "stock PyTorch-ROCm
 (MIOpen convolutions, bf16 autocast, channels_last)" on the same MI355X and config.  This is a
@@ -67,6 +67,45 @@ def vgg16():
     return nn.Sequential(*layers)
 
 
+def _div8(v):
+    n = max(8, int(v + 4) // 8 * 8)
+    return n + 8 if n < 0.9 * v else n
+
+
+class InvRes(nn.Module):
+    def __init__(self, cin, cout, stride, t):
+        super().__init__()
+        ch = cin * t
+        layers = []
+        if t != 1:
+            layers += [nn.Conv2d(cin, ch, 1, bias=False), nn.BatchNorm2d(ch, eps=1e-3, momentum=1e-3), nn.ReLU6()]
+        pad = (1, 1, 1, 1) if stride == 1 else (0, 1, 0, 1)
+        layers += [nn.ZeroPad2d(pad), nn.Conv2d(ch, ch, 3, stride, groups=ch, bias=False),
+                   nn.BatchNorm2d(ch, eps=1e-3, momentum=1e-3), nn.ReLU6(),
+                   nn.Conv2d(ch, cout, 1, bias=False), nn.BatchNorm2d(cout, eps=1e-3, momentum=1e-3)]
+        self.body = nn.Sequential(*layers)
+        self.res = stride == 1 and cin == cout
+
+    def forward(self, x):
+        y = self.body(x)
+        return x + y if self.res else y
+
+
+def mobilenetv2():
+    cfg = [(16, 1, 1), (24, 2, 6), (24, 1, 6), (32, 2, 6), (32, 1, 6), (32, 1, 6), (64, 2, 6), (64, 1, 6),
+           (64, 1, 6), (64, 1, 6), (96, 1, 6), (96, 1, 6), (96, 1, 6), (160, 2, 6), (160, 1, 6),
+           (160, 1, 6), (320, 1, 6)]
+    layers = [nn.ZeroPad2d((0, 1, 0, 1)), nn.Conv2d(3, 32, 3, 2, bias=False),
+              nn.BatchNorm2d(32, eps=1e-3, momentum=1e-3), nn.ReLU6()]
+    cin = 32
+    for c, s, t in cfg:
+        layers.append(InvRes(cin, _div8(c), s, t))
+        cin = _div8(c)
+    layers += [nn.Conv2d(cin, 1280, 1, bias=False), nn.BatchNorm2d(1280, eps=1e-3, momentum=1e-3),
+               nn.ReLU6(), nn.AdaptiveAvgPool2d(1), nn.Flatten(), nn.Linear(1280, 1)]
+    return nn.Sequential(*layers)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--model", default="densenet121")
@@ -77,7 +116,7 @@ def main():
     args = ap.parse_args()
     dev = torch.device("cuda")
     torch.backends.cudnn.benchmark = True
-    model = (DenseNet121() if args.model == "densenet121" else vgg16()).to(dev)
+    model = {"densenet121": DenseNet121, "vgg16": vgg16, "mobilenetv2": mobilenetv2}[args.model]().to(dev)
     fmt = torch.contiguous_format if args.no_channels_last else torch.channels_last
     model = model.to(memory_format=fmt)
     opt = torch.optim.RMSprop(model.parameters(), lr=1e-4, alpha=0.9, eps=1e-7)

@@ -17,9 +17,13 @@ struct DwArgs {
   const bf16_t* dy; int lddy;
   bf16_t* dx; int lddx;
   float* gsum; float* gsumx;
-  // wgrad
+  // wgrad: dw += sum over pixels; with a workspace (ws, >= dwconv_wgrad_ws_floats() floats)
+  // the reduction is two-stage (per-block partials + column sums) instead of global atomics
   float* dw;
+  float* ws;
 };
+
+long long dwconv_wgrad_ws_floats(long long M, int C, int taps);
 
 hipError_t dwconv_fwd(const DwArgs& a, hipStream_t st);
 hipError_t dwconv_bwd_data(const DwArgs& a, hipStream_t st);

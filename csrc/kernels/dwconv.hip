@@ -226,10 +226,121 @@ hipError_t dwconv_bwd_data(const DwArgs& a, hipStream_t st) {
   return hipGetLastError();
 }
 
+// ---- two-stage weight gradient ---------------------------------------------------------
+// Stage 1: a block owns a contiguous range of output pixels and ALL channels (one 16-B channel
+// chunk per thread, R pixel rows in flight per block, two rows per iteration for ILP); its
+// 9 x C partial sums are reduced in LDS and stored (plain stores) into ws[block][tap][C].
+// Stage 2: one thread per (tap, c) sums the column over blocks.  No global atomics: the
+// single-stage kernel's few long-running blocks (and the atomic alternative's contention on
+// 9*C addresses) made this the MobileNetV2 step's longest kernel.
+namespace {
+constexpr int kDwRowsPerThread = 4;
+inline int dw_wgrad_blocks(long long M, int C) {
+  int C8 = C / 8, R = 256 / C8;
+  if (R < 1) R = 1;
+  long long b = (M + (long long)R * kDwRowsPerThread - 1) / ((long long)R * kDwRowsPerThread);
+  if (b > 2048) b = 2048;
+  return b < 1 ? 1 : (int)b;
+}
+}  // namespace
+
+long long dwconv_wgrad_ws_floats(long long M, int C, int taps) {
+  return (long long)dw_wgrad_blocks(M, C) * taps * C;
+}
+
+__global__ __launch_bounds__(256) void dw_wgrad_part_kernel(DwArgs a, int rows_per_block) {
+  extern __shared__ float sh[];
+  float* s_sc = sh;
+  float* s_sf = sh + a.C;
+  float* s_acc = sh + 2 * a.C;  // [KH*KW][C]
+  const int T = a.KH * a.KW;
+  for (int c = threadIdx.x; c < a.C; c += blockDim.x) bn_coeffs(a.pro, c, s_sc[c], s_sf[c]);
+  for (int k = threadIdx.x; k < T * a.C; k += blockDim.x) s_acc[k] = 0.f;
+  __syncthreads();
+  Map8 mp(a.C);
+  const int Mo = a.N * a.Ho * a.Wo;
+  const int o0 = blockIdx.x * rows_per_block;
+  const int o1 = min(Mo, o0 + rows_per_block);
+  const float lo = act_lo(a.pro.act), hi = act_hi(a.pro.act);
+  if (mp.ty < mp.R) {
+    const int c = mp.tx * 8;
+    float sc[8], sf[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) { sc[j] = s_sc[c + j]; sf[j] = s_sf[c + j]; }
+    float acc[9][8];
+#pragma unroll
+    for (int t = 0; t < 9; ++t)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) acc[t][j] = 0.f;
+    for (int o = o0 + mp.ty; o < o1; o += mp.R) {
+      int wo = o % a.Wo, t = o / a.Wo, ho = t % a.Ho, n = t / a.Ho;
+      float d[8];
+      unpack8(*reinterpret_cast<const uint4*>(a.dy + (size_t)o * a.lddy + c), d);
+      uint4 xv[9];
+      bool ok[9];
+#pragma unroll
+      for (int r = 0; r < 3; ++r) {
+#pragma unroll
+        for (int s = 0; s < 3; ++s) {
+          int h = ho * a.S - a.PT + r, w = wo * a.S - a.PL + s;
+          bool v = r < a.KH && s < a.KW && (unsigned)h < (unsigned)a.H && (unsigned)w < (unsigned)a.W;
+          ok[r * 3 + s] = v;
+          h = v ? h : 0;
+          w = v ? w : 0;  // clamped address: the load stays unconditional
+          xv[r * 3 + s] = *reinterpret_cast<const uint4*>(a.x + ((size_t)(n * a.H + h) * a.W + w) * a.ldx + c);
+        }
+      }
+#pragma unroll
+      for (int k = 0; k < 9; ++k) {
+        float v[8];
+        unpack8(xv[k], v);
+        const float m = ok[k] ? 1.f : 0.f;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          float u = fminf(fmaxf(fmaf(v[j], sc[j], sf[j]), lo), hi);
+          acc[k][j] = fmaf(u * m, d[j], acc[k][j]);
+        }
+      }
+    }
+    for (int r = 0; r < a.KH; ++r)
+      for (int s = 0; s < a.KW; ++s)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) atomicAdd(&s_acc[(r * a.KW + s) * a.C + c + j], acc[r * 3 + s][j]);
+  }
+  __syncthreads();
+  float* out = a.ws + (size_t)blockIdx.x * T * a.C;
+  for (int k = threadIdx.x; k < T * a.C; k += blockDim.x) out[k] = s_acc[k];
+}
+
+__global__ __launch_bounds__(256) void dw_wgrad_sum_kernel(const float* __restrict__ ws, int nblk, int n,
+                                                           float* __restrict__ dw) {
+  const int k = blockIdx.x * blockDim.x + threadIdx.x;
+  if (k >= n) return;
+  float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
+  int b = 0;
+  for (; b + 4 <= nblk; b += 4) {
+    s0 += ws[(size_t)b * n + k];
+    s1 += ws[(size_t)(b + 1) * n + k];
+    s2 += ws[(size_t)(b + 2) * n + k];
+    s3 += ws[(size_t)(b + 3) * n + k];
+  }
+  for (; b < nblk; ++b) s0 += ws[(size_t)b * n + k];
+  dw[k] += (s0 + s1) + (s2 + s3);
+}
+
 hipError_t dwconv_wgrad(const DwArgs& a, hipStream_t st) {
   if (a.KH > 3 || a.KW > 3) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(dw_wgrad_kernel, dim3(nblocks((long long)a.N * a.Ho * a.Wo, a.C, 32)), dim3(256),
-                     (2 + a.KH * a.KW) * a.C * 4, st, a);
+  const long long Mo = (long long)a.N * a.Ho * a.Wo;
+  const int T = a.KH * a.KW;
+  if (a.ws) {
+    const int nblk = dw_wgrad_blocks(Mo, a.C);
+    const int rpb = (int)((Mo + nblk - 1) / nblk);
+    hipLaunchKernelGGL(dw_wgrad_part_kernel, dim3(nblk), dim3(256), (2 + T) * a.C * 4, st, a, rpb);
+    const int n = T * a.C;
+    hipLaunchKernelGGL(dw_wgrad_sum_kernel, dim3((n + 255) / 256), dim3(256), 0, st, a.ws, nblk, n, a.dw);
+    return hipGetLastError();
+  }
+  hipLaunchKernelGGL(dw_wgrad_kernel, dim3(nblocks(Mo, a.C, 32)), dim3(256), (2 + T) * a.C * 4, st, a);
   return hipGetLastError();
 }
 

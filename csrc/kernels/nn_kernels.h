@@ -96,7 +96,10 @@ hipError_t head_fwd(const HeadArgs& a, hipStream_t st);
 hipError_t head_bwd(const HeadBwdArgs& a, hipStream_t st);
 hipError_t zero_fill(void* p, long long nbytes, hipStream_t st);
 hipError_t rmsprop(float* w, const float* g, float* ms, long long n, float lr, float rho,
-                   float eps, float grad_scale, hipStream_t st);
+                   float eps, float grad_scale, const int* skip, hipStream_t st);
+hipError_t finite_check(const float* g, long long n, int* flag, hipStream_t st);
+// status[0] = flag (last step skipped?), status[1] += flag (skipped steps), flag = 0
+hipError_t finite_flag_reset(int* flag, int* status, hipStream_t st);
 hipError_t cast_weights(const CastEntry* d_entries, int n, long long total, hipStream_t st);
 hipError_t input_stage(const void* x, int x_u8, int N, int H, int W, int C, bf16_t* y, int Cpad,
                        hipStream_t st);

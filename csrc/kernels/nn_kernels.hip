@@ -244,7 +244,7 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(BnBwdReduceArgs a) {
 
 hipError_t bn_bwd_reduce(const BnBwdReduceArgs& a, hipStream_t st) {
   if (a.M == 0) return hipSuccess;
-  hipLaunchKernelGGL(bn_bwd_reduce_kernel, dim3(grid_rows(a.M, a.C, 16)), dim3(256), 6 * a.C * 4, st, a);
+  hipLaunchKernelGGL(bn_bwd_reduce_kernel, dim3(grid_rows(a.M, a.C, 4)), dim3(256), 6 * a.C * 4, st, a);
   return hipGetLastError();
 }
 
@@ -552,7 +552,9 @@ hipError_t head_bwd(const HeadBwdArgs& a, hipStream_t st) {
 // ------------------------------------------------------------------------------------------
 __global__ __launch_bounds__(256) void rmsprop_kernel(float* __restrict__ w, const float* __restrict__ g,
                                                       float* __restrict__ ms, long long n4, float lr,
-                                                      float rho, float eps, float gs) {
+                                                      float rho, float eps, float gs,
+                                                      const int* __restrict__ skip) {
+  if (skip && *skip) return;  // non-finite gradients this step: keep weights and slots unchanged
   for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n4;
        i += (long long)gridDim.x * blockDim.x) {
     float4 gv = reinterpret_cast<const float4*>(g)[i];
@@ -594,14 +596,46 @@ hipError_t zero_fill(void* p, long long nbytes, hipStream_t st) {
   return hipGetLastError();
 }
 
+// any non-finite value in g[0:n) -> *flag = 1 (the flag is cleared at the start of backward)
+__global__ __launch_bounds__(256) void finite_check_kernel(const float* __restrict__ g, long long n4,
+                                                           int* __restrict__ flag) {
+  int bad = 0;
+  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n4;
+       i += (long long)gridDim.x * blockDim.x) {
+    float4 v = reinterpret_cast<const float4*>(g)[i];
+    bad |= !isfinite(v.x) | !isfinite(v.y) | !isfinite(v.z) | !isfinite(v.w);
+  }
+  if (__any(bad) && (threadIdx.x & 63) == 0) atomicOr(flag, 1);
+}
+
+hipError_t finite_check(const float* g, long long n, int* flag, hipStream_t st) {
+  long long n4 = n / 4;
+  long long blocks = (n4 + 255) / 256;
+  if (blocks > 2048) blocks = 2048;
+  if (blocks < 1) blocks = 1;
+  hipLaunchKernelGGL(finite_check_kernel, dim3((int)blocks), dim3(256), 0, st, g, n4, flag);
+  return hipGetLastError();
+}
+
+__global__ void finite_flag_reset_kernel(int* flag, int* status) {
+  status[0] = flag[0];
+  status[1] += flag[0];  // running count of skipped steps
+  flag[0] = 0;
+}
+
+hipError_t finite_flag_reset(int* flag, int* status, hipStream_t st) {
+  hipLaunchKernelGGL(finite_flag_reset_kernel, dim3(1), dim3(1), 0, st, flag, status);
+  return hipGetLastError();
+}
+
 hipError_t rmsprop(float* w, const float* g, float* ms, long long n, float lr, float rho, float eps,
-                   float grad_scale, hipStream_t st) {
+                   float grad_scale, const int* skip, hipStream_t st) {
   long long n4 = n / 4;  // arena sizes are multiples of 64 elements
   long long blocks = (n4 + 255) / 256;
   if (blocks > 8192) blocks = 8192;
   if (blocks < 1) blocks = 1;
   hipLaunchKernelGGL(rmsprop_kernel, dim3((int)blocks), dim3(256), 0, st, w, g, ms, n4, lr, rho, eps,
-                     grad_scale);
+                     grad_scale, skip);
   return hipGetLastError();
 }
 

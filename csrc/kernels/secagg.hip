@@ -29,7 +29,7 @@ __device__ __forceinline__ uint32_t philox(uint32_t c0, uint32_t c1, uint32_t c2
 
 __global__ void secagg_mask_kernel(const float* __restrict__ x, uint32_t* __restrict__ out, long long n,
                                    float scale, float clip, int K, int rank, unsigned long long seed,
-                                   unsigned long long rnd) {
+                                   unsigned long long rnd, unsigned long long alive) {
   for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n;
        i += (long long)gridDim.x * blockDim.x) {
     float v = x[i] * scale;
@@ -37,7 +37,7 @@ __global__ void secagg_mask_kernel(const float* __restrict__ x, uint32_t* __rest
     int32_t q = (int32_t)rintf(v);
     uint32_t acc = (uint32_t)q;
     for (int j = 0; j < K; ++j) {
-      if (j == rank) continue;
+      if (j == rank || !((alive >> j) & 1ull)) continue;  // dropped clients: re-keyed round
       int lo = j < rank ? j : rank, hi = j < rank ? rank : j;
       uint32_t k0 = (uint32_t)seed ^ (uint32_t)(lo * 0x9E3779B1u);
       uint32_t k1 = (uint32_t)(seed >> 32) ^ (uint32_t)(hi * 0x85EBCA77u);
@@ -56,12 +56,14 @@ __global__ void secagg_unmask_kernel(const uint32_t* __restrict__ s, float* __re
 }
 
 hipError_t secagg_quantize_mask(const float* x, uint32_t* out, long long n, float scale, float clip, int K,
-                                int rank, unsigned long long seed, unsigned long long rnd, hipStream_t st) {
+                                int rank, unsigned long long seed, unsigned long long rnd, unsigned long long alive,
+                                hipStream_t st) {
+  if (K > 64) return hipErrorInvalidValue;
   long long b = (n + 255) / 256;
   if (b > 8192) b = 8192;
   if (b < 1) b = 1;
   hipLaunchKernelGGL(secagg_mask_kernel, dim3((int)b), dim3(256), 0, st, x, out, n, scale, clip, K, rank, seed,
-                     rnd);
+                     rnd, alive);
   return hipGetLastError();
 }
 

@@ -63,6 +63,7 @@ enum OpKind : int {
   OP_DW_BWD_DATA = 17,
   OP_DW_WGRAD = 18,
   OP_COPY = 19,
+  OP_FINITE_CHECK = 20,
 };
 
 struct Op {
@@ -170,9 +171,9 @@ class Plan {
     static const char* names[] = {"conv", "wgrad", "bn_bwd_apply", "bn_bwd_reduce", "maxpool", "avgpool",
                                   "pool_bwd", "bn_moving", "head_fwd", "head_bwd", "rmsprop", "cast",
                                   "input", "memset", "bn_stats", "bn_apply", "dw_fwd", "dw_bwd_data",
-                                  "dw_wgrad", "copy"};
+                                  "dw_wgrad", "copy", "finite_check"};
     int k = ops_.at(idx).kind;
-    return (k >= 0 && k < 20) ? names[k] : "?";
+    return (k >= 0 && k < 21) ? names[k] : "?";
   }
 
  private:
@@ -236,7 +237,8 @@ class Plan {
       case OP_HEAD_BWD: check(head_bwd(as<HeadBwdArgs>(op), st), "head_bwd"); break;
       case OP_RMSPROP:
         check(rmsprop(reinterpret_cast<float*>(op.p[0]), reinterpret_cast<const float*>(op.p[1]),
-                      reinterpret_cast<float*>(op.p[2]), op.l[0], op.f[0], op.f[1], op.f[2], op.f[3], st),
+                      reinterpret_cast<float*>(op.p[2]), op.l[0], op.f[0], op.f[1], op.f[2], op.f[3],
+                      reinterpret_cast<const int*>(op.p[3]), st),
               "rmsprop");
         break;
       case OP_CAST:
@@ -266,6 +268,14 @@ class Plan {
       case OP_DW_FWD: check(dwconv_fwd(as<DwArgs>(op), st), "dwconv_fwd"); break;
       case OP_DW_BWD_DATA: check(dwconv_bwd_data(as<DwArgs>(op), st), "dwconv_bwd_data"); break;
       case OP_DW_WGRAD: check(dwconv_wgrad(as<DwArgs>(op), st), "dwconv_wgrad"); break;
+      case OP_FINITE_CHECK:
+        if (op.i[0] == 0)
+          check(finite_check(reinterpret_cast<const float*>(op.p[0]), op.l[0], reinterpret_cast<int*>(op.p[1]), st),
+                "finite_check");
+        else
+          check(finite_flag_reset(reinterpret_cast<int*>(op.p[1]), reinterpret_cast<int*>(op.p[2]), st),
+                "finite_flag_reset");
+        break;
       case OP_COPY:
         check(hipMemcpyAsync(reinterpret_cast<void*>(op.p[0]), reinterpret_cast<const void*>(op.p[1]),
                              (size_t)op.l[0], hipMemcpyDeviceToDevice, st),
@@ -336,9 +346,10 @@ bool py_halo_ok(py::bytes payload) {
 int py_pick_splits(int M, int K, int Cout) { return wgrad_pick_splits(M, K, Cout); }
 
 void py_secagg_mask(uintptr_t x, uintptr_t out, long long n, float scale, float clip, int nclients,
-                    int rank, unsigned long long seed, unsigned long long round_, uintptr_t stream) {
+                    int rank, unsigned long long seed, unsigned long long round_, unsigned long long alive,
+                    uintptr_t stream) {
   check(secagg_quantize_mask(reinterpret_cast<const float*>(x), reinterpret_cast<uint32_t*>(out), n, scale, clip,
-                             nclients, rank, seed, round_, reinterpret_cast<hipStream_t>(stream)),
+                             nclients, rank, seed, round_, alive, reinterpret_cast<hipStream_t>(stream)),
         "secagg_quantize_mask");
 }
 
@@ -352,7 +363,7 @@ void py_secagg_unmask(uintptr_t sum, uintptr_t out, long long n, float scale, in
 void py_rmsprop(uintptr_t w, uintptr_t g, uintptr_t ms, long long n, float lr, float rho, float eps, float gs,
                 uintptr_t stream) {
   check(rmsprop(reinterpret_cast<float*>(w), reinterpret_cast<const float*>(g), reinterpret_cast<float*>(ms), n,
-                lr, rho, eps, gs, reinterpret_cast<hipStream_t>(stream)),
+                lr, rho, eps, gs, nullptr, reinterpret_cast<hipStream_t>(stream)),
         "rmsprop");
 }
 
@@ -382,6 +393,7 @@ PYBIND11_MODULE(_idc_native, m) {
   m.def("struct_sizes", &struct_sizes);
   m.def("pick_tile", &py_pick_tile);
   m.def("halo_ok", &py_halo_ok);
+  m.def("dw_wgrad_ws_floats", &dwconv_wgrad_ws_floats);
   m.attr("TILE_HALO") = TILE_HALO;
   m.def("pick_splits", &py_pick_splits);
   m.def("num_tiles", &conv_num_tiles);

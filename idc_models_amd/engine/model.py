@@ -141,11 +141,13 @@ class Model:
 
     # ------------------------------------------------------------------ compile
     def compile(self, optimizer="rmsprop", loss="binary_crossentropy", metrics=("accuracy",),
-                keras_compat_accuracy: bool = False, backend: str = "auto", **backend_opts):
+                keras_compat_accuracy: bool = False, backend: str = "auto", skip_nonfinite: bool = False,
+                **backend_opts):
         """(Re)compile: fresh optimizer state and a fresh arena over the current trainable set
         (Keras recompile semantics after changing ``trainable``, ``dist_model_tf_vgg.py:148-154``)."""
         self._release_impl()
         self.optimizer = optim_mod.get(optimizer)
+        self.optimizer.skip_nonfinite = skip_nonfinite  # skip updates with inf/nan gradients
         self.loss = losses_mod.get(loss)
         self.keras_compat_accuracy = keras_compat_accuracy
         self.metric_specs = list(metrics or [])
@@ -153,9 +155,18 @@ class Model:
         self.arena = ParamArena(params, device=self.device)
         self.optimizer.bind(self.arena)
         self.backend = backend
-        self.backend_opts = backend_opts
+        self.backend_opts = dict(backend_opts)
+        if skip_nonfinite:
+            self.backend_opts["skip_nonfinite"] = True
         self.impl = self._make_impl(backend)
         return self
+
+    def skipped_steps(self) -> int:
+        """Number of training steps skipped for non-finite gradients (``skip_nonfinite=True``)."""
+        n = self.optimizer.skipped if self.optimizer is not None else 0
+        if self.impl is not None and hasattr(self.impl, "skipped_steps"):
+            n += self.impl.skipped_steps()
+        return n
 
     def reset_optimizer(self):
         """Fresh optimizer slot state without re-lowering (TFF re-creates the client optimizer

@@ -37,6 +37,17 @@ class Optimizer:
     def get_config(self):
         return {"name": self.name, "learning_rate": self.learning_rate}
 
+    # non-finite guard (SURVEY §5 failure detection): skip the whole update when any (reduced)
+    # gradient is inf/nan; the fused backend does the same check on the device
+    skip_nonfinite = False
+    skipped = 0
+
+    def _should_skip(self, arena) -> bool:
+        if self.skip_nonfinite and not bool(torch.isfinite(arena.grad).all()):
+            self.skipped += 1
+            return True
+        return False
+
     def state_tensors(self):
         return {}
 
@@ -68,6 +79,8 @@ class RMSprop(Optimizer):
 
     def step(self, arena=None, lr=None, grad_scale: float = 1.0):
         arena = arena or self._arena
+        if self._should_skip(arena):
+            return
         lr = self.learning_rate if lr is None else lr
         w, g = arena.data, arena.grad
         if w.is_cuda and self.momentum == 0 and not self.centered:
@@ -113,6 +126,8 @@ class SGD(Optimizer):
 
     def step(self, arena=None, lr=None, grad_scale: float = 1.0):
         arena = arena or self._arena
+        if self._should_skip(arena):
+            return
         lr = self.learning_rate if lr is None else lr
         g = arena.grad * grad_scale if grad_scale != 1.0 else arena.grad
         if self.buf is not None:

@@ -98,10 +98,15 @@ class FedAvgProcess:
         _load_into(m, weights)
 
     # -------------------------------------------------------------- round
-    def next(self, state: ServerState, federated_train_data: Sequence):
+    def next(self, state: ServerState, federated_train_data: Sequence, participating=None):
+        """One round.  ``participating``: indices of the clients that report this round (default
+        all) — absent clients simply carry no weight, as in TFF's sampled rounds."""
         m = self.worker()
         rank, world = comm.rank(), comm.world_size()
         mine = assign_clients(len(federated_train_data), rank, world)
+        if participating is not None:
+            keep = set(int(k) for k in participating)
+            mine = [k for k in mine if k in keep]
         dev = state.model.trainable[0].device if state.model.trainable else m.device
         flat_server = torch.cat([w.reshape(-1) for w in state.model.trainable]).to(m.device)
         delta_sum = torch.zeros_like(flat_server)

@@ -57,17 +57,34 @@ def default_clip(nclients: int) -> float:
     return float((2 ** 31 - 1) // max(nclients, 1))
 
 
+def _alive_mask(nclients: int, participants) -> int:
+    if participants is None:
+        return (1 << nclients) - 1
+    m = 0
+    for j in participants:
+        m |= 1 << int(j)
+    return m
+
+
 def mask_quantize(x: torch.Tensor, scale: float, nclients: int, rank: int, seed: int, round_: int,
-                  clip: float = None) -> torch.Tensor:
-    """Fixed-point quantise ``x`` and add this client's pairwise masks -> int32 tensor."""
+                  clip: float = None, participants=None) -> torch.Tensor:
+    """Fixed-point quantise ``x`` and add this client's pairwise masks -> int32 tensor.
+
+    ``participants``: the clients taking part in this round (default: all).  Masks are only
+    exchanged between participants, so when a client drops out before masking the round is
+    re-keyed among the survivors and their masks still cancel exactly."""
+    if nclients > 64:
+        raise ValueError("secure aggregation supports at most 64 clients per round")
     clip = default_clip(nclients) if clip is None else clip
+    alive = _alive_mask(nclients, participants)
     x = x.reshape(-1).contiguous().float()
     n = x.numel()
     if x.is_cuda:
         from ..ops import _native as nat
         out = torch.empty(n, dtype=torch.int32, device=x.device)
         nat.require().secagg_mask(x.data_ptr(), out.data_ptr(), n, float(scale), float(clip), int(nclients),
-                                  int(rank), int(seed) & ((1 << 64) - 1), int(round_), nat.stream_handle())
+                                  int(rank), int(seed) & ((1 << 64) - 1), int(round_), alive,
+                                  nat.stream_handle())
         return out
     q = _quantize(x, scale, clip).numpy().view(np.uint32).astype(np.uint64)
     idx = np.arange(n, dtype=np.uint64)
@@ -75,7 +92,7 @@ def mask_quantize(x: torch.Tensor, scale: float, nclients: int, rank: int, seed:
     c1 = idx >> np.uint64(32)
     acc = q
     for j in range(nclients):
-        if j == rank:
+        if j == rank or not (alive >> j) & 1:
             continue
         lo, hi = min(j, rank), max(j, rank)
         k0, k1 = _pair_keys(int(seed), lo, hi)

@@ -100,9 +100,18 @@ class SecureFederatedProcess:
         self._swap_out(k)
         return h
 
-    def aggregate(self) -> List[torch.Tensor]:
-        """Unweighted mean of every weight tensor over all K clients (secure_fed_model.py:160-168)."""
+    def aggregate(self, dropped=()) -> List[torch.Tensor]:
+        """Unweighted mean of every weight tensor over the participating clients
+        (secure_fed_model.py:160-168).  ``dropped``: clients that dropped out of this round before
+        sending — the mean is over the survivors and the pairwise masks are re-keyed among them
+        (the reference has no dropout handling at all)."""
         from ..utils.timer import Timer
+        dropped = set(int(k) for k in dropped)
+        self.alive = [k for k in range(self.K) if k not in dropped]
+        if not self.alive:
+            raise RuntimeError("every client dropped out of the round")
+        mine = [k for k in self.mine if k not in dropped]
+        n_alive = len(self.alive)
         shapes = [w.shape for w in self.states[self.mine[0]].weights] if self.mine else \
             [t.shape for t in self.m.net.weights]
         n_prot = int(len(shapes) * self.percent)
@@ -110,25 +119,25 @@ class SecureFederatedProcess:
         prot_sizes = [int(torch.Size(s).numel()) for s in shapes[:n_prot]]
         plain_sizes = [int(torch.Size(s).numel()) for s in shapes[n_prot:]]
         plain_sum = torch.zeros(sum(plain_sizes), device=dev)
-        for k in self.mine:
+        for k in mine:
             ws = self.states[k].weights
             if plain_sizes:
                 plain_sum += torch.cat([w.reshape(-1).to(dev) for w in ws[n_prot:]])
         comm.all_reduce_(plain_sum)
-        plain_mean = plain_sum / self.K
+        plain_mean = plain_sum / n_alive
         prot_mean = torch.zeros(sum(prot_sizes), device=dev)
         if n_prot:
             with Timer("Encryption/aggregation", self.printer if self.verbose else None):
                 if self.mode == "mask":
-                    prot_mean = self._masked_mean(n_prot, sum(prot_sizes), dev)
+                    prot_mean = self._masked_mean(n_prot, sum(prot_sizes), dev, mine)
                 elif self.mode == "paillier":
-                    prot_mean = self._paillier_mean(n_prot, dev)
+                    prot_mean = self._paillier_mean(n_prot, dev, mine)
                 else:
                     s = torch.zeros(sum(prot_sizes), device=dev)
-                    for k in self.mine:
+                    for k in mine:
                         s += torch.cat([w.reshape(-1).to(dev) for w in self.states[k].weights[:n_prot]])
                     comm.all_reduce_(s)
-                    prot_mean = s / self.K
+                    prot_mean = s / n_alive
         flat = torch.cat([prot_mean, plain_mean])
         out, off = [], 0
         for s in shapes:
@@ -137,37 +146,40 @@ class SecureFederatedProcess:
             off += n
         return out
 
-    def _masked_mean(self, n_prot: int, n: int, dev) -> torch.Tensor:
-        vecs = {k: torch.cat([w.reshape(-1).to(dev) for w in self.states[k].weights[:n_prot]]) for k in self.mine}
+    def _masked_mean(self, n_prot: int, n: int, dev, mine) -> torch.Tensor:
+        vecs = {k: torch.cat([w.reshape(-1).to(dev) for w in self.states[k].weights[:n_prot]]) for k in mine}
         mx = max([float(v.abs().max()) for v in vecs.values()] or [0.0])
         mx = comm.all_reduce_max(mx, dev) if self.world > 1 else mx
         scale = secagg.choose_scale(mx, self.K)
         total = torch.zeros(n, dtype=torch.int64, device=dev)
         for k, v in vecs.items():
-            masked = secagg.mask_quantize(v, scale, self.K, k, seed=self.seed + 7919, round_=self.round)
+            masked = secagg.mask_quantize(v, scale, self.K, k, seed=self.seed + 7919, round_=self.round,
+                                          participants=self.alive)
             total = (total + masked.to(dev).to(torch.int64)) % (1 << 32)
         t32 = torch.where(total >= (1 << 31), total - (1 << 32), total).to(torch.int32)
         comm.all_reduce_(t32)  # int32 SUM wraps mod 2^32 on RCCL / gloo
-        return secagg.unmask_mean(t32, scale, self.K, float(self.K)).to(dev)
+        return secagg.unmask_mean(t32, scale, self.K, float(len(self.alive))).to(dev)
 
-    def _paillier_mean(self, n_prot: int, dev) -> torch.Tensor:
+    def _paillier_mean(self, n_prot: int, dev, mine) -> torch.Tensor:
         from .paillier import decrypt_vector, encrypt_vector, sum_ciphertexts
         if self.world > 1:
             raise NotImplementedError("Paillier parity mode runs single-process (as the reference)")
         scale = float(2 ** 24)
         cts = []
-        for k in self.mine:
+        for k in mine:
             v = torch.cat([w.reshape(-1).float().cpu() for w in self.states[k].weights[:n_prot]])
             cts.append(encrypt_vector(self.pub, v.tolist(), scale))
         summed = sum_ciphertexts(self.pub, cts)
-        mean = decrypt_vector(self.priv, summed, scale, float(self.K))
+        mean = decrypt_vector(self.priv, summed, scale, float(len(self.alive)))
         return torch.tensor(mean, dtype=torch.float32, device=dev)
 
-    def run_round(self, test_data=None):
+    def run_round(self, test_data=None, dropped=()):
+        dropped = set(int(k) for k in dropped)
         for k in self.mine:
-            self.client_fit(k)
-        avg = self.aggregate()
-        for k in self.mine:
+            if k not in dropped:
+                self.client_fit(k)
+        avg = self.aggregate(dropped)
+        for k in self.mine:  # every client (a dropped one rejoins next round) takes the new mean
             self.states[k].weights = [w.clone() for w in avg]
         self.round += 1
         if test_data is not None and 0 in self.states:

@@ -97,7 +97,7 @@ class DwArgs(C.Structure):
                 ("pro", BnArgs), ("w", vp), ("KH", ci), ("KW", ci), ("S", ci), ("PT", ci),
                 ("PL", ci), ("Ho", ci), ("Wo", ci), ("y", vp), ("ldy", ci), ("stats", vp),
                 ("stats_ld", ci), ("dy", vp), ("lddy", ci), ("dx", vp), ("lddx", ci),
-                ("gsum", vp), ("gsumx", vp), ("dw", vp)]
+                ("gsum", vp), ("gsumx", vp), ("dw", vp), ("ws", vp)]
 
 
 _STRUCTS = {"BnArgs": BnArgs, "ConvArgs": ConvArgs, "WgradArgs": WgradArgs,
@@ -109,7 +109,7 @@ _STRUCTS = {"BnArgs": BnArgs, "ConvArgs": ConvArgs, "WgradArgs": WgradArgs,
 # op kinds (csrc/runtime/plan.cpp)
 OP_CONV, OP_WGRAD, OP_BN_BWD_APPLY, OP_BN_BWD_REDUCE, OP_MAXPOOL, OP_AVGPOOL, OP_POOL_BWD = range(7)
 OP_BN_MOVING, OP_HEAD_FWD, OP_HEAD_BWD, OP_RMSPROP, OP_CAST, OP_INPUT, OP_MEMSET = range(7, 14)
-OP_BN_STATS, OP_BN_APPLY, OP_DW_FWD, OP_DW_BWD_DATA, OP_DW_WGRAD, OP_COPY = range(14, 20)
+OP_BN_STATS, OP_BN_APPLY, OP_DW_FWD, OP_DW_BWD_DATA, OP_DW_WGRAD, OP_COPY, OP_FINITE_CHECK = range(14, 21)
 
 ACT = {None: 0, "none": 0, "linear": 0, "relu": 1, "relu6": 2}
 OUT_BF16, OUT_F32, OUT_F32_ACC = 0, 1, 2

@@ -278,6 +278,9 @@ def dwconv_bwd(x, kernel, dy, stride=1, pads=(1, 1), pro: Optional[BN] = None, g
     a.dx, a.lddx = dx.data_ptr(), C
     a.gsum, a.gsumx = nat.ptr(gsum), nat.ptr(gsumx)
     a.dw = dw.data_ptr()
+    ws = torch.empty(int(nat.require().dw_wgrad_ws_floats(N * Ho * Wo, C, kernel.shape[0] * kernel.shape[1])),
+                     dtype=torch.float32, device=x.device)
+    a.ws = ws.data_ptr()
     _plan1(nat.OP_DW_BWD_DATA, a)
     _plan1(nat.OP_DW_WGRAD, a)
     return dx, dw

@@ -471,6 +471,9 @@ class Builder:
         a = self._dw_args(x, layer, dy.H, dy.W, stride, pads, pro)
         a.dy, a.lddy = dy.ptr, dy.ld
         a.dw = dw.data_ptr()
+        kh, kw = layer.kernel_size
+        ws = self.alloc((int(nat.load().dw_wgrad_ws_floats(dy.M, dy.C, kh * kw)),), F32)
+        a.ws = ws.data_ptr()  # per-op workspace: two-stage reduction, no global atomics
         self.emit(nat.OP_DW_WGRAD, a, lane=lane)
 
     def memset(self, t: torch.Tensor, nbytes: Optional[int] = None):

@@ -59,7 +59,7 @@ def fused_supported(net, loss) -> bool:
 
 class FusedProgram:
     def __init__(self, model, batch: int, training: bool, input_dtype, grad_scale: float = 1.0,
-                 use_graphs: bool = True):
+                 use_graphs: bool = True, skip_nonfinite: bool = False):
         nat.require()
         self.model = model
         self.training = training
@@ -76,20 +76,33 @@ class FusedProgram:
         b.finalize_casts()
         b.finalize_moving()
         # optimizer segment
+        self.nonfinite_status = None
         if training and model.arena.params:
-            b.segment = "opt"
             opt = model.optimizer
-            if not isinstance(opt, RMSprop) or opt.momentum or opt.centered:
-                self.host_optimizer = True
-            else:
-                self.host_optimizer = False
+            self.host_optimizer = not isinstance(opt, RMSprop) or bool(opt.momentum) or bool(opt.centered)
+            flag = 0
+            if skip_nonfinite and not self.host_optimizer:
+                # non-finite guard: the gradient arena is checked at the end of the
+                # backward; RMSprop skips the whole update when anything is inf/nan
+                # (opt segment: under data parallelism it runs after the all-reduce, so every
+                # replica sees the same reduced gradients and makes the same decision)
+                fl = b.alloc((4,), torch.int32)
+                self.nonfinite_status = b.alloc((4,), torch.int32)
+                flag = fl.data_ptr()
+            b.segment = "opt"
+            if flag:
+                b.emit(nat.OP_FINITE_CHECK, ints=(0,), longs=(model.arena.numel,),
+                       ptrs=(model.arena.grad.data_ptr(), flag))
+            if not self.host_optimizer:
                 ms = opt.ms
                 b.emit(nat.OP_RMSPROP, floats=(opt.learning_rate, opt.rho, opt.epsilon, grad_scale),
                        longs=(model.arena.numel,),
-                       ptrs=(model.arena.data.data_ptr(), model.arena.grad.data_ptr(), ms.data_ptr()))
+                       ptrs=(model.arena.data.data_ptr(), model.arena.grad.data_ptr(), ms.data_ptr(), flag))
             if b.cast_tr_n:
                 b.emit(nat.OP_CAST, ints=(b.cast_tr_n,), longs=(b.cast_tr_total,),
                        ptrs=(b.cast_tr_dev.data_ptr(),))
+            if flag:
+                b.emit(nat.OP_FINITE_CHECK, ints=(1,), ptrs=(0, flag, self.nonfinite_status.data_ptr()))
         else:
             self.host_optimizer = False
         self.plan = nat.load().Plan()
@@ -204,9 +217,12 @@ class FusedStep:
 
     name = "fused"
 
-    def __init__(self, model, use_graphs: bool = True):
+    def __init__(self, model, use_graphs: bool = True, skip_nonfinite: Optional[bool] = None):
         self.m = model
         self.use_graphs = use_graphs
+        if skip_nonfinite is None:
+            skip_nonfinite = os.environ.get("IDC_SKIP_NONFINITE", "0") == "1"
+        self.skip_nonfinite = skip_nonfinite
         self.progs: Dict[tuple, FusedProgram] = {}
         self._lr = model.optimizer.learning_rate if model.optimizer else None
 
@@ -215,7 +231,8 @@ class FusedStep:
         p = self.progs.get(key)
         if p is None:
             gs = 1.0 / self.m.strategy.num_replicas_in_sync
-            p = FusedProgram(self.m, batch, training, dtype, grad_scale=gs, use_graphs=self.use_graphs)
+            p = FusedProgram(self.m, batch, training, dtype, grad_scale=gs, use_graphs=self.use_graphs,
+                             skip_nonfinite=self.skip_nonfinite)
             self.progs[key] = p
         return p
 
@@ -301,7 +318,7 @@ class FusedStep:
         with torch.cuda.stream(p.stream):
             dist.reduce(m.arena.grad, 0, op=dist.ReduceOp.SUM)
         if "opt" in p.seg:
-            lo, hi = p.seg["opt"]
+            lo, hi = p.seg["opt"]  # [finite check] rmsprop | cast [flag reset]
             if p.host_optimizer:
                 if st.rank == 0:
                     with torch.cuda.stream(p.stream):
@@ -316,6 +333,14 @@ class FusedStep:
             p.run_range(cast_lo, hi, graph=False)
         torch.cuda.current_stream(m.device).wait_stream(p.stream)
         return p.io.loss.reshape(()).clone(), p.io.logits.clone()
+
+    def skipped_steps(self) -> int:
+        """Training steps whose update was skipped for non-finite gradients (skip_nonfinite)."""
+        n = 0
+        for p in self.progs.values():
+            if p.nonfinite_status is not None:
+                n += int(p.nonfinite_status[1].item())
+        return n
 
     def eval_step(self, x, y):
         dtype = torch.uint8 if x.dtype == torch.uint8 else torch.float32

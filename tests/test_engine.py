@@ -157,3 +157,20 @@ def test_reset_optimizer_in_place():
     ms.fill_(3.0)
     m.reset_optimizer()
     assert m.optimizer.ms is ms and float(ms.abs().max()) == 0.0
+
+
+def test_skip_nonfinite_gradients():
+    ds = synthetic_dataset(16, (10, 10, 3), seed=7)
+    m = Model(build_model("tinycnn", seed=0), CPU)
+    m.compile(RMSprop(1e-3), "binary_crossentropy", [], skip_nonfinite=True)
+    w0 = [w.copy() for w in m.get_weights()]
+    x, y = next(iter(prepare_for_training(ds, 16)))
+    xf = x.float() / 255.0
+    xf[0, 0, 0, 0] = float("nan")
+    m.impl.train_step(xf, y)
+    assert m.skipped_steps() == 1
+    for a, b in zip(w0, m.get_weights()):
+        assert np.array_equal(a, b)
+    m.impl.train_step(x, y)
+    assert m.skipped_steps() == 1
+    assert not all(np.array_equal(a, b) for a, b in zip(w0, m.get_weights()))

@@ -149,3 +149,52 @@ def test_secure_process_paillier_equals_plain_mean():
     assert {"loss", "accuracy", "auc"} <= set(logs)
     # Q15: client optimizer state persists across rounds
     assert float(proc.states[0].opt_slots["ms"].abs().sum()) > 0
+
+
+def test_fedavg_participating_subset_reweights():
+    from idc_models_amd.engine import RMSprop
+    proc, clients, model_fn = _tiny_fed(n_clients=3)
+    state = proc.initialize()
+    new, _ = proc.next(state, clients, participating=[0, 2])
+    finals = []
+    for k in (0, 2):
+        m = model_fn()
+        m.compile(RMSprop(1e-2), "binary_crossentropy", ["binary_accuracy"])
+        for t, w in zip(m.net.trainable_weights, state.model.trainable):
+            t.data.copy_(w)
+        m.fit(clients[k], epochs=1, verbose=0)
+        finals.append([t.detach().clone() for t in m.net.trainable_weights])
+    for i, w in enumerate(new.model.trainable):
+        assert torch.allclose(w, (finals[0][i] + finals[1][i]) / 2, atol=1e-6)
+
+
+@pytest.mark.parametrize("mode", ["mask", "paillier"])
+def test_secure_aggregation_survives_client_dropout(mode):
+    """A client drops out before masking: the round is re-keyed among the survivors, whose masks
+    still cancel, and the result is the survivors' plain mean."""
+    from idc_models_amd.data import shard_clients, synthetic_dataset
+    from idc_models_amd.engine import Model, RMSprop
+    from idc_models_amd.fed import SecureFederatedProcess
+    from idc_models_amd.models import build_model
+    from idc_models_amd.parallel import OneDeviceStrategy
+    ds = synthetic_dataset(80, (10, 10, 3), seed=5)
+    cdata = [(s.take(12).batch(6), s.skip(12).batch(6)) for s in shard_clients(ds, 4)]
+
+    def model_fn():
+        m = Model(build_model("tinycnn", seed=0), OneDeviceStrategy("cpu"))
+        m.compile(RMSprop(1e-3), "binary_crossentropy", ["binary_accuracy"])
+        return m
+
+    proc = SecureFederatedProcess(model_fn, cdata, percent=1.0, mode=mode, epochs=1, paillier_bits=256)
+    for k in (0, 1, 3):
+        proc.client_fit(k)
+    avg = proc.aggregate(dropped={2})
+    for i, a in enumerate(avg):
+        plain = sum(proc.states[k].weights[i] for k in (0, 1, 3)) / 3
+        assert torch.allclose(a, plain, atol=1e-5)
+    # without re-keying the dropped client's masks would not cancel: check that it matters
+    from idc_models_amd.fed import secagg
+    x = torch.ones(16)
+    full = [secagg.mask_quantize(x, 1.0, 4, k, 1, 0) for k in (0, 1, 3)]
+    s = sum(t.to(torch.int64) for t in full) % (1 << 32)
+    assert not torch.equal(s, torch.full((16,), 3, dtype=torch.int64))

@@ -165,3 +165,29 @@ def test_fused_fit_and_evaluate_api():
     m.set_weights(w)
     r = m.evaluate(prepare_for_training(va, 32))
     assert len(r) == 2
+
+
+def test_fused_skip_nonfinite_step():
+    """Non-finite guard on the device: an inf input poisons the gradients, RMSprop skips the
+    whole update (weights and slots unchanged), the next clean step trains normally."""
+    from idc_models_amd.engine import Model, RMSprop
+    from idc_models_amd.models import build_model
+    net = build_model("densenet121", None, num_outputs=1, seed=0)
+    m = Model(net, device=DEV)
+    m.compile(RMSprop(1e-3), "binary_crossentropy", [], backend="fused", skip_nonfinite=True)
+    g = torch.Generator().manual_seed(1)
+    x = torch.rand(8, 50, 50, 3, generator=g)
+    y = torch.randint(0, 2, (8,), generator=g)
+    m.impl.train_step(x, y)  # builds the float-input program
+    torch.cuda.synchronize()
+    w0 = m.arena.data.clone()
+    ms0 = m.optimizer.ms.clone()
+    xb = x.clone()
+    xb[0, 10, 10, 0] = float("inf")
+    m.impl.train_step(xb, y)
+    torch.cuda.synchronize()
+    assert m.skipped_steps() == 1
+    assert torch.equal(m.arena.data, w0) and torch.equal(m.optimizer.ms, ms0)
+    m.impl.train_step(x, y)
+    torch.cuda.synchronize()
+    assert m.skipped_steps() == 1 and not torch.equal(m.arena.data, w0)
