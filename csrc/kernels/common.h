@@ -135,6 +135,44 @@ __device__ __forceinline__ void bn_coeffs(const BnArgs& b, int c, float& scale, 
   shift = be - mean * scale;
 }
 
+// BN scale/shift table for channels [0, C) into LDS, NT threads.  All global loads of a thread
+// (up to 4 channels per batch) are issued before any arithmetic so the table costs ONE memory
+// latency, not one per channel slot (loads retire in order: a per-channel loop would wait for
+// each slot's loads in turn).
+template <int NT>
+__device__ __forceinline__ void bn_coeff_table(const BnArgs& b, int C, float* s_scale, float* s_shift) {
+  const int tid = threadIdx.x;
+  if (b.mode == 0) {
+    for (int c = tid; c < C; c += NT) { s_scale[c] = 1.f; s_shift[c] = 0.f; }
+    return;
+  }
+  const float* p0 = b.mode == 1 ? b.stats : b.mmean;
+  const float* p1 = b.mode == 1 ? b.stats + b.C : b.mvar;
+  const float mul = b.mode == 1 ? b.inv_count : 1.f;
+  for (int base = 0; base < C; base += 4 * NT) {
+    float v0[4], v1[4], g[4], be[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      int c = base + u * NT + tid;
+      int cc = c < C ? c : 0;
+      v0[u] = p0[cc];
+      v1[u] = p1[cc];
+      g[u] = b.gamma ? b.gamma[cc] : 1.f;
+      be[u] = b.beta ? b.beta[cc] : 0.f;
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      int c = base + u * NT + tid;
+      if (c >= C) break;
+      float mean = v0[u] * mul;
+      float var = b.mode == 1 ? fmaxf(v1[u] * mul - mean * mean, 0.f) : v1[u];
+      float sc = g[u] * rsqrtf(var + b.eps);
+      s_scale[c] = sc;
+      s_shift[c] = be[u] - mean * sc;
+    }
+  }
+}
+
 // mean and 1/sigma of a channel (for x-hat in backward)
 __device__ __forceinline__ void bn_mean_rstd(const BnArgs& b, int c, float& mean, float& rstd) {
   float var;

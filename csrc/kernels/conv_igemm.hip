@@ -35,7 +35,8 @@ namespace idc {
 template <int BK>
 __device__ __forceinline__ int swz_chunk(int row, int chunk) {
   if constexpr (BK == 32) return chunk ^ (((row >> 2) & 1) << 1);
-  else return chunk ^ (row & 6);
+  else if constexpr (BK == 64) return chunk ^ (row & 6);
+  else return chunk ^ (row & 15);  // BK 128: 16 chunks per 256-B row (brute-force checked)
 }
 
 template <int BM, int BN, int BK, int WM, int WN>
@@ -91,28 +92,6 @@ __global__ __launch_bounds__(256) void conv_igemm_kernel(ConvArgs a) {
   const int bid = xcd_remap(blockIdx.x, mtiles * ntiles);
   const int mt = bid / ntiles, nt = bid % ntiles;
   const int m0 = mt * BM, n0 = nt * BN;
-
-  // ---- prologue tables -------------------------------------------------------------------
-  if constexpr (PRO) {
-    for (int c = tid; c < a.Cin; c += NT) {
-      float sc, sh;
-      bn_coeffs(a.pro, c, sc, sh);
-      s_scale[c] = sc;
-      s_shift[c] = sh;
-    }
-  }
-  if constexpr (EPI == 1) {
-    for (int j = tid; j < BN; j += NT) {
-      int c = n0 + j;
-      float sc = 1.f, sh = 0.f, mean = 0.f, rstd = 1.f;
-      if (c < a.Cout) {
-        bn_coeffs(a.mbn, c, sc, sh);
-        if (a.mbn.mode) bn_mean_rstd(a.mbn, c, mean, rstd);
-      }
-      s_e0[j] = sc; s_e1[j] = sh; s_e2[j] = mean; s_e3[j] = rstd;
-    }
-  }
-  for (int j = tid; j < BN; j += NT) { s_sum[j] = 0.f; s_sq[j] = 0.f; }
 
   // ---- per-thread A row decode (fixed for the whole K loop) -------------------------------
   const int my_chunk = tid % CPR;  // the k-chunk this thread stages (same for all its rows)
@@ -262,10 +241,28 @@ __global__ __launch_bounds__(256) void conv_igemm_kernel(ConvArgs a) {
     for (int j = 0; j < TN; ++j) acc[i][j] = (v4f){0.f, 0.f, 0.f, 0.f};
 
   const int nk = (K + BK - 1) / BK;
-  __syncthreads();  // prologue tables visible
+  // the first two tiles are issued BEFORE the prologue tables are built: the tables' own global
+  // loads (BN statistics, gamma, beta) then overlap the tile loads instead of adding a second
+  // full memory latency in front of the K loop
   load_tile(st0);
   advance_k();
   load_tile(st1);
+  // ---- prologue tables ----
+  if constexpr (PRO) bn_coeff_table<NT>(a.pro, a.Cin, s_scale, s_shift);
+  if constexpr (EPI == 1) {
+    for (int j = tid; j < BN; j += NT) {
+      int c = n0 + j;
+      float sc = 1.f, sh = 0.f, mean = 0.f, rstd = 1.f;
+      if (c < a.Cout) {
+        bn_coeffs(a.mbn, c, sc, sh);
+        if (a.mbn.mode) bn_mean_rstd(a.mbn, c, mean, rstd);
+      }
+      s_e0[j] = sc; s_e1[j] = sh; s_e2[j] = mean; s_e3[j] = rstd;
+    }
+  }
+  for (int j = tid; j < BN; j += NT) { s_sum[j] = 0.f; s_sq[j] = 0.f; }
+
+  __syncthreads();  // prologue tables visible
   store_tile(st0, 0);
   __syncthreads();
 
@@ -462,7 +459,8 @@ struct TileInfo { int bm, bn; };
 static const TileInfo kTiles[] = {
     {128, 128}, {128, 64}, {256, 32}, {64, 64}, {64, 32},   // BK 32
     {128, 128}, {128, 64}, {128, 32}, {64, 64}, {64, 32},   // BK 64
-    {256, 32}, {64, 128}};                                 // BK 64
+    {256, 32}, {64, 128},                                  // BK 64
+    {64, 32}, {128, 32}, {64, 64}, {64, 128}, {128, 64}};  // BK 128: half the K steps of BK 64
 
 int conv_num_tiles() { return (int)(sizeof(kTiles) / sizeof(kTiles[0])); }
 int conv_tile_bm(int t) { return kTiles[t].bm; }
@@ -487,6 +485,11 @@ hipError_t conv_igemm(const ConvArgs& a, int tile, bool a_f32, hipStream_t st) {
     case 9: return launch_cfg<64, 32, 64, 2, 2>(a, is1x1, a_f32, pro, epi, st);
     case 10: return launch_cfg<256, 32, 64, 4, 1>(a, is1x1, a_f32, pro, epi, st);
     case 11: return launch_cfg<64, 128, 64, 2, 2>(a, is1x1, a_f32, pro, epi, st);
+    case 12: return launch_cfg<64, 32, 128, 2, 2>(a, is1x1, a_f32, pro, epi, st);
+    case 13: return launch_cfg<128, 32, 128, 4, 1>(a, is1x1, a_f32, pro, epi, st);
+    case 14: return launch_cfg<64, 64, 128, 2, 2>(a, is1x1, a_f32, pro, epi, st);
+    case 15: return launch_cfg<64, 128, 128, 2, 2>(a, is1x1, a_f32, pro, epi, st);
+    case 16: return launch_cfg<128, 64, 128, 2, 2>(a, is1x1, a_f32, pro, epi, st);
     default: return hipErrorInvalidValue;
   }
 }

@@ -91,15 +91,6 @@ __global__ __launch_bounds__(256) void conv_wgrad_kernel(WgradArgs a) {
   const int pend = min(M, pbeg + per);
   if (pbeg >= pend) return;
 
-  if constexpr (PRO) {
-    for (int c = tid; c < a.Cin; c += NT) {
-      float sc, sh;
-      bn_coeffs(a.pro, c, sc, sh);
-      s_scale[c] = sc;
-      s_shift[c] = sh;
-    }
-  }
-
   // ---- A (im2col) staging: thread owns k-chunk `ach` (fixed) for pixel rows arow + 32/..*i ----
   const int ach = tid % ACH;
   const int arow0 = tid / ACH;            // first pixel row (0..BP) this thread stages
@@ -219,9 +210,10 @@ __global__ __launch_bounds__(256) void conv_wgrad_kernel(WgradArgs a) {
 #pragma unroll
     for (int j = 0; j < TN; ++j) acc[i][j] = (v4f){0.f, 0.f, 0.f, 0.f};
 
-  __syncthreads();
   const int nsteps = (pend - pbeg + BP - 1) / BP;
-  load(pbeg);
+  load(pbeg);  // first tile in flight while the BN table is built (its loads overlap)
+  if constexpr (PRO) bn_coeff_table<NT>(a.pro, a.Cin, s_scale, s_shift);
+  __syncthreads();
   store(0);
   __syncthreads();
   for (int it = 0; it < nsteps; ++it) {

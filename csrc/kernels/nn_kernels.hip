@@ -109,6 +109,31 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(BnBwdApplyArgs a) {
   float* sA = sh;
   float* sB = sh + a.C;
   float* sC = sh + 2 * a.C;
+  // one grid-stride pass of RU rows per thread is the common case (grid sized for it): issue that
+  // pass's loads first so the coefficient loads below overlap them
+  ChunkMap cm(a.C);
+  const int c = cm.tx * 8;
+  const int step = gridDim.x * cm.R;
+  const int row0 = blockIdx.x * cm.R + cm.ty;
+  uint4 dz[RU], xx[RU];
+  float4 o0[RU], o1[RU];
+  int rows[RU];
+  auto load_pass = [&](int r0) {
+#pragma unroll
+    for (int u = 0; u < RU; ++u) {
+      int r = r0 + u * step;
+      rows[u] = r < a.M ? r : a.M - 1;  // clamped: loads stay unconditional
+      dz[u] = *reinterpret_cast<const uint4*>(a.dz + (size_t)rows[u] * a.lddz + c);
+      xx[u] = *reinterpret_cast<const uint4*>(a.x + (size_t)rows[u] * a.ldx + c);
+      if constexpr (F32 && ACC) {
+        const float* q = reinterpret_cast<const float*>(a.dst) + (size_t)rows[u] * a.lddst + c;
+        o0[u] = *reinterpret_cast<const float4*>(q);
+        o1[u] = *reinterpret_cast<const float4*>(q + 4);
+      }
+    }
+  };
+  const bool active = cm.active();
+  if (active && row0 < a.M) load_pass(row0);
   for (int c = threadIdx.x; c < a.C; c += blockDim.x) {
     float mean, rstd;
     bn_mean_rstd(a.bn, c, mean, rstd);
@@ -125,29 +150,13 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(BnBwdApplyArgs a) {
     }
   }
   __syncthreads();
-  ChunkMap cm(a.C);
-  if (!cm.active()) return;
-  const int c = cm.tx * 8;
+  if (!active) return;
   float ka[8], kb[8], kc[8];
 #pragma unroll
   for (int j = 0; j < 8; ++j) { ka[j] = sA[c + j]; kb[j] = sB[c + j]; kc[j] = sC[c + j]; }
-  const int step = gridDim.x * cm.R;
-  for (int row0 = blockIdx.x * cm.R + cm.ty; row0 < a.M; row0 += step * RU) {
-    uint4 dz[RU], xx[RU];
-    float4 o0[RU], o1[RU];
-    int rows[RU];
-#pragma unroll
-    for (int u = 0; u < RU; ++u) {
-      int r = row0 + u * step;
-      rows[u] = r < a.M ? r : a.M - 1;  // clamped: loads stay unconditional
-      dz[u] = *reinterpret_cast<const uint4*>(a.dz + (size_t)rows[u] * a.lddz + c);
-      xx[u] = *reinterpret_cast<const uint4*>(a.x + (size_t)rows[u] * a.ldx + c);
-      if constexpr (F32 && ACC) {
-        const float* q = reinterpret_cast<const float*>(a.dst) + (size_t)rows[u] * a.lddst + c;
-        o0[u] = *reinterpret_cast<const float4*>(q);
-        o1[u] = *reinterpret_cast<const float4*>(q + 4);
-      }
-    }
+  for (int row0_ = row0; row0_ < a.M; row0_ += step * RU) {
+    if (row0_ != row0) load_pass(row0_);
+    const int row0 = row0_;
 #pragma unroll
     for (int u = 0; u < RU; ++u) {
       if (row0 + u * step >= a.M) break;

@@ -1,0 +1,85 @@
+"""Per-kernel PMC summary of a ``rocprofv3 --pmc ... --kernel-trace --output-format csv`` run.
+
+usage: python tools/pmc_summary.py DIR/PREFIX --steps 3 [--marker input_stage] [--md out.md]
+
+Counters expected: SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_VALU_MFMA_BUSY_CYCLES SQ_LDS_BANK_CONFLICT
+SQ_LDS_IDX_ACTIVE SQ_WAIT_INST_LDS SQ_INSTS_MFMA SQ_WAIT_ANY.  Only the last ``--steps`` training
+steps are used (a step starts at the ``--marker`` kernel), so autotuning and warm-up are excluded.
+
+Derived (per kernel class, summed over its dispatches):
+  MFMA util   = SQ_VALU_MFMA_BUSY_CYCLES / (kernel time x 2.4 GHz x 1024 SIMDs)
+  LDS confl.  = SQ_LDS_BANK_CONFLICT / SQ_LDS_IDX_ACTIVE   (extra cycles per LDS-array cycle)
+  wait frac.  = SQ_WAIT_ANY / SQ_WAVE_CYCLES,  LDS-issue stall = SQ_WAIT_INST_LDS / SQ_WAVE_CYCLES
+Kernel times come from the PMC run (serialised dispatches), so they are upper bounds.
+"""
+import argparse
+import collections
+import csv
+import re
+
+CLK = 2.4e9
+SIMDS = 256 * 4
+
+
+def short(name):
+    name = re.sub(r"^void ", "", name)
+    name = re.sub(r"\(.*\)$", "", name)
+    return name.replace("idc::", "")
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("prefix")
+    ap.add_argument("--steps", type=int, default=3)
+    ap.add_argument("--marker", default="input_stage")
+    ap.add_argument("--md", default=None)
+    a = ap.parse_args()
+    disp = {}
+    order = []
+    with open(a.prefix + "_counter_collection.csv") as f:
+        for r in csv.DictReader(f):
+            d = int(r["Dispatch_Id"])
+            if d not in disp:
+                disp[d] = {"name": r["Kernel_Name"], "t": int(r["End_Timestamp"]) - int(r["Start_Timestamp"])}
+                order.append(d)
+            disp[d][r["Counter_Name"]] = disp[d].get(r["Counter_Name"], 0.0) + float(r["Counter_Value"])
+    order.sort()
+    marks = [d for d in order if a.marker in disp[d]["name"]]
+    first = marks[-a.steps]
+    sel = [d for d in order if d >= first]
+    agg = collections.OrderedDict()
+    for d in sel:
+        e = disp[d]
+        k = short(e["name"])
+        s = agg.setdefault(k, collections.Counter())
+        s["n"] += 1
+        for key, v in e.items():
+            if key != "name":
+                s[key] += v
+    rows = []
+    tot_t = sum(s["t"] for s in agg.values())
+    tot_mfma = sum(s["SQ_VALU_MFMA_BUSY_CYCLES"] for s in agg.values())
+    for k, s in agg.items():
+        t = s["t"] * 1e-9
+        util = s["SQ_VALU_MFMA_BUSY_CYCLES"] / (t * CLK * SIMDS) if t else 0.0
+        lds = s["SQ_LDS_BANK_CONFLICT"] / s["SQ_LDS_IDX_ACTIVE"] if s["SQ_LDS_IDX_ACTIVE"] else 0.0
+        wait = s["SQ_WAIT_ANY"] / s["SQ_WAVE_CYCLES"] if s["SQ_WAVE_CYCLES"] else 0.0
+        ldsw = s["SQ_WAIT_INST_LDS"] / s["SQ_WAVE_CYCLES"] if s["SQ_WAVE_CYCLES"] else 0.0
+        rows.append((s["t"], k, s["n"] / a.steps, s["t"] / 1e3 / a.steps, util, lds, wait, ldsw))
+    rows.sort(reverse=True)
+    lines = [f"# PMC summary per kernel ({a.steps} steps, rocprofv3 --pmc, serialised dispatches)", "",
+             f"- kernel time per step under PMC: {tot_t / 1e6 / a.steps:.3f} ms",
+             f"- whole-step MFMA utilisation: {tot_mfma / (tot_t * 1e-9 * CLK * SIMDS):.1%}", "",
+             "| kernel | calls/step | us/step | MFMA util | LDS bank-conflict cycles / LDS cycles | wave wait frac | LDS issue stall |",
+             "|---|---:|---:|---:|---:|---:|---:|"]
+    for _, k, n, us, util, lds, wait, ldsw in rows[:40]:
+        lines.append(f"| `{k}` | {n:.0f} | {us:.1f} | {util:.1%} | {lds:.3f} | {wait:.2f} | {ldsw:.3f} |")
+    out = "\n".join(lines) + "\n"
+    print(out)
+    if a.md:
+        with open(a.md, "w") as f:
+            f.write(out)
+
+
+if __name__ == "__main__":
+    main()
