@@ -34,6 +34,7 @@
 #include "../kernels/conv_igemm.h"
 #include "../kernels/conv_wgrad.h"
 #include "../kernels/dwconv.h"
+#include "../kernels/mlp_head.h"
 #include "../kernels/nn_kernels.h"
 #include "../kernels/secagg.h"
 
@@ -64,6 +65,9 @@ enum OpKind : int {
   OP_DW_WGRAD = 18,
   OP_COPY = 19,
   OP_FINITE_CHECK = 20,
+  OP_MLP_FWD = 21,
+  OP_MLP_BWD = 22,
+  OP_MLP_STEP = 23,
 };
 
 struct Op {
@@ -171,9 +175,9 @@ class Plan {
     static const char* names[] = {"conv", "wgrad", "bn_bwd_apply", "bn_bwd_reduce", "maxpool", "avgpool",
                                   "pool_bwd", "bn_moving", "head_fwd", "head_bwd", "rmsprop", "cast",
                                   "input", "memset", "bn_stats", "bn_apply", "dw_fwd", "dw_bwd_data",
-                                  "dw_wgrad", "copy", "finite_check"};
+                                  "dw_wgrad", "copy", "finite_check", "mlp_fwd", "mlp_bwd", "mlp_step"};
     int k = ops_.at(idx).kind;
-    return (k >= 0 && k < 21) ? names[k] : "?";
+    return (k >= 0 && k < 24) ? names[k] : "?";
   }
 
  private:
@@ -276,6 +280,9 @@ class Plan {
           check(finite_flag_reset(reinterpret_cast<int*>(op.p[1]), reinterpret_cast<int*>(op.p[2]), st),
                 "finite_flag_reset");
         break;
+      case OP_MLP_FWD: check(mlp2_fwd(as<Mlp2Args>(op), st), "mlp2_fwd"); break;
+      case OP_MLP_BWD: check(mlp2_bwd(as<Mlp2Args>(op), st), "mlp2_bwd"); break;
+      case OP_MLP_STEP: check(mlp2_step(reinterpret_cast<unsigned int*>(op.p[0]), st), "mlp2_step"); break;
       case OP_COPY:
         check(hipMemcpyAsync(reinterpret_cast<void*>(op.p[0]), reinterpret_cast<const void*>(op.p[1]),
                              (size_t)op.l[0], hipMemcpyDeviceToDevice, st),
@@ -326,6 +333,7 @@ py::dict struct_sizes() {
   d["HeadBwdArgs"] = sizeof(HeadBwdArgs);
   d["CastEntry"] = sizeof(CastEntry);
   d["DwArgs"] = sizeof(DwArgs);
+  d["Mlp2Args"] = sizeof(Mlp2Args);
   d["ConvArgs.mbn"] = offsetof(ConvArgs, mbn);
   d["ConvArgs.gsumx"] = offsetof(ConvArgs, gsumx);
   d["WgradArgs.pix_per_split"] = offsetof(WgradArgs, pix_per_split);

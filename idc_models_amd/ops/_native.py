@@ -100,16 +100,25 @@ class DwArgs(C.Structure):
                 ("gsum", vp), ("gsumx", vp), ("dw", vp), ("ws", vp)]
 
 
+class Mlp2Args(C.Structure):
+    _fields_ = [("x", vp), ("N", ci), ("D0", ci), ("D1", ci), ("U", ci), ("w1", vp), ("b1", vp),
+                ("w2", vp), ("b2", vp), ("p0", cf), ("p1", cf), ("seed", C.c_uint64), ("step", vp),
+                ("labels", vp), ("logits", vp), ("h1", vp), ("loss", vp), ("dlogits", vp),
+                ("loss_scale", cf), ("training", ci), ("dw1", vp), ("db1", vp), ("dw2", vp),
+                ("db2", vp), ("dx", vp)]
+
+
 _STRUCTS = {"BnArgs": BnArgs, "ConvArgs": ConvArgs, "WgradArgs": WgradArgs,
             "BnBwdApplyArgs": BnBwdApplyArgs, "BnBwdReduceArgs": BnBwdReduceArgs,
             "PoolArgs": PoolArgs, "PoolBwdArgs": PoolBwdArgs, "BnMovingDesc": BnMovingDesc,
             "HeadArgs": HeadArgs, "HeadBwdArgs": HeadBwdArgs, "CastEntry": CastEntry,
-            "DwArgs": DwArgs}
+            "DwArgs": DwArgs, "Mlp2Args": Mlp2Args}
 
 # op kinds (csrc/runtime/plan.cpp)
 OP_CONV, OP_WGRAD, OP_BN_BWD_APPLY, OP_BN_BWD_REDUCE, OP_MAXPOOL, OP_AVGPOOL, OP_POOL_BWD = range(7)
 OP_BN_MOVING, OP_HEAD_FWD, OP_HEAD_BWD, OP_RMSPROP, OP_CAST, OP_INPUT, OP_MEMSET = range(7, 14)
 OP_BN_STATS, OP_BN_APPLY, OP_DW_FWD, OP_DW_BWD_DATA, OP_DW_WGRAD, OP_COPY, OP_FINITE_CHECK = range(14, 21)
+OP_MLP_FWD, OP_MLP_BWD, OP_MLP_STEP = range(21, 24)
 
 ACT = {None: 0, "none": 0, "linear": 0, "relu": 1, "relu6": 2}
 OUT_BF16, OUT_F32, OUT_F32_ACC = 0, 1, 2

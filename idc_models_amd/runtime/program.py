@@ -30,6 +30,10 @@ def _lowering_for(net):
     from ..models.mobilenet_v2 import MobileNetV2
     from ..models.vgg import VGG16
 
+    from ..models.tiny_cnn import TinyCNN
+    if isinstance(net, TinyCNN):
+        from .lower_tiny import lower_tiny, tiny_supported
+        return lower_tiny if tiny_supported(net) else None
     if not isinstance(net, Sequential):
         return None
     base = net.base

@@ -191,3 +191,36 @@ def test_fused_skip_nonfinite_step():
     m.impl.train_step(x, y)
     torch.cuda.synchronize()
     assert m.skipped_steps() == 1 and not torch.equal(m.arena.data, w0)
+
+
+def _tiny(B, drop=True, seed=0):
+    from idc_models_amd.engine import Model, RMSprop
+    from idc_models_amd.models import build_model
+    net = build_model("tinycnn", seed=seed)
+    if not drop:
+        for l in net.layers:
+            if l.keras_class == "Dropout":
+                l.rate = 0.0
+    ref = copy.deepcopy(net).to(DEV)
+    m = Model(net, device=DEV)
+    m.compile(RMSprop(1e-3), "binary_crossentropy", ["accuracy"], backend="fused")
+    g = torch.Generator().manual_seed(seed + 1)
+    x = torch.randint(0, 256, (B, 10, 10, 3), generator=g, dtype=torch.uint8)
+    y = torch.randint(0, 2, (B,), generator=g)
+    return m, ref, x, y
+
+
+def test_tinycnn_fused_matches_eager_without_dropout():
+    from idc_models_amd.runtime.lower_tiny import lower_tiny  # noqa: F401  (fused path exists)
+    m, ref, x, y = _tiny(32, drop=False)
+    assert type(m.impl).__name__ == "FusedStep"
+    _check(m, ref, x, y)
+
+
+def test_tinycnn_fused_dropout_trains_and_eval_is_deterministic():
+    m, ref, x, y = _tiny(32, drop=True)
+    losses = [m.impl.train_step(x, y)[0].item() for _ in range(30)]
+    assert losses[-1] < losses[0], losses
+    l1, g1 = m.impl.eval_step(x, y)
+    l2, g2 = m.impl.eval_step(x, y)
+    assert torch.equal(g1, g2)  # no dropout at inference

@@ -11,7 +11,8 @@ from idc_models_amd.ops import _native as nat
 pytestmark = pytest.mark.skipif(not nat.available(), reason="native extension not built")
 
 CASES = [("densenet121", None), ("densenet121", 150), ("densenet121", "frozen"), ("vgg16", None),
-         ("vgg16", 15), ("mobilenetv2", None), ("mobilenetv2", 100), ("mobilenetv2", "frozen")]
+         ("vgg16", 15), ("mobilenetv2", None), ("mobilenetv2", 100), ("mobilenetv2", "frozen"),
+         ("tinycnn", None)]
 
 
 def _lower(arch, ft, training, B=4):
@@ -21,10 +22,11 @@ def _lower(arch, ft, training, B=4):
     from idc_models_amd.runtime.builder import Builder
     from idc_models_amd.runtime.program import _lowering_for
     net = build_model(arch, None, 1, seed=0)
+    base = getattr(net, "base", net)
     if ft == "frozen":
-        net.base.trainable = False
+        base.trainable = False
     elif ft:
-        for l in net.base.layers[:ft]:
+        for l in base.layers[:ft]:
             l.trainable = False
     m = Model(net, OneDeviceStrategy("cpu"))
     m.compile(RMSprop(1e-4), "binary_crossentropy", [], backend="eager")
@@ -39,7 +41,8 @@ STRUCTS = {nat.OP_CONV: nat.ConvArgs, nat.OP_WGRAD: nat.WgradArgs, nat.OP_BN_BWD
            nat.OP_BN_BWD_REDUCE: nat.BnBwdReduceArgs, nat.OP_MAXPOOL: nat.PoolArgs,
            nat.OP_AVGPOOL: nat.PoolArgs, nat.OP_POOL_BWD: nat.PoolBwdArgs, nat.OP_HEAD_FWD: nat.HeadArgs,
            nat.OP_HEAD_BWD: nat.HeadBwdArgs, nat.OP_DW_FWD: nat.DwArgs, nat.OP_DW_BWD_DATA: nat.DwArgs,
-           nat.OP_DW_WGRAD: nat.DwArgs, nat.OP_BN_APPLY: nat.BnArgs}
+           nat.OP_DW_WGRAD: nat.DwArgs, nat.OP_BN_APPLY: nat.BnArgs, nat.OP_MLP_FWD: nat.Mlp2Args,
+           nat.OP_MLP_BWD: nat.Mlp2Args}
 
 
 def _pointers(obj, out):

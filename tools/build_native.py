@@ -30,6 +30,7 @@ SOURCES = [
     "kernels/conv_wgrad.hip",
     "kernels/nn_kernels.hip",
     "kernels/dwconv.hip",
+    "kernels/mlp_head.hip",
     "kernels/secagg.hip",
     "runtime/plan.cpp",
 ]
