@@ -123,6 +123,17 @@ class BatchedDataset:
         self.seed = seed
         self.repeat = repeat
         self._epoch = 0
+        self.device = None       # prefetch_to(): batches are delivered on this device
+        self._prefetcher = None
+
+    def prefetch_to(self, device) -> "BatchedDataset":
+        """Deliver batches as ``device`` tensors through the native pinned-memory prefetcher
+        (``tf.data``'s ``prefetch(AUTOTUNE)``, ``dist_model_tf_vgg.py:63``)."""
+        device = torch.device(device)
+        if self.device != device:
+            self.device = device
+            self._prefetcher = None
+        return self
 
     def __len__(self):
         n = len(self.ds) * self.repeat
@@ -137,8 +148,13 @@ class BatchedDataset:
         for r in range(self.repeat):
             idx = self.ds.index
             if self.shuffle:
-                rng = np.random.default_rng((self.seed, self._epoch, r))
-                idx = _buffer_shuffle(idx, self.buffer, rng)
+                from . import native
+                if native.available():
+                    key = ((self.seed * 1000003 + self._epoch) * 1000003 + r) & ((1 << 64) - 1)
+                    idx = native.shuffle_order(idx, self.buffer, key)
+                else:
+                    rng = np.random.default_rng((self.seed, self._epoch, r))
+                    idx = _buffer_shuffle(idx, self.buffer, rng)
             parts.append(idx)
         self._epoch += 1
         return np.concatenate(parts) if len(parts) > 1 else parts[0]
@@ -150,6 +166,14 @@ class BatchedDataset:
         stop = n - (n % bs) if self.drop_remainder else n
         x, y = self.ds.x, self.ds.y
         on_dev = isinstance(x, torch.Tensor) and x.is_cuda
+        if isinstance(x, np.ndarray) and isinstance(y, np.ndarray) and stop > 0:
+            from . import native
+            if native.available():
+                if self._prefetcher is None:
+                    self._prefetcher = native.PrefetchIterator(x, y, bs, device=self.device)
+                yield from self._prefetcher.epoch(order[:stop] if self.drop_remainder else order,
+                                                  self.drop_remainder)
+                return
         for s in range(0, stop, bs):
             idx = order[s:s + bs]
             if on_dev:

@@ -54,8 +54,14 @@ def label_of(file_path: str) -> int:
 
 
 def load_files(files: List[str], size: int = 50, workers: int = 8) -> ArrayDataset:
-    x = np.zeros((len(files), size, size, 3), np.uint8)
     y = np.array([label_of(f) for f in files], np.int64)
+    from . import native
+    if native.available():  # libpng + resize on C++ threads (csrc/data/loader.cpp)
+        x, bad = native.decode_pngs(files, size, workers)
+        if bad:
+            raise ValueError(f"{len(bad)} images failed to decode, first: {bad[0][1]}")
+        return ArrayDataset(x, y)
+    x = np.zeros((len(files), size, size, 3), np.uint8)
 
     def work(i):
         x[i] = _load_png(files[i], size)

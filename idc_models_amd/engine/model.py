@@ -203,6 +203,8 @@ class Model:
     # ------------------------------------------------------------------ loops
     def _run_epoch(self, data, steps, train: bool, callbacks=None):
         ms = self._new_metrics()
+        if self.device.type == "cuda" and hasattr(data, "prefetch_to"):
+            data.prefetch_to(self.device)
         it = self.strategy.distribute(data)
         for step, (x, y) in enumerate(it):
             if steps is not None and step >= steps:

@@ -2,16 +2,44 @@
 
 Only what the reference needs: a keypair, encryption/decryption of (fixed-point) integers, and
 homomorphic addition of ciphertexts.  ``phe`` is not installed here, so this is a small pure-Python
-implementation on Python's arbitrary-precision ``pow``.  It is the PARITY mode of secure
-aggregation (CPU bound, fine for the 1,937-parameter tiny CNN); the default mode is the additive
-pairwise-mask scheme in ``secagg.py``, which runs on the GPU at HBM bandwidth.
+implementation on Python's arbitrary-precision ``pow``; when the native GMP module
+(``csrc/fed/paillier_gmp.cpp`` -> ``_idc_paillier``) is built, the vector entry points
+(``encrypt_vector`` / ``decrypt_vector``) run their modular exponentiations there, on C++ threads,
+with CRT decryption.  It is the PARITY mode of secure aggregation (CPU bound); the default mode is
+the additive pairwise-mask scheme in ``secagg.py``, which runs on the GPU at HBM bandwidth.
 """
 from __future__ import annotations
 
+import importlib
+import os
 import secrets
 from dataclasses import dataclass
 from math import gcd
-from typing import List
+from typing import List, Optional
+
+import numpy as np
+
+_NATIVE = None
+
+
+def _native():
+    global _NATIVE
+    if _NATIVE is None:
+        _NATIVE = False
+        if os.environ.get("IDC_NATIVE_PAILLIER", "1") != "0":
+            try:
+                _NATIVE = importlib.import_module("idc_models_amd._idc_paillier")
+            except ImportError:
+                _NATIVE = False
+    return _NATIVE or None
+
+
+def _threads() -> int:
+    return max(1, min(16, os.cpu_count() or 1))
+
+
+def _be(x: int) -> bytes:
+    return x.to_bytes((x.bit_length() + 7) // 8, "big")
 
 _SMALL_PRIMES = [p for p in range(3, 2000, 2) if all(p % q for q in range(3, int(p ** 0.5) + 1, 2))]
 
@@ -74,6 +102,8 @@ class PrivateKey:
     pub: PublicKey
     lam: int
     mu: int
+    p: Optional[int] = None  # the factors enable CRT decryption (native path)
+    q: Optional[int] = None
 
     def decrypt(self, c: int) -> int:
         n, n2 = self.pub.n, self.pub.n2
@@ -93,14 +123,29 @@ def generate_paillier_keypair(n_length: int = 3072):
     lam = (p - 1) * (q - 1) // gcd(p - 1, q - 1)
     pub = PublicKey(n)
     mu = pow(lam, -1, n)
-    return pub, PrivateKey(pub, lam, mu)
+    return pub, PrivateKey(pub, lam, mu, p, q)
 
 
 def encrypt_vector(pub: PublicKey, values, scale: float) -> List[int]:
-    return [pub.encrypt(int(round(float(v) * scale))) for v in values]
+    ms = [int(round(float(v) * scale)) for v in values]
+    nat = _native()
+    if nat is not None and ms and all(-(1 << 62) < m < (1 << 62) for m in ms):
+        blk = nat.encrypt(_be(pub.n), np.asarray(ms, dtype=np.int64), _threads())
+        return [int.from_bytes(row.tobytes(), "big") for row in blk]
+    return [pub.encrypt(m) for m in ms]
 
 
 def decrypt_vector(priv: PrivateKey, cts: List[int], scale: float, divisor: float = 1.0) -> List[float]:
+    nat = _native()
+    if nat is not None and priv.p and priv.q and cts:
+        n2 = priv.pub.n2
+        w = (n2.bit_length() + 7) // 8
+        blk = np.frombuffer(b"".join(c.to_bytes(w, "big") for c in cts), dtype=np.uint8).reshape(len(cts), w)
+        try:
+            ms = nat.decrypt(_be(priv.p), _be(priv.q), blk, _threads())
+            return [float(m) / scale / divisor for m in ms.tolist()]
+        except OverflowError:
+            pass  # plaintext beyond int64: exact Python path below
     return [priv.decrypt(c) / scale / divisor for c in cts]
 
 

@@ -99,8 +99,53 @@ def build_h5(verbose: bool = True):
     return out
 
 
+CONDA_PREFIX = os.environ.get("IDC_HOSTLIB_PREFIX", "/opt/conda")
+
+# host-only pybind11 modules: (module name, source, include subdir, libs)
+HOST_MODULES = [
+    ("_idc_data", "data/loader.cpp", "libpng16", ["png16", "z"]),
+    ("_idc_paillier", "fed/paillier_gmp.cpp", "", ["gmp"]),
+]
+
+
+def host_ext_path(name: str) -> str:
+    return os.path.join(PKG, name + sysconfig.get_config_var("EXT_SUFFIX"))
+
+
+def build_host_module(name: str, src_rel: str, inc_sub: str, libs, verbose: bool = True):
+    """g++ build of a host-only pybind11 module against libraries of the image's /opt/conda
+    prefix (rpath'd; libstdc++ linked statically because that prefix ships an older one)."""
+    import pybind11
+
+    src = os.path.join(CSRC, src_rel)
+    out = host_ext_path(name)
+    inc = os.path.join(CONDA_PREFIX, "include", inc_sub) if inc_sub else os.path.join(CONDA_PREFIX, "include")
+    if not os.path.isdir(inc):
+        if verbose:
+            print(f"[build_native] {inc} not found; {name} disabled")
+        return None
+    if os.path.exists(out) and os.path.getmtime(out) >= os.path.getmtime(src):
+        return out
+    # the module's own include dir only (not all of /opt/conda/include, which carries headers that
+    # would shadow the system's)
+    cmd = ["g++", "-O3", "-std=c++17", "-shared", "-fPIC", "-pthread", src, "-o", out + ".tmp",
+           f"-I{pybind11.get_include()}", f"-I{sysconfig.get_paths()['include']}", f"-I{inc}",
+           f"-L{CONDA_PREFIX}/lib"] + [f"-l{l}" for l in libs] + [
+           f"-Wl,-rpath,{CONDA_PREFIX}/lib", "-static-libstdc++", "-static-libgcc"]
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    if r.returncode != 0:
+        raise RuntimeError(f"{name} build failed:\n{r.stderr[-4000:]}")
+    os.replace(out + ".tmp", out)
+    if verbose:
+        print(f"[build_native] {out}")
+    return out
+
+
 def build(clean: bool = False, jobs: int = 8, verbose: bool = True) -> str:
     build_h5(verbose)
+    for name, src, inc, libs in HOST_MODULES:
+        if os.path.exists(os.path.join(CSRC, src)):
+            build_host_module(name, src, inc, libs, verbose)
     if clean and os.path.isdir(BUILD):
         shutil.rmtree(BUILD)
     os.makedirs(BUILD, exist_ok=True)
