@@ -80,6 +80,18 @@ __device__ __forceinline__ void affine_act8(float* v, const float* sc, const flo
   for (int j = 0; j < 8; ++j) v[j] = fminf(fmaxf(fmaf(v[j], s[j], h[j]), lo), hi);
 }
 
+// Sum 8 per-lane column partials over the lanes of a wave that own the same 8-column chunk
+// (lane % CPB): afterwards every lane holds its chunk's wave total.  Used before the per-block
+// statistics flush so LDS sees CPB-way instead of (64/CPB)-way same-address float atomics.
+template <int CPB>
+__device__ __forceinline__ void wave_reduce_chunks(float* v) {
+#pragma unroll
+  for (int o = CPB; o < 64; o <<= 1) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) v[j] += __shfl_xor(v[j], o, 64);
+  }
+}
+
 __device__ __forceinline__ float wave_sum(float v) {
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);

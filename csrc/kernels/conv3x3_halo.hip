@@ -264,7 +264,9 @@ __global__ __launch_bounds__(NT) void conv3x3_halo_kernel(ConvArgs a) {
   }
   const bool want = (EPI == 1) || (a.stats_out != nullptr);
   if (want) {
-    if (lane < (64 < 16 * CPB ? 64 : 16 * CPB)) {
+    wave_reduce_chunks<CPB < 64 ? CPB : 64>(psum);
+    wave_reduce_chunks<CPB < 64 ? CPB : 64>(psq);
+    if (lane < CPB) {
 #pragma unroll
       for (int jj = 0; jj < 8; ++jj) {
         atomicAdd(&s_sum[my_c8 * 8 + jj], psum[jj]);

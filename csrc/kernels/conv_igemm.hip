@@ -403,7 +403,9 @@ __global__ __launch_bounds__(256) void conv_igemm_kernel(ConvArgs a) {
     }
   }
   if (want_stats) {
-    if (tid < ((WTM * CPB < NT) ? WTM * CPB : NT)) {
+    wave_reduce_chunks<CPB>(psum);
+    wave_reduce_chunks<CPB>(psq);
+    if ((tid & 63) < CPB && (tid & ~63) < WTM * CPB) {
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
         atomicAdd(&s_sum[my_c8 * 8 + j], psum[j]);
