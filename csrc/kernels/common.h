@@ -27,8 +27,14 @@ __device__ __forceinline__ bf16_t f2bf(float f) {
   return __builtin_bit_cast(bf16_t, b);
 }
 
+typedef __bf16 v2bf_t __attribute__((ext_vector_type(2)));
+typedef float v2f_t __attribute__((ext_vector_type(2)));
+
+// two floats -> packed bf16 pair in ONE v_cvt_pk_bf16_f32 (the scalar-cast form compiles to two
+// single-lane converts plus a shift and an or)
 __device__ __forceinline__ uint32_t pack2bf(float a, float b) {
-  return (uint32_t)f2bf(a) | ((uint32_t)f2bf(b) << 16);
+  v2f_t v = {a, b};
+  return __builtin_bit_cast(uint32_t, __builtin_convertvector(v, v2bf_t));
 }
 
 __device__ __forceinline__ void unpack8(const uint4& v, float* f) {
@@ -57,8 +63,13 @@ enum Act : int { ACT_NONE = 0, ACT_RELU = 1, ACT_RELU6 = 2 };
 __device__ __forceinline__ float act_lo(int act) { return act ? 0.f : -INFINITY; }
 __device__ __forceinline__ float act_hi(int act) { return act == ACT_RELU6 ? 6.f : INFINITY; }
 
+// clamp to [lo, hi] in one v_med3_f32
+__device__ __forceinline__ float clampf(float v, float lo, float hi) {
+  return __builtin_amdgcn_fmed3f(v, lo, hi);
+}
+
 __device__ __forceinline__ float apply_act(float v, int act) {
-  return fminf(fmaxf(v, act_lo(act)), act_hi(act));
+  return clampf(v, act_lo(act), act_hi(act));
 }
 
 // derivative mask of the activation evaluated at pre-activation value z (TF: relu' = z > 0,
@@ -77,7 +88,7 @@ __device__ __forceinline__ void affine_act8(float* v, const float* sc, const flo
   const float s[8] = {s0.x, s0.y, s0.z, s0.w, s1.x, s1.y, s1.z, s1.w};
   const float h[8] = {h0.x, h0.y, h0.z, h0.w, h1.x, h1.y, h1.z, h1.w};
 #pragma unroll
-  for (int j = 0; j < 8; ++j) v[j] = fminf(fmaxf(fmaf(v[j], s[j], h[j]), lo), hi);
+  for (int j = 0; j < 8; ++j) v[j] = clampf(fmaf(v[j], s[j], h[j]), lo, hi);
 }
 
 // Sum 8 per-lane column partials over the lanes of a wave that own the same 8-column chunk

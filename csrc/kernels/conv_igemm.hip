@@ -195,25 +195,30 @@ __global__ __launch_bounds__(256) void conv_igemm_kernel(ConvArgs a) {
       int idx = tid + i * NT;
       if (idx >= BM * CPR) break;
       int row = idx / CPR, ch = idx % CPR;
-      uint4 v = make_uint4(0, 0, 0, 0);
-      if (rvalid[i]) {
-        if constexpr (sizeof(TA) == 2) {
-          if constexpr (PRO) {
-            float f[8];
-            unpack8(ra[i], f);
-            affine_act8(f, s_scale + kc, s_shift + kc, pro_lo, pro_hi);
-            v = pack8(f);
-          } else {
-            v = ra[i];
-          }
-        } else {
+      // branch-free: transform unconditionally, then select zero for padding / tails (an
+      // exec-masked branch per chunk costs a scalar branch + waitcnt split per chunk)
+      uint4 v;
+      if constexpr (sizeof(TA) == 2) {
+        if constexpr (PRO) {
           float f[8];
-#pragma unroll
-          for (int j = 0; j < 8; ++j) f[j] = rpre[i][j];
-          if constexpr (PRO) affine_act8(f, s_scale + kc, s_shift + kc, pro_lo, pro_hi);
+          unpack8(ra[i], f);
+          affine_act8(f, s_scale + kc, s_shift + kc, pro_lo, pro_hi);
           v = pack8(f);
+        } else {
+          v = ra[i];
         }
+      } else {
+        float f[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) f[j] = rpre[i][j];
+        if constexpr (PRO) affine_act8(f, s_scale + kc, s_shift + kc, pro_lo, pro_hi);
+        v = pack8(f);
       }
+      const bool ok = rvalid[i];
+      v.x = ok ? v.x : 0u;
+      v.y = ok ? v.y : 0u;
+      v.z = ok ? v.z : 0u;
+      v.w = ok ? v.w : 0u;
       *reinterpret_cast<uint4*>(as + row * BK + swz_chunk<BK>(row, ch) * 8) = v;
     }
 #pragma unroll
@@ -221,8 +226,13 @@ __global__ __launch_bounds__(256) void conv_igemm_kernel(ConvArgs a) {
       int idx = tid + i * NT;
       if (idx >= BN * CPR) break;
       int row = idx / CPR, ch = idx % CPR;
-      *reinterpret_cast<uint4*>(bs + row * BK + swz_chunk<BK>(row, ch) * 8) =
-          S.bvalid[i] ? rb[i] : make_uint4(0, 0, 0, 0);
+      const bool ok = S.bvalid[i];
+      uint4 v = rb[i];
+      v.x = ok ? v.x : 0u;
+      v.y = ok ? v.y : 0u;
+      v.z = ok ? v.z : 0u;
+      v.w = ok ? v.w : 0u;
+      *reinterpret_cast<uint4*>(bs + row * BK + swz_chunk<BK>(row, ch) * 8) = v;
     }
   };
 
@@ -353,7 +363,7 @@ __global__ __launch_bounds__(256) void conv_igemm_kernel(ConvArgs a) {
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
           float t = v[j] + (a.bias ? a.bias[n + j] : 0.f);
-          v[j] = fminf(fmaxf(t, epi_lo), epi_hi);
+          v[j] = clampf(t, epi_lo, epi_hi);
         }
         if (a.out_mode == OUT_BF16) {
           uint4 p = pack8(v);
