@@ -196,6 +196,47 @@ __device__ __forceinline__ void bn_coeff_table(const BnArgs& b, int C, float* s_
   }
 }
 
+// Backward tables for channels [0, C): BN scale/shift (to recompute z = bn(x)) and mean/rstd
+// (for x-hat), all global loads of a batch of 4 channels per thread issued before any arithmetic.
+// mode 0 gives the identity (1, 0, 0, 1).
+template <int NT>
+__device__ __forceinline__ void bn_full_table(const BnArgs& b, int C, float* s_sc, float* s_sh, float* s_mu,
+                                              float* s_rs) {
+  const int tid = threadIdx.x;
+  if (b.mode == 0) {
+    for (int c = tid; c < C; c += NT) { s_sc[c] = 1.f; s_sh[c] = 0.f; s_mu[c] = 0.f; s_rs[c] = 1.f; }
+    return;
+  }
+  const float* p0 = b.mode == 1 ? b.stats : b.mmean;
+  const float* p1 = b.mode == 1 ? b.stats + b.C : b.mvar;
+  const float mul = b.mode == 1 ? b.inv_count : 1.f;
+  for (int base = 0; base < C; base += 4 * NT) {
+    float v0[4], v1[4], g[4], be[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      int c = base + u * NT + tid;
+      int cc = c < C ? c : 0;
+      v0[u] = p0[cc];
+      v1[u] = p1[cc];
+      g[u] = b.gamma ? b.gamma[cc] : 1.f;
+      be[u] = b.beta ? b.beta[cc] : 0.f;
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      int c = base + u * NT + tid;
+      if (c >= C) break;
+      float mean = v0[u] * mul;
+      float var = b.mode == 1 ? fmaxf(v1[u] * mul - mean * mean, 0.f) : v1[u];
+      float rs = rsqrtf(var + b.eps);
+      float sc = g[u] * rs;
+      s_sc[c] = sc;
+      s_sh[c] = be[u] - mean * sc;
+      s_mu[c] = mean;
+      s_rs[c] = rs;
+    }
+  }
+}
+
 // mean and 1/sigma of a channel (for x-hat in backward)
 __device__ __forceinline__ void bn_mean_rstd(const BnArgs& b, int c, float& mean, float& rstd) {
   float var;

@@ -34,6 +34,16 @@ struct ConvArgs {
   BnArgs mbn;         // the forward BN(+act) that was applied to mx
   float* gsum;        // [Cout] += sum(dZ)
   float* gsumx;       // [Cout] += sum(dZ * xhat)
+  // split-K (small-M, deep-K layers are K-loop latency bound): with ksplit > 1 each output tile's
+  // K range is split over `ksplit` workgroups; each publishes an fp32 partial tile to `slab`
+  // ([tiles][ksplit][TM*TN][256] float4) and takes a ticket; the tile's last arriver sums the
+  // partials and runs the epilogue.  Tickets count modulo ksplit (never reset in-kernel): one
+  // ticket array per op, zeroed whenever the op's split factor changes.
+  float* slab;
+  unsigned* tickets;
+  long long slab_floats;  // capacities, checked by the launcher before a split launch
+  int tickets_n;
+  int ksplit;
 };
 
 // tile TILE_HALO selects the one-image-per-workgroup direct 3x3 kernel (conv3x3_halo.hip)

@@ -36,7 +36,7 @@ template <int BK>
 __device__ __forceinline__ int swz_chunk(int row, int chunk) {
   if constexpr (BK == 32) return chunk ^ (((row >> 2) & 1) << 1);
   else if constexpr (BK == 64) return chunk ^ (row & 6);
-  else return chunk ^ (row & 15);  // BK 128: 16 chunks per 256-B row (brute-force checked)
+  else return chunk ^ (row & 15);  // BK 128 / 256: XOR within 16-chunk groups (brute-force checked)
 }
 
 template <int BM, int BN, int BK, int WM, int WN>
@@ -89,9 +89,17 @@ __global__ __launch_bounds__(256) void conv_igemm_kernel(ConvArgs a) {
   const int K = a.KH * a.KW * a.Cin;
   const int ntiles = (a.Cout + BN - 1) / BN;
   const int mtiles = (M + BM - 1) / BM;
-  const int bid = xcd_remap(blockIdx.x, mtiles * ntiles);
-  const int mt = bid / ntiles, nt = bid % ntiles;
+  const int nsplit = a.ksplit > 1 ? a.ksplit : 1;
+  // the slices of one output tile are consecutive logical ids -> same XCD under the remap, so the
+  // reducer reads same-XCD partials (a speed choice only: the hand-off is placement independent)
+  const int bid = xcd_remap(blockIdx.x, mtiles * ntiles * nsplit);
+  const int tile = bid / nsplit, slice = bid - tile * nsplit;
+  const int mt = tile / ntiles, nt = tile % ntiles;
   const int m0 = mt * BM, n0 = nt * BN;
+  const int nk_all = (K + BK - 1) / BK;
+  const int per_slice = (nk_all + nsplit - 1) / nsplit;
+  const int kt_begin = slice * per_slice;
+  const int nk = max(0, min(nk_all, kt_begin + per_slice) - kt_begin);
 
   // ---- per-thread A row decode (fixed for the whole K loop) -------------------------------
   const int my_chunk = tid % CPR;  // the k-chunk this thread stages (same for all its rows)
@@ -115,7 +123,7 @@ __global__ __launch_bounds__(256) void conv_igemm_kernel(ConvArgs a) {
       a_w0[i] = wo * a.SW - a.PL;
     }
   }
-  int kglob = my_chunk * 8;  // global k of this thread's chunk in the current tile
+  int kglob = kt_begin * BK + my_chunk * 8;  // global k of this thread's chunk in the current tile
   int kc = kglob, kr = 0, ks = 0;
   if constexpr (!IS1X1) {
     while (kc >= a.Cin) { kc -= a.Cin; if (++ks == a.KW) { ks = 0; ++kr; } }
@@ -250,7 +258,6 @@ __global__ __launch_bounds__(256) void conv_igemm_kernel(ConvArgs a) {
 #pragma unroll
     for (int j = 0; j < TN; ++j) acc[i][j] = (v4f){0.f, 0.f, 0.f, 0.f};
 
-  const int nk = (K + BK - 1) / BK;
   // the first two tiles are issued BEFORE the prologue tables are built: the tables' own global
   // loads (BN statistics, gamma, beta) then overlap the tile loads instead of adding a second
   // full memory latency in front of the K loop
@@ -326,6 +333,66 @@ __global__ __launch_bounds__(256) void conv_igemm_kernel(ConvArgs a) {
   if (kt < nk) {
     compute(0);  // odd tile count: the last tile sits in LDS0
     __syncthreads();  // the epilogue's fp32 staging tile aliases LDS0
+  }
+
+  // ---- split-K: publish this slice's partial tile; the last arriver of the tile reduces ------
+  // (guide §5 "In-launch split-K reduction": plain stores -> every wave vmcnt(0) -> barrier ->
+  //  lane 0 agent release -> asm vmcnt(0) -> relaxed agent ticket; reducer: agent acquire ->
+  //  asm vmcnt(0) -> barrier -> plain loads)
+  if (nsplit > 1) {
+    constexpr int NF = TM * TN;
+    float4* slab = reinterpret_cast<float4*>(a.slab) + (size_t)tile * nsplit * NF * NT;
+    {
+      float4* mine = slab + (size_t)slice * NF * NT;
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+          mine[(i * TN + j) * NT + tid] = make_float4(acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    int* s_flag = reinterpret_cast<int*>(smem);
+    if (tid == 0) {
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      const unsigned prev =
+          __hip_atomic_fetch_add(&a.tickets[tile], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      const int last = (prev % (unsigned)nsplit) == (unsigned)(nsplit - 1);
+      if (last) {
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      }
+      s_flag[0] = last;
+    }
+    __syncthreads();
+    const int last = s_flag[0];
+    __syncthreads();  // the epilogue reuses this LDS
+    if (!last) return;
+    // sum the other slices, four at a time with every load issued before the adds
+    for (int s0 = 0; s0 < nsplit; s0 += 4) {
+      float4 v[4][NF];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int sl = s0 + u;
+        const bool use = sl < nsplit && sl != slice;
+        const float4* o = slab + (size_t)(use ? sl : slice) * NF * NT;
+#pragma unroll
+        for (int f = 0; f < NF; ++f) v[u][f] = use ? o[f * NT + tid] : make_float4(0.f, 0.f, 0.f, 0.f);
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u)
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+          for (int j = 0; j < TN; ++j) {
+            const float4 q = v[u][i * TN + j];
+            acc[i][j][0] += q.x;
+            acc[i][j][1] += q.y;
+            acc[i][j][2] += q.z;
+            acc[i][j][3] += q.w;
+          }
+    }
   }
 
   // ---- epilogue: WM passes, each stages one wave-row (WTM x BN) of fp32 results in LDS ------
@@ -444,7 +511,12 @@ template <int BM, int BN, int BK, int WM, int WN>
 static hipError_t launch_cfg(const ConvArgs& a, bool is1x1, bool a_f32, int pro, int epi,
                              hipStream_t st) {
   const int M = a.N * a.Ho * a.Wo;
-  const int grid = ((M + BM - 1) / BM) * ((a.Cout + BN - 1) / BN);
+  const int tiles = ((M + BM - 1) / BM) * ((a.Cout + BN - 1) / BN);
+  if (a.ksplit > 1) {
+    // the partial slabs and tickets of every tile must fit the workspace the caller provided
+    if ((long long)tiles * a.ksplit * BM * BN > a.slab_floats || tiles > a.tickets_n) return hipErrorInvalidValue;
+  }
+  const int grid = tiles * (a.ksplit > 1 ? a.ksplit : 1);
   if (grid == 0) return hipSuccess;
   const size_t shm = IgemmCfg<BM, BN, BK, WM, WN>::smem_bytes(pro ? a.Cin : 0);
 #define IDC_L(IS1, TA, P, E)                                                                   \
@@ -472,7 +544,8 @@ static const TileInfo kTiles[] = {
     {128, 128}, {128, 64}, {256, 32}, {64, 64}, {64, 32},   // BK 32
     {128, 128}, {128, 64}, {128, 32}, {64, 64}, {64, 32},   // BK 64
     {256, 32}, {64, 128},                                  // BK 64
-    {64, 32}, {128, 32}, {64, 64}, {64, 128}, {128, 64}};  // BK 128: half the K steps of BK 64
+    {64, 32}, {128, 32}, {64, 64}, {64, 128}, {128, 64},   // BK 128: half the K steps of BK 64
+    {64, 32}, {64, 64}};  // BK 256: deep-K, small-M layers (stages 3-4) are K-loop latency bound
 
 int conv_num_tiles() { return (int)(sizeof(kTiles) / sizeof(kTiles[0])); }
 int conv_tile_bm(int t) { return kTiles[t].bm; }
@@ -483,7 +556,11 @@ hipError_t conv_igemm(const ConvArgs& a, int tile, bool a_f32, hipStream_t st) {
   const int pro = (a.pro.mode != 0 || a.pro.act != ACT_NONE) ? 1 : 0;
   const int epi = a.epi_mode;
   if ((a.Cin % 8) || (a.Cout % 8) || (a.ldx % 8) || (a.ldy % 8)) return hipErrorInvalidValue;
-  if (tile == TILE_HALO) return conv3x3_halo(a, a_f32, st);
+  if (a.ksplit > 1 && (a.slab == nullptr || a.tickets == nullptr)) return hipErrorInvalidValue;
+  if (tile == TILE_HALO) {
+    if (a.ksplit > 1) return hipErrorInvalidValue;
+    return conv3x3_halo(a, a_f32, st);
+  }
   switch (tile) {
     case 0: return launch_cfg<128, 128, 32, 2, 2>(a, is1x1, a_f32, pro, epi, st);
     case 1: return launch_cfg<128, 64, 32, 2, 2>(a, is1x1, a_f32, pro, epi, st);
@@ -502,6 +579,8 @@ hipError_t conv_igemm(const ConvArgs& a, int tile, bool a_f32, hipStream_t st) {
     case 14: return launch_cfg<64, 64, 128, 2, 2>(a, is1x1, a_f32, pro, epi, st);
     case 15: return launch_cfg<64, 128, 128, 2, 2>(a, is1x1, a_f32, pro, epi, st);
     case 16: return launch_cfg<128, 64, 128, 2, 2>(a, is1x1, a_f32, pro, epi, st);
+    case 17: return launch_cfg<64, 32, 256, 2, 2>(a, is1x1, a_f32, pro, epi, st);
+    case 18: return launch_cfg<64, 64, 256, 2, 2>(a, is1x1, a_f32, pro, epi, st);
     default: return hipErrorInvalidValue;
   }
 }

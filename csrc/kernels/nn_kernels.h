@@ -82,8 +82,8 @@ struct CastEntry {
   bf16_t* fwd;       // [Cout][KH][KW][Cpad]
   bf16_t* dgrad;     // [Cin][KH][KW][Cout] flipped (may be null)
   int KH, KW, Cin, Cout, Cpad;
-  int dw;            // 1: depthwise kernel (KH,KW,C,1) -> [C][KH][KW] (fwd only)
-  long long begin;   // prefix offset in the flat thread space
+  int dw;            // reserved (depthwise kernels are read from the fp32 master directly)
+  long long begin;   // first tile of this entry in the launch's tile space (64x64 tiles of [KH*KW*Cin][Cout])
 };
 
 hipError_t bn_bwd_apply(const BnBwdApplyArgs& a, hipStream_t st);
@@ -100,7 +100,7 @@ hipError_t rmsprop(float* w, const float* g, float* ms, long long n, float lr, f
 hipError_t finite_check(const float* g, long long n, int* flag, hipStream_t st);
 // status[0] = flag (last step skipped?), status[1] += flag (skipped steps), flag = 0
 hipError_t finite_flag_reset(int* flag, int* status, hipStream_t st);
-hipError_t cast_weights(const CastEntry* d_entries, int n, long long total, hipStream_t st);
+hipError_t cast_weights(const CastEntry* d_entries, const int* tile_entry, long long ntiles, hipStream_t st);
 hipError_t input_stage(const void* x, int x_u8, int N, int H, int W, int C, bf16_t* y, int Cpad,
                        hipStream_t st);
 hipError_t bn_stats(const bf16_t* x, int ldx, int M, int C, float* stats, int stats_ld,

@@ -96,6 +96,33 @@ __device__ __forceinline__ void flush_sums(float* s_a, float* s_b, int C, float*
   }
 }
 
+// Per-channel block totals of per-thread 8-channel partials laid out by ChunkMap (thread (tx, ty)
+// owns channels [8tx, 8tx+8) of row group ty): partials are transposed through LDS and summed
+// down the row groups, so no LDS address sees more than one writer (per-thread LDS float atomics
+// here serialise R = 256/(C/8) ways).  `tmp` holds 2*256*8 floats; results land in s_a / s_b.
+__device__ __forceinline__ void chunk_reduce(const ChunkMap& cm, int C, const float* pa, const float* pb,
+                                             float* tmp, float* s_a, float* s_b) {
+  float* ta = tmp;
+  float* tb = tmp + 256 * 8;
+  if (cm.active()) {
+    const int o = cm.ty * C + cm.tx * 8;
+    *reinterpret_cast<float4*>(ta + o) = make_float4(pa[0], pa[1], pa[2], pa[3]);
+    *reinterpret_cast<float4*>(ta + o + 4) = make_float4(pa[4], pa[5], pa[6], pa[7]);
+    *reinterpret_cast<float4*>(tb + o) = make_float4(pb[0], pb[1], pb[2], pb[3]);
+    *reinterpret_cast<float4*>(tb + o + 4) = make_float4(pb[4], pb[5], pb[6], pb[7]);
+  }
+  __syncthreads();
+  for (int c = threadIdx.x; c < C; c += blockDim.x) {
+    float sa = 0.f, sb = 0.f;
+    for (int r = 0; r < cm.R; ++r) {
+      sa += ta[r * C + c];
+      sb += tb[r * C + c];
+    }
+    s_a[c] = sa;
+    s_b[c] = sb;
+  }
+}
+
 }  // namespace
 
 // ------------------------------------------------------------------------------------------
@@ -211,15 +238,8 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(BnBwdReduceArgs a) {
   float* s_rs = sh + 3 * a.C;
   float* s_a = sh + 4 * a.C;
   float* s_b = sh + 5 * a.C;
-  for (int c = threadIdx.x; c < a.C; c += blockDim.x) {
-    bn_coeffs(a.bn, c, s_sc[c], s_sh[c]);
-    float mean = 0.f, rstd = 1.f;
-    if (a.bn.mode) bn_mean_rstd(a.bn, c, mean, rstd);
-    s_mu[c] = mean;
-    s_rs[c] = rstd;
-    s_a[c] = 0.f;
-    s_b[c] = 0.f;
-  }
+  float* s_tmp = sh + 6 * a.C;
+  bn_full_table<256>(a.bn, a.C, s_sc, s_sh, s_mu, s_rs);
   __syncthreads();
   ChunkMap cm(a.C);
   float ps[8] = {0}, px[8] = {0};
@@ -242,18 +262,15 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(BnBwdReduceArgs a) {
         px[j] += d[j] * (x[j] - s_mu[c + j]) * s_rs[c + j];
       }
     }
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      atomicAdd(&s_a[c + j], ps[j]);
-      atomicAdd(&s_b[c + j], px[j]);
-    }
   }
+  chunk_reduce(cm, a.C, ps, px, s_tmp, s_a, s_b);
   flush_sums(s_a, s_b, a.C, a.gsum, a.gsumx);
 }
 
 hipError_t bn_bwd_reduce(const BnBwdReduceArgs& a, hipStream_t st) {
   if (a.M == 0) return hipSuccess;
-  hipLaunchKernelGGL(bn_bwd_reduce_kernel, dim3(grid_rows(a.M, a.C, 4)), dim3(256), 6 * a.C * 4, st, a);
+  hipLaunchKernelGGL(bn_bwd_reduce_kernel, dim3(grid_rows(a.M, a.C, 4)), dim3(256),
+                     (6 * a.C + 2 * 256 * 8) * 4, st, a);
   return hipGetLastError();
 }
 
@@ -265,11 +282,8 @@ __global__ __launch_bounds__(256) void pool_fwd_kernel(PoolArgs a) {
   float* s_sh = sh + a.C;
   float* s_a = sh + 2 * a.C;
   float* s_b = sh + 3 * a.C;
-  for (int c = threadIdx.x; c < a.C; c += blockDim.x) {
-    bn_coeffs(a.pro, c, s_sc[c], s_sh[c]);
-    s_a[c] = 0.f;
-    s_b[c] = 0.f;
-  }
+  float* s_tmp = sh + 4 * a.C;
+  bn_coeff_table<256>(a.pro, a.C, s_sc, s_sh);
   __syncthreads();
   ChunkMap cm(a.C);
   const int Mo = a.N * a.Ho * a.Wo;
@@ -324,28 +338,30 @@ __global__ __launch_bounds__(256) void pool_fwd_kernel(PoolArgs a) {
         for (int j = 0; j < 8; ++j) { ps[j] += out[j]; pq[j] += out[j] * out[j]; }
       }
     }
-    if (a.stats) {
-#pragma unroll
-      for (int j = 0; j < 8; ++j) { atomicAdd(&s_a[c + j], ps[j]); atomicAdd(&s_b[c + j], pq[j]); }
-    }
   }
+  if (a.stats) chunk_reduce(cm, a.C, ps, pq, s_tmp, s_a, s_b);
   if (a.stats)
     flush_sums(s_a, s_b, a.C, a.stats + a.stats_off, a.stats + a.stats_ld + a.stats_off);
 }
 
 hipError_t maxpool_fwd(const PoolArgs& a, hipStream_t st) {
   hipLaunchKernelGGL(pool_fwd_kernel<true>, dim3(grid_rows(a.N * a.Ho * a.Wo, a.C)), dim3(256),
-                     4 * a.C * 4, st, a);
+                     (4 * a.C + 2 * 256 * 8) * 4, st, a);
   return hipGetLastError();
 }
 
 hipError_t avgpool_fwd(const PoolArgs& a, hipStream_t st) {
   hipLaunchKernelGGL(pool_fwd_kernel<false>, dim3(grid_rows(a.N * a.Ho * a.Wo, a.C)), dim3(256),
-                     4 * a.C * 4, st, a);
+                     (4 * a.C + 2 * 256 * 8) * 4, st, a);
   return hipGetLastError();
 }
 
-// gather-form pool backward: each input element collects from the windows that contain it
+// Gather-form pool backward: each input element collects from the windows that contain it, then
+// (optionally) the backward of the pending BN+act that fed the pool: dZ = g * act'(bn(x)) and the
+// BN-backward sums.  WIN = windows covering an input pixel per spatial dim (1 when k <= s, 2 when
+// k <= 2s): the window loop is unrolled and predicated, and each thread issues the loads of RU
+// rows (every window's dy / argmax, and x) before any arithmetic.
+template <int WIN, int RU>
 __global__ __launch_bounds__(256) void pool_bwd_kernel(PoolBwdArgs a) {
   extern __shared__ float sh[];
   float* s_sc = sh;
@@ -354,78 +370,119 @@ __global__ __launch_bounds__(256) void pool_bwd_kernel(PoolBwdArgs a) {
   float* s_rs = sh + 3 * a.C;
   float* s_a = sh + 4 * a.C;
   float* s_b = sh + 5 * a.C;
+  float* s_tmp = sh + 6 * a.C;
   const bool epi = (a.bn.mode != 0 || a.bn.act != ACT_NONE);
-  for (int c = threadIdx.x; c < a.C; c += blockDim.x) {
-    bn_coeffs(a.bn, c, s_sc[c], s_sh[c]);
-    float mean = 0.f, rstd = 1.f;
-    if (a.bn.mode) bn_mean_rstd(a.bn, c, mean, rstd);
-    s_mu[c] = mean; s_rs[c] = rstd; s_a[c] = 0.f; s_b[c] = 0.f;
-  }
+  const bool sums = epi && (a.gsum || a.gsumx);
+  if (epi) bn_full_table<256>(a.bn, a.C, s_sc, s_sh, s_mu, s_rs);
   __syncthreads();
   ChunkMap cm(a.C);
   const int Mi = a.N * a.H * a.W;
-  float ps[8] = {0}, px[8] = {0};
+  float ps[8] = {0, 0, 0, 0, 0, 0, 0, 0}, px[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  const float lo = act_lo(a.bn.act), hi = act_hi(a.bn.act);
   if (cm.active()) {
     const int c = cm.tx * 8;
     const float inv = 1.f / (float)(a.k * a.k);
-    for (int i = blockIdx.x * cm.R + cm.ty; i < Mi; i += gridDim.x * cm.R) {
-      int w = i % a.W, t = i / a.W, h = t % a.H, n = t / a.H;
-      float g[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-      // windows oh with oh*s - pt <= h <= oh*s - pt + k - 1
-      int oh_lo = (h + a.pt - a.k + 1 + a.s - 1);
-      oh_lo = oh_lo < 0 ? 0 : oh_lo / a.s;
-      int oh_hi = (h + a.pt) / a.s;
-      int ow_lo = (w + a.pl - a.k + 1 + a.s - 1);
-      ow_lo = ow_lo < 0 ? 0 : ow_lo / a.s;
-      int ow_hi = (w + a.pl) / a.s;
-      if (oh_hi >= a.Ho) oh_hi = a.Ho - 1;
-      if (ow_hi >= a.Wo) ow_hi = a.Wo - 1;
-      for (int oh = oh_lo; oh <= oh_hi; ++oh)
-        for (int ow = ow_lo; ow <= ow_hi; ++ow) {
-          size_t o = (size_t)(n * a.Ho + oh) * a.Wo + ow;
-          float d[8];
-          load8(a.dy, a.dy_f32, o * a.lddy + c, d);
+    const int step = gridDim.x * cm.R;
+    for (int i0 = blockIdx.x * cm.R + cm.ty; i0 < Mi; i0 += step * RU) {
+      float d[RU][WIN * WIN][8];
+      uint2 am[RU][WIN * WIN];
+      bool ok[RU][WIN * WIN];
+      uint8_t mine[RU][WIN * WIN];
+      uint4 xr[RU];
+      int rows[RU];
+#pragma unroll
+      for (int u = 0; u < RU; ++u) {
+        const int i = i0 + u * step;
+        rows[u] = i < Mi ? i : Mi - 1;
+        const int ii = rows[u];
+        const int w = ii % a.W, t = ii / a.W, h = t % a.H, n = t / a.H;
+        // windows oh with oh*s - pt <= h <= oh*s - pt + k - 1
+        int oh_lo = h + a.pt - a.k + 1 + a.s - 1;
+        oh_lo = oh_lo < 0 ? 0 : oh_lo / a.s;
+        int oh_hi = (h + a.pt) / a.s;
+        int ow_lo = w + a.pl - a.k + 1 + a.s - 1;
+        ow_lo = ow_lo < 0 ? 0 : ow_lo / a.s;
+        int ow_hi = (w + a.pl) / a.s;
+        oh_hi = oh_hi < a.Ho - 1 ? oh_hi : a.Ho - 1;
+        ow_hi = ow_hi < a.Wo - 1 ? ow_hi : a.Wo - 1;
+#pragma unroll
+        for (int dh = 0; dh < WIN; ++dh)
+#pragma unroll
+          for (int dw = 0; dw < WIN; ++dw) {
+            const int q = dh * WIN + dw;
+            const int oh = oh_lo + dh, ow = ow_lo + dw;
+            const bool v = (i < Mi) && oh <= oh_hi && ow <= ow_hi;
+            ok[u][q] = v;
+            const size_t o = v ? (size_t)(n * a.Ho + oh) * a.Wo + ow : 0;
+            load8(a.dy, a.dy_f32, o * a.lddy + c, d[u][q]);
+            if (!a.is_avg) {
+              am[u][q] = *reinterpret_cast<const uint2*>(a.argmax + o * a.C + c);
+              mine[u][q] = (uint8_t)((h - (oh * a.s - a.pt)) * a.k + (w - (ow * a.s - a.pl)));
+            }
+          }
+        if (epi) xr[u] = *reinterpret_cast<const uint4*>(a.x + (size_t)rows[u] * a.ldx + c);
+      }
+#pragma unroll
+      for (int u = 0; u < RU; ++u) {
+        if (i0 + u * step >= Mi) break;
+        float g[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+#pragma unroll
+        for (int q = 0; q < WIN * WIN; ++q) {
+          if (!ok[u][q]) continue;
           if (a.is_avg) {
 #pragma unroll
-            for (int j = 0; j < 8; ++j) g[j] += d[j] * inv;
+            for (int j = 0; j < 8; ++j) g[j] += d[u][q][j] * inv;
           } else {
-            int rr = h - (oh * a.s - a.pt), ss = w - (ow * a.s - a.pl);
-            uint8_t mine = (uint8_t)(rr * a.k + ss);
-            uint2 ar = *reinterpret_cast<const uint2*>(a.argmax + o * a.C + c);
-            uint8_t am[8] = {(uint8_t)(ar.x), (uint8_t)(ar.x >> 8), (uint8_t)(ar.x >> 16), (uint8_t)(ar.x >> 24),
-                             (uint8_t)(ar.y), (uint8_t)(ar.y >> 8), (uint8_t)(ar.y >> 16), (uint8_t)(ar.y >> 24)};
+            const uint2 ar = am[u][q];
 #pragma unroll
-            for (int j = 0; j < 8; ++j) g[j] += (am[j] == mine) ? d[j] : 0.f;
+            for (int j = 0; j < 8; ++j) {
+              const uint32_t word = j < 4 ? ar.x : ar.y;
+              const uint8_t b = (uint8_t)(word >> (8 * (j & 3)));
+              g[j] += (b == mine[u][q]) ? d[u][q][j] : 0.f;
+            }
           }
         }
-      if (epi) {
-        float x[8];
-        unpack8(*reinterpret_cast<const uint4*>(a.x + (size_t)i * a.ldx + c), x);
+        bf16_t* dst = a.dx + (size_t)rows[u] * a.lddx + c;
+        if (epi) {
+          float x[8];
+          unpack8(xr[u], x);
 #pragma unroll
-        for (int j = 0; j < 8; ++j) g[j] *= act_mask(x[j] * s_sc[c + j] + s_sh[c + j], a.bn.act);
-        uint4 p = pack8(g);
-        *reinterpret_cast<uint4*>(a.dx + (size_t)i * a.lddx + c) = p;
-        unpack8(p, g);
+          for (int j = 0; j < 8; ++j) {
+            const float z = x[j] * s_sc[c + j] + s_sh[c + j];
+            g[j] = (z > lo && z < hi) ? g[j] : 0.f;
+          }
+          const uint4 p = pack8(g);
+          *reinterpret_cast<uint4*>(dst) = p;
+          if (sums) {
+            unpack8(p, g);  // reduce exactly what was stored
 #pragma unroll
-        for (int j = 0; j < 8; ++j) {
-          ps[j] += g[j];
-          px[j] += g[j] * (x[j] - s_mu[c + j]) * s_rs[c + j];
+            for (int j = 0; j < 8; ++j) {
+              ps[j] += g[j];
+              px[j] += g[j] * (x[j] - s_mu[c + j]) * s_rs[c + j];
+            }
+          }
+        } else {
+          *reinterpret_cast<uint4*>(dst) = pack8(g);
         }
-      } else {
-        *reinterpret_cast<uint4*>(a.dx + (size_t)i * a.lddx + c) = pack8(g);
       }
     }
-    if (epi && (a.gsum || a.gsumx)) {
-#pragma unroll
-      for (int j = 0; j < 8; ++j) { atomicAdd(&s_a[c + j], ps[j]); atomicAdd(&s_b[c + j], px[j]); }
-    }
   }
-  if (epi && (a.gsum || a.gsumx)) flush_sums(s_a, s_b, a.C, a.gsum, a.gsumx);
+  if (sums) {
+    chunk_reduce(cm, a.C, ps, px, s_tmp, s_a, s_b);
+    flush_sums(s_a, s_b, a.C, a.gsum, a.gsumx);
+  }
 }
 
 hipError_t pool_bwd(const PoolBwdArgs& a, hipStream_t st) {
-  hipLaunchKernelGGL(pool_bwd_kernel, dim3(grid_rows(a.N * a.H * a.W, a.C)), dim3(256),
-                     6 * a.C * 4, st, a);
+  const size_t shm = (6 * a.C + 2 * 256 * 8) * 4;
+  const int M = a.N * a.H * a.W;
+  if (a.k <= a.s) {
+    hipLaunchKernelGGL((pool_bwd_kernel<1, 4>), dim3(grid_rows(M, a.C, 4)), dim3(256), shm, st, a);
+  } else if (a.k <= 2 * a.s) {
+    hipLaunchKernelGGL((pool_bwd_kernel<2, 2>), dim3(grid_rows(M, a.C, 2)), dim3(256), shm, st, a);
+  } else {
+    return hipErrorInvalidValue;  // windows overlapping more than 2 per dim: not used by any model
+  }
   return hipGetLastError();
 }
 
@@ -515,46 +572,74 @@ hipError_t head_fwd(const HeadArgs& a, hipStream_t st) {
   return hipGetLastError();
 }
 
-// head backward: block per 64-channel slice; reduces over the batch for dW, writes dA
+// head backward on a 2-D grid: blockIdx.x = 64-channel slice, blockIdx.y = chunk of HB samples.
+// Each of the 4 waves owns HB/4 samples of the chunk; dW partials are reduced over the waves in
+// LDS and added once per (channel, unit) per chunk; dA = (dlogits . W^T) / HW is broadcast over
+// the pixels with 4 loads/stores in flight per lane.  (One block per channel slice — the old
+// form — left 16 blocks looping over all 256 samples: ~50 us for a 1 us job.)
+template <int HB>
 __global__ __launch_bounds__(256) void head_bwd_kernel(HeadBwdArgs a) {
-  __shared__ float s_dw[64][17];
+  __shared__ float s_dw[4][64][17];
+  __shared__ float s_dl[HB][16];
   const int c0 = blockIdx.x * 64;
-  const int cl = threadIdx.x & 63, grp = threadIdx.x >> 6;  // 4 sample groups
+  const int n0 = blockIdx.y * HB;
+  const int cl = threadIdx.x & 63, grp = threadIdx.x >> 6;
   const int c = c0 + cl;
+  const bool cok = c < a.C;
+  for (int i = threadIdx.x; i < HB * a.U; i += blockDim.x) {
+    const int n = n0 + i / a.U;
+    s_dl[i / a.U][i % a.U] = n < a.N ? a.dlogits[n * a.U + i % a.U] : 0.f;
+  }
+  float wc[16];
+#pragma unroll
+  for (int u = 0; u < 16; ++u) wc[u] = (cok && u < a.U) ? a.w[(size_t)c * a.U + u] : 0.f;
+  __syncthreads();
   float acc[16];
+#pragma unroll
   for (int u = 0; u < 16; ++u) acc[u] = 0.f;
   const float inv_hw = 1.f / (float)a.HW;
-  for (int n = grp; n < a.N; n += 4) {
-    float f = (c < a.C) ? a.feats[(size_t)n * a.C + c] : 0.f;
+  constexpr int PER = HB / 4;
+  float f[PER];
+#pragma unroll
+  for (int k = 0; k < PER; ++k) {
+    const int n = n0 + grp * PER + k;
+    f[k] = (cok && n < a.N) ? a.feats[(size_t)n * a.C + c] : 0.f;
+  }
+#pragma unroll
+  for (int k = 0; k < PER; ++k) {
+    const int nl = grp * PER + k, n = n0 + nl;
     float df = 0.f;
-    for (int u = 0; u < a.U; ++u) {
-      float dl = a.dlogits[n * a.U + u];
-      acc[u] += f * dl;
-      if (c < a.C) df += dl * a.w[(size_t)c * a.U + u];
+#pragma unroll
+    for (int u = 0; u < 16; ++u) {
+      const float dl = u < a.U ? s_dl[nl][u] : 0.f;
+      acc[u] += f[k] * dl;
+      df += dl * wc[u];
     }
-    if (c < a.C) {
-      float v = df * inv_hw;
-      for (int p = 0; p < a.HW; ++p) a.dA[((size_t)n * a.HW + p) * a.ldda + c] = v;
+    if (a.dA && cok && n < a.N) {
+      const float v = df * inv_hw;
+      float* dst = a.dA + (size_t)n * a.HW * a.ldda + c;
+      for (int p = 0; p < a.HW; ++p) dst[(size_t)p * a.ldda] = v;
     }
   }
-  for (int u = 0; u < a.U; ++u) {
-    if (grp == 0) s_dw[cl][u] = 0.f;
-  }
+#pragma unroll
+  for (int u = 0; u < 16; ++u)
+    if (u < a.U) s_dw[grp][cl][u] = acc[u];
   __syncthreads();
-  for (int u = 0; u < a.U; ++u) atomicAdd(&s_dw[cl][u], acc[u]);
-  __syncthreads();
-  if (grp == 0 && c < a.C)
-    for (int u = 0; u < a.U; ++u) atomicAdd(&a.dw[(size_t)c * a.U + u], s_dw[cl][u]);
+  if (grp == 0 && cok)
+    for (int u = 0; u < a.U; ++u)
+      atomicAdd(&a.dw[(size_t)c * a.U + u], s_dw[0][cl][u] + s_dw[1][cl][u] + s_dw[2][cl][u] + s_dw[3][cl][u]);
   if (blockIdx.x == 0 && threadIdx.x < a.U && a.db) {
-    float s = 0.f;
-    for (int n = 0; n < a.N; ++n) s += a.dlogits[n * a.U + threadIdx.x];
-    atomicAdd(&a.db[threadIdx.x], s);
+    float sdb = 0.f;
+    for (int k = 0; k < HB; ++k) sdb += s_dl[k][threadIdx.x];
+    atomicAdd(&a.db[threadIdx.x], sdb);
   }
 }
 
 hipError_t head_bwd(const HeadBwdArgs& a, hipStream_t st) {
   if (a.U > 16) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(head_bwd_kernel, dim3((a.C + 63) / 64), dim3(256), 0, st, a);
+  constexpr int HB = 16;
+  dim3 grid((a.C + 63) / 64, (a.N + HB - 1) / HB);
+  hipLaunchKernelGGL(head_bwd_kernel<HB>, grid, dim3(256), 0, st, a);
   return hipGetLastError();
 }
 
@@ -649,46 +734,74 @@ hipError_t rmsprop(float* w, const float* g, float* ms, long long n, float lr, f
 }
 
 // ------------------------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void cast_weights_kernel(const CastEntry* __restrict__ es, int n,
-                                                           long long total) {
-  for (long long t = blockIdx.x * (long long)blockDim.x + threadIdx.x; t < total;
-       t += (long long)gridDim.x * blockDim.x) {
-    int lo = 0, hi = n - 1;
-    while (lo < hi) {
-      int mid = (lo + hi + 1) >> 1;
-      if (es[mid].begin <= t) lo = mid; else hi = mid - 1;
+// fp32 Keras HWIO masters -> bf16 kernel layouts, as a tiled transpose.  A kernel is the
+// row-major matrix src[R = KH*KW*Cin][Cout]; one block moves one 64x64 tile of it:
+//   dgrad [Cin][KH][KW][Cout] (spatially flipped): rows stay rows -> written straight from the
+//         coalesced loads (Cout contiguous on both sides);
+//   fwd   [Cout][KH][KW][Cpad]: the transpose -> staged through LDS, written K-contiguous.
+// Blocks map to (entry, tile) through a host-built tile -> entry table (`begin` = the entry's
+// first tile), so there is no per-element search and every global access is coalesced.
+__global__ __launch_bounds__(256) void cast_weights_kernel(const CastEntry* __restrict__ es,
+                                                           const int* __restrict__ tile_entry,
+                                                           long long ntiles) {
+  __shared__ float tile[64][65];
+  for (long long b = blockIdx.x; b < ntiles; b += gridDim.x) {
+    const CastEntry& e = es[tile_entry[b]];
+    const int R = e.KH * e.KW * e.Cin;
+    const int tiles_c = (e.Cout + 63) / 64;
+    const long long lt = b - e.begin;
+    const int r0 = (int)(lt / tiles_c) * 64, c0 = (int)(lt % tiles_c) * 64;
+    const int col = c0 + (threadIdx.x & 15) * 4;
+    const bool vec = (e.Cout & 3) == 0;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const int rl = (threadIdx.x >> 4) + 16 * k, r = r0 + rl;
+      float v[4] = {0.f, 0.f, 0.f, 0.f};
+      if (r < R) {
+        const float* src = e.src + (size_t)r * e.Cout;
+        if (vec && col + 3 < e.Cout) {
+          const float4 q = *reinterpret_cast<const float4*>(src + col);
+          v[0] = q.x; v[1] = q.y; v[2] = q.z; v[3] = q.w;
+        } else {
+#pragma unroll
+          for (int j = 0; j < 4; ++j) v[j] = col + j < e.Cout ? src[col + j] : 0.f;
+        }
+        if (e.dgrad) {
+          // src row r = (ri, si, ci) -> dgrad row (ci, KH-1-ri, KW-1-si)
+          const int ci = r % e.Cin, rs = r / e.Cin, si = rs % e.KW, ri = rs / e.KW;
+          bf16_t* dst = e.dgrad + (((size_t)ci * e.KH + (e.KH - 1 - ri)) * e.KW + (e.KW - 1 - si)) * e.Cout;
+          if (vec && col + 3 < e.Cout) {
+            *reinterpret_cast<uint2*>(dst + col) = make_uint2(pack2bf(v[0], v[1]), pack2bf(v[2], v[3]));
+          } else {
+            for (int j = 0; j < 4; ++j)
+              if (col + j < e.Cout) dst[col + j] = f2bf(v[j]);
+          }
+        }
+      }
+#pragma unroll
+      for (int j = 0; j < 4; ++j) tile[rl][(threadIdx.x & 15) * 4 + j] = v[j];
     }
-    const CastEntry& e = es[lo];
-    long long i = t - e.begin;
-    if (e.dw) {
-      // depthwise (KH,KW,C,1) -> [C][KH][KW]
-      int rs = (int)(i % (e.KH * e.KW));
-      int c = (int)(i / (e.KH * e.KW));
-      e.fwd[i] = f2bf(e.src[(size_t)rs * e.Cin + c]);
-      continue;
+    __syncthreads();
+    // fwd: 64 output channels x 64 K rows; consecutive lanes write consecutive K positions
+    const int ldd = e.KH * e.KW * e.Cpad;
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+      const int idx = threadIdx.x + 256 * k;
+      const int cl = idx >> 6, rl = idx & 63;
+      const int co = c0 + cl, r = r0 + rl;
+      if (co < e.Cout && r < R) {
+        const int ci = r % e.Cin, rs = r / e.Cin;
+        e.fwd[(size_t)co * ldd + (size_t)rs * e.Cpad + ci] = f2bf(tile[rl][cl]);
+      }
     }
-    // destination index i over [Cout][KH][KW][Cpad]
-    int c = (int)(i % e.Cpad);
-    long long t2 = i / e.Cpad;
-    int s = (int)(t2 % e.KW);
-    t2 /= e.KW;
-    int r = (int)(t2 % e.KH);
-    int co = (int)(t2 / e.KH);
-    float v = 0.f;
-    if (c < e.Cin) v = e.src[(((size_t)r * e.KW + s) * e.Cin + c) * e.Cout + co];
-    e.fwd[i] = f2bf(v);
-    if (e.dgrad && c < e.Cin) {
-      // Wf[c][KH-1-r][KW-1-s][co]
-      e.dgrad[(((size_t)c * e.KH + (e.KH - 1 - r)) * e.KW + (e.KW - 1 - s)) * e.Cout + co] = f2bf(v);
-    }
+    __syncthreads();
   }
 }
 
-hipError_t cast_weights(const CastEntry* d_entries, int n, long long total, hipStream_t st) {
-  if (n == 0 || total == 0) return hipSuccess;
-  long long blocks = (total + 255) / 256;
-  if (blocks > 4096) blocks = 4096;
-  hipLaunchKernelGGL(cast_weights_kernel, dim3((int)blocks), dim3(256), 0, st, d_entries, n, total);
+hipError_t cast_weights(const CastEntry* d_entries, const int* tile_entry, long long ntiles, hipStream_t st) {
+  if (d_entries == nullptr || ntiles == 0) return hipSuccess;
+  long long blocks = ntiles < 8192 ? ntiles : 8192;
+  hipLaunchKernelGGL(cast_weights_kernel, dim3((int)blocks), dim3(256), 0, st, d_entries, tile_entry, ntiles);
   return hipGetLastError();
 }
 

@@ -226,7 +226,12 @@ class Plan {
 
   void exec(const Op& op, hipStream_t st) {
     switch (op.kind) {
-      case OP_CONV: check(conv_igemm(as<ConvArgs>(op), op.i[0], op.i[1] != 0, st), "conv_igemm"); break;
+      case OP_CONV: {
+        ConvArgs a = as<ConvArgs>(op);
+        a.ksplit = op.i[2] > 1 ? op.i[2] : 1;  // split factor lives in the op (autotuned)
+        check(conv_igemm(a, op.i[0], op.i[1] != 0, st), "conv_igemm");
+        break;
+      }
       case OP_WGRAD: check(conv_wgrad(as<WgradArgs>(op), op.i[0], op.i[1] != 0, st), "conv_wgrad"); break;
       case OP_BN_BWD_APPLY: check(bn_bwd_apply(as<BnBwdApplyArgs>(op), st), "bn_bwd_apply"); break;
       case OP_BN_BWD_REDUCE: check(bn_bwd_reduce(as<BnBwdReduceArgs>(op), st), "bn_bwd_reduce"); break;
@@ -246,7 +251,9 @@ class Plan {
               "rmsprop");
         break;
       case OP_CAST:
-        check(cast_weights(reinterpret_cast<const CastEntry*>(op.p[0]), op.i[0], op.l[0], st), "cast_weights");
+        check(cast_weights(reinterpret_cast<const CastEntry*>(op.p[0]), reinterpret_cast<const int*>(op.p[1]),
+                           op.l[0], st),
+              "cast_weights");
         break;
       case OP_INPUT:
         check(input_stage(reinterpret_cast<const void*>(op.p[0]), op.i[0], op.i[1], op.i[2], op.i[3], op.i[4],
@@ -336,6 +343,7 @@ py::dict struct_sizes() {
   d["Mlp2Args"] = sizeof(Mlp2Args);
   d["ConvArgs.mbn"] = offsetof(ConvArgs, mbn);
   d["ConvArgs.gsumx"] = offsetof(ConvArgs, gsumx);
+  d["ConvArgs.ksplit"] = offsetof(ConvArgs, ksplit);
   d["WgradArgs.pix_per_split"] = offsetof(WgradArgs, pix_per_split);
   d["HeadArgs.training"] = offsetof(HeadArgs, training);
   d["PoolBwdArgs.is_avg"] = offsetof(PoolBwdArgs, is_avg);

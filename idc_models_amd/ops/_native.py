@@ -36,7 +36,9 @@ class ConvArgs(C.Structure):
                 ("w", vp), ("KH", ci), ("KW", ci), ("SH", ci), ("SW", ci), ("PT", ci), ("PL", ci),
                 ("pro", BnArgs), ("epi_mode", ci), ("bias", vp), ("epi_act", ci), ("out_mode", ci),
                 ("stats_out", vp), ("stats_ld", ci), ("stats_off", ci),
-                ("mx", vp), ("ldmx", ci), ("mbn", BnArgs), ("gsum", vp), ("gsumx", vp)]
+                ("mx", vp), ("ldmx", ci), ("mbn", BnArgs), ("gsum", vp), ("gsumx", vp),
+                ("slab", vp), ("tickets", vp), ("slab_floats", cll), ("tickets_n", ci),
+                ("ksplit", ci)]
 
 
 class WgradArgs(C.Structure):
@@ -130,6 +132,7 @@ def _verify(ext):
         if C.sizeof(cls) != sizes[name]:
             raise RuntimeError(f"native struct {name}: ctypes {C.sizeof(cls)} != C++ {sizes[name]}")
     checks = {"ConvArgs.mbn": ConvArgs.mbn.offset, "ConvArgs.gsumx": ConvArgs.gsumx.offset,
+              "ConvArgs.ksplit": ConvArgs.ksplit.offset,
               "WgradArgs.pix_per_split": WgradArgs.pix_per_split.offset,
               "HeadArgs.training": HeadArgs.training.offset,
               "PoolBwdArgs.is_avg": PoolBwdArgs.is_avg.offset}

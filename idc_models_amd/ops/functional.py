@@ -66,7 +66,7 @@ def conv2d(x: torch.Tensor, kernel_hwio: torch.Tensor, stride=(1, 1), pads=(0, 0
            out_hw: Optional[Tuple[int, int]] = None, pro: Optional[BN] = None,
            bias: Optional[torch.Tensor] = None, act: int = 0, out_f32: bool = False,
            stats: Optional[torch.Tensor] = None, tile: int = -1,
-           w_layout: Optional[torch.Tensor] = None) -> torch.Tensor:
+           w_layout: Optional[torch.Tensor] = None, ksplit: int = 1) -> torch.Tensor:
     """y = act(conv(pro(x)) + bias); x NHWC (bf16 or fp32), Cin % 8 == 0.  Optional output
     statistics [sum|sumsq] accumulated into ``stats``."""
     N, H, W, Cin = x.shape
@@ -93,14 +93,28 @@ def conv2d(x: torch.Tensor, kernel_hwio: torch.Tensor, stride=(1, 1), pads=(0, 0
     if stats is not None:
         a.stats_out, a.stats_ld, a.stats_off = stats.data_ptr(), cout, 0
     a.mbn = _ident()
+    keep = _splitk_args(a, N * Ho * Wo, cout, ksplit)
     nat.require().conv(nat.raw(a), tile, 1 if x.dtype == torch.float32 else 0, nat.stream_handle())
+    del keep
     return y
+
+
+def _splitk_args(a, M: int, cout: int, ksplit: int):
+    """Split-K workspace for a one-off launch: fp32 partial slabs + zeroed tickets."""
+    if ksplit <= 1:
+        return None
+    tiles = -(-M // 64) * -(-cout // 32)
+    slab = torch.empty(tiles * ksplit * 64 * 32, dtype=torch.float32, device="cuda")
+    tickets = torch.zeros(tiles, dtype=torch.int32, device="cuda")
+    a.slab, a.tickets, a.ksplit = slab.data_ptr(), tickets.data_ptr(), ksplit
+    a.slab_floats, a.tickets_n = slab.numel(), tiles
+    return slab, tickets
 
 
 def conv2d_dgrad(dy: torch.Tensor, kernel_hwio: torch.Tensor, in_hw: Tuple[int, int], pads=(0, 0),
                  mx: Optional[torch.Tensor] = None, mbn: Optional[BN] = None,
                  gsum: Optional[torch.Tensor] = None, gsumx: Optional[torch.Tensor] = None,
-                 out_f32: bool = False, tile: int = -1) -> torch.Tensor:
+                 out_f32: bool = False, tile: int = -1, ksplit: int = 1) -> torch.Tensor:
     """Stride-1 data gradient.  With ``mx``/``mbn``: returns dZ = dX * act'(bn(mx)) and
     accumulates sum(dZ) into gsum, sum(dZ*xhat) into gsumx."""
     N, Ho, Wo, Cout = dy.shape
@@ -126,7 +140,9 @@ def conv2d_dgrad(dy: torch.Tensor, kernel_hwio: torch.Tensor, in_hw: Tuple[int, 
         a.gsum, a.gsumx = nat.ptr(gsum), nat.ptr(gsumx)
     else:
         a.out_mode = nat.OUT_F32 if out_f32 else nat.OUT_BF16
+    keep = _splitk_args(a, N * H * W, cin, ksplit)
     nat.require().conv(nat.raw(a), tile, 1 if dy.dtype == torch.float32 else 0, nat.stream_handle())
+    del keep
     return dx
 
 

@@ -73,8 +73,22 @@ def _conv_candidates(ext, M: int, cout: int, payload: bytes = None):
     return out
 
 
-def autotune_plan(plan, stream, verbose: bool = False) -> int:
-    """Tune every conv / wgrad op of ``plan`` in place.  Returns the number of ops tuned."""
+def _splits_for(ext, a, t: int, M: int, slab_floats: int):
+    """Feasible split-K factors for conv tile ``t``: the partial slabs must fit the workspace, each
+    slice must keep >= 2 K-steps, and only grids that leave the GPU under-filled are split."""
+    bm, bn = ext.tile_bm(t), ext.tile_bn(t)
+    tiles = -(-M // bm) * -(-a.Cout // bn)
+    if tiles >= 256:
+        return []
+    K = a.KH * a.KW * a.Cin
+    bk = 256 if t >= 17 else (128 if t >= 12 else (64 if t >= 5 else 32))
+    nk = -(-K // bk)
+    return [s for s in (2, 4, 8) if tiles * s * bm * bn <= slab_floats and nk >= 2 * s]
+
+
+def autotune_plan(plan, stream, verbose: bool = False, reset_tickets=None, slab_floats: int = 0) -> int:
+    """Tune every conv / wgrad op of ``plan`` in place: tile shape, then the split-K factor of the
+    best few tiles (ops whose payload carries a split-K workspace).  Returns the number tuned."""
     _load_cache()
     ext = nat.load()
     n = 0
@@ -90,14 +104,30 @@ def autotune_plan(plan, stream, verbose: bool = False) -> int:
             best = _CACHE.get(key)
             if best is None:
                 times = {}
+                plan.set_int(i, 2, 1)
                 for t in _conv_candidates(ext, M, a.Cout, plan.payload(i)) or [ext.pick_tile(M, a.Cout)]:
                     plan.set_int(i, 0, t)
-                    times[t] = _time_op(plan, i, stream)
+                    times[(t, 1)] = _time_op(plan, i, stream)
+                if a.slab and a.tickets and reset_tickets is not None and \
+                        os.environ.get("IDC_SPLITK", "1") != "0":
+                    top = sorted((v, t) for (t, s), v in times.items() if t != ext.TILE_HALO)[:3]
+                    for _, t in top:
+                        for s in _splits_for(ext, a, t, M, slab_floats):
+                            plan.set_int(i, 0, t)
+                            plan.set_int(i, 2, s)
+                            reset_tickets()
+                            times[(t, s)] = _time_op(plan, i, stream)
                 best = min(times, key=times.get)
                 _CACHE[key] = best
                 if verbose:
-                    print("tune conv", key, {k: round(v * 1e3, 1) for k, v in times.items()}, "->", best)
-            plan.set_int(i, 0, best)
+                    print("tune conv", key, {f"{k[0]}/{k[1]}": round(v * 1e3, 1) for k, v in times.items()},
+                          "->", best)
+            if isinstance(best, list):  # JSON round trip
+                best = tuple(best)
+            if not isinstance(best, tuple):
+                best = (best, 1)
+            plan.set_int(i, 0, best[0])
+            plan.set_int(i, 2, best[1] if (a.slab and a.tickets) else 1)
             n += 1
         elif kind == nat.OP_WGRAD:
             a = nat.WgradArgs.from_buffer_copy(plan.payload(i))

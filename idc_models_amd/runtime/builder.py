@@ -124,6 +124,8 @@ class Builder:
         # its 90-150 KB LDS footprint blocks the side-lane wgrads from sharing CUs (net loss)
         self.use_halo = os.environ.get("IDC_HALO", "0") == "1"
         self.guards: List[tuple] = []
+        self.splitk_slab: Optional[torch.Tensor] = None
+        self.tickets: List[torch.Tensor] = []
         self.bwd_marks: List[Tuple[int, int]] = []  # (op index, lowest arena param index ready)
         # stats arena is allocated lazily with a generous capacity; views are handed out in order
         self._stats_cap = 1 << 20
@@ -220,22 +222,31 @@ class Builder:
             entries_all.append(e)
             if id(layer.kernel) in trainable_ids:
                 entries_tr.append(e)
-        self.cast_all_dev, self.cast_all_total, self.cast_all_n = self._upload_cast(entries_all)
-        self.cast_tr_dev, self.cast_tr_total, self.cast_tr_n = self._upload_cast(entries_tr)
+        (self.cast_all_dev, self.cast_all_map, self.cast_all_total,
+         self.cast_all_n) = self._upload_cast(entries_all)
+        (self.cast_tr_dev, self.cast_tr_map, self.cast_tr_total,
+         self.cast_tr_n) = self._upload_cast(entries_tr)
 
     def _upload_cast(self, entries):
-        total = 0
-        for e in entries:
-            e.begin = total
-            total += e.Cout * e.KH * e.KW * e.Cpad
+        """Device CastEntry array + tile -> entry map for the tiled cast kernel (64x64 tiles of
+        each kernel's [KH*KW*Cin, Cout] matrix; ``begin`` = the entry's first tile)."""
         if not entries:
-            return None, 0, 0
+            return None, None, 0, 0
+        total = 0
+        owner = []
+        for i, e in enumerate(entries):
+            e = entries[i]
+            e.begin = total
+            n = -(-(e.KH * e.KW * e.Cin) // 64) * -(-e.Cout // 64)
+            owner += [i] * n
+            total += n
         arr = (nat.CastEntry * len(entries))(*entries)
         host = torch.frombuffer(bytearray(C.string_at(C.addressof(arr), C.sizeof(arr))),
                                 dtype=torch.uint8)
         dev = host.to(self.device)
-        self.keep.append(dev)
-        return dev, total, len(entries)
+        tmap = torch.tensor(owner, dtype=torch.int32).to(self.device)
+        self.keep += [dev, tmap]
+        return dev, tmap, total, len(entries)
 
     def finalize_moving(self):
         if not self.moving:
@@ -298,7 +309,25 @@ class Builder:
         M = x.N * y.H * y.W
         if tile < 0:
             tile = self._default_tile(a, M, y.C)
-        self.emit(nat.OP_CONV, a, ints=(tile, 1 if x.is_f32 else 0))
+        self._splitk(a, M, y.C)
+        self.emit(nat.OP_CONV, a, ints=(tile, 1 if x.is_f32 else 0, 1))
+
+    # split-K workspace (conv_igemm.h): one fp32 partial-tile slab shared by every main-lane conv
+    # (they run one after another on the plan stream) and one ticket array per op
+    SLAB_FLOATS = 4 << 20
+
+    def _splitk(self, a, M: int, cout: int):
+        if self.splitk_slab is None:
+            self.splitk_slab = self.alloc((self.SLAB_FLOATS,), F32)
+        tiles = -(-M // 64) * -(-cout // 32)  # the smallest tile shape has the most tiles
+        t = self.alloc((tiles,), torch.int32)
+        self.tickets.append(t)
+        a.slab, a.tickets, a.ksplit = self.splitk_slab.data_ptr(), t.data_ptr(), 1
+        a.slab_floats, a.tickets_n = self.SLAB_FLOATS, tiles
+
+    def reset_tickets(self):
+        for t in self.tickets:
+            t.zero_()
 
     def _default_tile(self, a, M: int, cout: int) -> int:
         ext = nat.load()
@@ -334,7 +363,8 @@ class Builder:
             a.epi_mode = 0
             a.out_mode = out_mode
         tile = self._default_tile(a, dx.M, dx.C)
-        self.emit(nat.OP_CONV, a, ints=(tile, 1 if dy.is_f32 else 0))
+        self._splitk(a, dx.M, dx.C)
+        self.emit(nat.OP_CONV, a, ints=(tile, 1 if dy.is_f32 else 0, 1))
 
     def wgrad(self, x: Tensor4, layer, g: Tensor4, dw: torch.Tensor, *, stride=(1, 1), pads=(0, 0),
               pro=None, cin_real=0, splits=-1, lane=0):

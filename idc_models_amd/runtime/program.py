@@ -104,7 +104,7 @@ class FusedProgram:
                        ptrs=(model.arena.data.data_ptr(), model.arena.grad.data_ptr(), ms.data_ptr(), flag))
             if b.cast_tr_n:
                 b.emit(nat.OP_CAST, ints=(b.cast_tr_n,), longs=(b.cast_tr_total,),
-                       ptrs=(b.cast_tr_dev.data_ptr(),))
+                       ptrs=(b.cast_tr_dev.data_ptr(), b.cast_tr_map.data_ptr()))
             if flag:
                 b.emit(nat.OP_FINITE_CHECK, ints=(1,), ptrs=(0, flag, self.nonfinite_status.data_ptr()))
         else:
@@ -150,14 +150,17 @@ class FusedProgram:
         # initial bf16 weight casts (all convs, frozen ones included)
         if b.cast_all_n:
             cast = nat.load().Plan()
-            cast.add(nat.OP_CAST, b"", [b.cast_all_n], [], [b.cast_all_total], [b.cast_all_dev.data_ptr()])
+            cast.add(nat.OP_CAST, b"", [b.cast_all_n], [], [b.cast_all_total],
+                     [b.cast_all_dev.data_ptr(), b.cast_all_map.data_ptr()])
             self._cast_all_plan = cast
         else:
             self._cast_all_plan = None
         self.recast_all()
         if os.environ.get("IDC_AUTOTUNE", "1") != "0":
             from .autotune import autotune_plan
-            autotune_plan(self.plan, self.stream, verbose=os.environ.get("IDC_TUNE_VERBOSE") == "1")
+            autotune_plan(self.plan, self.stream, verbose=os.environ.get("IDC_TUNE_VERBOSE") == "1",
+                          reset_tickets=b.reset_tickets, slab_floats=b.SLAB_FLOATS)
+        b.reset_tickets()  # split-K tickets count modulo the op's split: start every op aligned
 
     # ------------------------------------------------------------------ execution
     def _sh(self):

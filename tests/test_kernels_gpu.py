@@ -73,7 +73,7 @@ def test_conv_fwd(fn, N, H, Cin, Cout, k, s, pads, outhw):
     assert relerr(y, ref) < 1e-2
 
 
-@pytest.mark.parametrize("tile", list(range(17)))
+@pytest.mark.parametrize("tile", list(range(19)))
 def test_conv_every_tile_large_m_odd_ktiles(fn, tile):
     """Every tile config at scale: M = 40000 with an odd K-tile count (K = 392 -> 7 / 13 tiles)
     exercises the pipeline tail + epilogue LDS aliasing (a missing barrier once raced here)."""
@@ -85,6 +85,38 @@ def test_conv_every_tile_large_m_odd_ktiles(fn, tile):
     ref = ref_conv(x, w, 2, (3, 3, 3, 3))
     assert relerr(y, ref) < 1e-2
     assert relerr(st[:Cout], ref.sum((0, 1, 2))) < 1e-2
+
+
+@pytest.mark.parametrize("tile,ks", [(4, 2), (9, 4), (12, 2), (17, 2), (18, 4), (8, 8), (7, 3)])
+def test_conv_split_k_matches_reference(fn, tile, ks):
+    """Split-K (in-launch last-arriver reduction) on a small-M deep-K layer with the BN prologue
+    and output statistics; launched three times to check the modulo tickets realign."""
+    N, H, Cin, Cout = 16, 6, 480, 128
+    x = bf(torch.randn(N, H, H, Cin, device=DEV))
+    w = bf(torch.randn(1, 1, Cin, Cout, device=DEV) * 0.05)
+    st_in = torch.cat([x.sum((0, 1, 2)), (x * x).sum((0, 1, 2))])
+    g = torch.rand(Cin, device=DEV) + 0.5
+    be = torch.randn(Cin, device=DEV) * 0.1
+    bn = fn.BN(stats=st_in, gamma=g, beta=be, count=N * H * H, eps=1e-3, act=1)
+    mean = x.mean((0, 1, 2))
+    var = (x * x).mean((0, 1, 2)) - mean * mean
+    xa = torch.relu((x - mean) / torch.sqrt(var + 1e-3) * g + be)
+    ref = ref_conv(xa, w, 1, (0, 0, 0, 0))
+    for _ in range(3):
+        st = torch.zeros(2 * Cout, device=DEV)
+        y = fn.conv2d(x.to(torch.bfloat16), w, pro=bn, out_f32=True, tile=tile, stats=st, ksplit=ks)
+        assert relerr(y, ref) < 1e-2
+        assert relerr(st[:Cout], ref.sum((0, 1, 2))) < 1e-2
+
+
+def test_conv_dgrad_split_k(fn):
+    N, H, Cin, Cout = 16, 3, 128, 32
+    dy = bf(torch.randn(N, H, H, Cout, device=DEV))
+    w = bf(torch.randn(3, 3, Cin, Cout, device=DEV) * 0.05)
+    ref = torch.nn.grad.conv2d_input((N, Cin, H, H), w.permute(3, 2, 0, 1), dy.permute(0, 3, 1, 2),
+                                     padding=1).permute(0, 2, 3, 1)
+    dx = fn.conv2d_dgrad(dy.to(torch.bfloat16), w, (H, H), pads=(1, 1), out_f32=True, tile=9, ksplit=4)
+    assert relerr(dx, ref) < 1e-2
 
 
 def test_conv_fwd_asymmetric_B(fn):

@@ -37,7 +37,10 @@ def time_plan(adds, reps):
     return e0.elapsed_time(e1) / (3 * reps) * 1e3
 
 
-def conv_op(x, w_layout, N, H, W, Cin, Cout, k, pads, pro, stats, tile, y):
+_WS = {}
+
+
+def conv_op(x, w_layout, N, H, W, Cin, Cout, k, pads, pro, stats, tile, y, ks=1):
     a = nat.ConvArgs()
     a.x = x.data_ptr()
     a.N, a.H, a.W, a.Cin, a.ldx = N, H, W, Cin, Cin
@@ -54,7 +57,14 @@ def conv_op(x, w_layout, N, H, W, Cin, Cout, k, pads, pro, stats, tile, y):
     if stats is not None:
         a.stats_out, a.stats_ld, a.stats_off = stats.data_ptr(), Cout, 0
     a.mbn = nat.bn_args(mode=0, act=0)
-    return (nat.OP_CONV, nat.raw(a), [tile, 0], [], [], [], 0)
+    if ks > 1:
+        if "slab" not in _WS:
+            _WS["slab"] = torch.empty(1 << 24, device=DEV)
+        t = torch.zeros(1 << 16, dtype=torch.int32, device=DEV)
+        _WS.setdefault("t", []).append(t)
+        a.slab, a.tickets = _WS["slab"].data_ptr(), t.data_ptr()
+        a.slab_floats, a.tickets_n = _WS["slab"].numel(), t.numel()
+    return (nat.OP_CONV, nat.raw(a), [tile, 0, ks], [], [], [], 0)
 
 
 def wgrad_op(x, dy, N, H, W, Cin, Cout, k, pads, pro, dw, splits):
@@ -110,6 +120,18 @@ def main():
         print(f"{name:22s} M={N * H * H:6d} best t{b[1]:2d}: {b[0]:6.1f} us ({flops / b[0] / 1e6:6.1f} TF/s) "
               f"plain {b[2]:6.1f} pro-only {b[3]:6.1f} stats-only {b[4]:6.1f} | " +
               " ".join(f"t{t}:{u:.1f}/{u0:.1f}/{u1:.1f}/{u2:.1f}" for u, t, u0, u1, u2 in res[:6]), flush=True)
+        for t in sorted({b[1], 4, 9, 12, 17}):
+            if ext.tile_bn(t) > max(32, cout):
+                continue
+            row = []
+            tiles = -(-(N * H * H) // ext.tile_bm(t)) * -(-cout // ext.tile_bn(t))
+            for ks in (1, 2, 4, 8):
+                if ks > 1 and tiles * ks * ext.tile_bm(t) * ext.tile_bn(t) > (1 << 24):
+                    continue
+                us = time_plan([conv_op(x, wl, N, H, H, cin, cout, k, pads, None, None, t, y, ks)], args.reps)
+                us2 = time_plan([conv_op(x, wl, N, H, H, cin, cout, k, pads, bn, sout, t, y, ks)], args.reps)
+                row.append(f"ks{ks}:{us:.1f}/{us2:.1f}")
+            print(f"    split-K t{t:2d} plain/full " + " ".join(row), flush=True)
         if args.wgrad:
             dy = torch.randn(N, H, H, cout, device=DEV).to(torch.bfloat16)
             dw = torch.zeros(k * k * cin * cout, device=DEV)
