@@ -93,18 +93,23 @@ def conv2d(x: torch.Tensor, kernel_hwio: torch.Tensor, stride=(1, 1), pads=(0, 0
     if stats is not None:
         a.stats_out, a.stats_ld, a.stats_off = stats.data_ptr(), cout, 0
     a.mbn = _ident()
-    keep = _splitk_args(a, N * Ho * Wo, cout, ksplit)
+    keep = _splitk_args(a, N * Ho * Wo, cout, ksplit, tile)
     nat.require().conv(nat.raw(a), tile, 1 if x.dtype == torch.float32 else 0, nat.stream_handle())
     del keep
     return y
 
 
-def _splitk_args(a, M: int, cout: int, ksplit: int):
-    """Split-K workspace for a one-off launch: fp32 partial slabs + zeroed tickets."""
+def _splitk_args(a, M: int, cout: int, ksplit: int, tile: int):
+    """Split-K workspace for a one-off launch: fp32 partial slabs + zeroed tickets, sized for the
+    tile shape that will actually run (the launcher rejects an undersized workspace)."""
     if ksplit <= 1:
         return None
-    tiles = -(-M // 64) * -(-cout // 32)
-    slab = torch.empty(tiles * ksplit * 64 * 32, dtype=torch.float32, device="cuda")
+    ext = nat.require()
+    if tile < 0:
+        tile = ext.pick_tile(M, cout)
+    bm, bn = ext.tile_bm(tile), ext.tile_bn(tile)
+    tiles = -(-M // bm) * -(-cout // bn)
+    slab = torch.empty(tiles * ksplit * bm * bn, dtype=torch.float32, device="cuda")
     tickets = torch.zeros(tiles, dtype=torch.int32, device="cuda")
     a.slab, a.tickets, a.ksplit = slab.data_ptr(), tickets.data_ptr(), ksplit
     a.slab_floats, a.tickets_n = slab.numel(), tiles
@@ -140,7 +145,7 @@ def conv2d_dgrad(dy: torch.Tensor, kernel_hwio: torch.Tensor, in_hw: Tuple[int, 
         a.gsum, a.gsumx = nat.ptr(gsum), nat.ptr(gsumx)
     else:
         a.out_mode = nat.OUT_F32 if out_f32 else nat.OUT_BF16
-    keep = _splitk_args(a, N * H * W, cin, ksplit)
+    keep = _splitk_args(a, N * H * W, cin, ksplit, tile)
     nat.require().conv(nat.raw(a), tile, 1 if dy.dtype == torch.float32 else 0, nat.stream_handle())
     del keep
     return dx
