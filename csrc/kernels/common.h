@@ -135,7 +135,49 @@ struct BnArgs {
   int mode;
   int act;
   int C;                  // channels covered by stats/gamma (stats row length)
+  int slots;              // mode 1: `stats` holds this many [sum|sumsq] copies (0/1: one), see below
 };
+
+// Statistics slots.  Per-channel sums are accumulated with global float atomics, which execute
+// at the memory side and serialise per ADDRESS (measured ~24 ns per add, tools/micro/
+// atomic_flush.hip: 676 workgroups adding into one array cost +14 us, 2500 cost +58 us, the same
+// adds spread over 32 copies cost nothing).  Producers with many row blocks therefore add into
+// copy (row block % slots) of a [slots][2][C] array, and every consumer sums the copies while it
+// builds its coefficient table (slots x 2C L2-resident floats per workgroup).
+__device__ __forceinline__ int stat_slots(int s) { return s > 1 ? s : 1; }
+
+// Slot-summed [sum, sumsq] of channel cc, every one of the 2*MAX_STAT_SLOTS loads issued before the
+// first add (slots past S re-read copy S-1 and are masked out: unconditional loads keep hipcc from
+// branching around each one and waiting per element), so a table costs one memory round trip.
+constexpr int MAX_STAT_SLOTS = 16;
+__device__ __forceinline__ void slot_sums_1(const float* p0, const float* p1, int S, size_t stride, int cc,
+                                            float& v0, float& v1) {
+  float t0[MAX_STAT_SLOTS], t1[MAX_STAT_SLOTS];
+#pragma unroll
+  for (int s = 0; s < MAX_STAT_SLOTS; ++s) {
+    const size_t o = (size_t)(s < S ? s : S - 1) * stride + cc;
+    t0[s] = p0[o];
+    t1[s] = p1[o];
+  }
+  v0 = 0.f;
+  v1 = 0.f;
+#pragma unroll
+  for (int s = 0; s < MAX_STAT_SLOTS; ++s) {
+    v0 += s < S ? t0[s] : 0.f;
+    v1 += s < S ? t1[s] : 0.f;
+  }
+}
+
+// [sum, sumsq] of channel c over all slot copies (mode 1)
+__device__ __forceinline__ void bn_slot_sums(const BnArgs& b, int c, float& s0, float& s1) {
+  const int S = min(stat_slots(b.slots), MAX_STAT_SLOTS);
+  if (S == 1) {
+    s0 = b.stats[c];
+    s1 = b.stats[b.C + c];
+    return;
+  }
+  slot_sums_1(b.stats, b.stats + b.C, S, 2 * (size_t)b.C, c, s0, s1);
+}
 
 __device__ __forceinline__ void bn_coeffs(const BnArgs& b, int c, float& scale, float& shift) {
   if (b.mode == 0) {
@@ -145,8 +187,10 @@ __device__ __forceinline__ void bn_coeffs(const BnArgs& b, int c, float& scale, 
   }
   float mean, var;
   if (b.mode == 1) {
-    mean = b.stats[c] * b.inv_count;
-    var = fmaxf(b.stats[b.C + c] * b.inv_count - mean * mean, 0.f);
+    float s0, s1;
+    bn_slot_sums(b, c, s0, s1);
+    mean = s0 * b.inv_count;
+    var = fmaxf(s1 * b.inv_count - mean * mean, 0.f);
   } else {
     mean = b.mmean[c];
     var = b.mvar[c];
@@ -172,7 +216,21 @@ __device__ __forceinline__ void bn_coeff_table(const BnArgs& b, int C, float* s_
   const float* p0 = b.mode == 1 ? b.stats : b.mmean;
   const float* p1 = b.mode == 1 ? b.stats + b.C : b.mvar;
   const float mul = b.mode == 1 ? b.inv_count : 1.f;
-  for (int base = 0; base < C; base += 4 * NT) {
+  const int S = b.mode == 1 ? min(stat_slots(b.slots), MAX_STAT_SLOTS) : 1;
+  const size_t stride = 2 * (size_t)b.C;
+  // slotted statistics: one channel per thread per pass, all slot copies in flight at once
+  for (int c = tid; S > 1 && c < C; c += NT) {
+    float v0, v1;
+    slot_sums_1(p0, p1, S, stride, c, v0, v1);
+    const float g = b.gamma ? b.gamma[c] : 1.f;
+    const float be = b.beta ? b.beta[c] : 0.f;
+    const float mean = v0 * mul;
+    const float var = fmaxf(v1 * mul - mean * mean, 0.f);
+    const float rs = rsqrtf(var + b.eps);
+    s_scale[c] = g * rs;
+    s_shift[c] = be - mean * g * rs;
+  }
+  for (int base = 0; S == 1 && base < C; base += 4 * NT) {
     float v0[4], v1[4], g[4], be[4];
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
@@ -210,7 +268,23 @@ __device__ __forceinline__ void bn_full_table(const BnArgs& b, int C, float* s_s
   const float* p0 = b.mode == 1 ? b.stats : b.mmean;
   const float* p1 = b.mode == 1 ? b.stats + b.C : b.mvar;
   const float mul = b.mode == 1 ? b.inv_count : 1.f;
-  for (int base = 0; base < C; base += 4 * NT) {
+  const int S = b.mode == 1 ? min(stat_slots(b.slots), MAX_STAT_SLOTS) : 1;
+  const size_t stride = 2 * (size_t)b.C;
+  // slotted statistics: one channel per thread per pass, all slot copies in flight at once
+  for (int c = tid; S > 1 && c < C; c += NT) {
+    float v0, v1;
+    slot_sums_1(p0, p1, S, stride, c, v0, v1);
+    const float g = b.gamma ? b.gamma[c] : 1.f;
+    const float be = b.beta ? b.beta[c] : 0.f;
+    const float mean = v0 * mul;
+    const float var = fmaxf(v1 * mul - mean * mean, 0.f);
+    const float rs = rsqrtf(var + b.eps);
+    s_sc[c] = g * rs;
+    s_sh[c] = be - mean * g * rs;
+    s_mu[c] = mean;
+    s_rs[c] = rs;
+  }
+  for (int base = 0; S == 1 && base < C; base += 4 * NT) {
     float v0[4], v1[4], g[4], be[4];
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
@@ -241,8 +315,10 @@ __device__ __forceinline__ void bn_full_table(const BnArgs& b, int C, float* s_s
 __device__ __forceinline__ void bn_mean_rstd(const BnArgs& b, int c, float& mean, float& rstd) {
   float var;
   if (b.mode == 1) {
-    mean = b.stats[c] * b.inv_count;
-    var = fmaxf(b.stats[b.C + c] * b.inv_count - mean * mean, 0.f);
+    float s0, s1;
+    bn_slot_sums(b, c, s0, s1);
+    mean = s0 * b.inv_count;
+    var = fmaxf(s1 * b.inv_count - mean * mean, 0.f);
   } else {
     mean = b.mmean[c];
     var = b.mvar[c];

@@ -274,13 +274,16 @@ __global__ __launch_bounds__(NT) void conv3x3_halo_kernel(ConvArgs a) {
       }
     }
     __syncthreads();
+    // one workgroup per image: the image index picks the statistics slot
+    const size_t so = EPI == 0 ? (size_t)(blockIdx.x % stat_slots(a.stats_slots)) * 2 * a.stats_ld
+                               : (size_t)(blockIdx.x % stat_slots(a.gsum_slots)) * a.gsum_ld;
     for (int c = tid; c < COUT; c += NT) {
       if constexpr (EPI == 0) {
-        atomicAdd(&a.stats_out[a.stats_off + c], s_sum[c]);
-        atomicAdd(&a.stats_out[a.stats_ld + a.stats_off + c], s_sq[c]);
+        atomicAdd(&a.stats_out[so + a.stats_off + c], s_sum[c]);
+        atomicAdd(&a.stats_out[so + a.stats_ld + a.stats_off + c], s_sq[c]);
       } else {
-        if (a.gsum) atomicAdd(&a.gsum[c], s_sum[c]);
-        if (a.gsumx) atomicAdd(&a.gsumx[c], s_sq[c]);
+        if (a.gsum) atomicAdd(&a.gsum[so + c], s_sum[c]);
+        if (a.gsumx) atomicAdd(&a.gsumx[so + c], s_sq[c]);
       }
     }
   }

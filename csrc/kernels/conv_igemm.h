@@ -44,6 +44,11 @@ struct ConvArgs {
   long long slab_floats;  // capacities, checked by the launcher before a split launch
   int tickets_n;
   int ksplit;
+  // statistics slots (common.h): stats_out holds stats_slots copies of [sum|sumsq] (stride
+  // 2*stats_ld), gsum/gsumx gsum_slots copies (stride gsum_ld); a tile adds into copy mtile % slots
+  int stats_slots;
+  int gsum_slots;
+  int gsum_ld;
 };
 
 // tile TILE_HALO selects the one-image-per-workgroup direct 3x3 kernel (conv3x3_halo.hip)

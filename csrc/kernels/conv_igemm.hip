@@ -490,15 +490,17 @@ __global__ __launch_bounds__(256) void conv_igemm_kernel(ConvArgs a) {
       }
     }
     __syncthreads();
+    const size_t so = EPI == 0 ? (size_t)(mt % stat_slots(a.stats_slots)) * 2 * a.stats_ld
+                               : (size_t)(mt % stat_slots(a.gsum_slots)) * a.gsum_ld;
     for (int j = tid; j < BN; j += NT) {
       int c = n0 + j;
       if (c >= a.Cout) continue;
       if constexpr (EPI == 0) {
-        atomicAdd(&a.stats_out[a.stats_off + c], s_sum[j]);
-        atomicAdd(&a.stats_out[a.stats_ld + a.stats_off + c], s_sq[j]);
+        atomicAdd(&a.stats_out[so + a.stats_off + c], s_sum[j]);
+        atomicAdd(&a.stats_out[so + a.stats_ld + a.stats_off + c], s_sq[j]);
       } else {
-        if (a.gsum) atomicAdd(&a.gsum[c], s_sum[j]);
-        if (a.gsumx) atomicAdd(&a.gsumx[c], s_sq[j]);
+        if (a.gsum) atomicAdd(&a.gsum[so + c], s_sum[j]);
+        if (a.gsumx) atomicAdd(&a.gsumx[so + c], s_sq[j]);
       }
     }
   }

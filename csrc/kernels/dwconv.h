@@ -21,6 +21,7 @@ struct DwArgs {
   // the reduction is two-stage (per-block partials + column sums) instead of global atomics
   float* dw;
   float* ws;
+  int stats_slots, gsum_slots, gsum_ld;  // statistics slots (common.h)
 };
 
 long long dwconv_wgrad_ws_floats(long long M, int C, int taps);

@@ -85,9 +85,10 @@ __global__ __launch_bounds__(256) void dw_fwd_kernel(DwArgs a) {
   }
   if (a.stats) {
     __syncthreads();
+    float* so = a.stats + (size_t)(blockIdx.x % stat_slots(a.stats_slots)) * 2 * a.stats_ld;
     for (int c = threadIdx.x; c < a.C; c += blockDim.x) {
-      atomicAdd(&a.stats[c], s_a[c]);
-      atomicAdd(&a.stats[a.stats_ld + c], s_b[c]);
+      atomicAdd(&so[c], s_a[c]);
+      atomicAdd(&so[a.stats_ld + c], s_b[c]);
     }
   }
 }
@@ -157,9 +158,10 @@ __global__ __launch_bounds__(256) void dw_bwd_data_kernel(DwArgs a) {
   }
   if (epi) {
     __syncthreads();
+    const size_t so = (size_t)(blockIdx.x % stat_slots(a.gsum_slots)) * a.gsum_ld;
     for (int c = threadIdx.x; c < a.C; c += blockDim.x) {
-      if (a.gsum) atomicAdd(&a.gsum[c], s_a[c]);
-      if (a.gsumx) atomicAdd(&a.gsumx[c], s_b[c]);
+      if (a.gsum) atomicAdd(&a.gsum[so + c], s_a[c]);
+      if (a.gsumx) atomicAdd(&a.gsumx[so + c], s_b[c]);
     }
   }
 }

@@ -14,6 +14,8 @@ struct BnBwdApplyArgs {
   void* dst; int lddst;
   int dst_f32, accumulate;
   int M, C;
+  int gsum_slots, gsum_ld;  // statistics slots of gsum/gsumx (common.h)
+  float* fold_sum; float* fold_sumx;  // optional: block 0 adds the slot-summed gsum/gsumx here
 };
 
 // dZ = dy * act'(bn(x)); sums of dZ and dZ*xhat per channel; optional dZ store
@@ -24,6 +26,7 @@ struct BnBwdReduceArgs {
   bf16_t* dz; int lddz;   // may be null
   float* gsum; float* gsumx;
   int M, C;
+  int gsum_slots, gsum_ld;
 };
 
 struct PoolArgs {
@@ -35,6 +38,7 @@ struct PoolArgs {
   bf16_t* y; int ldy;  // output slice
   uint8_t* argmax;     // [N*Ho*Wo*C] (max pool)
   float* stats; int stats_ld; int stats_off;  // output statistics (optional)
+  int stats_slots;
 };
 
 struct PoolBwdArgs {
@@ -47,12 +51,14 @@ struct PoolBwdArgs {
   bf16_t* dx; int lddx;    // output (dZ if bn active, else plain grad)
   float* gsum; float* gsumx;
   int is_avg;
+  int gsum_slots, gsum_ld;
 };
 
 struct BnMovingDesc {
   const float* stats; int C; float inv_count; float unbias;  // unbias = n/(n-1)
   float* mmean; float* mvar; float momentum;
   int ld;  // statistics row length (sumsq of channel c at stats[ld + c])
+  int slots;  // statistics slot copies (stride 2*ld)
 };
 
 struct HeadArgs {
@@ -104,8 +110,13 @@ hipError_t cast_weights(const CastEntry* d_entries, const int* tile_entry, long 
 hipError_t input_stage(const void* x, int x_u8, int N, int H, int W, int C, bf16_t* y, int Cpad,
                        hipStream_t st);
 hipError_t bn_stats(const bf16_t* x, int ldx, int M, int C, float* stats, int stats_ld,
-                    int stats_off, hipStream_t st);
+                    int stats_off, int stats_slots, hipStream_t st);
 hipError_t bn_apply(const bf16_t* x, int ldx, BnArgs bn, const bf16_t* res, int ldres,
-                    bf16_t* y, int ldy, int M, int C, float* stats, int stats_ld, hipStream_t st);
+                    bf16_t* y, int ldy, int M, int C, float* stats, int stats_ld, int stats_slots,
+                    hipStream_t st);
+// dst[c] += sum_s src[s*ld + c] (and the same for src2/dst2 when given): folds statistics slots
+// into one array (BatchNorm gamma/beta gradients in the parameter-gradient arena)
+hipError_t slot_collapse(const float* src, float* dst, const float* src2, float* dst2, int slots,
+                         int ld, int C, hipStream_t st);
 
 }  // namespace idc

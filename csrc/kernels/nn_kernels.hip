@@ -88,6 +88,11 @@ inline int grid_rows(int M, int C, int per_thread_rows = 4) {
 }
 
 // block-level: s_a/s_b partial sums -> global atomics
+// this block's statistics slot copy of p (null stays null); stride between copies in floats
+__device__ __forceinline__ float* slot_ptr(float* p, int slots, size_t stride) {
+  return p ? p + (size_t)(blockIdx.x % stat_slots(slots)) * stride : nullptr;
+}
+
 __device__ __forceinline__ void flush_sums(float* s_a, float* s_b, int C, float* ga, float* gb) {
   __syncthreads();
   for (int c = threadIdx.x; c < C; c += blockDim.x) {
@@ -166,7 +171,20 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(BnBwdApplyArgs a) {
     bn_mean_rstd(a.bn, c, mean, rstd);
     float g = a.bn.gamma ? a.bn.gamma[c] : 1.f;
     if (a.bn.mode == 1) {
-      float sd = a.gsum[c] * a.inv_n, sdx = a.gsumx[c] * a.inv_n;
+      float sd, sdx;
+      const int S = min(stat_slots(a.gsum_slots), MAX_STAT_SLOTS);
+      if (S == 1) {
+        sd = a.gsum[c];
+        sdx = a.gsumx[c];
+      } else {
+        slot_sums_1(a.gsum, a.gsumx, S, a.gsum_ld, c, sd, sdx);
+      }
+      if (blockIdx.x == 0 && a.fold_sum) {  // d beta / d gamma into the gradient arena
+        a.fold_sum[c] += sd;
+        a.fold_sumx[c] += sdx;
+      }
+      sd *= a.inv_n;
+      sdx *= a.inv_n;
       sA[c] = g * rstd;
       sB[c] = -g * rstd * rstd * sdx;
       sC[c] = -g * rstd * sd + g * rstd * rstd * mean * sdx;
@@ -264,7 +282,7 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(BnBwdReduceArgs a) {
     }
   }
   chunk_reduce(cm, a.C, ps, px, s_tmp, s_a, s_b);
-  flush_sums(s_a, s_b, a.C, a.gsum, a.gsumx);
+  flush_sums(s_a, s_b, a.C, slot_ptr(a.gsum, a.gsum_slots, a.gsum_ld), slot_ptr(a.gsumx, a.gsum_slots, a.gsum_ld));
 }
 
 hipError_t bn_bwd_reduce(const BnBwdReduceArgs& a, hipStream_t st) {
@@ -341,7 +359,8 @@ __global__ __launch_bounds__(256) void pool_fwd_kernel(PoolArgs a) {
   }
   if (a.stats) chunk_reduce(cm, a.C, ps, pq, s_tmp, s_a, s_b);
   if (a.stats)
-    flush_sums(s_a, s_b, a.C, a.stats + a.stats_off, a.stats + a.stats_ld + a.stats_off);
+    flush_sums(s_a, s_b, a.C, slot_ptr(a.stats, a.stats_slots, 2 * (size_t)a.stats_ld) + a.stats_off,
+               slot_ptr(a.stats, a.stats_slots, 2 * (size_t)a.stats_ld) + a.stats_ld + a.stats_off);
 }
 
 hipError_t maxpool_fwd(const PoolArgs& a, hipStream_t st) {
@@ -469,7 +488,8 @@ __global__ __launch_bounds__(256) void pool_bwd_kernel(PoolBwdArgs a) {
   }
   if (sums) {
     chunk_reduce(cm, a.C, ps, px, s_tmp, s_a, s_b);
-    flush_sums(s_a, s_b, a.C, a.gsum, a.gsumx);
+    flush_sums(s_a, s_b, a.C, slot_ptr(a.gsum, a.gsum_slots, a.gsum_ld),
+               slot_ptr(a.gsumx, a.gsum_slots, a.gsum_ld));
   }
 }
 
@@ -490,8 +510,13 @@ hipError_t pool_bwd(const PoolBwdArgs& a, hipStream_t st) {
 __global__ void bn_update_moving_kernel(const BnMovingDesc* d, int n) {
   const BnMovingDesc& b = d[blockIdx.y];
   for (int c = blockIdx.x * blockDim.x + threadIdx.x; c < b.C; c += gridDim.x * blockDim.x) {
-    float mean = b.stats[c] * b.inv_count;
-    float var = fmaxf(b.stats[b.ld + c] * b.inv_count - mean * mean, 0.f) * b.unbias;
+    float s0 = 0.f, s1 = 0.f;
+    for (int s = 0; s < stat_slots(b.slots); ++s) {
+      s0 += b.stats[(size_t)s * 2 * b.ld + c];
+      s1 += b.stats[(size_t)s * 2 * b.ld + b.ld + c];
+    }
+    float mean = s0 * b.inv_count;
+    float var = fmaxf(s1 * b.inv_count - mean * mean, 0.f) * b.unbias;
     b.mmean[c] = b.momentum * b.mmean[c] + (1.f - b.momentum) * mean;
     b.mvar[c] = b.momentum * b.mvar[c] + (1.f - b.momentum) * var;
   }
@@ -833,7 +858,8 @@ hipError_t input_stage(const void* x, int x_u8, int N, int H, int W, int C, bf16
 
 // ------------------------------------------------------------------------------------------
 __global__ __launch_bounds__(256) void bn_stats_kernel(const bf16_t* x, int ldx, int M, int C,
-                                                       float* stats, int stats_ld, int stats_off) {
+                                                       float* stats, int stats_ld, int stats_off,
+                                                       int stats_slots) {
   extern __shared__ float sh[];
   float* s_a = sh;
   float* s_b = sh + C;
@@ -852,20 +878,21 @@ __global__ __launch_bounds__(256) void bn_stats_kernel(const bf16_t* x, int ldx,
 #pragma unroll
     for (int j = 0; j < 8; ++j) { atomicAdd(&s_a[c + j], ps[j]); atomicAdd(&s_b[c + j], pq[j]); }
   }
-  flush_sums(s_a, s_b, C, stats + stats_off, stats + stats_ld + stats_off);
+  float* so = slot_ptr(stats, stats_slots, 2 * (size_t)stats_ld);
+  flush_sums(s_a, s_b, C, so + stats_off, so + stats_ld + stats_off);
 }
 
 hipError_t bn_stats(const bf16_t* x, int ldx, int M, int C, float* stats, int stats_ld, int stats_off,
-                    hipStream_t st) {
+                    int stats_slots, hipStream_t st) {
   hipLaunchKernelGGL(bn_stats_kernel, dim3(grid_rows(M, C, 16)), dim3(256), 2 * C * 4, st, x, ldx, M, C,
-                     stats, stats_ld, stats_off);
+                     stats, stats_ld, stats_off, stats_slots);
   return hipGetLastError();
 }
 
 // y = act(bn(x)) [+ res]; optional stats of y  (MobileNetV2 block outputs, eval paths)
 __global__ __launch_bounds__(256) void bn_apply_kernel(const bf16_t* x, int ldx, BnArgs bn, const bf16_t* res,
                                                        int ldres, bf16_t* y, int ldy, int M, int C,
-                                                       float* stats, int stats_ld) {
+                                                       float* stats, int stats_ld, int stats_slots) {
   extern __shared__ float sh[];
   float* s_sc = sh;
   float* s_sh = sh + C;
@@ -904,13 +931,40 @@ __global__ __launch_bounds__(256) void bn_apply_kernel(const bf16_t* x, int ldx,
       for (int j = 0; j < 8; ++j) { atomicAdd(&s_a[c + j], ps[j]); atomicAdd(&s_b[c + j], pq[j]); }
     }
   }
-  if (stats) flush_sums(s_a, s_b, C, stats, stats + stats_ld);
+  if (stats) {
+    float* so = slot_ptr(stats, stats_slots, 2 * (size_t)stats_ld);
+    flush_sums(s_a, s_b, C, so, so + stats_ld);
+  }
 }
 
 hipError_t bn_apply(const bf16_t* x, int ldx, BnArgs bn, const bf16_t* res, int ldres, bf16_t* y, int ldy,
-                    int M, int C, float* stats, int stats_ld, hipStream_t st) {
+                    int M, int C, float* stats, int stats_ld, int stats_slots, hipStream_t st) {
   hipLaunchKernelGGL(bn_apply_kernel, dim3(grid_rows(M, C)), dim3(256), 4 * C * 4, st, x, ldx, bn, res, ldres,
-                     y, ldy, M, C, stats, stats_ld);
+                     y, ldy, M, C, stats, stats_ld, stats_slots);
+  return hipGetLastError();
+}
+
+// ------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void slot_collapse_kernel(const float* src, float* dst, const float* src2,
+                                                            float* dst2, int slots, int ld, int C) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  float a = 0.f, b = 0.f;
+  for (int s = 0; s < slots; ++s) {
+    a += src[(size_t)s * ld + c];
+    if (src2) b += src2[(size_t)s * ld + c];
+  }
+  dst[c] += a;
+  if (dst2) dst2[c] += b;
+}
+
+hipError_t slot_collapse(const float* src, float* dst, const float* src2, float* dst2, int slots, int ld,
+                         int C, hipStream_t st) {
+  if (C <= 0) return hipSuccess;
+  if (src == nullptr || dst == nullptr || (src2 == nullptr) != (dst2 == nullptr) || slots < 1 || ld < C)
+    return hipErrorInvalidValue;
+  hipLaunchKernelGGL(slot_collapse_kernel, dim3((C + 255) / 256), dim3(256), 0, st, src, dst, src2, dst2, slots,
+                     ld, C);
   return hipGetLastError();
 }
 

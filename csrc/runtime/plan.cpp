@@ -68,6 +68,7 @@ enum OpKind : int {
   OP_MLP_FWD = 21,
   OP_MLP_BWD = 22,
   OP_MLP_STEP = 23,
+  OP_COLLAPSE = 24,
 };
 
 struct Op {
@@ -175,9 +176,10 @@ class Plan {
     static const char* names[] = {"conv", "wgrad", "bn_bwd_apply", "bn_bwd_reduce", "maxpool", "avgpool",
                                   "pool_bwd", "bn_moving", "head_fwd", "head_bwd", "rmsprop", "cast",
                                   "input", "memset", "bn_stats", "bn_apply", "dw_fwd", "dw_bwd_data",
-                                  "dw_wgrad", "copy", "finite_check", "mlp_fwd", "mlp_bwd", "mlp_step"};
+                                  "dw_wgrad", "copy", "finite_check", "mlp_fwd", "mlp_bwd", "mlp_step",
+                                  "collapse"};
     int k = ops_.at(idx).kind;
-    return (k >= 0 && k < 24) ? names[k] : "?";
+    return (k >= 0 && k < 25) ? names[k] : "?";
   }
 
  private:
@@ -265,14 +267,14 @@ class Plan {
         break;
       case OP_BN_STATS:
         check(bn_stats(reinterpret_cast<const bf16_t*>(op.p[0]), op.i[0], op.i[1], op.i[2],
-                       reinterpret_cast<float*>(op.p[1]), op.i[3], op.i[4], st),
+                       reinterpret_cast<float*>(op.p[1]), op.i[3], op.i[4], op.i[5], st),
               "bn_stats");
         break;
       case OP_BN_APPLY: {
         const BnArgs& bn = as<BnArgs>(op);
         check(bn_apply(reinterpret_cast<const bf16_t*>(op.p[0]), op.i[0], bn,
                        reinterpret_cast<const bf16_t*>(op.p[1]), op.i[1], reinterpret_cast<bf16_t*>(op.p[2]),
-                       op.i[2], op.i[3], op.i[4], reinterpret_cast<float*>(op.p[3]), op.i[5], st),
+                       op.i[2], op.i[3], op.i[4], reinterpret_cast<float*>(op.p[3]), op.i[5], op.i[6], st),
               "bn_apply");
         break;
       }
@@ -290,6 +292,12 @@ class Plan {
       case OP_MLP_FWD: check(mlp2_fwd(as<Mlp2Args>(op), st), "mlp2_fwd"); break;
       case OP_MLP_BWD: check(mlp2_bwd(as<Mlp2Args>(op), st), "mlp2_bwd"); break;
       case OP_MLP_STEP: check(mlp2_step(reinterpret_cast<unsigned int*>(op.p[0]), st), "mlp2_step"); break;
+      case OP_COLLAPSE:
+        check(slot_collapse(reinterpret_cast<const float*>(op.p[0]), reinterpret_cast<float*>(op.p[1]),
+                            reinterpret_cast<const float*>(op.p[2]), reinterpret_cast<float*>(op.p[3]), op.i[0],
+                            op.i[1], op.i[2], st),
+              "slot_collapse");
+        break;
       case OP_COPY:
         check(hipMemcpyAsync(reinterpret_cast<void*>(op.p[0]), reinterpret_cast<const void*>(op.p[1]),
                              (size_t)op.l[0], hipMemcpyDeviceToDevice, st),
@@ -347,6 +355,9 @@ py::dict struct_sizes() {
   d["WgradArgs.pix_per_split"] = offsetof(WgradArgs, pix_per_split);
   d["HeadArgs.training"] = offsetof(HeadArgs, training);
   d["PoolBwdArgs.is_avg"] = offsetof(PoolBwdArgs, is_avg);
+  d["ConvArgs.gsum_ld"] = offsetof(ConvArgs, gsum_ld);
+  d["BnArgs.slots"] = offsetof(BnArgs, slots);
+  d["DwArgs.gsum_ld"] = offsetof(DwArgs, gsum_ld);
   return d;
 }
 

@@ -27,7 +27,7 @@ cll = C.c_longlong
 
 class BnArgs(C.Structure):
     _fields_ = [("stats", vp), ("gamma", vp), ("beta", vp), ("mmean", vp), ("mvar", vp),
-                ("inv_count", cf), ("eps", cf), ("mode", ci), ("act", ci), ("C", ci)]
+                ("inv_count", cf), ("eps", cf), ("mode", ci), ("act", ci), ("C", ci), ("slots", ci)]
 
 
 class ConvArgs(C.Structure):
@@ -38,7 +38,7 @@ class ConvArgs(C.Structure):
                 ("stats_out", vp), ("stats_ld", ci), ("stats_off", ci),
                 ("mx", vp), ("ldmx", ci), ("mbn", BnArgs), ("gsum", vp), ("gsumx", vp),
                 ("slab", vp), ("tickets", vp), ("slab_floats", cll), ("tickets_n", ci),
-                ("ksplit", ci)]
+                ("ksplit", ci), ("stats_slots", ci), ("gsum_slots", ci), ("gsum_ld", ci)]
 
 
 class WgradArgs(C.Structure):
@@ -51,31 +51,33 @@ class WgradArgs(C.Structure):
 class BnBwdApplyArgs(C.Structure):
     _fields_ = [("dz", vp), ("lddz", ci), ("x", vp), ("ldx", ci), ("bn", BnArgs),
                 ("gsum", vp), ("gsumx", vp), ("inv_n", cf), ("dst", vp), ("lddst", ci),
-                ("dst_f32", ci), ("accumulate", ci), ("M", ci), ("C", ci)]
+                ("dst_f32", ci), ("accumulate", ci), ("M", ci), ("C", ci), ("gsum_slots", ci),
+                ("gsum_ld", ci), ("fold_sum", vp), ("fold_sumx", vp)]
 
 
 class BnBwdReduceArgs(C.Structure):
     _fields_ = [("dy", vp), ("lddy", ci), ("dy_f32", ci), ("x", vp), ("ldx", ci), ("bn", BnArgs),
-                ("dz", vp), ("lddz", ci), ("gsum", vp), ("gsumx", vp), ("M", ci), ("C", ci)]
+                ("dz", vp), ("lddz", ci), ("gsum", vp), ("gsumx", vp), ("M", ci), ("C", ci),
+                ("gsum_slots", ci), ("gsum_ld", ci)]
 
 
 class PoolArgs(C.Structure):
     _fields_ = [("x", vp), ("ldx", ci), ("N", ci), ("H", ci), ("W", ci), ("C", ci),
                 ("pro", BnArgs), ("k", ci), ("s", ci), ("pt", ci), ("pl", ci), ("Ho", ci),
                 ("Wo", ci), ("y", vp), ("ldy", ci), ("argmax", vp), ("stats", vp),
-                ("stats_ld", ci), ("stats_off", ci)]
+                ("stats_ld", ci), ("stats_off", ci), ("stats_slots", ci)]
 
 
 class PoolBwdArgs(C.Structure):
     _fields_ = [("dy", vp), ("lddy", ci), ("dy_f32", ci), ("argmax", vp), ("N", ci), ("H", ci),
                 ("W", ci), ("C", ci), ("k", ci), ("s", ci), ("pt", ci), ("pl", ci), ("Ho", ci),
                 ("Wo", ci), ("x", vp), ("ldx", ci), ("bn", BnArgs), ("dx", vp), ("lddx", ci),
-                ("gsum", vp), ("gsumx", vp), ("is_avg", ci)]
+                ("gsum", vp), ("gsumx", vp), ("is_avg", ci), ("gsum_slots", ci), ("gsum_ld", ci)]
 
 
 class BnMovingDesc(C.Structure):
     _fields_ = [("stats", vp), ("C", ci), ("inv_count", cf), ("unbias", cf), ("mmean", vp),
-                ("mvar", vp), ("momentum", cf), ("ld", ci)]
+                ("mvar", vp), ("momentum", cf), ("ld", ci), ("slots", ci)]
 
 
 class HeadArgs(C.Structure):
@@ -99,7 +101,8 @@ class DwArgs(C.Structure):
                 ("pro", BnArgs), ("w", vp), ("KH", ci), ("KW", ci), ("S", ci), ("PT", ci),
                 ("PL", ci), ("Ho", ci), ("Wo", ci), ("y", vp), ("ldy", ci), ("stats", vp),
                 ("stats_ld", ci), ("dy", vp), ("lddy", ci), ("dx", vp), ("lddx", ci),
-                ("gsum", vp), ("gsumx", vp), ("dw", vp), ("ws", vp)]
+                ("gsum", vp), ("gsumx", vp), ("dw", vp), ("ws", vp), ("stats_slots", ci),
+                ("gsum_slots", ci), ("gsum_ld", ci)]
 
 
 class Mlp2Args(C.Structure):
@@ -120,7 +123,7 @@ _STRUCTS = {"BnArgs": BnArgs, "ConvArgs": ConvArgs, "WgradArgs": WgradArgs,
 OP_CONV, OP_WGRAD, OP_BN_BWD_APPLY, OP_BN_BWD_REDUCE, OP_MAXPOOL, OP_AVGPOOL, OP_POOL_BWD = range(7)
 OP_BN_MOVING, OP_HEAD_FWD, OP_HEAD_BWD, OP_RMSPROP, OP_CAST, OP_INPUT, OP_MEMSET = range(7, 14)
 OP_BN_STATS, OP_BN_APPLY, OP_DW_FWD, OP_DW_BWD_DATA, OP_DW_WGRAD, OP_COPY, OP_FINITE_CHECK = range(14, 21)
-OP_MLP_FWD, OP_MLP_BWD, OP_MLP_STEP = range(21, 24)
+OP_MLP_FWD, OP_MLP_BWD, OP_MLP_STEP, OP_COLLAPSE = range(21, 25)
 
 ACT = {None: 0, "none": 0, "linear": 0, "relu": 1, "relu6": 2}
 OUT_BF16, OUT_F32, OUT_F32_ACC = 0, 1, 2
@@ -135,7 +138,9 @@ def _verify(ext):
               "ConvArgs.ksplit": ConvArgs.ksplit.offset,
               "WgradArgs.pix_per_split": WgradArgs.pix_per_split.offset,
               "HeadArgs.training": HeadArgs.training.offset,
-              "PoolBwdArgs.is_avg": PoolBwdArgs.is_avg.offset}
+              "PoolBwdArgs.is_avg": PoolBwdArgs.is_avg.offset,
+              "ConvArgs.gsum_ld": ConvArgs.gsum_ld.offset, "BnArgs.slots": BnArgs.slots.offset,
+              "DwArgs.gsum_ld": DwArgs.gsum_ld.offset}
     for k, v in checks.items():
         if sizes[k] != v:
             raise RuntimeError(f"native struct field {k}: ctypes offset {v} != C++ {sizes[k]}")
@@ -198,7 +203,7 @@ def raw(struct) -> bytes:
 
 
 def bn_args(stats=None, gamma=None, beta=None, mmean=None, mvar=None, count=1, eps=1e-3,
-            mode=0, act=0, C_=0) -> BnArgs:
+            mode=0, act=0, C_=0, slots=1) -> BnArgs:
     b = BnArgs()
     b.stats, b.gamma, b.beta = ptr(stats), ptr(gamma), ptr(beta)
     b.mmean, b.mvar = ptr(mmean), ptr(mvar)
@@ -207,4 +212,5 @@ def bn_args(stats=None, gamma=None, beta=None, mmean=None, mvar=None, count=1, e
     b.mode = int(mode)
     b.act = int(act)
     b.C = int(C_)
+    b.slots = int(slots)
     return b

@@ -57,7 +57,7 @@ def _time_op(plan, i, stream, reps=4) -> float:
     return e0.elapsed_time(e1) / reps
 
 
-def _conv_candidates(ext, M: int, cout: int, payload: bytes = None):
+def _conv_candidates(ext, M: int, cout: int, payload: bytes = None, halo: bool = False):
     ntile = ext.num_tiles()
     cap = 32 if cout <= 32 else (64 if cout <= 64 else 128)
     out = []
@@ -68,7 +68,7 @@ def _conv_candidates(ext, M: int, cout: int, payload: bytes = None):
         if bm > 64 and M <= 2 * 64:
             continue
         out.append(t)
-    if payload is not None and os.environ.get("IDC_HALO", "0") == "1" and ext.halo_ok(payload):
+    if payload is not None and (halo or os.environ.get("IDC_HALO", "0") == "1") and ext.halo_ok(payload):
         out.append(ext.TILE_HALO)
     return out
 
@@ -86,9 +86,16 @@ def _splits_for(ext, a, t: int, M: int, slab_floats: int):
     return [s for s in (2, 4, 8) if tiles * s * bm * bn <= slab_floats and nk >= 2 * s]
 
 
-def autotune_plan(plan, stream, verbose: bool = False, reset_tickets=None, slab_floats: int = 0) -> int:
+def autotune_plan(plan, stream, verbose: bool = False, reset_tickets=None, slab_floats: int = 0,
+                  halo_ops=()) -> int:
     """Tune every conv / wgrad op of ``plan`` in place: tile shape, then the split-K factor of the
-    best few tiles (ops whose payload carries a split-K workspace).  Returns the number tuned."""
+    best few tiles (ops whose payload carries a split-K workspace).  Returns the number tuned.
+
+    ``halo_ops``: op indices that may also use the direct 3x3 halo kernel (conv3x3_halo.hip).  The
+    program passes its forward segment: there no side-lane kernel competes for LDS, so the
+    isolated timing is the in-situ one (in the backward the halo kernel's 90-150 KB LDS footprint
+    starves the concurrent weight-gradient kernels)."""
+    halo_ops = set(halo_ops)
     _load_cache()
     ext = nat.load()
     n = 0
@@ -100,12 +107,12 @@ def autotune_plan(plan, stream, verbose: bool = False, reset_tickets=None, slab_
             M = a.N * a.Ho * a.Wo
             pro = int(a.pro.mode != 0 or a.pro.act != 0)
             key = ("conv", M, a.Cout, a.Cin, a.KH, a.KW, a.SH, a.PT, a.ldx, f32, pro, a.epi_mode,
-                   a.out_mode, int(bool(a.bias)), a.H, a.W)
+                   a.out_mode, int(bool(a.bias)), a.H, a.W, int(i in halo_ops))
             best = _CACHE.get(key)
             if best is None:
                 times = {}
                 plan.set_int(i, 2, 1)
-                for t in _conv_candidates(ext, M, a.Cout, plan.payload(i)) or [ext.pick_tile(M, a.Cout)]:
+                for t in _conv_candidates(ext, M, a.Cout, plan.payload(i), i in halo_ops) or [ext.pick_tile(M, a.Cout)]:
                     plan.set_int(i, 0, t)
                     times[(t, 1)] = _time_op(plan, i, stream)
                 if a.slab and a.tickets and reset_tickets is not None and \

@@ -55,12 +55,26 @@ class Tensor4:
         return Tensor4(self.t, self.N, self.H, self.W, c, self.ld, self.coff + c0)
 
 
+def stat_slots_for(rows: int) -> int:
+    """Statistics slot copies for a reduction over ``rows`` rows (csrc/kernels/common.h,
+    "Statistics slots"): global float atomics serialise per address at ~24 ns each, so producers
+    with many row blocks spread their per-channel adds over copies that consumers sum.  About
+    one copy per 4096 rows keeps every address under ~70 adds (block-1 DenseNet convs: 676 row
+    tiles -> 16 copies, ~42 adds each) while a consumer's table read stays <= 32 x C floats."""
+    s = 1
+    while s < 16 and s * 4096 < rows:
+        s *= 2
+    return s
+
+
 @dataclass
 class Stats:
-    """[sum | sumsq] statistics of a tensor: row length ``ld`` channels, ``count`` samples."""
-    t: torch.Tensor   # view into the stats arena, 2*ld floats
+    """[sum | sumsq] statistics of a tensor: row length ``ld`` channels, ``count`` samples,
+    ``slots`` copies of the [sum | sumsq] pair (stride 2*ld) that consumers add up."""
+    t: torch.Tensor   # view into the stats arena, 2*ld*slots floats
     ld: int
     count: int
+    slots: int = 1
 
     @property
     def ptr(self):
@@ -91,7 +105,8 @@ class BNRef:
                            gamma=self.gamma, beta=self.beta,
                            mmean=self.layer.moving_mean, mvar=self.layer.moving_variance,
                            count=st.count if st is not None else 1, eps=self.layer.epsilon,
-                           mode=self.mode, act=self.act, C_=st.ld if st is not None else self.C)
+                           mode=self.mode, act=self.act, C_=st.ld if st is not None else self.C,
+                           slots=st.slots if (st is not None and self.mode == 1) else 1)
 
 
 def act_only(act: int) -> nat.BnArgs:
@@ -123,6 +138,9 @@ class Builder:
         # direct 3x3 kernel (conv3x3_halo.hip): opt-in — ~25% faster per kernel in isolation, but
         # its 90-150 KB LDS footprint blocks the side-lane wgrads from sharing CUs (net loss)
         self.use_halo = os.environ.get("IDC_HALO", "0") == "1"
+        # statistics slots (stat_slots_for); IDC_STAT_SLOTS=0 restores single-copy reductions
+        self.stat_slots_on = os.environ.get("IDC_STAT_SLOTS", "1") != "0"
+        self.pending_sums: List["BNRef"] = []  # BatchNorms whose gradient slot copies await a fold
         self.guards: List[tuple] = []
         self.splitk_slab: Optional[torch.Tensor] = None
         self.tickets: List[torch.Tensor] = []
@@ -159,13 +177,59 @@ class Builder:
     def nhwc(self, N, H, W, C, dtype=BF16) -> Tensor4:
         return Tensor4(self.alloc((N, H, W, C), dtype), N, H, W, C, C)
 
-    def stats(self, ld: int, count: int) -> Stats:
-        n = 2 * ((ld + 3) // 4 * 4)
+    def _stats_floats(self, n: int) -> torch.Tensor:
+        """A view of ``n`` floats of the stats arena (zeroed at the start of every step)."""
+        n = (n + 3) // 4 * 4
         if self._stats_size + n > self._stats_cap:
             raise RuntimeError("stats arena capacity exceeded")
         v = self.stats_arena[self._stats_size:self._stats_size + n]
         self._stats_size += n
-        return Stats(v, ld, count)
+        return v
+
+    def stats(self, ld: int, count: int) -> Stats:
+        slots = stat_slots_for(count) if self.stat_slots_on else 1
+        return Stats(self._stats_floats(2 * ld * slots), ld, count, slots)
+
+    def grad_sums(self, bn: Optional["BNRef"], rows: int):
+        """(gsum, gsumx, slots, ld) for the producer of a BatchNorm backward's reductions
+        (sum dZ -> d beta, sum dZ*xhat -> d gamma).  With several row blocks the producer adds
+        into slot copies in the stats arena and ``finish_grad_sums`` folds them into the gradient
+        arena on the side lane; consumers (bn_bwd_apply) read the copies directly."""
+        if bn is None or bn.dbeta is None:
+            return 0, 0, 1, 0
+        if getattr(bn, "gsums", None) is not None:
+            raise RuntimeError(f"{bn.layer.name}: a second BatchNorm-backward reduction producer")
+        S = stat_slots_for(rows) if self.stat_slots_on else 1
+        if S == 1:
+            bn.gsums = (bn.dbeta.data_ptr(), bn.dgamma.data_ptr(), 1, 0)
+        else:
+            v = self._stats_floats(2 * S * bn.C)
+            bn.gsums = (v.data_ptr(), v.data_ptr() + 4 * S * bn.C, S, bn.C)
+        return bn.gsums
+
+    def finish_grad_sums(self, bn: Optional["BNRef"]):
+        """After the producer op: slot copies still have to be folded into d beta / d gamma.
+        The BatchNorm's bn_bwd_apply does it for free (its block 0 already sums the copies);
+        ``mark_grads_ready`` and ``flush_grad_sums`` emit a collapse op for any BatchNorm whose
+        apply never comes (freeze boundaries) or comes after its gradients are declared final."""
+        if bn is None or getattr(bn, "gsums", None) is None:
+            return
+        if bn.gsums[2] > 1:
+            self.pending_sums.append(bn)
+
+    def _collapse(self, bn: "BNRef"):
+        g, gx, S, ld = bn.gsums
+        self.emit(nat.OP_COLLAPSE, ints=(S, ld, bn.C), ptrs=(g, bn.dbeta.data_ptr(), gx, bn.dgamma.data_ptr()))
+
+    def flush_grad_sums(self, params=None):
+        """Collapse pending slot copies (of the BatchNorms owning ``params``, or all)."""
+        keep = []
+        for bn in self.pending_sums:
+            if params is None or any(bn.gamma is q or bn.beta is q for q in params):
+                self._collapse(bn)
+            else:
+                keep.append(bn)
+        self.pending_sums = keep
 
     # ------------------------------------------------------------------ op emission
     def emit(self, kind, payload=None, ints=(), floats=(), longs=(), ptrs=(), lane=0):
@@ -177,6 +241,7 @@ class Builder:
 
     def mark_grads_ready(self, params):
         """Backward has finished producing the grads of ``params`` (for DP bucket overlap)."""
+        self.flush_grad_sums(params)
         idx = [i for i, p in enumerate(self.arena.params) if any(p is q for q in params)]
         if idx:
             self.bwd_marks.append((len(self.ops), min(idx)))
@@ -267,6 +332,7 @@ class Builder:
         d.stats = st.ptr
         d.C = bn.C
         d.ld = st.ld
+        d.slots = st.slots
         d.inv_count = 1.0 / st.count
         d.unbias = st.count / max(st.count - 1, 1)
         d.mmean = bn.layer.moving_mean.data_ptr()
@@ -305,6 +371,7 @@ class Builder:
         a.out_mode = out_mode
         if stats is not None:
             a.stats_out, a.stats_ld, a.stats_off = stats.ptr, stats.ld, stats_off
+            a.stats_slots = stats.slots
         a.mbn = act_only(0)
         M = x.N * y.H * y.W
         if tile < 0:
@@ -336,9 +403,11 @@ class Builder:
         return ext.pick_tile(M, cout)
 
     def dgrad(self, dy: Tensor4, layer, dx: Tensor4, *, pads=(0, 0), mx: Optional[Tensor4] = None,
-              mbn: Optional[nat.BnArgs] = None, gsum=None, gsumx=None, out_mode=nat.OUT_BF16):
+              mbn: Optional[nat.BnArgs] = None, gsum=None, gsumx=None, gbn: Optional["BNRef"] = None,
+              out_mode=nat.OUT_BF16):
         """Stride-1 data gradient: conv of dy with the flipped kernel; optional BN-backward
-        epilogue through the BN+act that produced the forward input ``mx``."""
+        epilogue through the BN+act that produced the forward input ``mx`` whose reductions go
+        to ``gbn``'s gradient sums (or to explicit ``gsum``/``gsumx`` arrays)."""
         kh, kw = layer.kernel_size
         center = self.is_center_only(layer, dx.H, dx.W, (1, 1), pads)
         if center:
@@ -358,13 +427,17 @@ class Builder:
             a.epi_mode = 1
             a.mx, a.ldmx = mx.ptr, mx.ld
             a.mbn = mbn
-            a.gsum, a.gsumx = nat.ptr(gsum), nat.ptr(gsumx)
+            if gbn is not None:
+                a.gsum, a.gsumx, a.gsum_slots, a.gsum_ld = self.grad_sums(gbn, dx.M)
+            else:
+                a.gsum, a.gsumx = nat.ptr(gsum), nat.ptr(gsumx)
         else:
             a.epi_mode = 0
             a.out_mode = out_mode
         tile = self._default_tile(a, dx.M, dx.C)
         self._splitk(a, dx.M, dx.C)
         self.emit(nat.OP_CONV, a, ints=(tile, 1 if dy.is_f32 else 0, 1))
+        self.finish_grad_sums(gbn)
 
     def wgrad(self, x: Tensor4, layer, g: Tensor4, dw: torch.Tensor, *, stride=(1, 1), pads=(0, 0),
               pro=None, cin_real=0, splits=-1, lane=0):
@@ -403,7 +476,13 @@ class Builder:
         a.dz, a.lddz = dz.ptr, dz.ld
         a.x, a.ldx = x.ptr, x.ld
         a.bn = bn.args()
-        a.gsum, a.gsumx = nat.ptr(bn.dbeta), nat.ptr(bn.dgamma)
+        if bn.mode == 1:
+            if getattr(bn, "gsums", None) is None:
+                raise RuntimeError(f"{bn.layer.name}: BatchNorm backward apply before its reductions")
+            a.gsum, a.gsumx, a.gsum_slots, a.gsum_ld = bn.gsums
+            if bn in self.pending_sums:
+                a.fold_sum, a.fold_sumx = bn.dbeta.data_ptr(), bn.dgamma.data_ptr()
+                self.pending_sums.remove(bn)
         a.inv_n = 1.0 / float(x.M)
         a.dst, a.lddst = dst.ptr, dst.ld
         a.dst_f32 = 1 if dst.is_f32 else 0
@@ -419,9 +498,10 @@ class Builder:
         a.x, a.ldx = x.ptr, x.ld
         a.bn = bn.args()
         a.dz, a.lddz = dz.ptr, dz.ld
-        a.gsum, a.gsumx = nat.ptr(bn.dbeta), nat.ptr(bn.dgamma)
+        a.gsum, a.gsumx, a.gsum_slots, a.gsum_ld = self.grad_sums(bn, x.M)
         a.M, a.C = x.M, x.C
         self.emit(nat.OP_BN_BWD_REDUCE, a)
+        self.finish_grad_sums(bn)
 
     def pool(self, x: Tensor4, y: Tensor4, *, k, s, pt=0, pl=0, pro=None, is_max=True,
              argmax: Optional[torch.Tensor] = None, stats: Optional[Stats] = None, stats_off=0):
@@ -435,6 +515,7 @@ class Builder:
         a.argmax = nat.ptr(argmax)
         if stats is not None:
             a.stats, a.stats_ld, a.stats_off = stats.ptr, stats.ld, stats_off
+            a.stats_slots = stats.slots
         self.emit(nat.OP_MAXPOOL if is_max else nat.OP_AVGPOOL, a)
 
     def pool_bwd(self, dy: Tensor4, dx: Tensor4, *, k, s, pt=0, pl=0, is_max=True, argmax=None,
@@ -449,12 +530,13 @@ class Builder:
             a.x, a.ldx = x.ptr, x.ld
             a.bn = bn.args() if bn is not None else act_only(act)
             if bn is not None:
-                a.gsum, a.gsumx = nat.ptr(bn.dbeta), nat.ptr(bn.dgamma)
+                a.gsum, a.gsumx, a.gsum_slots, a.gsum_ld = self.grad_sums(bn, dx.M)
         else:
             a.bn = act_only(0)
         a.dx, a.lddx = dx.ptr, dx.ld
         a.is_avg = 0 if is_max else 1
         self.emit(nat.OP_POOL_BWD, a)
+        self.finish_grad_sums(bn if x is not None else None)
 
     def bn_apply(self, x: Tensor4, bn: "BNRef", y: Tensor4, *, act: Optional[int] = None,
                  res: Optional[Tensor4] = None, stats: Optional[Stats] = None):
@@ -464,7 +546,7 @@ class Builder:
             args.act = act
         self.emit(nat.OP_BN_APPLY, args,
                   ints=(x.ld, res.ld if res is not None else 0, y.ld, x.M, x.C,
-                        stats.ld if stats is not None else 0),
+                        stats.ld if stats is not None else 0, stats.slots if stats is not None else 1),
                   ptrs=(x.ptr, res.ptr if res is not None else 0, y.ptr,
                         stats.ptr if stats is not None else 0))
 
@@ -484,6 +566,7 @@ class Builder:
         a.y, a.ldy = y.ptr, y.ld
         if stats is not None:
             a.stats, a.stats_ld = stats.ptr, stats.ld
+            a.stats_slots = stats.slots
         self.emit(nat.OP_DW_FWD, a)
 
     def dw_bwd_data(self, x: Tensor4, layer, dy: Tensor4, dz: Tensor4, *, stride=1, pads=(1, 1),
@@ -493,8 +576,9 @@ class Builder:
         a.dy, a.lddy = dy.ptr, dy.ld
         a.dx, a.lddx = dz.ptr, dz.ld
         if bn is not None:
-            a.gsum, a.gsumx = nat.ptr(bn.dbeta), nat.ptr(bn.dgamma)
+            a.gsum, a.gsumx, a.gsum_slots, a.gsum_ld = self.grad_sums(bn, dz.M)
         self.emit(nat.OP_DW_BWD_DATA, a)
+        self.finish_grad_sums(bn)
 
     def dw_wgrad(self, x: Tensor4, layer, dy: Tensor4, dw: torch.Tensor, *, stride=1, pads=(1, 1),
                  pro=None, lane=0):

@@ -113,11 +113,13 @@ def lower_densenet(b: Builder, net, U: int, input_dtype):
     M4 = last["buf"].M
     zf = b.nhwc(last["buf"].N, last["buf"].H, last["buf"].W, last["ctot"])
     b.bn_bwd_reduce(dA, last["buf"], bnf, zf)
-    b.mark_grads_ready([bnf.gamma, bnf.beta])
     if not fz.before(L["bn"]):
+        b.mark_grads_ready([bnf.gamma, bnf.beta])
         return
     dbuf = b.nhwc(last["buf"].N, last["H"], last["W"], last["ctot"], F32)
+    # marks follow the BatchNorm's apply: it folds the statistics-slot copies of d gamma / d beta
     b.bn_bwd_apply(zf, last["buf"], bnf, dbuf, accumulate=False)
+    b.mark_grads_ready([bnf.gamma, bnf.beta])
 
     for si in range(len(stages) - 1, -1, -1):
         st = stages[si]
@@ -136,7 +138,7 @@ def lower_densenet(b: Builder, net, U: int, input_dtype):
             if not fz.before(cv2):
                 stop = True
                 break
-            b.dgrad(dO, cv2, z2, pads=(1, 1), mx=t, mbn=bn2.args(), gsum=bn2.dbeta, gsumx=bn2.dgamma)
+            b.dgrad(dO, cv2, z2, pads=(1, 1), mx=t, mbn=bn2.args(), gbn=bn2)
             if not fz.before(bn2.layer):
                 stop = True
                 break
@@ -148,12 +150,14 @@ def lower_densenet(b: Builder, net, U: int, input_dtype):
                 stop = True
                 break
             z1v = Tensor4(z1.t, N, Hs, Ws, cin, cin)
-            b.dgrad(dt, cv1, z1v, mx=buf.slice(0, cin), mbn=bn1.args(), gsum=bn1.dbeta, gsumx=bn1.dgamma)
-            b.mark_grads_ready([cv2.kernel, cv1.kernel, bn2.gamma, bn2.beta, bn1.gamma, bn1.beta])
+            b.dgrad(dt, cv1, z1v, mx=buf.slice(0, cin), mbn=bn1.args(), gbn=bn1)
+            ready = [cv2.kernel, cv1.kernel, bn2.gamma, bn2.beta, bn1.gamma, bn1.beta]
             if not fz.before(bn1.layer):
+                b.mark_grads_ready(ready)
                 stop = True
                 break
             b.bn_bwd_apply(z1v, buf.slice(0, cin), bn1, dbuf.slice(0, cin), accumulate=True)
+            b.mark_grads_ready(ready)
         if stop:
             return
         if si == 0:
@@ -172,11 +176,12 @@ def lower_densenet(b: Builder, net, U: int, input_dtype):
         pbuf = prev["buf"]
         zt = b.nhwc(pbuf.N, prev["H"], prev["W"], prev["ctot"])
         b.pool_bwd(dp, zt, k=2, s=2, is_max=False, x=pbuf, bn=bnt)
-        b.mark_grads_ready([cvt.kernel, bnt.gamma, bnt.beta])
         if not fz.before(bnt.layer):
+            b.mark_grads_ready([cvt.kernel, bnt.gamma, bnt.beta])
             return
         dbuf = b.nhwc(pbuf.N, prev["H"], prev["W"], prev["ctot"], F32)
         b.bn_bwd_apply(zt, pbuf, bnt, dbuf, accumulate=False)
+        b.mark_grads_ready([cvt.kernel, bnt.gamma, bnt.beta])
 
     # stem: maxpool backward through BN+ReLU of conv1, then conv1 wgrad
     if not fz.at_or_before(bn1l):

@@ -122,11 +122,12 @@ def lower_mobilenet(b: Builder, net, U: int, input_dtype):
         return
     zc = b.nhwc(c1.N, c1.H, c1.W, c1.C)
     b.bn_bwd_reduce(dA, c1, bn_c1, zc)
-    b.mark_grads_ready([bn_c1.gamma, bn_c1.beta])
     if not fz.before(c1bnl):
+        b.mark_grads_ready([bn_c1.gamma, bn_c1.beta])
         return
     dc1 = b.nhwc(c1.N, c1.H, c1.W, c1.C)
     b.bn_bwd_apply(zc, c1, bn_c1, dc1, accumulate=False)
+    b.mark_grads_ready([bn_c1.gamma, bn_c1.beta])
     h_last = blocks[-1]["h_out"]
     if fz.trainable(c1l):
         b.wgrad(h_last, c1l, dc1, b.arena.grad_of(c1l.kernel), lane=1)
@@ -142,23 +143,25 @@ def lower_mobilenet(b: Builder, net, U: int, input_dtype):
         # project BN (no activation): G is the gradient of BN_p(p) (+ residual passthrough)
         zp = b.nhwc(p.N, p.H, p.W, p.C)
         b.bn_bwd_reduce(G, p, bn_p, zp)
-        b.mark_grads_ready([bn_p.gamma, bn_p.beta])
         if not fz.before(bn_p.layer):
+            b.mark_grads_ready([bn_p.gamma, bn_p.beta])
             return
         dp = b.nhwc(p.N, p.H, p.W, p.C)
         b.bn_bwd_apply(zp, p, bn_p, dp, accumulate=False)
+        b.mark_grads_ready([bn_p.gamma, bn_p.beta])
         if fz.trainable(prj):
             b.wgrad(d, prj, dp, b.arena.grad_of(prj.kernel), pro=bn_d.args(), lane=1)
         b.mark_grads_ready([prj.kernel])
         if not fz.before(prj):
             return
         zd = b.nhwc(d.N, d.H, d.W, d.C)
-        b.dgrad(dp, prj, zd, mx=d, mbn=bn_d.args(), gsum=bn_d.dbeta, gsumx=bn_d.dgamma)
-        b.mark_grads_ready([bn_d.gamma, bn_d.beta])
+        b.dgrad(dp, prj, zd, mx=d, mbn=bn_d.args(), gbn=bn_d)
         if not fz.before(bn_d.layer):
+            b.mark_grads_ready([bn_d.gamma, bn_d.beta])
             return
         dd = b.nhwc(d.N, d.H, d.W, d.C)
         b.bn_bwd_apply(zd, d, bn_d, dd, accumulate=False)
+        b.mark_grads_ready([bn_d.gamma, bn_d.beta])
         e, bn_in = blk["e"], blk["bn_in"]
         if fz.trainable(dwl):
             b.dw_wgrad(e, dwl, dd, b.arena.grad_of(dwl.depthwise_kernel), stride=blk["stride"],
@@ -168,11 +171,12 @@ def lower_mobilenet(b: Builder, net, U: int, input_dtype):
             return
         ze = b.nhwc(e.N, e.H, e.W, e.C)
         b.dw_bwd_data(e, dwl, dd, ze, stride=blk["stride"], pads=blk["pads"], bn=bn_in)
-        b.mark_grads_ready([bn_in.gamma, bn_in.beta])
         if not fz.before(bn_in.layer):
+            b.mark_grads_ready([bn_in.gamma, bn_in.beta])
             return
         de = b.nhwc(e.N, e.H, e.W, e.C)
         b.bn_bwd_apply(ze, e, bn_in, de, accumulate=False)
+        b.mark_grads_ready([bn_in.gamma, bn_in.beta])
         ex = blk["ex"]
         if ex is None:  # block 0: de is the gradient of the raw stem conv output
             if fz.trainable(conv1):

@@ -72,6 +72,9 @@ class FusedProgram:
         self.U = net.num_outputs
         b = Builder(net, model.arena, model.device, batch, training)
         _lowering_for(net)(b, net, self.U, input_dtype)
+        if b.pending_sums:  # BatchNorm gradient slot copies no apply kernel folded
+            b.segment = "bwd"
+            b.flush_grad_sums()
         self.b = b
         if os.environ.get("IDC_KEEP_BUFFERS") == "1":
             _GRAVEYARD.append(b.keep)
@@ -158,8 +161,11 @@ class FusedProgram:
         self.recast_all()
         if os.environ.get("IDC_AUTOTUNE", "1") != "0":
             from .autotune import autotune_plan
+            halo = ()
+            if "fwd" in self.seg and os.environ.get("IDC_HALO_FWD", "0") == "1":
+                halo = range(*self.seg["fwd"])
             autotune_plan(self.plan, self.stream, verbose=os.environ.get("IDC_TUNE_VERBOSE") == "1",
-                          reset_tickets=b.reset_tickets, slab_floats=b.SLAB_FLOATS)
+                          reset_tickets=b.reset_tickets, slab_floats=b.SLAB_FLOATS, halo_ops=halo)
         b.reset_tickets()  # split-K tickets count modulo the op's split: start every op aligned
 
     # ------------------------------------------------------------------ execution

@@ -15,6 +15,11 @@ def rel(a, b):
     return ((a - b).norm() / (b.norm() + 1e-12)).item()
 
 
+def folded(st):
+    """[sum | sumsq] of a Stats view with its slot copies added up."""
+    return st.t[:2 * st.ld * st.slots].view(st.slots, 2 * st.ld).sum(0)
+
+
 def main():
     dev = torch.device("cuda", 0)
     B = int(sys.argv[1]) if len(sys.argv) > 1 else 8
@@ -50,7 +55,7 @@ def main():
             acts[layer.name] = h
     ys = dbg["ys"].t.float()
     print("stem conv", rel(ys, acts["conv1/conv"]))
-    ss = dbg["ss"].t
+    ss = folded(dbg["ss"])
     yr = acts["conv1/conv"]
     print("stem stats sum", rel(ss[:64], yr.sum((0, 1, 2))), "sq", rel(ss[64:128], (yr * yr).sum((0, 1, 2))))
     for si, st in enumerate(dbg["stages"]):
@@ -61,7 +66,7 @@ def main():
             print(rel(buf[..., :64], acts["pool1"]))
         else:
             print(rel(buf[..., :c0], acts[f"pool{si + 1}_pool"]))
-        stt = st["stats"].t
+        stt = folded(st["stats"])
         ctot = st["ctot"]
         for li, lay in enumerate(st["layers"]):
             name = f"conv{si + 2}_block{li + 1}"
