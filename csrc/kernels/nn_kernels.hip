@@ -166,32 +166,60 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(BnBwdApplyArgs a) {
   };
   const bool active = cm.active();
   if (active && row0 < a.M) load_pass(row0);
-  for (int c = threadIdx.x; c < a.C; c += blockDim.x) {
-    float mean, rstd;
-    bn_mean_rstd(a.bn, c, mean, rstd);
-    float g = a.bn.gamma ? a.bn.gamma[c] : 1.f;
-    if (a.bn.mode == 1) {
-      float sd, sdx;
-      const int S = min(stat_slots(a.gsum_slots), MAX_STAT_SLOTS);
-      if (S == 1) {
-        sd = a.gsum[c];
-        sdx = a.gsumx[c];
+  // coefficient table, up to 4 channels per thread per batch with every load of the batch issued
+  // before any arithmetic (gamma is required: no per-element "pointer or 1" select, which makes
+  // hipcc branch around each load and wait for it)
+  const bool batch_mode = a.bn.mode == 1;
+  const int SG = min(stat_slots(a.gsum_slots), MAX_STAT_SLOTS);
+  const int SS = min(stat_slots(a.bn.slots), MAX_STAT_SLOTS);
+  // single-copy statistics (small maps, many channels): 4 channels per thread per batch; slotted
+  // ones (large maps, <= 512 channels): one channel per batch, its 2*(SS+SG) loads in flight
+  const int per = (SG == 1 && SS == 1) ? 4 : 1;
+  for (int base = 0; base < a.C; base += per * 256) {
+    float m0[4], m1[4], g[4], q0[4], q1[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      if (u >= per) break;
+      const int c = base + u * 256 + threadIdx.x;
+      const int cc = c < a.C ? c : 0;
+      g[u] = a.bn.gamma[cc];
+      if (batch_mode) {
+        if (SS == 1) {
+          m0[u] = a.bn.stats[cc];
+          m1[u] = a.bn.stats[a.bn.C + cc];
+        } else {
+          slot_sums_1(a.bn.stats, a.bn.stats + a.bn.C, SS, 2 * (size_t)a.bn.C, cc, m0[u], m1[u]);
+        }
+        if (SG == 1) {
+          q0[u] = a.gsum[cc];
+          q1[u] = a.gsumx[cc];
+        } else {
+          slot_sums_1(a.gsum, a.gsumx, SG, a.gsum_ld, cc, q0[u], q1[u]);
+        }
       } else {
-        slot_sums_1(a.gsum, a.gsumx, S, a.gsum_ld, c, sd, sdx);
+        m0[u] = a.bn.mmean[cc];
+        m1[u] = a.bn.mvar[cc];
+        q0[u] = q1[u] = 0.f;
       }
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int c = base + u * 256 + threadIdx.x;
+      if (u >= per || c >= a.C) break;
+      float mean = m0[u], var = m1[u];
+      if (batch_mode) {
+        mean *= a.bn.inv_count;
+        var = fmaxf(var * a.bn.inv_count - mean * mean, 0.f);
+      }
+      const float rstd = rsqrtf(var + a.bn.eps);
       if (blockIdx.x == 0 && a.fold_sum) {  // d beta / d gamma into the gradient arena
-        a.fold_sum[c] += sd;
-        a.fold_sumx[c] += sdx;
+        a.fold_sum[c] += q0[u];
+        a.fold_sumx[c] += q1[u];
       }
-      sd *= a.inv_n;
-      sdx *= a.inv_n;
-      sA[c] = g * rstd;
-      sB[c] = -g * rstd * rstd * sdx;
-      sC[c] = -g * rstd * sd + g * rstd * rstd * mean * sdx;
-    } else {
-      sA[c] = g * rstd;
-      sB[c] = 0.f;
-      sC[c] = 0.f;
+      const float sd = q0[u] * a.inv_n, sdx = q1[u] * a.inv_n;
+      sA[c] = g[u] * rstd;
+      sB[c] = -g[u] * rstd * rstd * sdx;
+      sC[c] = -g[u] * rstd * sd + g[u] * rstd * rstd * mean * sdx;
     }
   }
   __syncthreads();
@@ -234,6 +262,9 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(BnBwdApplyArgs a) {
 
 hipError_t bn_bwd_apply(const BnBwdApplyArgs& a, hipStream_t st) {
   if (a.M == 0) return hipSuccess;
+  if (a.bn.gamma == nullptr || (a.bn.mode == 1 && (a.gsum == nullptr || a.gsumx == nullptr)) ||
+      (a.bn.mode == 2 && (a.bn.mmean == nullptr || a.bn.mvar == nullptr)) || (a.bn.mode != 1 && a.bn.mode != 2))
+    return hipErrorInvalidValue;
   // ~1 iteration of RU rows per thread: enough blocks to fill all 256 CUs several times over
   dim3 grid(grid_rows(a.M, a.C, 4)), block(256);
   size_t shm = 3 * a.C * 4;
@@ -293,7 +324,7 @@ hipError_t bn_bwd_reduce(const BnBwdReduceArgs& a, hipStream_t st) {
 }
 
 // ------------------------------------------------------------------------------------------
-template <bool IS_MAX>
+template <bool IS_MAX, int K>
 __global__ __launch_bounds__(256) void pool_fwd_kernel(PoolArgs a) {
   extern __shared__ float sh[];
   float* s_sc = sh;
@@ -315,12 +346,32 @@ __global__ __launch_bounds__(256) void pool_fwd_kernel(PoolArgs a) {
       uint8_t arg[8];
 #pragma unroll
       for (int j = 0; j < 8; ++j) { best[j] = -3.4e38f; sum[j] = 0.f; arg[j] = 0; }
-      for (int r = 0; r < a.k; ++r)
-        for (int s2 = 0; s2 < a.k; ++s2) {
-          int h = ho * a.s - a.pt + r, w = wo * a.s - a.pl + s2;
+      const int k = K > 0 ? K : a.k;
+      // K > 0 (the model shapes: 3x3 stem max pool, 2x2 pools): every tap's load is issued before
+      // any arithmetic — out-of-image taps load a clamped in-image pixel and are replaced by the
+      // zero padding afterwards — instead of k*k dependent round trips; K == 0: runtime k
+      constexpr int KK = K > 0 ? K * K : 1;
+      uint4 raw[KK];
+      if constexpr (K > 0) {
+#pragma unroll
+        for (int q = 0; q < KK; ++q) {
+          const int h = min(max(ho * a.s - a.pt + q / K, 0), a.H - 1);
+          const int w = min(max(wo * a.s - a.pl + q % K, 0), a.W - 1);
+          raw[q] = *reinterpret_cast<const uint4*>(a.x + ((size_t)(n * a.H + h) * a.W + w) * a.ldx + c);
+        }
+      }
+#pragma unroll
+      for (int q = 0; q < (K > 0 ? KK : 1); ++q)
+        for (int qq = (K > 0 ? q : 0); qq < (K > 0 ? q + 1 : k * k); ++qq) {
+          const int r = qq / k, s2 = qq - r * k;
+          const int h = ho * a.s - a.pt + r, w = wo * a.s - a.pl + s2;
           float v[8];
           if ((unsigned)h < (unsigned)a.H && (unsigned)w < (unsigned)a.W) {
-            unpack8(*reinterpret_cast<const uint4*>(a.x + ((size_t)(n * a.H + h) * a.W + w) * a.ldx + c), v);
+            if constexpr (K > 0) {
+              unpack8(raw[q], v);
+            } else {
+              unpack8(*reinterpret_cast<const uint4*>(a.x + ((size_t)(n * a.H + h) * a.W + w) * a.ldx + c), v);
+            }
             if (!ident) {
 #pragma unroll
               for (int j = 0; j < 8; ++j) v[j] = apply_act(v[j] * s_sc[c + j] + s_sh[c + j], a.pro.act);
@@ -332,14 +383,14 @@ __global__ __launch_bounds__(256) void pool_fwd_kernel(PoolArgs a) {
 #pragma unroll
           for (int j = 0; j < 8; ++j) {
             if (IS_MAX) {
-              if (v[j] > best[j]) { best[j] = v[j]; arg[j] = (uint8_t)(r * a.k + s2); }
+              if (v[j] > best[j]) { best[j] = v[j]; arg[j] = (uint8_t)qq; }
             } else {
               sum[j] += v[j];
             }
           }
         }
       float out[8];
-      const float inv = 1.f / (float)(a.k * a.k);
+      const float inv = 1.f / (float)(k * k);
 #pragma unroll
       for (int j = 0; j < 8; ++j) out[j] = IS_MAX ? best[j] : sum[j] * inv;
       uint4 p = pack8(out);
@@ -363,17 +414,20 @@ __global__ __launch_bounds__(256) void pool_fwd_kernel(PoolArgs a) {
                slot_ptr(a.stats, a.stats_slots, 2 * (size_t)a.stats_ld) + a.stats_ld + a.stats_off);
 }
 
-hipError_t maxpool_fwd(const PoolArgs& a, hipStream_t st) {
-  hipLaunchKernelGGL(pool_fwd_kernel<true>, dim3(grid_rows(a.N * a.Ho * a.Wo, a.C)), dim3(256),
-                     (4 * a.C + 2 * 256 * 8) * 4, st, a);
+template <bool IS_MAX>
+static hipError_t pool_fwd(const PoolArgs& a, hipStream_t st) {
+  // one output row per thread per pass: the k*k taps already give k*k loads in flight
+  const dim3 grid(grid_rows(a.N * a.Ho * a.Wo, a.C, 1)), block(256);
+  const size_t shm = (4 * a.C + 2 * 256 * 8) * 4;
+  if (a.k == 3) hipLaunchKernelGGL((pool_fwd_kernel<IS_MAX, 3>), grid, block, shm, st, a);
+  else if (a.k == 2) hipLaunchKernelGGL((pool_fwd_kernel<IS_MAX, 2>), grid, block, shm, st, a);
+  else hipLaunchKernelGGL((pool_fwd_kernel<IS_MAX, 0>), grid, block, shm, st, a);
   return hipGetLastError();
 }
 
-hipError_t avgpool_fwd(const PoolArgs& a, hipStream_t st) {
-  hipLaunchKernelGGL(pool_fwd_kernel<false>, dim3(grid_rows(a.N * a.Ho * a.Wo, a.C)), dim3(256),
-                     (4 * a.C + 2 * 256 * 8) * 4, st, a);
-  return hipGetLastError();
-}
+hipError_t maxpool_fwd(const PoolArgs& a, hipStream_t st) { return pool_fwd<true>(a, st); }
+
+hipError_t avgpool_fwd(const PoolArgs& a, hipStream_t st) { return pool_fwd<false>(a, st); }
 
 // Gather-form pool backward: each input element collects from the windows that contain it, then
 // (optionally) the backward of the pending BN+act that fed the pool: dZ = g * act'(bn(x)) and the
