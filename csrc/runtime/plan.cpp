@@ -185,7 +185,14 @@ class Plan {
  private:
   void ensure_side() {
     if (side_) return;
-    check(hipStreamCreateWithFlags(&side_, hipStreamNonBlocking), "hipStreamCreate(side)");
+    // IDC_SIDE_PRIO=low gives the side lane (weight gradients, off the critical path) the lowest
+    // stream priority, so the dgrad chain's workgroups dispatch first when both lanes have work
+    // queued.  Opt-in: measured neutral on DenseNet-121 (runtime/program.py).
+    int least = 0, greatest = 0;
+    check(hipDeviceGetStreamPriorityRange(&least, &greatest), "hipDeviceGetStreamPriorityRange");
+    const char* sp = std::getenv("IDC_SIDE_PRIO");
+    const int prio = (sp && std::strcmp(sp, "low") == 0) ? least : 0;
+    check(hipStreamCreateWithPriority(&side_, hipStreamNonBlocking, prio), "hipStreamCreate(side)");
     check(hipEventCreateWithFlags(&fork_, hipEventDisableTiming), "hipEventCreate(fork)");
     check(hipEventCreateWithFlags(&join_, hipEventDisableTiming), "hipEventCreate(join)");
   }

@@ -18,6 +18,7 @@ import torch
 from ..engine.losses import BinaryCrossentropy, CategoricalCrossentropy, SparseCategoricalCrossentropy
 from ..engine.optimizers import RMSprop
 from ..ops import _native as nat
+from ..utils import trace
 from .builder import Builder
 
 
@@ -149,7 +150,11 @@ class FusedProgram:
         self.graph_segments = set(os.environ.get("IDC_GRAPH_SEGMENTS", "fwd,opt").split(","))
         self.graphs: Dict[Tuple[int, int], int] = {}
         self.grad_scale = grad_scale
-        self.stream = torch.cuda.Stream(device=model.device)
+        # stream priorities are opt-in (IDC_MAIN_PRIO=high, IDC_SIDE_PRIO=low in plan.cpp): measured
+        # neutral on DenseNet-121 bs256 (4.90-4.96 vs 4.92-5.01 ms/step), and 1.2 ms/step slower
+        # under rocprofv3 kernel tracing
+        main_prio = -1 if os.environ.get("IDC_MAIN_PRIO", "normal") == "high" else 0
+        self.stream = torch.cuda.Stream(device=model.device, priority=main_prio)
         # initial bf16 weight casts (all convs, frozen ones included)
         if b.cast_all_n:
             cast = nat.load().Plan()
@@ -202,7 +207,8 @@ class FusedProgram:
 
     def run_segment(self, name: str):
         if name in self.seg:
-            self.run_range(*self.seg[name])
+            with trace.range("seg:" + name):
+                self.run_range(*self.seg[name])
 
     def set_lr(self, lr: float):
         if self.rms_index is not None:
@@ -273,6 +279,10 @@ class FusedStep:
         return not bad
 
     def train_step(self, x, y):
+        with trace.range("train_step"):
+            return self._train_step(x, y)
+
+    def _train_step(self, x, y):
         m = self.m
         dtype = torch.uint8 if x.dtype == torch.uint8 else torch.float32
         p = self._prog(x.shape[0], True, dtype)
@@ -288,6 +298,7 @@ class FusedStep:
         if world > 1 and getattr(strategy, "central_storage", False):
             return self._central_storage_step(p, validate)
         if "bwd" in p.seg:
+            trace.push("seg:bwd")
             lo, hi = p.seg["bwd"]
             bucketer = strategy.bucketer(m.arena) if world > 1 else None
             if bucketer is not None and p.bwd_marks:
@@ -299,7 +310,7 @@ class FusedStep:
                         continue
                     p.run_range(pos, mark)
                     pos = mark
-                    with torch.cuda.stream(p.stream):
+                    with torch.cuda.stream(p.stream), trace.range("allreduce:from_param%d" % low_param):
                         bucketer.launch_range(low_param, None)
                 p.run_range(pos, hi)
                 with torch.cuda.stream(p.stream):
@@ -309,6 +320,7 @@ class FusedStep:
                 if bucketer is not None:
                     with torch.cuda.stream(p.stream):
                         bucketer.finish()
+            trace.pop()
         if p.host_optimizer:
             with torch.cuda.stream(p.stream):
                 m.optimizer.step(m.arena, grad_scale=1.0 / strategy.num_replicas_in_sync)

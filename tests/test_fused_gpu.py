@@ -47,7 +47,7 @@ def _cos(a, b):
     return (a @ b / (a.norm() * b.norm() + 1e-30)).item()
 
 
-def _check(m, ref, x, y, slack=0.03):
+def _check(m, ref, x, y, slack=0.03, loss_slack=None):
     """Fused (bf16) vs eager fp32, judged against the eager bf16-autocast drift from fp32 (the
     precision floor of bf16 training): per parameter, 1-cos(fused,fp32) must stay within
     3x the autocast deficit + ``slack``; logits within 2x the autocast deviation + 0.05."""
@@ -60,7 +60,8 @@ def _check(m, ref, x, y, slack=0.03):
     loss_ref, logits_ref, grads_ref = _ref_grads(ref, x, y)
     loss16, logits16, grads16 = _ref_grads(ref16, x, y, bf16=True)
     loss = p.io.loss.item()
-    assert abs(loss - loss_ref.item()) < 2 * abs(loss16.item() - loss_ref.item()) + slack, \
+    loss_slack = slack if loss_slack is None else loss_slack
+    assert abs(loss - loss_ref.item()) < 2 * abs(loss16.item() - loss_ref.item()) + loss_slack, \
         (loss, loss_ref.item(), loss16.item())
     lg = p.io.logits.reshape(-1)
     dev_fused = (lg - logits_ref.reshape(-1)).abs().max().item()
@@ -120,7 +121,11 @@ def test_densenet201_cifar_shape():
     # batch 32: at batch 8 random-init DenseNet-201 is chaotic in bf16 (autocast's own gradient
     # cosine vs fp32 drops to ~0.4), which makes any comparison meaningless
     m, ref, x, y = _setup("densenet201", 32, shape=(32, 32, 3))
-    _check(m, ref, x, y)
+    # 201 layers deep, the loss moves ~0.03-0.04 between runs of the fused program itself (float
+    # atomics in the BN statistics reduce in a different order each run, and every BN input is a
+    # bf16-stored activation while autocast normalises fp32 copies): the loss gets 0.06 of slack,
+    # logits and every gradient keep the default bounds
+    _check(m, ref, x, y, loss_slack=0.06)
 
 
 def test_vgg16_fused_matches_eager():
