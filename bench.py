@@ -48,7 +48,11 @@ def main():
     from idc_models_amd.parallel.comm import all_reduce_max, barrier
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
-    if world > 1:
+    if world > 1 and os.environ.get("IDC_BENCH_REHEARSE") == "1":
+        # rehearsal of the N>1 path on a one-GPU box: every rank on cuda:0, gloo collectives
+        # (RCCL refuses two ranks on one device); numbers from this mode are not throughput
+        strategy = MirroredStrategy(backend="gloo", device="cuda:0")
+    elif world > 1:
         strategy = MirroredStrategy()
     else:
         strategy = OneDeviceStrategy("cuda:0")
