@@ -152,6 +152,28 @@ __device__ __forceinline__ int stat_slots(int s) { return s > 1 ? s : 1; }
 constexpr int MAX_STAT_SLOTS = 16;
 __device__ __forceinline__ void slot_sums_1(const float* p0, const float* p1, int S, size_t stride, int cc,
                                             float& v0, float& v1) {
+  if (S == 1) {  // single copy (small maps): two loads, not 2*MAX_STAT_SLOTS
+    v0 = p0[cc];
+    v1 = p1[cc];
+    return;
+  }
+  if (S <= 4) {
+    float t0[4], t1[4];
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      const size_t o = (size_t)(s < S ? s : S - 1) * stride + cc;
+      t0[s] = p0[o];
+      t1[s] = p1[o];
+    }
+    v0 = 0.f;
+    v1 = 0.f;
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      v0 += s < S ? t0[s] : 0.f;
+      v1 += s < S ? t1[s] : 0.f;
+    }
+    return;
+  }
   float t0[MAX_STAT_SLOTS], t1[MAX_STAT_SLOTS];
 #pragma unroll
   for (int s = 0; s < MAX_STAT_SLOTS; ++s) {
@@ -309,6 +331,98 @@ __device__ __forceinline__ void bn_full_table(const BnArgs& b, int C, float* s_s
       s_rs[c] = rs;
     }
   }
+}
+
+// Pending BatchNorm BACKWARD ("backward pending affine").  The input gradient of a training-mode
+// BatchNorm is  dX = A*dZ + B*X + C  per channel, with
+//   A = gamma*rstd,  B = -gamma*rstd^2 * mean(dZ*xhat),  C = -gamma*rstd*mean(dZ) - B*mean
+// where the two means are reductions over the whole batch that the PRODUCER of dZ accumulated.
+// Instead of materialising dX with a separate pass (one launch + a full write and re-read per BN),
+// every CONSUMER of dX stages  v' = A*v + B*x + C  while loading its operand v (= dZ), with x the
+// BN's raw forward input at the same pixel and channel.  With `unit_alpha` the operand already
+// holds the A*dZ terms (DenseNet's fp32 concat-gradient buffer, into which each BatchNorm's
+// producer accumulated A*dZ in its epilogue) and only the B*x + C part of ONE BatchNorm is
+// still pending.  mode 0 = off; inference-mode BatchNorms (mode 2) give A = gamma*rstd, B = C = 0.
+// All pointers are pre-offset to the operand's first channel.  Optionally one workgroup of the
+// consumer folds the statistics-slot copies of the reductions into the BatchNorm's d beta / d gamma
+// (fold_*: channels [0, fold_C) from gsum/gsumx bases fgsum/fgsumx).
+struct BwdAff {
+  const bf16_t* x; int ldx;
+  BnArgs bn;
+  const float* gsum; const float* gsumx;
+  int gsum_slots, gsum_ld;
+  float inv_n;
+  int unit_alpha;
+  int mode;
+  int fold_C;
+  const float* fgsum; const float* fgsumx;
+  float* fold_sum; float* fold_sumx;
+};
+
+// A/B/C table for channels c0 + [0, n) into sA/sB/sC[0, n) (LDS); channels at or past `lim` get
+// the identity; all loads of a channel are issued before its arithmetic.
+template <int NT>
+__device__ __forceinline__ void bwd_aff_table(const BwdAff& b, int c0, int n, int lim, float* sA, float* sB,
+                                              float* sC) {
+  const int tid = threadIdx.x;
+  const int SS = b.bn.mode == 1 ? min(stat_slots(b.bn.slots), MAX_STAT_SLOTS) : 1;
+  const int SG = b.bn.mode == 1 ? min(stat_slots(b.gsum_slots), MAX_STAT_SLOTS) : 1;
+  for (int i = tid; i < n; i += NT) {
+    const int c = c0 + i;
+    if (b.mode == 0 || c >= lim) {
+      sA[i] = 1.f;
+      sB[i] = 0.f;
+      sC[i] = 0.f;
+      continue;
+    }
+    float m0, m1, q0 = 0.f, q1 = 0.f;
+    const float g = b.bn.gamma ? b.bn.gamma[c] : 1.f;
+    if (b.bn.mode == 1) {
+      slot_sums_1(b.bn.stats, b.bn.stats + b.bn.C, SS, 2 * (size_t)b.bn.C, c, m0, m1);
+      slot_sums_1(b.gsum, b.gsumx, SG, (size_t)b.gsum_ld, c, q0, q1);
+    } else {
+      m0 = b.bn.mmean[c];
+      m1 = b.bn.mvar[c];
+    }
+    float mean = m0, var = m1;
+    if (b.bn.mode == 1) {
+      mean *= b.bn.inv_count;
+      var = fmaxf(var * b.bn.inv_count - mean * mean, 0.f);
+    }
+    const float rstd = rsqrtf(var + b.bn.eps);
+    const float sd = q0 * b.inv_n, sdx = q1 * b.inv_n;
+    const float Bc = -g * rstd * rstd * sdx;
+    sA[i] = b.unit_alpha ? 1.f : g * rstd;
+    sB[i] = Bc;
+    sC[i] = -g * rstd * sd - Bc * mean;
+  }
+}
+
+// d beta / d gamma of the BatchNorm: sum of the slot copies, once per step, spread over the
+// launch's workgroups (a 64-channel-aligned share each) so no single workgroup's prologue carries
+// the whole fold
+template <int NT>
+__device__ __forceinline__ void bwd_aff_fold(const BwdAff& b) {
+  if (b.fold_sum == nullptr) return;
+  const int nb = gridDim.x * gridDim.y * gridDim.z;
+  const int bid = blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z);
+  int share = (b.fold_C + nb - 1) / nb;
+  share = (share + 63) / 64 * 64;
+  const int c0 = bid * share, c1 = min(b.fold_C, c0 + share);
+  const int SG = min(stat_slots(b.gsum_slots), MAX_STAT_SLOTS);
+  for (int c = c0 + (int)threadIdx.x; c < c1; c += NT) {
+    float q0, q1;
+    slot_sums_1(b.fgsum, b.fgsumx, SG, (size_t)b.gsum_ld, c, q0, q1);
+    b.fold_sum[c] += q0;
+    b.fold_sumx[c] += q1;
+  }
+}
+
+// v[j] = A[j]*v[j] + B[j]*x[j] + C[j] for 8 channels (tables 32-B aligned in LDS)
+__device__ __forceinline__ void bwd_aff8(float* v, const float* x, const float* sA, const float* sB,
+                                         const float* sC) {
+#pragma unroll
+  for (int j = 0; j < 8; ++j) v[j] = fmaf(sA[j], v[j], fmaf(sB[j], x[j], sC[j]));
 }
 
 // mean and 1/sigma of a channel (for x-hat in backward)

@@ -294,6 +294,7 @@ bool conv3x3_halo_ok(const ConvArgs& a) {
   if (a.KH != 3 || a.KW != 3 || a.SH != 1 || a.SW != 1 || a.PT != 1 || a.PL != 1) return false;
   if (a.Ho != a.H || a.Wo != a.W || (a.Cin % 32) || (a.ldx % 8) || (a.ldy % 8)) return false;
   if (a.Cout != 32 && a.Cout != 64 && a.Cout != 128) return false;
+  if (a.bpro.mode != 0 || a.epi_mode > 1) return false;  // backward-affine forms: igemm only
   if (a.epi_mode == 0 && (a.bias != nullptr || a.out_mode != OUT_BF16)) return false;
   const int mtiles = (a.H * a.W + 15) / 16;
   if (mtiles > 16) return false;

@@ -49,6 +49,19 @@ struct ConvArgs {
   int stats_slots;
   int gsum_slots;
   int gsum_ld;
+  // backward pending affine on the A operand (common.h BwdAff; bpro.mode != 0 selects it): the
+  // staged operand is A*v + B*x + C with x read from bpro.x at the same pixel and channel
+  BwdAff bpro;
+  // epi 2 (DenseNet concat gradient): y is the fp32 stage-gradient buffer, and the epilogue adds
+  //   y += gamma*rstd * dZ  +  B'*x + C'
+  // where dZ = dA * act'(mbn(x)) (reduced into gsum/gsumx as in epi 1) and B', C' are the pending
+  // coefficients of the PREVIOUS BatchNorm over these channels (bepi; x = mx)
+  BwdAff bepi;
+  // PRO 2 only (optional): the staged operand (after the affine, bf16) is also stored here, one
+  // write per element (centre tap, first column tile) — the side-lane weight gradient then reads
+  // a plain bf16 gradient instead of redoing the affine on the fp32 / two-tensor form
+  bf16_t* aout;
+  int ldaout;
 };
 
 // tile TILE_HALO selects the one-image-per-workgroup direct 3x3 kernel (conv3x3_halo.hip)

@@ -1,545 +1,18 @@
-// Implicit-GEMM convolution on MFMA (v_mfma_f32_16x16x32_bf16), NHWC bf16, gfx950.
-//
-// out[m, n] = sum_k A[m, k] * Wt[n, k]
-//   m = (img, ho, wo)  in [0, M = N*Ho*Wo)
-//   n = output channel in [0, Cout)
-//   k = (r, s, c)      in [0, K = KH*KW*Cin)   (Cin % 8 == 0: one 16-B chunk never straddles (r,s))
-//   A[m, k] = act(bn(x[img, ho*SH-PT+r, wo*SW-PL+s, c]))   (0 outside the image: padding is
-//             applied AFTER the activation, as Keras' ZeroPadding/'same' conv does)
-//
-// Used for: every forward conv (3x3 s1 'same', 1x1, 7x7 s2 stem, 3x3 s2), and every stride-1
-// dgrad (a conv of dY with the spatially flipped, in/out-transposed kernel prepared by the
-// optimizer's cast kernel).
-//
-// Prologue (PRO=1): "pending BN" — the operand is the RAW output of a producer conv plus that
-// producer's batch statistics; the BN affine + ReLU/ReLU6 is applied while staging the tile in
-// LDS, so pre-activation DenseNet / post-activation MobileNetV2 need no
-// standalone BN or activation kernels.
-// Epilogue EPI=0: bias + activation, bf16/fp32 store into a channel slice of a wider buffer,
-//   optional per-channel [sum|sumsq] of the stored values (the NEXT BN's batch statistics,
-//   accumulated with one atomic per channel per block).
-// Epilogue EPI=1 (backward through a BN+act that fed this conv's forward input): the GEMM value
-//   is dA; dZ = dA * act'(z) with z recomputed from the saved forward input x; stores dZ (bf16)
-//   and accumulates sum(dZ) (= dbeta, or the previous conv's dbias) and sum(dZ*xhat) (= dgamma).
-//
-// Tiling: BM x BN x BK block tile, 4 waves in a WM x WN grid, each wave (BM/WM) x (BN/WN) of 16x16
-// MFMA fragments.  Global -> registers -> (prologue) -> LDS double buffer, one barrier per K-step;
-// LDS chunk XOR swizzle verified conflict-free for ds_read_b128 fragment reads and ds_write_b128.
-// The epilogue stages the fp32 tile through LDS so global stores (and the epilogue loads of x)
-// are 16-byte coalesced.  Block ids are remapped XCD-aware (guide §5 T1).
-#include "common.h"
+// Implicit-GEMM convolution dispatch (kernel: conv_igemm_impl.h; variants: conv_igemm_g*.hip).
 #include "conv_igemm.h"
 
 namespace idc {
 
-template <int BK>
-__device__ __forceinline__ int swz_chunk(int row, int chunk) {
-  if constexpr (BK == 32) return chunk ^ (((row >> 2) & 1) << 1);
-  else if constexpr (BK == 64) return chunk ^ (row & 6);
-  else return chunk ^ (row & 15);  // BK 128 / 256: XOR within 16-chunk groups (brute-force checked)
-}
-
-template <int BM, int BN, int BK, int WM, int WN>
-struct IgemmCfg {
-  static constexpr int NT = 256;
-  static constexpr int CPR = BK / 8;
-  static constexpr int WTM = BM / WM, WTN = BN / WN;
-  static constexpr int A_ELEMS = BM * BK, B_ELEMS = BN * BK;
-  static constexpr int STAGE_BYTES = 2 * (A_ELEMS + B_ELEMS) * 2;
-  static constexpr int CS_LD = BN + 4;
-  static constexpr int EPI_BYTES = WTM * CS_LD * 4;  // one wave-row of the tile per pass
-  static constexpr int MAIN = STAGE_BYTES > EPI_BYTES ? STAGE_BYTES : EPI_BYTES;
-  static int smem_bytes(int cpro) {
-    int t = (cpro + 3) / 4 * 4;
-    return MAIN + 2 * t * 4 + 6 * BN * 4;
-  }
-};
-
-template <int BM, int BN, int BK, int WM, int WN, bool IS1X1, typename TA, int PRO, int EPI>
-__global__ __launch_bounds__(256) void conv_igemm_kernel(ConvArgs a) {
-  using C = IgemmCfg<BM, BN, BK, WM, WN>;
-  constexpr int NT = C::NT, CPR = C::CPR, WTM = C::WTM, WTN = C::WTN;
-  constexpr int NA = (BM * CPR + NT - 1) / NT;  // A chunks per thread
-  constexpr int NB = (BN * CPR + NT - 1) / NT;  // B chunks per thread
-  constexpr int TM = WTM / 16, TN = WTN / 16;
-  constexpr int A_ELEMS = C::A_ELEMS, B_ELEMS = C::B_ELEMS, CS_LD = C::CS_LD;
-  static_assert(TM >= 1 && TN >= 1, "bad wave tile");
-  static_assert(NT % CPR == 0, "chunk mapping");
-
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  bf16_t* As = reinterpret_cast<bf16_t*>(smem);
-  bf16_t* Bs = As + 2 * A_ELEMS;
-  float* Cs = reinterpret_cast<float*>(smem);
-  const int cpro = PRO ? (a.Cin + 3) / 4 * 4 : 0;
-  float* s_scale = reinterpret_cast<float*>(smem + C::MAIN);
-  float* s_shift = s_scale + cpro;
-  float* s_sum = s_shift + cpro;
-  float* s_sq = s_sum + BN;
-  float* s_e0 = s_sq + BN;
-  float* s_e1 = s_e0 + BN;
-  float* s_e2 = s_e1 + BN;
-  float* s_e3 = s_e2 + BN;
-
-  const int tid = threadIdx.x;
-  const int lane = tid & 63;
-  const int wid = tid >> 6;
-  const int wr = wid / WN, wc = wid % WN;
-
-  const int M = a.N * a.Ho * a.Wo;
-  const int K = a.KH * a.KW * a.Cin;
-  const int ntiles = (a.Cout + BN - 1) / BN;
-  const int mtiles = (M + BM - 1) / BM;
-  const int nsplit = a.ksplit > 1 ? a.ksplit : 1;
-  // the slices of one output tile are consecutive logical ids -> same XCD under the remap, so the
-  // reducer reads same-XCD partials (a speed choice only: the hand-off is placement independent)
-  const int bid = xcd_remap(blockIdx.x, mtiles * ntiles * nsplit);
-  const int tile = bid / nsplit, slice = bid - tile * nsplit;
-  const int mt = tile / ntiles, nt = tile % ntiles;
-  const int m0 = mt * BM, n0 = nt * BN;
-  const int nk_all = (K + BK - 1) / BK;
-  const int per_slice = (nk_all + nsplit - 1) / nsplit;
-  const int kt_begin = slice * per_slice;
-  const int nk = max(0, min(nk_all, kt_begin + per_slice) - kt_begin);
-
-  // ---- per-thread A row decode (fixed for the whole K loop) -------------------------------
-  const int my_chunk = tid % CPR;  // the k-chunk this thread stages (same for all its rows)
-  int a_img[NA], a_h0[NA], a_w0[NA];
-  bool a_ok[NA];
-#pragma unroll
-  for (int i = 0; i < NA; ++i) {
-    int idx = tid + i * NT;
-    int row = idx / CPR;
-    int m = m0 + row;
-    a_ok[i] = (idx < BM * CPR) && (m < M);
-    int mm = a_ok[i] ? m : 0;
-    if constexpr (IS1X1) {
-      a_img[i] = mm; a_h0[i] = 0; a_w0[i] = 0;
-    } else {
-      int wo = mm % a.Wo;
-      int t = mm / a.Wo;
-      int ho = t % a.Ho;
-      a_img[i] = t / a.Ho;
-      a_h0[i] = ho * a.SH - a.PT;
-      a_w0[i] = wo * a.SW - a.PL;
-    }
-  }
-  int kglob = kt_begin * BK + my_chunk * 8;  // global k of this thread's chunk in the current tile
-  int kc = kglob, kr = 0, ks = 0;
-  if constexpr (!IS1X1) {
-    while (kc >= a.Cin) { kc -= a.Cin; if (++ks == a.KW) { ks = 0; ++kr; } }
-  }
-
-  const TA* __restrict__ X = reinterpret_cast<const TA*>(a.x);
-  const bf16_t* __restrict__ Wt = a.w;
-  const float pro_lo = act_lo(a.pro.act), pro_hi = act_hi(a.pro.act);
-  const float epi_lo = act_lo(a.epi_act), epi_hi = act_hi(a.epi_act);
-  const float msk_lo = act_lo(a.mbn.act), msk_hi = act_hi(a.mbn.act);
-
-  // two staging register sets: tile t+2 is loaded while tile t is computed and tile t+1 (already
-  // in registers) waits to be written to LDS, so each global load has two compute phases to land
-  struct Stage {
-    uint4 ra[NA];
-    bool rvalid[NA];
-    float rpre[sizeof(TA) == 4 ? NA : 1][8];
-    uint4 rb[NB];
-    bool bvalid[NB];
-    int kc;
-  };
-  Stage st0, st1;
-
-  auto load_tile = [&](Stage& S) {
-    uint4* ra = S.ra;
-    bool* rvalid = S.rvalid;
-    auto& rpre = S.rpre;
-    uint4* rb = S.rb;
-    S.kc = kc;
-#pragma unroll
-    for (int i = 0; i < NA; ++i) {
-      bool ok = a_ok[i] && (kglob < K);
-      size_t off = 0;
-      if constexpr (IS1X1) {
-        off = (size_t)a_img[i] * a.ldx + kc;
-      } else {
-        int h = a_h0[i] + kr, w = a_w0[i] + ks;
-        ok = ok && (unsigned)h < (unsigned)a.H && (unsigned)w < (unsigned)a.W;
-        off = ((size_t)(a_img[i] * a.H + h) * a.W + w) * a.ldx + kc;
-      }
-      // unconditional loads from a clamped address: a guarded "ok ? load : 0" makes hipcc branch
-      // around each load and drain vmcnt(0), which destroys the two-deep prefetch
-      rvalid[i] = ok;
-      off = ok ? off : 0;
-      if constexpr (sizeof(TA) == 2) {
-        ra[i] = *reinterpret_cast<const uint4*>(X + off);
-      } else {
-        float4 u = *reinterpret_cast<const float4*>(X + off);
-        float4 v = *reinterpret_cast<const float4*>(X + off + 4);
-        rpre[i][0] = u.x; rpre[i][1] = u.y; rpre[i][2] = u.z; rpre[i][3] = u.w;
-        rpre[i][4] = v.x; rpre[i][5] = v.y; rpre[i][6] = v.z; rpre[i][7] = v.w;
-      }
-    }
-    const int k0 = kglob - my_chunk * 8;
-#pragma unroll
-    for (int i = 0; i < NB; ++i) {
-      int idx = tid + i * NT;
-      int row = idx / CPR, ch = idx % CPR;
-      int n = n0 + row;
-      int k = k0 + ch * 8;
-      bool ok = (idx < BN * CPR) && (n < a.Cout) && (k < K);
-      S.bvalid[i] = ok;
-      rb[i] = *reinterpret_cast<const uint4*>(Wt + (ok ? (size_t)n * K + k : 0));
-    }
-  };
-
-  auto store_tile = [&](Stage& S, int buf) {
-    bf16_t* as = As + buf * A_ELEMS;
-    bf16_t* bs = Bs + buf * B_ELEMS;
-    const uint4* ra = S.ra;
-    const bool* rvalid = S.rvalid;
-    const auto& rpre = S.rpre;
-    const uint4* rb = S.rb;
-    const int kc = S.kc;
-#pragma unroll
-    for (int i = 0; i < NA; ++i) {
-      int idx = tid + i * NT;
-      if (idx >= BM * CPR) break;
-      int row = idx / CPR, ch = idx % CPR;
-      // branch-free: transform unconditionally, then select zero for padding / tails (an
-      // exec-masked branch per chunk costs a scalar branch + waitcnt split per chunk)
-      uint4 v;
-      if constexpr (sizeof(TA) == 2) {
-        if constexpr (PRO) {
-          float f[8];
-          unpack8(ra[i], f);
-          affine_act8(f, s_scale + kc, s_shift + kc, pro_lo, pro_hi);
-          v = pack8(f);
-        } else {
-          v = ra[i];
-        }
-      } else {
-        float f[8];
-#pragma unroll
-        for (int j = 0; j < 8; ++j) f[j] = rpre[i][j];
-        if constexpr (PRO) affine_act8(f, s_scale + kc, s_shift + kc, pro_lo, pro_hi);
-        v = pack8(f);
-      }
-      const bool ok = rvalid[i];
-      v.x = ok ? v.x : 0u;
-      v.y = ok ? v.y : 0u;
-      v.z = ok ? v.z : 0u;
-      v.w = ok ? v.w : 0u;
-      *reinterpret_cast<uint4*>(as + row * BK + swz_chunk<BK>(row, ch) * 8) = v;
-    }
-#pragma unroll
-    for (int i = 0; i < NB; ++i) {
-      int idx = tid + i * NT;
-      if (idx >= BN * CPR) break;
-      int row = idx / CPR, ch = idx % CPR;
-      const bool ok = S.bvalid[i];
-      uint4 v = rb[i];
-      v.x = ok ? v.x : 0u;
-      v.y = ok ? v.y : 0u;
-      v.z = ok ? v.z : 0u;
-      v.w = ok ? v.w : 0u;
-      *reinterpret_cast<uint4*>(bs + row * BK + swz_chunk<BK>(row, ch) * 8) = v;
-    }
-  };
-
-  auto advance_k = [&]() {
-    kglob += BK;
-    kc += BK;
-    if constexpr (!IS1X1) {
-      while (kc >= a.Cin) { kc -= a.Cin; if (++ks == a.KW) { ks = 0; ++kr; } }
-    }
-  };
-
-  v4f acc[TM][TN];
-#pragma unroll
-  for (int i = 0; i < TM; ++i)
-#pragma unroll
-    for (int j = 0; j < TN; ++j) acc[i][j] = (v4f){0.f, 0.f, 0.f, 0.f};
-
-  // the first two tiles are issued BEFORE the prologue tables are built: the tables' own global
-  // loads (BN statistics, gamma, beta) then overlap the tile loads instead of adding a second
-  // full memory latency in front of the K loop
-  load_tile(st0);
-  advance_k();
-  load_tile(st1);
-  // ---- prologue tables ----
-  if constexpr (PRO) bn_coeff_table<NT>(a.pro, a.Cin, s_scale, s_shift);
-  if constexpr (EPI == 1) {
-    for (int j = tid; j < BN; j += NT) {
-      int c = n0 + j;
-      float sc = 1.f, sh = 0.f, mean = 0.f, rstd = 1.f;
-      if (c < a.Cout) {
-        bn_coeffs(a.mbn, c, sc, sh);
-        if (a.mbn.mode) bn_mean_rstd(a.mbn, c, mean, rstd);
-      }
-      s_e0[j] = sc; s_e1[j] = sh; s_e2[j] = mean; s_e3[j] = rstd;
-    }
-  }
-  for (int j = tid; j < BN; j += NT) { s_sum[j] = 0.f; s_sq[j] = 0.f; }
-
-  __syncthreads();  // prologue tables visible
-  store_tile(st0, 0);
-  __syncthreads();
-
-  const int frow = lane & 15;
-  const int fk = lane >> 4;
-
-  auto compute = [&](int buf) {
-    const bf16_t* as = As + buf * A_ELEMS;
-    const bf16_t* bs = Bs + buf * B_ELEMS;
-#pragma unroll
-    for (int q = 0; q < BK / 32; ++q) {
-      v8bf af[TM], bfr[TN];
-#pragma unroll
-      for (int i = 0; i < TM; ++i) {
-        int row = wr * WTM + i * 16 + frow;
-        af[i] = *reinterpret_cast<const v8bf*>(as + row * BK + swz_chunk<BK>(row, q * 4 + fk) * 8);
-      }
-#pragma unroll
-      for (int j = 0; j < TN; ++j) {
-        int row = wc * WTN + j * 16 + frow;
-        bfr[j] = *reinterpret_cast<const v8bf*>(bs + row * BK + swz_chunk<BK>(row, q * 4 + fk) * 8);
-      }
-#pragma unroll
-      for (int i = 0; i < TM; ++i)
-#pragma unroll
-        for (int j = 0; j < TN; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
-    }
-  };
-
-  // iteration kt: LDS[kt&1] holds tile kt, registers hold tile kt+1 (set (kt+1)&1);
-  // tile kt+2 is issued into the set that was written to LDS last iteration.
-  // Loads/stores are unconditional: tiles past the end are clamped + zero-filled (their LDS
-  // writes land in a buffer that is never read again).  Conditional load/store pairs made the
-  // waitcnt pass drain vmcnt(0) at the loop back-edge, serialising the prefetch.
-  int kt = 0;
-  for (; kt + 2 <= nk; kt += 2) {
-    // even step: compute LDS0 (tile kt), st1 holds kt+1, reload st0 with kt+2
-    advance_k();
-    load_tile(st0);
-    compute(0);
-    store_tile(st1, 1);
-    __syncthreads();
-    // odd step: compute LDS1 (tile kt+1), st0 holds kt+2, reload st1 with kt+3
-    advance_k();
-    load_tile(st1);
-    compute(1);
-    store_tile(st0, 0);
-    __syncthreads();
-  }
-  if (kt < nk) {
-    compute(0);  // odd tile count: the last tile sits in LDS0
-    __syncthreads();  // the epilogue's fp32 staging tile aliases LDS0
-  }
-
-  // ---- split-K: publish this slice's partial tile; the last arriver of the tile reduces ------
-  // (guide §5 "In-launch split-K reduction": plain stores -> every wave vmcnt(0) -> barrier ->
-  //  lane 0 agent release -> asm vmcnt(0) -> relaxed agent ticket; reducer: agent acquire ->
-  //  asm vmcnt(0) -> barrier -> plain loads)
-  if (nsplit > 1) {
-    constexpr int NF = TM * TN;
-    float4* slab = reinterpret_cast<float4*>(a.slab) + (size_t)tile * nsplit * NF * NT;
-    {
-      float4* mine = slab + (size_t)slice * NF * NT;
-#pragma unroll
-      for (int i = 0; i < TM; ++i)
-#pragma unroll
-        for (int j = 0; j < TN; ++j)
-          mine[(i * TN + j) * NT + tid] = make_float4(acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]);
-    }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    int* s_flag = reinterpret_cast<int*>(smem);
-    if (tid == 0) {
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      const unsigned prev =
-          __hip_atomic_fetch_add(&a.tickets[tile], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      const int last = (prev % (unsigned)nsplit) == (unsigned)(nsplit - 1);
-      if (last) {
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      }
-      s_flag[0] = last;
-    }
-    __syncthreads();
-    const int last = s_flag[0];
-    __syncthreads();  // the epilogue reuses this LDS
-    if (!last) return;
-    // sum the other slices, four at a time with every load issued before the adds
-    for (int s0 = 0; s0 < nsplit; s0 += 4) {
-      float4 v[4][NF];
-#pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        const int sl = s0 + u;
-        const bool use = sl < nsplit && sl != slice;
-        const float4* o = slab + (size_t)(use ? sl : slice) * NF * NT;
-#pragma unroll
-        for (int f = 0; f < NF; ++f) v[u][f] = use ? o[f * NT + tid] : make_float4(0.f, 0.f, 0.f, 0.f);
-      }
-#pragma unroll
-      for (int u = 0; u < 4; ++u)
-#pragma unroll
-        for (int i = 0; i < TM; ++i)
-#pragma unroll
-          for (int j = 0; j < TN; ++j) {
-            const float4 q = v[u][i * TN + j];
-            acc[i][j][0] += q.x;
-            acc[i][j][1] += q.y;
-            acc[i][j][2] += q.z;
-            acc[i][j][3] += q.w;
-          }
-    }
-  }
-
-  // ---- epilogue: WM passes, each stages one wave-row (WTM x BN) of fp32 results in LDS ------
-  constexpr int CPB = BN / 8;
-  const bool want_stats = (EPI == 1) || (a.stats_out != nullptr);
-  float psum[8], psq[8];
-#pragma unroll
-  for (int j = 0; j < 8; ++j) { psum[j] = 0.f; psq[j] = 0.f; }
-  const int my_c8 = tid % CPB;
-
-  for (int pass = 0; pass < WM; ++pass) {
-    if (pass) __syncthreads();
-    if (wr == pass) {
-#pragma unroll
-      for (int i = 0; i < TM; ++i)
-#pragma unroll
-        for (int j = 0; j < TN; ++j) {
-          int col = wc * WTN + j * 16 + (lane & 15);
-          int rbase = i * 16 + (lane >> 4) * 4;
-#pragma unroll
-          for (int r = 0; r < 4; ++r) Cs[(rbase + r) * CS_LD + col] = acc[i][j][r];
-        }
-    }
-    __syncthreads();
-    for (int idx = tid; idx < WTM * CPB; idx += NT) {
-      int lrow = idx / CPB, c8 = idx % CPB;
-      int m = m0 + pass * WTM + lrow, n = n0 + c8 * 8;
-      if (m >= M || n >= a.Cout) continue;
-      float v[8];
-      const float4 lo = *reinterpret_cast<const float4*>(&Cs[lrow * CS_LD + c8 * 8]);
-      const float4 hi = *reinterpret_cast<const float4*>(&Cs[lrow * CS_LD + c8 * 8 + 4]);
-      v[0] = lo.x; v[1] = lo.y; v[2] = lo.z; v[3] = lo.w;
-      v[4] = hi.x; v[5] = hi.y; v[6] = hi.z; v[7] = hi.w;
-      if constexpr (EPI == 0) {
-#pragma unroll
-        for (int j = 0; j < 8; ++j) {
-          float t = v[j] + (a.bias ? a.bias[n + j] : 0.f);
-          v[j] = clampf(t, epi_lo, epi_hi);
-        }
-        if (a.out_mode == OUT_BF16) {
-          uint4 p = pack8(v);
-          *reinterpret_cast<uint4*>(reinterpret_cast<bf16_t*>(a.y) + (size_t)m * a.ldy + n) = p;
-          if (want_stats) {
-            float r[8];
-            unpack8(p, r);
-#pragma unroll
-            for (int j = 0; j < 8; ++j) { psum[j] += r[j]; psq[j] += r[j] * r[j]; }
-          }
-        } else {
-          float* yp = reinterpret_cast<float*>(a.y) + (size_t)m * a.ldy + n;
-          if (a.out_mode == OUT_F32_ACC) {
-            const float4 o0 = *reinterpret_cast<const float4*>(yp);
-            const float4 o1 = *reinterpret_cast<const float4*>(yp + 4);
-            v[0] += o0.x; v[1] += o0.y; v[2] += o0.z; v[3] += o0.w;
-            v[4] += o1.x; v[5] += o1.y; v[6] += o1.z; v[7] += o1.w;
-          }
-          *reinterpret_cast<float4*>(yp) = make_float4(v[0], v[1], v[2], v[3]);
-          *reinterpret_cast<float4*>(yp + 4) = make_float4(v[4], v[5], v[6], v[7]);
-          if (want_stats) {
-#pragma unroll
-            for (int j = 0; j < 8; ++j) { psum[j] += v[j]; psq[j] += v[j] * v[j]; }
-          }
-        }
-      } else {
-        const uint4 xv = *reinterpret_cast<const uint4*>(a.mx + (size_t)m * a.ldmx + n);
-        float xf[8], d[8];
-        unpack8(xv, xf);
-#pragma unroll
-        for (int j = 0; j < 8; ++j) {
-          int cj = c8 * 8 + j;
-          float z = xf[j] * s_e0[cj] + s_e1[cj];
-          d[j] = (z > msk_lo && z < msk_hi) ? v[j] : 0.f;
-        }
-        uint4 p = pack8(d);
-        *reinterpret_cast<uint4*>(reinterpret_cast<bf16_t*>(a.y) + (size_t)m * a.ldy + n) = p;
-        float r[8];
-        unpack8(p, r);
-#pragma unroll
-        for (int j = 0; j < 8; ++j) {
-          int cj = c8 * 8 + j;
-          psum[j] += r[j];
-          psq[j] += r[j] * (xf[j] - s_e2[cj]) * s_e3[cj];
-        }
-      }
-    }
-  }
-  if (want_stats) {
-    wave_reduce_chunks<CPB>(psum);
-    wave_reduce_chunks<CPB>(psq);
-    if ((tid & 63) < CPB && (tid & ~63) < WTM * CPB) {
-#pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        atomicAdd(&s_sum[my_c8 * 8 + j], psum[j]);
-        atomicAdd(&s_sq[my_c8 * 8 + j], psq[j]);
-      }
-    }
-    __syncthreads();
-    const size_t so = EPI == 0 ? (size_t)(mt % stat_slots(a.stats_slots)) * 2 * a.stats_ld
-                               : (size_t)(mt % stat_slots(a.gsum_slots)) * a.gsum_ld;
-    for (int j = tid; j < BN; j += NT) {
-      int c = n0 + j;
-      if (c >= a.Cout) continue;
-      if constexpr (EPI == 0) {
-        atomicAdd(&a.stats_out[so + a.stats_off + c], s_sum[j]);
-        atomicAdd(&a.stats_out[so + a.stats_ld + a.stats_off + c], s_sq[j]);
-      } else {
-        if (a.gsum) atomicAdd(&a.gsum[so + c], s_sum[j]);
-        if (a.gsumx) atomicAdd(&a.gsumx[so + c], s_sq[j]);
-      }
-    }
-  }
-}
-
-// ----------------------------------------------------------------------------------------------
-// host-side dispatch
-// ----------------------------------------------------------------------------------------------
-template <int BM, int BN, int BK, int WM, int WN>
-static hipError_t launch_cfg(const ConvArgs& a, bool is1x1, bool a_f32, int pro, int epi,
-                             hipStream_t st) {
-  const int M = a.N * a.Ho * a.Wo;
-  const int tiles = ((M + BM - 1) / BM) * ((a.Cout + BN - 1) / BN);
-  if (a.ksplit > 1) {
-    // the partial slabs and tickets of every tile must fit the workspace the caller provided
-    if ((long long)tiles * a.ksplit * BM * BN > a.slab_floats || tiles > a.tickets_n) return hipErrorInvalidValue;
-  }
-  const int grid = tiles * (a.ksplit > 1 ? a.ksplit : 1);
-  if (grid == 0) return hipSuccess;
-  const size_t shm = IgemmCfg<BM, BN, BK, WM, WN>::smem_bytes(pro ? a.Cin : 0);
-#define IDC_L(IS1, TA, P, E)                                                                   \
-  hipLaunchKernelGGL((conv_igemm_kernel<BM, BN, BK, WM, WN, IS1, TA, P, E>), dim3(grid),     \
-                     dim3(256), shm, st, a)
-#define IDC_E(IS1, TA, P)      \
-  if (epi == 0) IDC_L(IS1, TA, P, 0); \
-  else IDC_L(IS1, TA, P, 1);
-  // fp32 operands (gradient buffers) never carry a pending-BN prologue
-  if (a_f32) {
-    if (pro) return hipErrorInvalidValue;
-    if (is1x1) { IDC_E(true, float, 0) } else { IDC_E(false, float, 0) }
-  } else if (pro) {
-    if (is1x1) { IDC_E(true, bf16_t, 1) } else { IDC_E(false, bf16_t, 1) }
-  } else {
-    if (is1x1) { IDC_E(true, bf16_t, 0) } else { IDC_E(false, bf16_t, 0) }
-  }
-#undef IDC_E
-#undef IDC_L
-  return hipGetLastError();
-}
+hipError_t conv_igemm_group0(const ConvArgs& a, int tile, bool is1x1, bool a_f32, int pro, int epi,
+                              hipStream_t st);
+hipError_t conv_igemm_group1(const ConvArgs& a, int tile, bool is1x1, bool a_f32, int pro, int epi,
+                              hipStream_t st);
+hipError_t conv_igemm_group2(const ConvArgs& a, int tile, bool is1x1, bool a_f32, int pro, int epi,
+                              hipStream_t st);
+hipError_t conv_igemm_group3(const ConvArgs& a, int tile, bool is1x1, bool a_f32, int pro, int epi,
+                              hipStream_t st);
+hipError_t conv_igemm_group4(const ConvArgs& a, int tile, bool is1x1, bool a_f32, int pro, int epi,
+                              hipStream_t st);
 
 struct TileInfo { int bm, bn; };
 static const TileInfo kTiles[] = {
@@ -554,36 +27,25 @@ int conv_tile_bm(int t) { return kTiles[t].bm; }
 int conv_tile_bn(int t) { return kTiles[t].bn; }
 
 hipError_t conv_igemm(const ConvArgs& a, int tile, bool a_f32, hipStream_t st) {
+  if (tile < 0 || (tile >= conv_num_tiles() && tile != TILE_HALO)) return hipErrorInvalidValue;
   const bool is1x1 = a.KH == 1 && a.KW == 1 && a.SH == 1 && a.SW == 1 && a.PT == 0 && a.PL == 0;
-  const int pro = (a.pro.mode != 0 || a.pro.act != ACT_NONE) ? 1 : 0;
+  const int pro = a.bpro.mode != 0 ? 2 : (a.pro.mode != 0 || a.pro.act != ACT_NONE) ? 1 : 0;
   const int epi = a.epi_mode;
   if ((a.Cin % 8) || (a.Cout % 8) || (a.ldx % 8) || (a.ldy % 8)) return hipErrorInvalidValue;
+  if (pro == 2 && (a.bpro.x == nullptr || (a.bpro.ldx % 8) || a.bpro.bn.gamma == nullptr)) return hipErrorInvalidValue;
+  if (epi == 2 && a.mx == nullptr) return hipErrorInvalidValue;
   if (a.ksplit > 1 && (a.slab == nullptr || a.tickets == nullptr)) return hipErrorInvalidValue;
   if (tile == TILE_HALO) {
-    if (a.ksplit > 1) return hipErrorInvalidValue;
+    if (a.ksplit > 1 || pro == 2 || epi == 2) return hipErrorInvalidValue;
     return conv3x3_halo(a, a_f32, st);
   }
-  switch (tile) {
-    case 0: return launch_cfg<128, 128, 32, 2, 2>(a, is1x1, a_f32, pro, epi, st);
-    case 1: return launch_cfg<128, 64, 32, 2, 2>(a, is1x1, a_f32, pro, epi, st);
-    case 2: return launch_cfg<256, 32, 32, 4, 1>(a, is1x1, a_f32, pro, epi, st);
-    case 3: return launch_cfg<64, 64, 32, 2, 2>(a, is1x1, a_f32, pro, epi, st);
-    case 4: return launch_cfg<64, 32, 32, 2, 2>(a, is1x1, a_f32, pro, epi, st);
-    case 5: return launch_cfg<128, 128, 64, 2, 2>(a, is1x1, a_f32, pro, epi, st);
-    case 6: return launch_cfg<128, 64, 64, 2, 2>(a, is1x1, a_f32, pro, epi, st);
-    case 7: return launch_cfg<128, 32, 64, 4, 1>(a, is1x1, a_f32, pro, epi, st);
-    case 8: return launch_cfg<64, 64, 64, 2, 2>(a, is1x1, a_f32, pro, epi, st);
-    case 9: return launch_cfg<64, 32, 64, 2, 2>(a, is1x1, a_f32, pro, epi, st);
-    case 10: return launch_cfg<256, 32, 64, 4, 1>(a, is1x1, a_f32, pro, epi, st);
-    case 11: return launch_cfg<64, 128, 64, 2, 2>(a, is1x1, a_f32, pro, epi, st);
-    case 12: return launch_cfg<64, 32, 128, 2, 2>(a, is1x1, a_f32, pro, epi, st);
-    case 13: return launch_cfg<128, 32, 128, 4, 1>(a, is1x1, a_f32, pro, epi, st);
-    case 14: return launch_cfg<64, 64, 128, 2, 2>(a, is1x1, a_f32, pro, epi, st);
-    case 15: return launch_cfg<64, 128, 128, 2, 2>(a, is1x1, a_f32, pro, epi, st);
-    case 16: return launch_cfg<128, 64, 128, 2, 2>(a, is1x1, a_f32, pro, epi, st);
-    case 17: return launch_cfg<64, 32, 256, 2, 2>(a, is1x1, a_f32, pro, epi, st);
-    case 18: return launch_cfg<64, 64, 256, 2, 2>(a, is1x1, a_f32, pro, epi, st);
-    default: return hipErrorInvalidValue;
+  const int group = tile < 4 ? 0 : tile < 8 ? 1 : tile < 12 ? 2 : tile < 16 ? 3 : 4;
+  switch (group) {
+    case 0: return conv_igemm_group0(a, tile, is1x1, a_f32, pro, epi, st);
+    case 1: return conv_igemm_group1(a, tile, is1x1, a_f32, pro, epi, st);
+    case 2: return conv_igemm_group2(a, tile, is1x1, a_f32, pro, epi, st);
+    case 3: return conv_igemm_group3(a, tile, is1x1, a_f32, pro, epi, st);
+    default: return conv_igemm_group4(a, tile, is1x1, a_f32, pro, epi, st);
   }
 }
 

@@ -15,6 +15,9 @@ struct WgradArgs {
   float scale;      // multiplies the contribution (1.0 normally)
   int cin_real;     // Keras Cin when the staged input is channel-padded (0: == Cin)
   int pix_per_split;
+  // backward pending affine on G (common.h BwdAff; gpro.mode != 0 selects it): the staged
+  // gradient is A*g + B*x + C, x read from gpro.x at the same pixel and output channel
+  BwdAff gpro;
 };
 
 hipError_t conv_wgrad(WgradArgs a, int splits, bool g_f32, hipStream_t st);

@@ -28,26 +28,26 @@ __device__ __forceinline__ int wswz(int row, int chunk) {
   else return chunk ^ (((row & 3) << 2) | ((row >> 2) & 3));
 }
 
-template <int BKR, int BC>
+template <int BKR, int BC, int BP_>
 struct WgCfg {
   static constexpr int NT = 256;
-  static constexpr int BP = 32;  // pixels per k-step
+  static constexpr int BP = BP_;  // pixels per k-step (a multiple of the MFMA k = 32)
   static constexpr int A_ELEMS = BP * BKR, G_ELEMS = BP * BC;
   static constexpr int STAGE = 2 * (A_ELEMS + G_ELEMS) * 2;
   static constexpr int CS_LD = BC + 4;
   static constexpr int EPI = BKR * CS_LD * 4;
   static constexpr int MAIN = STAGE > EPI ? STAGE : EPI;
-  static int smem_bytes(int cpro) { return MAIN + 2 * ((cpro + 3) / 4 * 4) * 4; }
+  static int smem_bytes(int cpro) { return MAIN + 2 * ((cpro + 3) / 4 * 4) * 4 + 3 * BC * 4; }
 };
 
-// 8 bf16 from two transposed 4-element reads (pixels 8g..8g+3 and 8g+4..8g+7)
+// 8 bf16 from two transposed 4-element reads (pixels r0+8g..+3 and r0+8g+4..+7)
 template <int ROWB>
-__device__ __forceinline__ v8bf tr_frag(const bf16_t* tile, int col_base, int lane) {
+__device__ __forceinline__ v8bf tr_frag(const bf16_t* tile, int col_base, int lane, int r0) {
   const int g = lane >> 4, q = (lane >> 2) & 3, p = lane & 3;
   v8bf out;
 #pragma unroll
   for (int t = 0; t < 2; ++t) {
-    int row = 8 * g + 4 * t + q;
+    int row = r0 + 8 * g + 4 * t + q;
     int col = col_base + 4 * p;
     int ch = col >> 3, sub = col & 7;
     const bf16_t* ptr = tile + row * (ROWB / 2) + wswz<ROWB>(row, ch) * 8 + sub;
@@ -60,9 +60,9 @@ __device__ __forceinline__ v8bf tr_frag(const bf16_t* tile, int col_base, int la
   return out;
 }
 
-template <int BKR, int BC, int WM, int WN, bool IS1X1, typename TG, int PRO>
+template <int BKR, int BC, int BP_, int WM, int WN, bool IS1X1, typename TG, int PRO, int GPRO>
 __global__ __launch_bounds__(256) void conv_wgrad_kernel(WgradArgs a) {
-  using C = WgCfg<BKR, BC>;
+  using C = WgCfg<BKR, BC, BP_>;
   constexpr int NT = C::NT, BP = C::BP;
   constexpr int WTM = BKR / WM, WTN = BC / WN;
   constexpr int TM = WTM / 16, TN = WTN / 16;
@@ -79,6 +79,9 @@ __global__ __launch_bounds__(256) void conv_wgrad_kernel(WgradArgs a) {
   const int cpro = PRO ? (a.Cin + 3) / 4 * 4 : 0;
   float* s_scale = reinterpret_cast<float*>(smem + C::MAIN);
   float* s_shift = s_scale + cpro;
+  float* s_ga = s_shift + cpro;  // GPRO: backward-affine coefficients of the G columns
+  float* s_gb = s_ga + BC;
+  float* s_gc = s_gb + BC;
 
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int wr = wid / WN, wc = wid % WN;
@@ -104,33 +107,13 @@ __global__ __launch_bounds__(256) void conv_wgrad_kernel(WgradArgs a) {
     kr = rs / a.KW;
     ks = rs - kr * a.KW;
   }
-  // incremental pixel decode for each of this thread's rows
-  int p_img[NA], p_ho[NA], p_wo[NA];
-#pragma unroll
-  for (int i = 0; i < NA; ++i) {
-    int m = pbeg + arow0 + i * AROW_STEP;
-    int wo = m % a.Wo;
-    int t = m / a.Wo;
-    p_wo[i] = wo;
-    p_ho[i] = t % a.Ho;
-    p_img[i] = t / a.Ho;
-  }
-  auto step_pixels = [&]() {
-#pragma unroll
-    for (int i = 0; i < NA; ++i) {
-      p_wo[i] += BP;
-      while (p_wo[i] >= a.Wo) {
-        p_wo[i] -= a.Wo;
-        if (++p_ho[i] == a.Ho) { p_ho[i] = 0; ++p_img[i]; }
-      }
-    }
-  };
 
   const bf16_t* __restrict__ X = a.x;
   const TG* __restrict__ G = reinterpret_cast<const TG*>(a.g);
   uint4 ra[NA];
   bool rv[NA];
   uint4 rg[NG];
+  uint4 rgx[GPRO ? NG : 1];
   bool gv[NG];
   float rgf[sizeof(TG) == 4 ? NG : 1][8];
 
@@ -144,9 +127,14 @@ __global__ __launch_bounds__(256) void conv_wgrad_kernel(WgradArgs a) {
       if constexpr (IS1X1) {
         off = (size_t)m * a.ldx + kc;
       } else {
-        int h = p_ho[i] * a.SH - a.PT + kr, w = p_wo[i] * a.SW - a.PL + ks;
+        // direct decode (a few integer divisions per row per step; an incremental walk costs
+        // BP/Wo iterations per row on the small late-stage maps)
+        const int mm = ok ? m : 0;
+        const int wo = mm % a.Wo, t = mm / a.Wo;
+        const int ho = t % a.Ho, img = t / a.Ho;
+        int h = ho * a.SH - a.PT + kr, w = wo * a.SW - a.PL + ks;
         ok = ok && (unsigned)h < (unsigned)a.H && (unsigned)w < (unsigned)a.W;
-        off = ((size_t)(p_img[i] * a.H + h) * a.W + w) * a.ldx + kc;
+        off = ((size_t)(img * a.H + h) * a.W + w) * a.ldx + kc;
       }
       rv[i] = ok;
       ra[i] = *reinterpret_cast<const uint4*>(X + (ok ? off : 0));  // unconditional (no drain)
@@ -158,8 +146,10 @@ __global__ __launch_bounds__(256) void conv_wgrad_kernel(WgradArgs a) {
       int m = mbase + row;
       int co = c0 + ch * 8;
       bool ok = (idx < BP * GCH) && (m < pend) && (co < a.Cout);
-      const size_t goff = ok ? (size_t)m * a.ldg + co : 0;
+      const size_t gm = ok ? (size_t)m : 0;
+      const size_t goff = ok ? gm * a.ldg + co : 0;
       gv[i] = ok;
+      if constexpr (GPRO) rgx[i] = *reinterpret_cast<const uint4*>(a.gpro.x + gm * a.gpro.ldx + (ok ? co : 0));
       if constexpr (sizeof(TG) == 2) {
         rg[i] = *reinterpret_cast<const uint4*>(G + goff);
       } else {
@@ -197,8 +187,22 @@ __global__ __launch_bounds__(256) void conv_wgrad_kernel(WgradArgs a) {
       if (idx >= BP * GCH) break;
       int row = idx / GCH, ch = idx % GCH;
       uint4 v;
-      if constexpr (sizeof(TG) == 2) v = rg[i];
-      else v = pack8(rgf[i]);
+      if constexpr (GPRO) {
+        float f[8], xf[8];
+        if constexpr (sizeof(TG) == 2) {
+          unpack8(rg[i], f);
+        } else {
+#pragma unroll
+          for (int j = 0; j < 8; ++j) f[j] = rgf[i][j];
+        }
+        unpack8(rgx[i], xf);
+        bwd_aff8(f, xf, s_ga + ch * 8, s_gb + ch * 8, s_gc + ch * 8);
+        v = pack8(f);
+      } else if constexpr (sizeof(TG) == 2) {
+        v = rg[i];
+      } else {
+        v = pack8(rgf[i]);
+      }
       if (!gv[i]) v = make_uint4(0, 0, 0, 0);
       *reinterpret_cast<uint4*>(gs + row * BC + wswz<GROWB>(row, ch) * 8) = v;
     }
@@ -213,26 +217,29 @@ __global__ __launch_bounds__(256) void conv_wgrad_kernel(WgradArgs a) {
   const int nsteps = (pend - pbeg + BP - 1) / BP;
   load(pbeg);  // first tile in flight while the BN table is built (its loads overlap)
   if constexpr (PRO) bn_coeff_table<NT>(a.pro, a.Cin, s_scale, s_shift);
+  if constexpr (GPRO) bwd_aff_table<NT>(a.gpro, c0, BC, a.Cout, s_ga, s_gb, s_gc);
   __syncthreads();
   store(0);
   __syncthreads();
   for (int it = 0; it < nsteps; ++it) {
     const int cur = it & 1;
     // unconditional prefetch (rows past `pend` are masked): no back-edge vmcnt(0) drain
-    if constexpr (!IS1X1) step_pixels();
     load(pbeg + (it + 1) * BP);
     const bf16_t* as = As + cur * C::A_ELEMS;
     const bf16_t* gs = Gs + cur * C::G_ELEMS;
-    v8bf af[TM], gf[TN];
 #pragma unroll
-    for (int i = 0; i < TM; ++i) af[i] = tr_frag<AROWB>(as, wr * WTM + i * 16, lane);
+    for (int kq = 0; kq < BP / 32; ++kq) {
+      v8bf af[TM], gf[TN];
 #pragma unroll
-    for (int j = 0; j < TN; ++j) gf[j] = tr_frag<GROWB>(gs, wc * WTN + j * 16, lane);
+      for (int i = 0; i < TM; ++i) af[i] = tr_frag<AROWB>(as, wr * WTM + i * 16, lane, kq * 32);
 #pragma unroll
-    for (int i = 0; i < TM; ++i)
+      for (int j = 0; j < TN; ++j) gf[j] = tr_frag<GROWB>(gs, wc * WTN + j * 16, lane, kq * 32);
 #pragma unroll
-      for (int j = 0; j < TN; ++j)
-        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], gf[j], acc[i][j], 0, 0, 0);
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], gf[j], acc[i][j], 0, 0, 0);
+    }
     store(cur ^ 1);
     __syncthreads();
   }
@@ -263,37 +270,46 @@ __global__ __launch_bounds__(256) void conv_wgrad_kernel(WgradArgs a) {
   }
 }
 
-template <int BKR, int BC, int WM, int WN>
+template <int BKR, int BC, int BP, int WM, int WN>
 static hipError_t launch_wg(const WgradArgs& a, bool is1x1, bool g_f32, int pro, int splits,
                             hipStream_t st) {
   const int K = a.KH * a.KW * a.Cin;
   dim3 grid((K + BKR - 1) / BKR, (a.Cout + BC - 1) / BC, splits);
-  const size_t shm = WgCfg<BKR, BC>::smem_bytes(pro ? a.Cin : 0);
-#define IDC_W(IS1, TG, P) \
-  hipLaunchKernelGGL((conv_wgrad_kernel<BKR, BC, WM, WN, IS1, TG, P>), grid, dim3(256), shm, st, a)
-#define IDC_WP(IS1, TG) if (pro) IDC_W(IS1, TG, 1); else IDC_W(IS1, TG, 0);
+  const size_t shm = WgCfg<BKR, BC, BP>::smem_bytes(pro ? a.Cin : 0);
+  const bool gpro = a.gpro.mode != 0;
+#define IDC_W(IS1, TG, P, GP) \
+  hipLaunchKernelGGL((conv_wgrad_kernel<BKR, BC, BP, WM, WN, IS1, TG, P, GP>), grid, dim3(256), shm, st, a)
+#define IDC_WG(IS1, TG, P) if (gpro) IDC_W(IS1, TG, P, 1); else IDC_W(IS1, TG, P, 0);
+#define IDC_WP(IS1, TG) if (pro) { IDC_WG(IS1, TG, 1) } else { IDC_WG(IS1, TG, 0) }
   if (g_f32) {
     if (is1x1) { IDC_WP(true, float) } else { IDC_WP(false, float) }
   } else {
     if (is1x1) { IDC_WP(true, bf16_t) } else { IDC_WP(false, bf16_t) }
   }
 #undef IDC_WP
+#undef IDC_WG
 #undef IDC_W
   return hipGetLastError();
 }
+
+// pixels per k-step of the tile chosen for Cout (launch_wg below)
+// (32: the deeper 64/128-pixel steps measured slower — their 58-83 KB LDS footprint cuts the
+// workgroups per CU, and these kernels are latency-bound, not MFMA-bound)
+static int wgrad_bp(int) { return 32; }
 
 hipError_t conv_wgrad(WgradArgs a, int splits, bool g_f32, hipStream_t st) {
   const bool is1x1 = a.KH == 1 && a.KW == 1 && a.SH == 1 && a.SW == 1 && a.PT == 0 && a.PL == 0;
   const int pro = (a.pro.mode != 0 || a.pro.act != ACT_NONE) ? 1 : 0;
   const int M = a.N * a.Ho * a.Wo;
   if (splits < 1) splits = 1;
+  const int bp = wgrad_bp(a.Cout);
   int per = (M + splits - 1) / splits;
-  per = (per + 31) / 32 * 32;
+  per = (per + bp - 1) / bp * bp;
   splits = (M + per - 1) / per;
   a.pix_per_split = per;
-  if (a.Cout <= 32) return launch_wg<128, 32, 4, 1>(a, is1x1, g_f32, pro, splits, st);
-  if (a.Cout <= 64) return launch_wg<128, 64, 2, 2>(a, is1x1, g_f32, pro, splits, st);
-  return launch_wg<64, 128, 2, 2>(a, is1x1, g_f32, pro, splits, st);
+  if (a.Cout <= 32) return launch_wg<128, 32, 32, 4, 1>(a, is1x1, g_f32, pro, splits, st);
+  if (a.Cout <= 64) return launch_wg<128, 64, 32, 2, 2>(a, is1x1, g_f32, pro, splits, st);
+  return launch_wg<64, 128, 32, 2, 2>(a, is1x1, g_f32, pro, splits, st);
 }
 
 int wgrad_pick_splits(int M, int K, int Cout) {
@@ -303,7 +319,8 @@ int wgrad_pick_splits(int M, int K, int Cout) {
   else tiles = ((K + 63) / 64) * ((Cout + 127) / 128);
   int target = 512;  // ~2 blocks per CU
   int s = (target + tiles - 1) / tiles;
-  int maxs = (M + 255) / 256;  // at least 8 k-steps of 32 pixels per slice
+  const int bp = wgrad_bp(Cout);
+  int maxs = (M + 8 * bp - 1) / (8 * bp);  // at least 8 k-steps per slice
   if (s > maxs) s = maxs;
   return s < 1 ? 1 : s;
 }

@@ -27,6 +27,9 @@ struct BnBwdReduceArgs {
   float* gsum; float* gsumx;
   int M, C;
   int gsum_slots, gsum_ld;
+  // dz_f32: `dz` is fp32 and receives gamma*rstd*dZ (the A*dZ part of the BatchNorm backward;
+  // B*x + C stays pending for the consumers, common.h BwdAff)
+  int dz_f32;
 };
 
 struct PoolArgs {
@@ -52,6 +55,10 @@ struct PoolBwdArgs {
   float* gsum; float* gsumx;
   int is_avg;
   int gsum_slots, gsum_ld;
+  // backward pending affine of a LATER BatchNorm on dy (x = its forward input at the pool-output
+  // positions), and dx_f32: `dx` is fp32 and receives gamma*rstd*dZ (BwdAff unit-alpha form)
+  BwdAff dyaff;
+  int dx_f32;
 };
 
 struct BnMovingDesc {

@@ -300,7 +300,14 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(BnBwdReduceArgs a) {
       unpack8(*reinterpret_cast<const uint4*>(a.x + (size_t)row * a.ldx + c), x);
 #pragma unroll
       for (int j = 0; j < 8; ++j) d[j] = dy[j] * act_mask(x[j] * s_sc[c + j] + s_sh[c + j], a.bn.act);
-      if (a.dz) {
+      if (a.dz && a.dz_f32) {
+        float o[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) o[j] = s_sc[c + j] * d[j];
+        float* q = reinterpret_cast<float*>(a.dz) + (size_t)row * a.lddz + c;
+        *reinterpret_cast<float4*>(q) = make_float4(o[0], o[1], o[2], o[3]);
+        *reinterpret_cast<float4*>(q + 4) = make_float4(o[4], o[5], o[6], o[7]);
+      } else if (a.dz) {
         uint4 p = pack8(d);
         *reinterpret_cast<uint4*>(a.dz + (size_t)row * a.lddz + c) = p;
         unpack8(p, d);  // reduce exactly what was stored
@@ -443,10 +450,18 @@ __global__ __launch_bounds__(256) void pool_bwd_kernel(PoolBwdArgs a) {
   float* s_rs = sh + 3 * a.C;
   float* s_a = sh + 4 * a.C;
   float* s_b = sh + 5 * a.C;
-  float* s_tmp = sh + 6 * a.C;
+  float* s_da = sh + 6 * a.C;  // dyaff coefficients
+  float* s_db = sh + 7 * a.C;
+  float* s_dc = sh + 8 * a.C;
+  float* s_tmp = sh + 9 * a.C;
   const bool epi = (a.bn.mode != 0 || a.bn.act != ACT_NONE);
   const bool sums = epi && (a.gsum || a.gsumx);
+  const bool dyaff = a.dyaff.mode != 0;
   if (epi) bn_full_table<256>(a.bn, a.C, s_sc, s_sh, s_mu, s_rs);
+  if (dyaff) {
+    bwd_aff_table<256>(a.dyaff, 0, a.C, a.C, s_da, s_db, s_dc);
+    bwd_aff_fold<256>(a.dyaff);
+  }
   __syncthreads();
   ChunkMap cm(a.C);
   const int Mi = a.N * a.H * a.W;
@@ -488,6 +503,11 @@ __global__ __launch_bounds__(256) void pool_bwd_kernel(PoolBwdArgs a) {
             ok[u][q] = v;
             const size_t o = v ? (size_t)(n * a.Ho + oh) * a.Wo + ow : 0;
             load8(a.dy, a.dy_f32, o * a.lddy + c, d[u][q]);
+            if (dyaff) {
+              float xo[8];
+              unpack8(*reinterpret_cast<const uint4*>(a.dyaff.x + o * a.dyaff.ldx + c), xo);
+              bwd_aff8(d[u][q], xo, s_da + c, s_db + c, s_dc + c);
+            }
             if (!a.is_avg) {
               am[u][q] = *reinterpret_cast<const uint2*>(a.argmax + o * a.C + c);
               mine[u][q] = (uint8_t)((h - (oh * a.s - a.pt)) * a.k + (w - (ow * a.s - a.pl)));
@@ -516,7 +536,21 @@ __global__ __launch_bounds__(256) void pool_bwd_kernel(PoolBwdArgs a) {
           }
         }
         bf16_t* dst = a.dx + (size_t)rows[u] * a.lddx + c;
-        if (epi) {
+        if (epi && a.dx_f32) {
+          float x[8], o[8];
+          unpack8(xr[u], x);
+#pragma unroll
+          for (int j = 0; j < 8; ++j) {
+            const float z = x[j] * s_sc[c + j] + s_sh[c + j];
+            g[j] = (z > lo && z < hi) ? g[j] : 0.f;
+            o[j] = s_sc[c + j] * g[j];
+            ps[j] += g[j];
+            px[j] += g[j] * (x[j] - s_mu[c + j]) * s_rs[c + j];
+          }
+          float* q = reinterpret_cast<float*>(a.dx) + (size_t)rows[u] * a.lddx + c;
+          *reinterpret_cast<float4*>(q) = make_float4(o[0], o[1], o[2], o[3]);
+          *reinterpret_cast<float4*>(q + 4) = make_float4(o[4], o[5], o[6], o[7]);
+        } else if (epi) {
           float x[8];
           unpack8(xr[u], x);
 #pragma unroll
@@ -548,7 +582,9 @@ __global__ __launch_bounds__(256) void pool_bwd_kernel(PoolBwdArgs a) {
 }
 
 hipError_t pool_bwd(const PoolBwdArgs& a, hipStream_t st) {
-  const size_t shm = (6 * a.C + 2 * 256 * 8) * 4;
+  if (a.dx_f32 && !(a.bn.mode != 0 || a.bn.act != ACT_NONE)) return hipErrorInvalidValue;
+  if (a.dyaff.mode != 0 && (a.dyaff.x == nullptr || (a.dyaff.ldx % 8))) return hipErrorInvalidValue;
+  const size_t shm = (9 * a.C + 2 * 256 * 8) * 4;
   const int M = a.N * a.H * a.W;
   if (a.k <= a.s) {
     hipLaunchKernelGGL((pool_bwd_kernel<1, 4>), dim3(grid_rows(M, a.C, 4)), dim3(256), shm, st, a);

@@ -365,6 +365,12 @@ py::dict struct_sizes() {
   d["ConvArgs.gsum_ld"] = offsetof(ConvArgs, gsum_ld);
   d["BnArgs.slots"] = offsetof(BnArgs, slots);
   d["DwArgs.gsum_ld"] = offsetof(DwArgs, gsum_ld);
+  d["BwdAff"] = sizeof(BwdAff);
+  d["ConvArgs.bepi"] = offsetof(ConvArgs, bepi);
+  d["WgradArgs.gpro"] = offsetof(WgradArgs, gpro);
+  d["PoolBwdArgs.dx_f32"] = offsetof(PoolBwdArgs, dx_f32);
+  d["BwdAff.fold_sumx"] = offsetof(BwdAff, fold_sumx);
+  d["ConvArgs.aout"] = offsetof(ConvArgs, aout);
   return d;
 }
 

@@ -30,6 +30,13 @@ class BnArgs(C.Structure):
                 ("inv_count", cf), ("eps", cf), ("mode", ci), ("act", ci), ("C", ci), ("slots", ci)]
 
 
+class BwdAff(C.Structure):
+    """csrc/kernels/common.h BwdAff: a BatchNorm backward applied by the consumer while staging."""
+    _fields_ = [("x", vp), ("ldx", ci), ("bn", BnArgs), ("gsum", vp), ("gsumx", vp),
+                ("gsum_slots", ci), ("gsum_ld", ci), ("inv_n", cf), ("unit_alpha", ci), ("mode", ci),
+                ("fold_C", ci), ("fgsum", vp), ("fgsumx", vp), ("fold_sum", vp), ("fold_sumx", vp)]
+
+
 class ConvArgs(C.Structure):
     _fields_ = [("x", vp), ("N", ci), ("H", ci), ("W", ci), ("Cin", ci), ("ldx", ci),
                 ("Ho", ci), ("Wo", ci), ("Cout", ci), ("y", vp), ("ldy", ci),
@@ -38,14 +45,16 @@ class ConvArgs(C.Structure):
                 ("stats_out", vp), ("stats_ld", ci), ("stats_off", ci),
                 ("mx", vp), ("ldmx", ci), ("mbn", BnArgs), ("gsum", vp), ("gsumx", vp),
                 ("slab", vp), ("tickets", vp), ("slab_floats", cll), ("tickets_n", ci),
-                ("ksplit", ci), ("stats_slots", ci), ("gsum_slots", ci), ("gsum_ld", ci)]
+                ("ksplit", ci), ("stats_slots", ci), ("gsum_slots", ci), ("gsum_ld", ci),
+                ("bpro", BwdAff), ("bepi", BwdAff), ("aout", vp), ("ldaout", ci)]
 
 
 class WgradArgs(C.Structure):
     _fields_ = [("x", vp), ("N", ci), ("H", ci), ("W", ci), ("Cin", ci), ("ldx", ci),
                 ("g", vp), ("ldg", ci), ("Ho", ci), ("Wo", ci), ("Cout", ci),
                 ("KH", ci), ("KW", ci), ("SH", ci), ("SW", ci), ("PT", ci), ("PL", ci),
-                ("pro", BnArgs), ("dw", vp), ("scale", cf), ("cin_real", ci), ("pix_per_split", ci)]
+                ("pro", BnArgs), ("dw", vp), ("scale", cf), ("cin_real", ci), ("pix_per_split", ci),
+                ("gpro", BwdAff)]
 
 
 class BnBwdApplyArgs(C.Structure):
@@ -58,7 +67,7 @@ class BnBwdApplyArgs(C.Structure):
 class BnBwdReduceArgs(C.Structure):
     _fields_ = [("dy", vp), ("lddy", ci), ("dy_f32", ci), ("x", vp), ("ldx", ci), ("bn", BnArgs),
                 ("dz", vp), ("lddz", ci), ("gsum", vp), ("gsumx", vp), ("M", ci), ("C", ci),
-                ("gsum_slots", ci), ("gsum_ld", ci)]
+                ("gsum_slots", ci), ("gsum_ld", ci), ("dz_f32", ci)]
 
 
 class PoolArgs(C.Structure):
@@ -72,7 +81,8 @@ class PoolBwdArgs(C.Structure):
     _fields_ = [("dy", vp), ("lddy", ci), ("dy_f32", ci), ("argmax", vp), ("N", ci), ("H", ci),
                 ("W", ci), ("C", ci), ("k", ci), ("s", ci), ("pt", ci), ("pl", ci), ("Ho", ci),
                 ("Wo", ci), ("x", vp), ("ldx", ci), ("bn", BnArgs), ("dx", vp), ("lddx", ci),
-                ("gsum", vp), ("gsumx", vp), ("is_avg", ci), ("gsum_slots", ci), ("gsum_ld", ci)]
+                ("gsum", vp), ("gsumx", vp), ("is_avg", ci), ("gsum_slots", ci), ("gsum_ld", ci),
+                ("dyaff", BwdAff), ("dx_f32", ci)]
 
 
 class BnMovingDesc(C.Structure):
@@ -113,7 +123,7 @@ class Mlp2Args(C.Structure):
                 ("db2", vp), ("dx", vp)]
 
 
-_STRUCTS = {"BnArgs": BnArgs, "ConvArgs": ConvArgs, "WgradArgs": WgradArgs,
+_STRUCTS = {"BnArgs": BnArgs, "BwdAff": BwdAff, "ConvArgs": ConvArgs, "WgradArgs": WgradArgs,
             "BnBwdApplyArgs": BnBwdApplyArgs, "BnBwdReduceArgs": BnBwdReduceArgs,
             "PoolArgs": PoolArgs, "PoolBwdArgs": PoolBwdArgs, "BnMovingDesc": BnMovingDesc,
             "HeadArgs": HeadArgs, "HeadBwdArgs": HeadBwdArgs, "CastEntry": CastEntry,
@@ -140,7 +150,9 @@ def _verify(ext):
               "HeadArgs.training": HeadArgs.training.offset,
               "PoolBwdArgs.is_avg": PoolBwdArgs.is_avg.offset,
               "ConvArgs.gsum_ld": ConvArgs.gsum_ld.offset, "BnArgs.slots": BnArgs.slots.offset,
-              "DwArgs.gsum_ld": DwArgs.gsum_ld.offset}
+              "DwArgs.gsum_ld": DwArgs.gsum_ld.offset, "ConvArgs.bepi": ConvArgs.bepi.offset,
+              "WgradArgs.gpro": WgradArgs.gpro.offset, "PoolBwdArgs.dx_f32": PoolBwdArgs.dx_f32.offset,
+              "BwdAff.fold_sumx": BwdAff.fold_sumx.offset, "ConvArgs.aout": ConvArgs.aout.offset}
     for k, v in checks.items():
         if sizes[k] != v:
             raise RuntimeError(f"native struct field {k}: ctypes offset {v} != C++ {sizes[k]}")

@@ -48,6 +48,29 @@ def _ident():
     return nat.bn_args(mode=0, act=0)
 
 
+def bwd_aff(x: torch.Tensor, bn: BN, gsum: Optional[torch.Tensor] = None,
+            gsumx: Optional[torch.Tensor] = None, unit_alpha: bool = False,
+            fold: Optional[Tuple[torch.Tensor, torch.Tensor]] = None) -> nat.BwdAff:
+    """Pending BatchNorm backward (csrc/kernels/common.h BwdAff) for a consumer kernel:
+    the operand v it stages becomes A*v + B*x + C with A = gamma*rstd (1 with ``unit_alpha``),
+    B, C from the reductions gsum = sum(dZ), gsumx = sum(dZ*xhat) over ``bn.count`` rows.
+    ``fold=(dbeta, dgamma)``: the consumer's block 0 also adds gsum/gsumx into them."""
+    a = nat.BwdAff()
+    a.x, a.ldx = x.data_ptr(), x.shape[-1]
+    a.bn = bn.args()
+    a.gsum, a.gsumx = nat.ptr(gsum), nat.ptr(gsumx)
+    a.gsum_slots, a.gsum_ld = 1, 0
+    a.inv_n = 1.0 / float(max(bn.count, 1))
+    a.unit_alpha = 1 if unit_alpha else 0
+    a.mode = 1
+    if fold is not None:
+        a.fold_C = x.shape[-1]
+        a.fgsum, a.fgsumx = nat.ptr(gsum), nat.ptr(gsumx)
+        a.fold_sum, a.fold_sumx = fold[0].data_ptr(), fold[1].data_ptr()
+    a._keep = (x, bn, gsum, gsumx, fold)  # the struct holds raw pointers only
+    return a
+
+
 def weight_fwd_layout(kernel_hwio: torch.Tensor, cpad: Optional[int] = None) -> torch.Tensor:
     """Keras HWIO fp32 -> bf16 [Cout][KH][KW][Cpad]."""
     kh, kw, cin, cout = kernel_hwio.shape
@@ -119,14 +142,21 @@ def _splitk_args(a, M: int, cout: int, ksplit: int, tile: int):
 def conv2d_dgrad(dy: torch.Tensor, kernel_hwio: torch.Tensor, in_hw: Tuple[int, int], pads=(0, 0),
                  mx: Optional[torch.Tensor] = None, mbn: Optional[BN] = None,
                  gsum: Optional[torch.Tensor] = None, gsumx: Optional[torch.Tensor] = None,
-                 out_f32: bool = False, tile: int = -1, ksplit: int = 1) -> torch.Tensor:
+                 out_f32: bool = False, tile: int = -1, ksplit: int = 1,
+                 bpro: Optional[nat.BwdAff] = None, bepi: Optional[nat.BwdAff] = None,
+                 acc: Optional[torch.Tensor] = None, aout: Optional[torch.Tensor] = None) -> torch.Tensor:
     """Stride-1 data gradient.  With ``mx``/``mbn``: returns dZ = dX * act'(bn(mx)) and
-    accumulates sum(dZ) into gsum, sum(dZ*xhat) into gsumx."""
+    accumulates sum(dZ) into gsum, sum(dZ*xhat) into gsumx.  ``bpro``: dy staged through a
+    pending BatchNorm backward.  ``bepi`` + ``acc`` (fp32): epilogue mode 2, acc += gamma*rstd*dZ
+    + bepi's B*mx + C (returns ``acc``)."""
     N, Ho, Wo, Cout = dy.shape
     kh, kw, cin, _ = kernel_hwio.shape
     H, W = in_hw
-    dx = torch.empty((N, H, W, cin), dtype=torch.float32 if out_f32 else torch.bfloat16,
-                     device=dy.device)
+    if acc is not None:
+        dx = acc
+    else:
+        dx = torch.empty((N, H, W, cin), dtype=torch.float32 if out_f32 else torch.bfloat16,
+                         device=dy.device)
     wl = weight_dgrad_layout(kernel_hwio)
     a = nat.ConvArgs()
     a.x = dy.data_ptr()
@@ -138,8 +168,14 @@ def conv2d_dgrad(dy: torch.Tensor, kernel_hwio: torch.Tensor, in_hw: Tuple[int, 
     a.PT, a.PL = kh - 1 - pads[0], kw - 1 - pads[1]
     a.pro = _ident()
     a.mbn = _ident()
+    if bpro is not None:
+        a.bpro = bpro
+        if aout is not None:  # the staged (affine-applied) dy, bf16, shaped like dy
+            a.aout, a.ldaout = aout.data_ptr(), aout.shape[-1]
+    if bepi is not None:
+        a.bepi = bepi
     if mx is not None:
-        a.epi_mode = 1
+        a.epi_mode = 2 if bepi is not None else 1
         a.mx, a.ldmx = mx.data_ptr(), cin
         a.mbn = mbn.args()
         a.gsum, a.gsumx = nat.ptr(gsum), nat.ptr(gsumx)
@@ -153,7 +189,7 @@ def conv2d_dgrad(dy: torch.Tensor, kernel_hwio: torch.Tensor, in_hw: Tuple[int, 
 
 def conv2d_wgrad(x: torch.Tensor, dy: torch.Tensor, kernel_shape, stride=(1, 1), pads=(0, 0),
                  pro: Optional[BN] = None, cin_real: int = 0, splits: int = -1,
-                 out: Optional[torch.Tensor] = None) -> torch.Tensor:
+                 out: Optional[torch.Tensor] = None, gpro: Optional[nat.BwdAff] = None) -> torch.Tensor:
     """dW (Keras HWIO fp32) accumulated into ``out`` (zeros if not given)."""
     N, H, W, Cin = x.shape
     _, Ho, Wo, Cout = dy.shape
@@ -172,6 +208,8 @@ def conv2d_wgrad(x: torch.Tensor, dy: torch.Tensor, kernel_shape, stride=(1, 1),
     a.dw = out.data_ptr()
     a.scale = 1.0
     a.cin_real = cin_real
+    if gpro is not None:
+        a.gpro = gpro
     nat.require().wgrad(nat.raw(a), splits, 1 if dy.dtype == torch.float32 else 0, nat.stream_handle())
     return out
 
@@ -205,11 +243,17 @@ def pool2d(x: torch.Tensor, k: int, s: int, pads=(0, 0), is_max=True, pro: Optio
 
 
 def pool2d_bwd(dy: torch.Tensor, in_shape, k: int, s: int, pads=(0, 0), is_max=True, argmax=None,
-               x: Optional[torch.Tensor] = None, bn: Optional[BN] = None, gsum=None, gsumx=None):
+               x: Optional[torch.Tensor] = None, bn: Optional[BN] = None, gsum=None, gsumx=None,
+               dyaff: Optional[nat.BwdAff] = None, out_f32: bool = False):
+    """Pool backward [through bn(x)]; ``dyaff``: dy staged through a pending BatchNorm
+    backward; ``out_f32``: returns gamma*rstd*dZ in fp32 instead of dZ."""
     N, H, W, C = in_shape
     _, Ho, Wo, _ = dy.shape
-    dx = torch.empty((N, H, W, C), dtype=torch.bfloat16, device=dy.device)
+    dx = torch.empty((N, H, W, C), dtype=torch.float32 if out_f32 else torch.bfloat16, device=dy.device)
     a = nat.PoolBwdArgs()
+    if dyaff is not None:
+        a.dyaff = dyaff
+    a.dx_f32 = 1 if out_f32 else 0
     a.dy, a.lddy, a.dy_f32 = dy.data_ptr(), C, 1 if dy.dtype == torch.float32 else 0
     a.argmax = nat.ptr(argmax)
     a.N, a.H, a.W, a.C, a.k, a.s, a.pt, a.pl, a.Ho, a.Wo = N, H, W, C, k, s, pads[0], pads[1], Ho, Wo
@@ -242,9 +286,11 @@ def bn_bwd_apply(dz, x, bn: BN, gsum, gsumx, out_f32=False, dst=None, accumulate
     return dst
 
 
-def bn_bwd_reduce(dy, x, bn: BN, gsum, gsumx, store_dz=True):
+def bn_bwd_reduce(dy, x, bn: BN, gsum, gsumx, store_dz=True, dz_f32=False):
+    """dZ = dy * act'(bn(x)) + reductions; ``dz_f32`` returns gamma*rstd*dZ in fp32."""
     M, C = x.reshape(-1, x.shape[-1]).shape
-    dz = torch.empty(x.shape, dtype=torch.bfloat16, device=x.device) if store_dz else None
+    dz = torch.empty(x.shape, dtype=torch.float32 if dz_f32 else torch.bfloat16,
+                     device=x.device) if store_dz else None
     a = nat.BnBwdReduceArgs()
     a.dy, a.lddy, a.dy_f32 = dy.data_ptr(), C, 1 if dy.dtype == torch.float32 else 0
     a.x, a.ldx = x.data_ptr(), C
@@ -252,6 +298,7 @@ def bn_bwd_reduce(dy, x, bn: BN, gsum, gsumx, store_dz=True):
     a.dz, a.lddz = nat.ptr(dz), C
     a.gsum, a.gsumx = nat.ptr(gsum), nat.ptr(gsumx)
     a.M, a.C = M, C
+    a.dz_f32 = 1 if dz_f32 else 0
     _plan1(nat.OP_BN_BWD_REDUCE, a)
     return dz
 

@@ -31,16 +31,25 @@ def _load_cache():
     _LOADED = True
     p = os.environ.get("IDC_TUNE_CACHE")
     if p and os.path.exists(p):
-        with open(p) as f:
-            for k, v in json.load(f).items():
+        try:
+            with open(p) as f:
+                entries = json.load(f)
+            for k, v in entries.items():
                 _CACHE[tuple(json.loads(k))] = v
+        except (OSError, ValueError) as e:  # a torn or foreign file: retune rather than fail
+            print(f"[autotune] ignoring unreadable tune cache {p}: {e}")
 
 
 def _save_cache():
+    """Persist the cache (IDC_TUNE_CACHE): rank 0 only, written to a temporary file and renamed
+    into place so concurrent readers never see a partial file."""
     p = os.environ.get("IDC_TUNE_CACHE")
-    if p:
-        with open(p, "w") as f:
-            json.dump({json.dumps(list(k)): v for k, v in _CACHE.items()}, f)
+    if not p or int(os.environ.get("RANK", "0")) != 0:
+        return
+    tmp = f"{p}.tmp{os.getpid()}"
+    with open(tmp, "w") as f:
+        json.dump({json.dumps(list(k)): v for k, v in _CACHE.items()}, f)
+    os.replace(tmp, p)
 
 
 def _time_op(plan, i, stream, reps=4) -> float:
@@ -105,7 +114,7 @@ def autotune_plan(plan, stream, verbose: bool = False, reset_tickets=None, slab_
             a = nat.ConvArgs.from_buffer_copy(plan.payload(i))
             f32 = plan.get_int(i, 1)
             M = a.N * a.Ho * a.Wo
-            pro = int(a.pro.mode != 0 or a.pro.act != 0)
+            pro = 2 if a.bpro.mode != 0 else int(a.pro.mode != 0 or a.pro.act != 0)
             key = ("conv", M, a.Cout, a.Cin, a.KH, a.KW, a.SH, a.PT, a.ldx, f32, pro, a.epi_mode,
                    a.out_mode, int(bool(a.bias)), a.H, a.W, int(i in halo_ops))
             best = _CACHE.get(key)
@@ -141,7 +150,8 @@ def autotune_plan(plan, stream, verbose: bool = False, reset_tickets=None, slab_
             f32 = plan.get_int(i, 1)
             s0 = max(plan.get_int(i, 0), 1)
             M = a.N * a.Ho * a.Wo
-            key = ("wgrad", M, a.Cout, a.Cin, a.KH, a.KW, a.SH, f32, int(a.pro.mode != 0 or a.pro.act != 0))
+            key = ("wgrad", M, a.Cout, a.Cin, a.KH, a.KW, a.SH, f32, int(a.pro.mode != 0 or a.pro.act != 0),
+                   int(a.gpro.mode != 0))
             best = _CACHE.get(key)
             if best is None:
                 cands = sorted({max(1, s0 // 4), max(1, s0 // 2), s0, s0 * 2, s0 * 4})

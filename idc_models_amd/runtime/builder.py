@@ -341,9 +341,44 @@ class Builder:
         self.moving.append(d)
 
     # ------------------------------------------------------------------ kernels
+    def bwd_aff(self, bn: "BNRef", x: Tensor4, c0: int = 0, unit_alpha: bool = False,
+                fold: bool = False) -> nat.BwdAff:
+        """The pending backward of BatchNorm ``bn`` for its channels [c0, c0 + x.C), applied by a
+        consumer while it stages its operand (common.h BwdAff): v' = A*v + B*x + C, with ``x`` the
+        BatchNorm's raw forward input at the consumer's positions (a view whose channel 0 is BN
+        channel c0).  ``unit_alpha``: the operand already holds A*dZ (DenseNet concat gradient).
+        ``fold``: this consumer (a main-lane kernel that runs after the reductions are complete)
+        also folds the statistics-slot copies of the reductions into d beta / d gamma."""
+        a = nat.BwdAff()
+        a.x, a.ldx = x.ptr, x.ld
+        bna = bn.args()
+        off = 4 * c0
+
+        def sh(v):
+            return (v or 0) + off if v else 0
+
+        bna.stats, bna.gamma, bna.beta = sh(bna.stats), sh(bna.gamma), sh(bna.beta)
+        bna.mmean, bna.mvar = sh(bna.mmean), sh(bna.mvar)
+        a.bn = bna
+        if bn.mode == 1:
+            if getattr(bn, "gsums", None) is None:
+                raise RuntimeError(f"{bn.layer.name}: backward affine before its reductions")
+            g, gx, S, ld = bn.gsums
+            a.gsum, a.gsumx, a.gsum_slots, a.gsum_ld = g + off, gx + off, S, ld
+            a.inv_n = 1.0 / float(bn.stats.count)
+            if fold and bn in self.pending_sums:
+                a.fold_C, a.fgsum, a.fgsumx = bn.C, g, gx
+                a.fold_sum, a.fold_sumx = bn.dbeta.data_ptr(), bn.dgamma.data_ptr()
+                self.pending_sums.remove(bn)
+        else:
+            a.inv_n = 1.0
+        a.unit_alpha = 1 if unit_alpha else 0
+        a.mode = 1
+        return a
+
     def conv(self, x: Tensor4, layer, y: Tensor4, *, stride=(1, 1), pads=(0, 0), pro=None,
              bias=None, epi_act=0, out_mode=nat.OUT_BF16, stats: Optional[Stats] = None,
-             stats_off=0, w=None, cin_override=None, tile=-1):
+             stats_off=0, w=None, cin_override=None, tile=-1, bpro: Optional[nat.BwdAff] = None):
         """Forward conv (or, with ``w`` given, a generic conv such as a dgrad)."""
         a = nat.ConvArgs()
         a.x = x.ptr
@@ -373,6 +408,8 @@ class Builder:
             a.stats_out, a.stats_ld, a.stats_off = stats.ptr, stats.ld, stats_off
             a.stats_slots = stats.slots
         a.mbn = act_only(0)
+        if bpro is not None:
+            a.bpro = bpro
         M = x.N * y.H * y.W
         if tile < 0:
             tile = self._default_tile(a, M, y.C)
@@ -404,10 +441,16 @@ class Builder:
 
     def dgrad(self, dy: Tensor4, layer, dx: Tensor4, *, pads=(0, 0), mx: Optional[Tensor4] = None,
               mbn: Optional[nat.BnArgs] = None, gsum=None, gsumx=None, gbn: Optional["BNRef"] = None,
-              out_mode=nat.OUT_BF16):
+              out_mode=nat.OUT_BF16, bpro: Optional[nat.BwdAff] = None,
+              bepi: Optional[nat.BwdAff] = None, aout: Optional[Tensor4] = None):
         """Stride-1 data gradient: conv of dy with the flipped kernel; optional BN-backward
         epilogue through the BN+act that produced the forward input ``mx`` whose reductions go
-        to ``gbn``'s gradient sums (or to explicit ``gsum``/``gsumx`` arrays)."""
+        to ``gbn``'s gradient sums (or to explicit ``gsum``/``gsumx`` arrays).
+
+        ``bpro``: dy is staged through a pending BatchNorm backward (common.h BwdAff).
+        ``bepi`` (with ``mx``; ``dx`` fp32): epilogue mode 2 — instead of storing dZ, accumulate
+        gamma*rstd*dZ plus ``bepi``'s pending B*x + C into the fp32 buffer ``dx`` (DenseNet).
+        ``aout`` (with ``bpro``): also store the staged dy (bf16) for a side-lane weight gradient."""
         kh, kw = layer.kernel_size
         center = self.is_center_only(layer, dx.H, dx.W, (1, 1), pads)
         if center:
@@ -423,8 +466,20 @@ class Builder:
         a.PT, a.PL = kh - 1 - pads[0], kw - 1 - pads[1]
         a.pro = act_only(0)
         a.mbn = act_only(0)
+        if bpro is not None:
+            a.bpro = bpro
+            if aout is not None:
+                if aout.C != dy.C or aout.M != dy.M or aout.is_f32:
+                    raise RuntimeError("operand side output must be a bf16 tensor shaped like dy")
+                a.aout, a.ldaout = aout.ptr, aout.ld
+        elif aout is not None:
+            raise RuntimeError("operand side output needs a backward-affine prologue")
+        if bepi is not None:
+            if mx is None or not dx.is_f32:
+                raise RuntimeError("epilogue mode 2 needs mx and an fp32 destination")
+            a.bepi = bepi
         if mx is not None:
-            a.epi_mode = 1
+            a.epi_mode = 2 if bepi is not None else 1
             a.mx, a.ldmx = mx.ptr, mx.ld
             a.mbn = mbn
             if gbn is not None:
@@ -440,7 +495,7 @@ class Builder:
         self.finish_grad_sums(gbn)
 
     def wgrad(self, x: Tensor4, layer, g: Tensor4, dw: torch.Tensor, *, stride=(1, 1), pads=(0, 0),
-              pro=None, cin_real=0, splits=-1, lane=0):
+              pro=None, cin_real=0, splits=-1, lane=0, gpro: Optional[nat.BwdAff] = None):
         kh, kw = layer.kernel_size
         if self.is_center_only(layer, x.H, x.W, stride, pads):
             # only the centre tap sees data: its gradient is the 1x1 wgrad; the other taps keep
@@ -458,6 +513,8 @@ class Builder:
         a.SH, a.SW = stride
         a.PT, a.PL = pads
         a.pro = pro if pro is not None else act_only(0)
+        if gpro is not None:
+            a.gpro = gpro
         a.dw = dw.data_ptr()
         a.scale = 1.0
         if not cin_real and x.C != layer.in_ch:
@@ -493,11 +550,14 @@ class Builder:
         self.emit(nat.OP_BN_BWD_APPLY, a)
 
     def bn_bwd_reduce(self, dy: Tensor4, x: Tensor4, bn: BNRef, dz: Tensor4):
+        """dZ = dy * act'(bn(x)) and its reductions; an fp32 ``dz`` receives gamma*rstd*dZ (the
+        A*dZ part of the BatchNorm backward, the rest pending for the consumers)."""
         a = nat.BnBwdReduceArgs()
         a.dy, a.lddy, a.dy_f32 = dy.ptr, dy.ld, 1 if dy.is_f32 else 0
         a.x, a.ldx = x.ptr, x.ld
         a.bn = bn.args()
         a.dz, a.lddz = dz.ptr, dz.ld
+        a.dz_f32 = 1 if dz.is_f32 else 0
         a.gsum, a.gsumx, a.gsum_slots, a.gsum_ld = self.grad_sums(bn, x.M)
         a.M, a.C = x.M, x.C
         self.emit(nat.OP_BN_BWD_REDUCE, a)
@@ -519,8 +579,15 @@ class Builder:
         self.emit(nat.OP_MAXPOOL if is_max else nat.OP_AVGPOOL, a)
 
     def pool_bwd(self, dy: Tensor4, dx: Tensor4, *, k, s, pt=0, pl=0, is_max=True, argmax=None,
-                 x: Optional[Tensor4] = None, bn: Optional[BNRef] = None, act=0):
+                 x: Optional[Tensor4] = None, bn: Optional[BNRef] = None, act=0,
+                 dyaff: Optional[nat.BwdAff] = None):
+        """Pool backward (+ backward through the pending BN+act of the forward input ``x``).
+        ``dyaff``: dy is staged through a pending BatchNorm backward; an fp32 ``dx`` receives
+        gamma*rstd*dZ instead of dZ."""
         a = nat.PoolBwdArgs()
+        if dyaff is not None:
+            a.dyaff = dyaff
+        a.dx_f32 = 1 if dx.is_f32 else 0
         a.dy, a.lddy, a.dy_f32 = dy.ptr, dy.ld, 1 if dy.is_f32 else 0
         a.argmax = nat.ptr(argmax)
         a.N, a.H, a.W, a.C = dx.N, dx.H, dx.W, dx.C

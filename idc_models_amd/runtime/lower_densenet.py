@@ -12,8 +12,10 @@ MI355X-specific structure:
 * **transition = pool first** — ``BN->ReLU->conv1x1->avgpool`` is computed as
   ``BN->ReLU->avgpool->conv1x1`` (a 1x1 conv commutes with 2x2 averaging): 4x fewer MFMA FLOPs;
 * **gradient of the concat buffer** — one fp32 gradient buffer per stage; the transition (or the
-  head) STORES it, every dense layer's BN1 backward ACCUMULATES into its channel prefix, so the
-  slice a layer reads is complete when backward reaches it and no zeroing pass is needed.
+  head) STORES it, every dense layer's dgrad cv1 epilogue ACCUMULATES into its channel prefix,
+  so the slice a layer reads is complete when backward reaches it and no zeroing pass is needed;
+* **no BatchNorm-backward passes** — each BN backward is applied by its consumers while they stage
+  their operands (the backward chain below), 2 main-lane kernels per dense layer.
 """
 from __future__ import annotations
 
@@ -103,6 +105,17 @@ def lower_densenet(b: Builder, net, U: int, input_dtype):
         return
 
     # ---------------------------------------------------------------- backward
+    # Every BatchNorm backward dX = A*dZ + B*X + C (csrc/kernels/common.h BwdAff) is applied by its
+    # CONSUMERS, never materialised by a pass of its own:
+    #   * bn2 (inside a dense layer): dgrad cv1 and wgrad cv1 stage A*z2 + B*t + C from the
+    #     per-layer z2 (= dZ of bn2) and the saved raw t;
+    #   * bn1 / transition / final BatchNorms feed the stage's fp32 concat-gradient buffer: their
+    #     producer ADDS A*dZ into it, and the B*x + C part of exactly ONE BatchNorm — ``pend``, the
+    #     last one processed — is outstanding at any time: the next dgrad cv1 epilogue folds it
+    #     into every channel it updates, and the consumers of the other channels (dgrad/wgrad cv2
+    #     of the next layer, the transition conv, the stem pool) apply it while staging.
+    #   The first main-lane consumer of a BatchNorm also folds its statistics-slot copies into
+    #   d beta / d gamma (BwdAff fold), so no standalone BN-backward kernel runs at all.
     b.segment = "bwd"
     b.memset(b.arena.grad)
     last = stages[-1]
@@ -110,88 +123,103 @@ def lower_densenet(b: Builder, net, U: int, input_dtype):
     dA = emit_head_bwd(b, last["buf"], dense, U, io, need_dA=need_base)
     if not need_base:
         return
-    M4 = last["buf"].M
-    zf = b.nhwc(last["buf"].N, last["buf"].H, last["buf"].W, last["ctot"])
-    b.bn_bwd_reduce(dA, last["buf"], bnf, zf)
+    lb = last["buf"]
     if not fz.before(L["bn"]):
+        zf = b.nhwc(lb.N, lb.H, lb.W, last["ctot"])
+        b.bn_bwd_reduce(dA, lb, bnf, zf)
         b.mark_grads_ready([bnf.gamma, bnf.beta])
         return
-    dbuf = b.nhwc(last["buf"].N, last["H"], last["W"], last["ctot"], F32)
-    # marks follow the BatchNorm's apply: it folds the statistics-slot copies of d gamma / d beta
-    b.bn_bwd_apply(zf, last["buf"], bnf, dbuf, accumulate=False)
-    b.mark_grads_ready([bnf.gamma, bnf.beta])
+    dbuf = b.nhwc(lb.N, last["H"], last["W"], last["ctot"], F32)
+    b.bn_bwd_reduce(dA, lb, bnf, dbuf)  # fp32 dbuf = A_f * dZ_f
+    pend = bnf
+
+    def pend_params():
+        return [pend.gamma, pend.beta]
 
     for si in range(len(stages) - 1, -1, -1):
         st = stages[si]
         buf = st["buf"]
-        N, Hs, Ws, ctot = buf.N, st["H"], st["W"], st["ctot"]
-        z1 = b.nhwc(N, Hs, Ws, ctot)
-        z2 = b.nhwc(N, Hs, Ws, 128)
-        stop = False
+        N, Hs, Ws = buf.N, st["H"], st["W"]
+        z2 = b.nhwc(N, Hs, Ws, 128)  # dZ of bn2, consumed by the next dgrad only
         for lay in reversed(st["layers"]):
             cin, bn1, cv1, bn2, cv2, t = lay["cin"], lay["bn1"], lay["cv1"], lay["bn2"], lay["cv2"], lay["t"]
             dO = dbuf.slice(cin, 32)
-            # weight gradients run on the side lane: their inputs (t, this layer's dO slice, the
-            # per-layer dt, the stage buffer) are never overwritten later in the backward
-            if fz.trainable(cv2):
-                b.wgrad(t, cv2, dO, b.arena.grad_of(cv2.kernel), pads=(1, 1), pro=bn2.args(), lane=1)
+            xO = buf.slice(cin, 32)
+            # Weight gradients run on the side lane and read plain bf16 gradients that the dgrads
+            # store while staging them (dO16, dt: per layer, never overwritten later); where the
+            # backward stops at a layer (no dgrad), the wgrad applies the pending affine itself.
             if not fz.before(cv2):
-                stop = True
-                break
-            b.dgrad(dO, cv2, z2, pads=(1, 1), mx=t, mbn=bn2.args(), gbn=bn2)
+                if fz.trainable(cv2):
+                    b.wgrad(t, cv2, dO, b.arena.grad_of(cv2.kernel), pads=(1, 1), pro=bn2.args(), lane=1,
+                            gpro=b.bwd_aff(pend, xO, c0=cin, unit_alpha=True))
+                b.mark_grads_ready([cv2.kernel] + pend_params())
+                return
+            dO16 = b.nhwc(N, Hs, Ws, 32)
+            b.dgrad(dO, cv2, z2, pads=(1, 1), mx=t, mbn=bn2.args(), gbn=bn2,
+                    bpro=b.bwd_aff(pend, xO, c0=cin, unit_alpha=True, fold=True), aout=dO16)
+            if fz.trainable(cv2):
+                b.wgrad(t, cv2, dO16, b.arena.grad_of(cv2.kernel), pads=(1, 1), pro=bn2.args(), lane=1)
             if not fz.before(bn2.layer):
-                stop = True
-                break
-            dt = b.nhwc(N, Hs, Ws, 128)  # per layer: read later by the side-lane wgrad
-            b.bn_bwd_apply(z2, t, bn2, dt, accumulate=False)
+                b.mark_grads_ready([cv2.kernel, bn2.gamma, bn2.beta] + pend_params())
+                return
+            ready = [cv2.kernel, cv1.kernel, bn2.gamma, bn2.beta] + pend_params()
+            if not fz.before(cv1):
+                if fz.trainable(cv1):
+                    b.wgrad(buf.slice(0, cin), cv1, z2, b.arena.grad_of(cv1.kernel), pro=bn1.args(), lane=1,
+                            gpro=b.bwd_aff(bn2, t))
+                b.mark_grads_ready(ready)
+                return
+            # concat gradient [0, cin) += A1*dZ1 + (pend's B*x + C); reductions of bn1
+            dt = b.nhwc(N, Hs, Ws, 128)
+            b.dgrad(z2, cv1, dbuf.slice(0, cin), mx=buf.slice(0, cin), mbn=bn1.args(), gbn=bn1,
+                    bpro=b.bwd_aff(bn2, t, fold=True),
+                    bepi=b.bwd_aff(pend, buf.slice(0, cin), unit_alpha=True), aout=dt)
             if fz.trainable(cv1):
                 b.wgrad(buf.slice(0, cin), cv1, dt, b.arena.grad_of(cv1.kernel), pro=bn1.args(), lane=1)
-            if not fz.before(cv1):
-                stop = True
-                break
-            z1v = Tensor4(z1.t, N, Hs, Ws, cin, cin)
-            b.dgrad(dt, cv1, z1v, mx=buf.slice(0, cin), mbn=bn1.args(), gbn=bn1)
-            ready = [cv2.kernel, cv1.kernel, bn2.gamma, bn2.beta, bn1.gamma, bn1.beta]
-            if not fz.before(bn1.layer):
-                b.mark_grads_ready(ready)
-                stop = True
-                break
-            b.bn_bwd_apply(z1v, buf.slice(0, cin), bn1, dbuf.slice(0, cin), accumulate=True)
             b.mark_grads_ready(ready)
-        if stop:
-            return
+            pend = bn1
+            if not fz.before(bn1.layer):
+                b.mark_grads_ready(pend_params())
+                return
         if si == 0:
             break
-        # transition of the previous stage (writes this stage's channels [0:c0))
+        # transition of the previous stage (wrote this stage's channels [0:c0)), through pend
         prev = stages[si - 1]
         tr = prev["trans"]
         bnt, cvt, p = tr["bn"], tr["conv"], tr["p"]
-        dO = dbuf.slice(0, st["c0"])
-        if fz.trainable(cvt):
-            b.wgrad(p, cvt, dO, b.arena.grad_of(cvt.kernel), lane=1)
+        c0 = st["c0"]
+        dO = dbuf.slice(0, c0)
+        xO = buf.slice(0, c0)
         if not fz.before(cvt):
+            if fz.trainable(cvt):
+                b.wgrad(p, cvt, dO, b.arena.grad_of(cvt.kernel), lane=1,
+                        gpro=b.bwd_aff(pend, xO, unit_alpha=True))
+            b.mark_grads_ready([cvt.kernel] + pend_params())
             return
         dp = b.nhwc(p.N, p.H, p.W, p.C)
-        b.dgrad(dO, cvt, dp)
+        dO16 = b.nhwc(N, Hs, Ws, c0)
+        b.dgrad(dO, cvt, dp, bpro=b.bwd_aff(pend, xO, unit_alpha=True, fold=True), aout=dO16)
+        if fz.trainable(cvt):
+            b.wgrad(p, cvt, dO16, b.arena.grad_of(cvt.kernel), lane=1)
+        b.mark_grads_ready(pend_params())
         pbuf = prev["buf"]
-        zt = b.nhwc(pbuf.N, prev["H"], prev["W"], prev["ctot"])
-        b.pool_bwd(dp, zt, k=2, s=2, is_max=False, x=pbuf, bn=bnt)
-        if not fz.before(bnt.layer):
-            b.mark_grads_ready([cvt.kernel, bnt.gamma, bnt.beta])
-            return
         dbuf = b.nhwc(pbuf.N, prev["H"], prev["W"], prev["ctot"], F32)
-        b.bn_bwd_apply(zt, pbuf, bnt, dbuf, accumulate=False)
-        b.mark_grads_ready([cvt.kernel, bnt.gamma, bnt.beta])
+        b.pool_bwd(dp, dbuf, k=2, s=2, is_max=False, x=pbuf, bn=bnt)  # fp32: A_t * dZ_t
+        b.mark_grads_ready([cvt.kernel])
+        pend = bnt
+        if not fz.before(bnt.layer):
+            b.mark_grads_ready(pend_params())
+            return
 
-    # stem: maxpool backward through BN+ReLU of conv1, then conv1 wgrad
+    # stem: max-pool backward through BN+ReLU of conv1 (dy = concat gradient + pend), conv1 wgrad
     if not fz.at_or_before(bn1l):
+        b.mark_grads_ready(pend_params())
         return
+    st0 = stages[0]
     zs = b.nhwc(B, H1, W1, 64)
     b.pool_bwd(dbuf.slice(0, 64), zs, k=3, s=2, pt=1, pl=1, is_max=True, argmax=argmax, x=ys,
-               bn=bn_stem)
+               bn=bn_stem, dyaff=b.bwd_aff(pend, st0["buf"].slice(0, 64), unit_alpha=True, fold=True))
     if fz.trainable(conv1):
-        dys = b.nhwc(B, H1, W1, 64)
-        b.bn_bwd_apply(zs, ys, bn_stem, dys, accumulate=False)
-        b.wgrad(x8, conv1, dys, b.arena.grad_of(conv1.kernel), stride=(2, 2), pads=(3, 3),
-                cin_real=Cimg, lane=1)
-    b.mark_grads_ready([conv1.kernel, bn_stem.gamma, bn_stem.beta])
+        b.wgrad(x8, conv1, zs, b.arena.grad_of(conv1.kernel), stride=(2, 2), pads=(3, 3),
+                cin_real=Cimg, lane=1, gpro=b.bwd_aff(bn_stem, ys))
+    b.mark_grads_ready([conv1.kernel, bn_stem.gamma, bn_stem.beta] + pend_params())

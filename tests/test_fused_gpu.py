@@ -229,3 +229,11 @@ def test_tinycnn_fused_dropout_trains_and_eval_is_deterministic():
     l1, g1 = m.impl.eval_step(x, y)
     l2, g2 = m.impl.eval_step(x, y)
     assert torch.equal(g1, g2)  # no dropout at inference
+
+
+@pytest.mark.parametrize("arch", ["densenet121", "vgg16", "mobilenetv2"])
+def test_fused_matches_eager_at_bench_batch(arch):
+    """The benchmarked configuration, bs=256: 16 statistics slot copies on the large maps, the
+    autotuner's split-K choices and the full-size workspaces — not only the small test batches."""
+    m, ref, x, y = _setup(arch, 256)
+    _check(m, ref, x, y)

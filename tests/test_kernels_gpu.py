@@ -413,3 +413,150 @@ def test_secagg_masks_cancel_exactly():
     # CPU numpy Philox produces the same bits as the GPU kernel
     cpu = mask_quantize(xs[1].cpu(), scale, K, 1, seed=1234, round_=7)
     assert torch.equal(cpu, masked[1].cpu())
+
+
+# ---------------------------------------------------------------------------------------------
+# Backward pending affine (csrc/kernels/common.h BwdAff): BatchNorm backward applied by consumers
+def _bn_case(N, H, C, x=None, seed=0, act=0):
+    """raw x, BN descriptor, upstream dZ (grad wrt the BN output), reductions and autograd dX."""
+    from idc_models_amd.ops import functional as fn
+    g0 = torch.Generator(device=DEV).manual_seed(seed)
+    if x is None:
+        x = bf(torch.randn(N, H, H, C, device=DEV, generator=g0) * 2 + 0.5)
+    st = torch.cat([x.sum((0, 1, 2)), (x * x).sum((0, 1, 2))])
+    g = torch.rand(C, device=DEV, generator=g0) + 0.5
+    b = torch.randn(C, device=DEV, generator=g0) * 0.1
+    cnt = N * H * H
+    dZ = bf(torch.randn(N, H, H, C, device=DEV, generator=g0))
+    xr = x.clone().requires_grad_(True)
+    mean, var = xr.mean((0, 1, 2)), xr.var((0, 1, 2), unbiased=False)
+    ((xr - mean) * torch.rsqrt(var + 1e-3) * g + b).backward(dZ)
+    rstd = torch.rsqrt(x.var((0, 1, 2), unbiased=False) + 1e-3)
+    xhat = (x - x.mean((0, 1, 2))) * rstd
+    gsum, gsumx = dZ.sum((0, 1, 2)), (dZ * xhat).sum((0, 1, 2))
+    bn = fn.BN(stats=st, gamma=g, beta=b, count=cnt, eps=1e-3, act=act)
+    return dict(x=x, bn=bn, dZ=dZ, gsum=gsum, gsumx=gsumx, dX=xr.grad, A=g * rstd, xhat=xhat)
+
+
+def test_dgrad_bwd_affine_prologue_1x1(fn):
+    """DenseNet dgrad cv1: the operand is z2 = dZ of bn2, staged as A*z2 + B*t + C (= dt)."""
+    N, H, C, cin = 4, 13, 128, 96
+    k = _bn_case(N, H, C)
+    w = bf(torch.randn(1, 1, cin, C, device=DEV) * 0.1)
+    x16 = k["x"].to(torch.bfloat16)
+    aff = fn.bwd_aff(x16, k["bn"], k["gsum"], k["gsumx"])
+    out = fn.conv2d_dgrad(k["dZ"].to(torch.bfloat16), w, (H, H), bpro=aff, out_f32=True)
+    ref = torch.nn.grad.conv2d_input((N, cin, H, H), w.permute(3, 2, 0, 1),
+                                     bf(k["dX"]).permute(0, 3, 1, 2)).permute(0, 2, 3, 1)
+    assert relerr(out, ref) < 2e-2
+
+
+@pytest.mark.parametrize("ksplit,tile", [(1, -1), (2, 9), (4, 12)])
+def test_dgrad_bwd_affine_unit_alpha_3x3_fp32_and_fold(fn, ksplit, tile):
+    """DenseNet dgrad cv2: fp32 concat-gradient operand already holding A*dZ; B*x + C of the
+    pending BatchNorm added while staging; block 0 folds the reductions into d beta / d gamma."""
+    N, H, C, cin = 4, 6, 32, 128
+    k = _bn_case(N, H, C, seed=1)
+    v = (k["dZ"] * k["A"]).contiguous()
+    w = bf(torch.randn(3, 3, cin, C, device=DEV) * 0.1)
+    db, dg = torch.zeros(C, device=DEV), torch.zeros(C, device=DEV)
+    x16 = k["x"].to(torch.bfloat16)
+    aff = fn.bwd_aff(x16, k["bn"], k["gsum"], k["gsumx"], unit_alpha=True, fold=(db, dg))
+    staged = torch.zeros(N, H, H, C, dtype=torch.bfloat16, device=DEV)
+    out = fn.conv2d_dgrad(v, w, (H, H), pads=(1, 1), bpro=aff, out_f32=True, ksplit=ksplit, tile=tile,
+                          aout=staged)
+    ref = torch.nn.grad.conv2d_input((N, cin, H, H), w.permute(3, 2, 0, 1),
+                                     bf(k["dX"]).permute(0, 3, 1, 2), padding=1).permute(0, 2, 3, 1)
+    assert relerr(out, ref) < 2e-2
+    assert relerr(staged, k["dX"]) < 1e-2  # the staged operand, for the side-lane wgrad
+    torch.cuda.synchronize()
+    assert torch.equal(db, k["gsum"]) and torch.equal(dg, k["gsumx"])
+
+
+@pytest.mark.parametrize("unit,Cout,k_", [(False, 128, 1), (True, 32, 3)])
+def test_wgrad_bwd_affine_on_g(fn, unit, Cout, k_):
+    """wgrad cv1 (G = A*z2 + B*t + C, bf16) and wgrad cv2 (G = fp32 concat grad + B*x + C)."""
+    N, H, Cin = 4, 13, 64
+    kc = _bn_case(N, H, Cout, seed=2)
+    xin = bf(torch.randn(N, H, H, Cin, device=DEV))
+    g = (kc["dZ"] * kc["A"]).contiguous() if unit else kc["dZ"].to(torch.bfloat16)
+    x16 = kc["x"].to(torch.bfloat16)
+    aff = fn.bwd_aff(x16, kc["bn"], kc["gsum"], kc["gsumx"], unit_alpha=unit)
+    p = k_ // 2
+    dw = fn.conv2d_wgrad(xin.to(torch.bfloat16), g, (k_, k_), pads=(p, p), gpro=aff)
+    ref = torch.nn.grad.conv2d_weight(xin.permute(0, 3, 1, 2), (Cout, Cin, k_, k_),
+                                      bf(kc["dX"]).permute(0, 3, 1, 2), padding=p).permute(2, 3, 1, 0)
+    assert relerr(dw, ref) < 2e-2
+
+
+def test_dgrad_epilogue_accumulates_concat_gradient(fn):
+    """Epilogue mode 2: acc += gamma1*rstd1*dZ1 + (pending BatchNorm's B'*x + C') on the same x,
+    with dZ1 = dA * relu'(bn1(x)) reduced into bn1's gsum / gsumx."""
+    N, H, C, cin = 4, 6, 128, 160
+    x = bf(torch.randn(N, H, H, cin, device=DEV) * 1.5 + 0.3)
+    kb = _bn_case(N, H, cin, x=x, seed=3, act=1)   # bn1 of this layer (its dZ is computed here)
+    kp = _bn_case(N, H, cin, x=x, seed=4)          # the pending BatchNorm over the same channels
+    k2 = _bn_case(N, H, C, seed=7)                 # the operand: z2 = dZ of bn2, staged as dt
+    t16, z16 = k2["x"].to(torch.bfloat16), k2["dZ"].to(torch.bfloat16)
+    bpro = fn.bwd_aff(t16, k2["bn"], k2["gsum"], k2["gsumx"])
+    w = bf(torch.randn(1, 1, cin, C, device=DEV) * 0.1)
+    acc0 = torch.randn(N, H, H, cin, device=DEV)
+    acc = acc0.clone()
+    gsum, gsumx = torch.zeros(cin, device=DEV), torch.zeros(cin, device=DEV)
+    x16 = x.to(torch.bfloat16)
+    bepi = fn.bwd_aff(x16, kp["bn"], kp["gsum"], kp["gsumx"], unit_alpha=True)
+    fn.conv2d_dgrad(z16, w, (H, H), mx=x16, mbn=kb["bn"], gsum=gsum, gsumx=gsumx, bpro=bpro, bepi=bepi, acc=acc)
+    dy = bf(k2["dX"])
+    dA = torch.nn.grad.conv2d_input((N, cin, H, H), w.permute(3, 2, 0, 1), dy.permute(0, 3, 1, 2)).permute(0, 2, 3, 1)
+    z = kb["xhat"] * kb["bn"].gamma + kb["bn"].beta
+    dZ1 = dA * (z > 0).float()
+    pend = kp["dX"] - kp["A"] * kp["dZ"]
+    ref = acc0 + kb["A"] * dZ1 + pend
+    assert relerr(acc - acc0, ref - acc0) < 2e-2
+    assert relerr(gsum, dZ1.sum((0, 1, 2))) < 2e-2
+    assert relerr(gsumx, (dZ1 * kb["xhat"]).sum((0, 1, 2))) < 2e-2
+
+
+def test_pool_bwd_dy_affine_and_f32_output(fn):
+    """Stem max-pool backward with dy = fp32 concat grad + pending B*x + C (x at the pool-output
+    positions), and the transition avg-pool backward writing gamma*rstd*dZ in fp32."""
+    N, H, C = 2, 25, 64
+    y = bf(torch.randn(N, H, H, C, device=DEV))
+    st = torch.cat([y.sum((0, 1, 2)), (y * y).sum((0, 1, 2))])
+    g, b = torch.rand(C, device=DEV) + 0.5, torch.randn(C, device=DEV) * 0.1
+    cnt = N * H * H
+    bn = fn.BN(stats=st, gamma=g, beta=b, count=cnt, eps=1.001e-5, act=1)
+    p, am = fn.pool2d(y.to(torch.bfloat16), 3, 2, pads=(1, 1), is_max=True, pro=bn)
+    kp = _bn_case(N, 13, C, x=bf(p.float()), seed=5)
+    dy = (kp["dZ"] * kp["A"]).contiguous()
+    db, dg = torch.zeros(C, device=DEV), torch.zeros(C, device=DEV)
+    aff = fn.bwd_aff(p, kp["bn"], kp["gsum"], kp["gsumx"], unit_alpha=True, fold=(db, dg))
+    dz = fn.pool2d_bwd(dy, (N, H, H, C), 3, 2, pads=(1, 1), is_max=True, argmax=am, x=y.to(torch.bfloat16),
+                       bn=bn, dyaff=aff)
+    dz_ref = fn.pool2d_bwd(kp["dX"].contiguous(), (N, H, H, C), 3, 2, pads=(1, 1), is_max=True, argmax=am,
+                           x=y.to(torch.bfloat16), bn=bn)
+    assert relerr(dz, dz_ref) < 2e-2
+    torch.cuda.synchronize()
+    assert torch.equal(db, kp["gsum"]) and torch.equal(dg, kp["gsumx"])
+    # transition form: avg-pool backward through bn, fp32 A*dZ output
+    gs1, gx1 = torch.zeros(C, device=DEV), torch.zeros(C, device=DEV)
+    gs2, gx2 = torch.zeros(C, device=DEV), torch.zeros(C, device=DEV)
+    dq = bf(torch.randn(N, 12, 12, C, device=DEV))
+    a32 = fn.pool2d_bwd(dq, (N, H, H, C), 2, 2, is_max=False, x=y.to(torch.bfloat16), bn=bn, gsum=gs1,
+                        gsumx=gx1, out_f32=True)
+    z16 = fn.pool2d_bwd(dq, (N, H, H, C), 2, 2, is_max=False, x=y.to(torch.bfloat16), bn=bn, gsum=gs2, gsumx=gx2)
+    A = g * torch.rsqrt(st[C:] / cnt - (st[:C] / cnt) ** 2 + 1.001e-5)
+    assert relerr(a32, z16.float() * A) < 1e-2
+    assert relerr(gs1, gs2) < 1e-2 and relerr(gx1, gx2) < 1e-2
+
+
+def test_bn_bwd_reduce_f32_scaled_output(fn):
+    N, H, C = 4, 6, 64
+    k = _bn_case(N, H, C, seed=6, act=1)
+    dy = torch.randn(N, H, H, C, device=DEV)
+    gs, gx = torch.zeros(C, device=DEV), torch.zeros(C, device=DEV)
+    a = fn.bn_bwd_reduce(dy, k["x"].to(torch.bfloat16), k["bn"], gs, gx, dz_f32=True)
+    z = k["xhat"] * k["bn"].gamma + k["bn"].beta
+    dZ = dy * (z > 0).float()
+    assert relerr(a, k["A"] * dZ) < 1e-2
+    assert relerr(gs, dZ.sum((0, 1, 2))) < 1e-2

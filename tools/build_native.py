@@ -26,6 +26,11 @@ HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 
 SOURCES = [
     "kernels/conv_igemm.hip",
+    "kernels/conv_igemm_g0.hip",
+    "kernels/conv_igemm_g1.hip",
+    "kernels/conv_igemm_g2.hip",
+    "kernels/conv_igemm_g3.hip",
+    "kernels/conv_igemm_g4.hip",
     "kernels/conv3x3_halo.hip",
     "kernels/conv_wgrad.hip",
     "kernels/nn_kernels.hip",

@@ -27,8 +27,14 @@ def main():
     ap.add_argument("--top", type=int, default=40)
     a = ap.parse_args()
     c = sqlite3.connect(a.db)
-    rows = list(c.execute("select name, start, end, grid_x, workgroup_x, vgpr_count, accum_vgpr_count, lds_size "
-                          "from kernels order by start"))
+    try:  # full 3-D launch geometry (grid sizes are in work-items)
+        rows = [(n, s, e, (gx // max(wx, 1)) * (gy // max(wy, 1)) * (gz // max(wz, 1)), 1, vg, ag, lds)
+                for n, s, e, gx, gy, gz, wx, wy, wz, vg, ag, lds in c.execute(
+                    "select name, start, end, grid_x, grid_y, grid_z, workgroup_x, workgroup_y, workgroup_z, "
+                    "vgpr_count, accum_vgpr_count, lds_size from kernels order by start")]
+    except sqlite3.OperationalError:  # older schema: x only
+        rows = list(c.execute("select name, start, end, grid_x, workgroup_x, vgpr_count, accum_vgpr_count, "
+                              "lds_size from kernels order by start"))
     marks = [i for i, r in enumerate(rows) if a.marker in r[0]]
     if len(marks) < a.steps:
         raise SystemExit(f"only {len(marks)} '{a.marker}' dispatches found")
