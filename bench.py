@@ -2,16 +2,25 @@
 """Headline benchmark: DenseNet-121 50x50x3 training, bs=256 per GPU, bf16, data-parallel.
 
 Metric (BASELINE.json): images/sec for the WHOLE job (all ranks), DenseNet-121 at 50x50x3,
-batch 256 per GPU, weak scaling over 1/2/4/8 MI355X.  Synthetic uint8 patches of that shape and
-random-init weights (no network on the box).  The timed region is the complete training step:
-input staging, forward, loss, backward, bucketed RCCL gradient all-reduce (N>1), fused RMSprop
-update and bf16 weight re-cast — nothing skipped.
+batch 256 per GPU, weak scaling over 1/2/4/8 MI355X; plus validation AUC.  Synthetic uint8
+patches of that shape and random-init weights (no network on the box).
+
+* ``value`` — the timed region is the complete training step on a device-resident batch: input
+  staging, forward, loss, backward, bucketed RCCL gradient all-reduce (N>1), fused RMSprop update
+  and bf16 weight re-cast — nothing skipped.  W warm-up steps, then exactly K steps between
+  barrier + synchronize on both sides, max over ranks.
+* ``fit_images_per_sec`` — after the timed region: ``Model.fit`` throughput on a host-resident
+  learnable synthetic dataset (pinned-memory prefetcher, per-rank index sharding, metrics),
+  training epochs only.
+* ``val_auc`` — exact (Mann-Whitney) AUC of ``Model.evaluate`` on a held-out synthetic set after
+  that fit (``secure_fed_model.py:81-82`` reports AUC; here over the whole set, not per batch).
 
     python bench.py                     # 1 GPU, defaults
     python -m torch.distributed.run --nproc-per-node 8 --master-addr 127.0.0.1 bench.py --gpus 8
 
-``vs_baseline`` is relative to the in-situ stock PyTorch-ROCm measurement recorded in
-BASELINE.md (the reference publishes no number): 9,379 img/s per GPU x N.
+``vs_baseline`` is relative to the in-situ stock PyTorch-ROCm measurement committed in
+``benchmarks/stock_baseline.json`` (the reference publishes no number): the faster of
+its eager and HIP-graph-captured steps, per GPU, times N.
 """
 from __future__ import annotations
 
@@ -24,7 +33,17 @@ import time
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
-STOCK_PYTORCH_IMG_S_PER_GPU = {"densenet121": 9379.3, "vgg16": 58586.2, "mobilenetv2": 19653.8}
+
+def stock_img_s_per_gpu(model: str):
+    """Best stock PyTorch-ROCm images/sec on one GPU for ``model`` (benchmarks/stock_baseline.json)."""
+    p = os.path.join(ROOT, "benchmarks", "stock_baseline.json")
+    try:
+        with open(p) as f:
+            runs = json.load(f)
+    except (OSError, ValueError):
+        return None
+    vals = [r["images_per_sec"] for r in runs.get("results", []) if r.get("model") == model]
+    return max(vals) if vals else None
 
 
 def main():
@@ -37,12 +56,19 @@ def main():
     ap.add_argument("--lr", type=float, default=1e-4)
     ap.add_argument("--no-graphs", action="store_true")
     ap.add_argument("--backend", default="fused")
+    # ~320 fit steps: Keras BatchNorm momentum 0.99 leaves the inference-mode moving statistics
+    # mostly at their init after a few dozen steps (0.99^36 = 0.70), so a short fit evaluates stale
+    # statistics; 0.99^320 = 0.04
+    ap.add_argument("--fit-steps", type=int, default=20, help="global batches per fit epoch (0: skip fit/AUC)")
+    ap.add_argument("--fit-epochs", type=int, default=16)
     args = ap.parse_args()
 
     import torch
     import torch.distributed as dist
 
+    from idc_models_amd.data import synthetic_dataset
     from idc_models_amd.engine import Model, RMSprop
+    from idc_models_amd.engine.callbacks import ThroughputMeter
     from idc_models_amd.models import build_model
     from idc_models_amd.parallel import MirroredStrategy, OneDeviceStrategy
     from idc_models_amd.parallel.comm import all_reduce_max, barrier
@@ -58,12 +84,18 @@ def main():
         strategy = OneDeviceStrategy("cuda:0")
     rank = strategy.rank
     dev = strategy.device
+    comm_backend = dist.get_backend() if world > 1 else None
+    world = strategy.num_replicas_in_sync
+    try:
+        rccl = ".".join(str(v) for v in torch.cuda.nccl.version()) if comm_backend == "nccl" else None
+    except Exception:  # pragma: no cover - version query unsupported
+        rccl = "unknown"
     torch.manual_seed(1234)
 
     with strategy.scope():
         net = build_model(args.model, num_outputs=1, seed=1234)
         model = Model(net, strategy)
-        model.compile(RMSprop(args.lr), "binary_crossentropy", ["accuracy"], backend=args.backend,
+        model.compile(RMSprop(args.lr), "binary_crossentropy", ["accuracy", "auc"], backend=args.backend,
                       **({"use_graphs": False} if args.no_graphs and args.backend == "fused" else {}))
     H, W, C = net.input_shape
     g = torch.Generator(device="cpu").manual_seed(1000 + rank)
@@ -87,11 +119,28 @@ def main():
     ms = dt / args.steps * 1e3
     total_imgs = args.batch * world * args.steps
     value = total_imgs / dt
-    base = STOCK_PYTORCH_IMG_S_PER_GPU.get(args.model)
     lossv = float(loss.item())
+
+    # ---- after the timed region: fit() throughput and held-out validation AUC ----------------
+    fit_ips = val_auc = val_acc = None
+    if args.fit_steps > 0:
+        gb = args.batch * world
+        train = synthetic_dataset(gb * args.fit_steps, (H, W, C), 2, seed=11)
+        held = synthetic_dataset(max(gb * 2, 1024), (H, W, C), 2, seed=12)
+        meter = ThroughputMeter()
+        model.fit(train.batch(gb, True, 1000, True, seed=5), epochs=args.fit_epochs, callbacks=[meter],
+                  verbose=0)
+        k = 1 if len(meter.epoch_seconds) > 1 else 0
+        t_ep = max(sum(meter.epoch_seconds[k:]) / len(meter.epoch_seconds[k:]), 1e-9)
+        t_ep = all_reduce_max(t_ep, dev) if world > 1 else t_ep  # slowest rank sets the pace
+        fit_ips = gb * args.fit_steps / t_ep
+        logs = model.evaluate(held.batch(gb, False, 1000, False), return_dict=True)
+        val_auc, val_acc = float(logs["auc"]), float(logs["accuracy"])
+
+    base = stock_img_s_per_gpu(args.model)
     if rank == 0:
         print(json.dumps({
-            "metric": "images/sec (whole node) DenseNet-121 50x50x3 bs=256 at 1/2/4/8 MI355X"
+            "metric": "images/sec (whole node) DenseNet-121 50x50x3 bs=256 at 1/2/4/8 MI355X; val AUC"
             if args.model == "densenet121" else f"images/sec (whole node) {args.model} 50x50x3",
             "value": round(value, 1),
             "unit": "images/sec",
@@ -104,12 +153,19 @@ def main():
             "vs_baseline": round(value / (base * world), 3) if base else None,
             "dtype": "bf16",
             "data": "synthetic uint8 50x50x3 patches, random-init weights",
+            "val_auc": round(val_auc, 4) if val_auc is not None else None,
+            "val_accuracy": round(val_acc, 4) if val_acc is not None else None,
+            "fit_images_per_sec": round(fit_ips, 1) if fit_ips is not None else None,
             "config": {"model": "DenseNet-121" if args.model == "densenet121" else args.model,
                        "global_batch": args.batch * world, "seq_len": None,
                        "input": [H, W, C], "per_gpu_batch": args.batch,
                        "parallelism": f"dp{world}", "optimizer": "RMSprop(lr=%g)" % args.lr,
                        "loss": "BCE(from_logits)", "final_loss": round(lossv, 5),
-                       "backend": args.backend},
+                       "backend": args.backend, "comm_backend": comm_backend, "rccl_version": rccl,
+                       "world_size": world,
+                       "stock_baseline_img_s_per_gpu": base,
+                       "val": "exact AUC on a held-out learnable synthetic set after %d fit epochs of %d "
+                              "global batches" % (args.fit_epochs, args.fit_steps)},
         }), flush=True)
     if world > 1:
         dist.destroy_process_group()

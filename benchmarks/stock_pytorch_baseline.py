@@ -106,6 +106,59 @@ def mobilenetv2():
     return nn.Sequential(*layers)
 
 
+def run(model_name: str, batch: int, steps: int, warmup: int, graph: bool, channels_last: bool = True) -> dict:
+    """Time one stock training step (bf16 autocast forward, fp32 loss, backward, RMSprop).
+    ``graph``: the whole step captured once into a HIP graph (torch.cuda.graphs, capturable
+    RMSprop) and replayed — the strongest stock configuration (no per-kernel host launches)."""
+    dev = torch.device("cuda")
+    torch.backends.cudnn.benchmark = True
+    torch.manual_seed(0)
+    model = {"densenet121": DenseNet121, "vgg16": vgg16, "mobilenetv2": mobilenetv2}[model_name]().to(dev)
+    fmt = torch.channels_last if channels_last else torch.contiguous_format
+    model = model.to(memory_format=fmt)
+    opt = torch.optim.RMSprop(model.parameters(), lr=1e-4, alpha=0.9, eps=1e-7, capturable=graph)
+    x = torch.rand(batch, 3, 50, 50, device=dev).to(memory_format=fmt)
+    y = torch.randint(0, 2, (batch, 1), device=dev).float()
+
+    def step():
+        with torch.autocast("cuda", dtype=torch.bfloat16):
+            out = model(x)
+        loss = F.binary_cross_entropy_with_logits(out.float(), y)
+        loss.backward()
+        opt.step()
+        return loss
+
+    side = torch.cuda.Stream()
+    side.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(side):
+        for _ in range(warmup):
+            opt.zero_grad(set_to_none=True)
+            step()
+    torch.cuda.current_stream().wait_stream(side)
+    if graph:
+        g = torch.cuda.CUDAGraph()
+        opt.zero_grad(set_to_none=True)
+        with torch.cuda.graph(g):
+            step()
+        run_step = g.replay
+    else:
+        def run_step():
+            opt.zero_grad(set_to_none=True)
+            step()
+    for _ in range(3):
+        run_step()
+    torch.cuda.synchronize()
+    t = time.perf_counter()
+    for _ in range(steps):
+        run_step()
+    torch.cuda.synchronize()
+    dt = (time.perf_counter() - t) / steps
+    return {"baseline": "stock_pytorch_%s_bf16_autocast" % ("hipgraph" if graph else "eager"),
+            "model": model_name, "batch": batch, "ms_per_step": round(dt * 1e3, 3),
+            "images_per_sec": round(batch / dt, 1), "channels_last": channels_last,
+            "torch": torch.__version__, "device": torch.cuda.get_device_name()}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--model", default="densenet121")
@@ -113,37 +166,28 @@ def main():
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--no-channels-last", action="store_true")
+    ap.add_argument("--graph", action="store_true", help="HIP-graph-captured step")
+    ap.add_argument("--all", metavar="OUT_JSON", help="every model, eager and graph; write JSON")
     args = ap.parse_args()
-    dev = torch.device("cuda")
-    torch.backends.cudnn.benchmark = True
-    model = {"densenet121": DenseNet121, "vgg16": vgg16, "mobilenetv2": mobilenetv2}[args.model]().to(dev)
-    fmt = torch.contiguous_format if args.no_channels_last else torch.channels_last
-    model = model.to(memory_format=fmt)
-    opt = torch.optim.RMSprop(model.parameters(), lr=1e-4, alpha=0.9, eps=1e-7)
-    x = torch.rand(args.batch, 3, 50, 50, device=dev).to(memory_format=fmt)
-    y = torch.randint(0, 2, (args.batch, 1), device=dev).float()
-
-    def step():
-        with torch.autocast("cuda", dtype=torch.bfloat16):
-            out = model(x)
-        loss = F.binary_cross_entropy_with_logits(out.float(), y)
-        opt.zero_grad(set_to_none=True)
-        loss.backward()
-        opt.step()
-        return loss
-
-    for _ in range(args.warmup):
-        step()
-    torch.cuda.synchronize()
-    t = time.perf_counter()
-    for _ in range(args.steps):
-        step()
-    torch.cuda.synchronize()
-    dt = (time.perf_counter() - t) / args.steps
-    print(json.dumps({"baseline": "stock_pytorch_eager_bf16_autocast", "model": args.model,
-                      "batch": args.batch, "ms_per_step": dt * 1e3,
-                      "images_per_sec": args.batch / dt,
-                      "channels_last": not args.no_channels_last}))
+    if args.all:
+        results = []
+        for m in ("densenet121", "vgg16", "mobilenetv2"):
+            for graph in (False, True):
+                try:
+                    r = run(m, args.batch, args.steps, args.warmup, graph, not args.no_channels_last)
+                except Exception as e:  # a stock configuration that cannot be captured is recorded
+                    r = {"model": m, "baseline": "stock_pytorch_%s" % ("hipgraph" if graph else "eager"),
+                         "error": repr(e)[:300], "images_per_sec": 0.0}
+                print(json.dumps(r), flush=True)
+                results.append(r)
+        with open(args.all, "w") as f:
+            json.dump({"note": "in-situ comparison point (BASELINE.md): stock PyTorch-ROCm, MIOpen "
+                               "convolutions, bf16 autocast, channels_last, RMSprop; one MI355X; "
+                               "synthetic 50x50x3, per-GPU batch %d" % args.batch,
+                       "results": results}, f, indent=1)
+        return
+    print(json.dumps(run(args.model, args.batch, args.steps, args.warmup, args.graph,
+                         not args.no_channels_last)))
 
 
 if __name__ == "__main__":

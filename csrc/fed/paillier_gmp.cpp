@@ -219,6 +219,26 @@ py::array_t<int64_t> decrypt(py::bytes p_be, py::bytes q_be, py::array_t<uint8_t
   return out;
 }
 
+// base^exp mod mod (big-endian byte strings): the finite-field Diffie-Hellman key agreement of
+// mask-based secure aggregation (idc_models_amd/fed/keyagree.py) — constant-time mpz_powm_sec
+// for the secret exponent
+py::bytes powm(py::bytes base_be, py::bytes exp_be, py::bytes mod_be) {
+  Mpz b, e, md, r;
+  mpz_from_pybytes(b.v, base_be);
+  mpz_from_pybytes(e.v, exp_be);
+  mpz_from_pybytes(md.v, mod_be);
+  if (mpz_cmp_ui(md.v, 3) < 0 || mpz_even_p(md.v)) throw std::invalid_argument("modulus must be odd and > 2");
+  {
+    py::gil_scoped_release nogil;
+    if (mpz_sgn(e.v) > 0) mpz_powm_sec(r.v, b.v, e.v, md.v);
+    else mpz_set_ui(r.v, 1);
+  }
+  const size_t w = (mpz_sizeinbase(md.v, 2) + 7) / 8;
+  std::string out(w, '\0');
+  to_bytes(r.v, reinterpret_cast<uint8_t*>(&out[0]), w);
+  return py::bytes(out);
+}
+
 }  // namespace
 
 PYBIND11_MODULE(_idc_paillier, m) {
@@ -226,4 +246,5 @@ PYBIND11_MODULE(_idc_paillier, m) {
   m.def("encrypt", &encrypt, py::arg("n"), py::arg("m"), py::arg("threads") = 8);
   m.def("add", &add, py::arg("n"), py::arg("a"), py::arg("b"));
   m.def("decrypt", &decrypt, py::arg("p"), py::arg("q"), py::arg("c"), py::arg("threads") = 8);
+  m.def("powm", &powm, py::arg("base"), py::arg("exp"), py::arg("mod"));
 }

@@ -2,9 +2,12 @@
 //
 // Replaces the reference's per-element Python Paillier encryption (secure_fed_model.py:109-129,
 // 3072-bit modexp per weight on the CPU) with one bandwidth-bound kernel: each element gets
-// K-1 counter-based Philox4x32-10 masks keyed by the unordered client pair and the round, added
-// with opposite signs by the two members of the pair, so the uint32 ring sum over all K clients
-// equals the plain fixed-point sum bit-exactly.
+// K-1 counter-based Philox4x32-10 masks keyed by the pair's Diffie-Hellman-derived key (one key
+// table entry per peer, loaded once per thread into registers) and counted by (round, index),
+// added with opposite signs by the two members of the pair, so the uint32 ring sum over all K
+// clients equals the plain fixed-point sum bit-exactly.  Each protected tensor has its own
+// fixed-point scale (segment table), so small kernels keep their resolution next to large BN
+// variances.
 #include "secagg.h"
 
 namespace idc {
@@ -27,53 +30,86 @@ __device__ __forceinline__ uint32_t philox(uint32_t c0, uint32_t c1, uint32_t c2
   return c0;
 }
 
-__global__ void secagg_mask_kernel(const float* __restrict__ x, uint32_t* __restrict__ out, long long n,
-                                   float scale, float clip, int K, int rank, unsigned long long seed,
-                                   unsigned long long rnd, unsigned long long alive) {
-  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n;
-       i += (long long)gridDim.x * blockDim.x) {
-    float v = x[i] * scale;
+// segment of element i (seg_end ascending, seg_end[nseg-1] == n)
+__device__ __forceinline__ int segment_of(long long i, const long long* seg_end, int nseg) {
+  int lo = 0, hi = nseg - 1;
+  while (lo < hi) {
+    const int mid = (lo + hi) >> 1;
+    if (i < seg_end[mid]) hi = mid;
+    else lo = mid + 1;
+  }
+  return lo;
+}
+
+__global__ __launch_bounds__(256) void secagg_mask_kernel(const float* __restrict__ x, uint32_t* __restrict__ out,
+                                                          long long n, const float* __restrict__ seg_scale,
+                                                          const long long* __restrict__ seg_end, int nseg,
+                                                          float clip, int K, int rank,
+                                                          const uint32_t* __restrict__ keys, unsigned long long rnd,
+                                                          unsigned long long alive) {
+  // a thread owns a contiguous run of elements: its segment search is done once per run
+  const long long per = (n + (long long)gridDim.x * blockDim.x - 1) / ((long long)gridDim.x * blockDim.x);
+  const long long i0 = (blockIdx.x * (long long)blockDim.x + threadIdx.x) * per;
+  if (i0 >= n) return;
+  const long long i1 = i0 + per < n ? i0 + per : n;
+  int s = segment_of(i0, seg_end, nseg);
+  for (long long i = i0; i < i1; ++i) {
+    while (i >= seg_end[s]) ++s;
+    float v = x[i] * seg_scale[s];
     v = fminf(fmaxf(v, -clip), clip);
-    int32_t q = (int32_t)rintf(v);
-    uint32_t acc = (uint32_t)q;
+    uint32_t acc = (uint32_t)(int32_t)rintf(v);
     for (int j = 0; j < K; ++j) {
       if (j == rank || !((alive >> j) & 1ull)) continue;  // dropped clients: re-keyed round
-      int lo = j < rank ? j : rank, hi = j < rank ? rank : j;
-      uint32_t k0 = (uint32_t)seed ^ (uint32_t)(lo * 0x9E3779B1u);
-      uint32_t k1 = (uint32_t)(seed >> 32) ^ (uint32_t)(hi * 0x85EBCA77u);
-      uint32_t m = philox((uint32_t)i, (uint32_t)(i >> 32), (uint32_t)rnd, (uint32_t)(rnd >> 32), k0, k1);
-      acc += (rank == lo) ? m : (0u - m);
+      const uint32_t m = philox((uint32_t)i, (uint32_t)(i >> 32), (uint32_t)rnd, (uint32_t)(rnd >> 32),
+                                keys[2 * j], keys[2 * j + 1]);
+      acc += (rank < j) ? m : (0u - m);
     }
     out[i] = acc;
   }
 }
 
-__global__ void secagg_unmask_kernel(const uint32_t* __restrict__ s, float* __restrict__ out, long long n,
-                                     float inv_scale_div) {
-  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n;
-       i += (long long)gridDim.x * blockDim.x)
-    out[i] = (float)(int32_t)s[i] * inv_scale_div;
+__global__ __launch_bounds__(256) void secagg_unmask_kernel(const uint32_t* __restrict__ s, float* __restrict__ out,
+                                                            long long n, const float* __restrict__ seg_scale,
+                                                            const long long* __restrict__ seg_end, int nseg,
+                                                            float divisor) {
+  const long long per = (n + (long long)gridDim.x * blockDim.x - 1) / ((long long)gridDim.x * blockDim.x);
+  const long long i0 = (blockIdx.x * (long long)blockDim.x + threadIdx.x) * per;
+  if (i0 >= n) return;
+  const long long i1 = i0 + per < n ? i0 + per : n;
+  int g = segment_of(i0, seg_end, nseg);
+  float inv = 1.f / (seg_scale[g] * divisor);
+  for (long long i = i0; i < i1; ++i) {
+    while (i >= seg_end[g]) {
+      ++g;
+      inv = 1.f / (seg_scale[g] * divisor);
+    }
+    out[i] = (float)(int32_t)s[i] * inv;
+  }
 }
 
-hipError_t secagg_quantize_mask(const float* x, uint32_t* out, long long n, float scale, float clip, int K,
-                                int rank, unsigned long long seed, unsigned long long rnd, unsigned long long alive,
-                                hipStream_t st) {
-  if (K > 64) return hipErrorInvalidValue;
+static int grid_for(long long n) {
   long long b = (n + 255) / 256;
-  if (b > 8192) b = 8192;
-  if (b < 1) b = 1;
-  hipLaunchKernelGGL(secagg_mask_kernel, dim3((int)b), dim3(256), 0, st, x, out, n, scale, clip, K, rank, seed,
-                     rnd, alive);
+  if (b > 2048) b = 2048;
+  return b < 1 ? 1 : (int)b;
+}
+
+hipError_t secagg_quantize_mask(const float* x, uint32_t* out, long long n, const float* seg_scale,
+                                const long long* seg_end, int nseg, float clip, int K, int rank,
+                                const uint32_t* keys, unsigned long long rnd, unsigned long long alive,
+                                hipStream_t st) {
+  if (K > 64 || nseg < 1 || (K > 1 && keys == nullptr)) return hipErrorInvalidValue;
+  if (n == 0) return hipSuccess;
+  hipLaunchKernelGGL(secagg_mask_kernel, dim3(grid_for(n)), dim3(256), 0, st, x, out, n, seg_scale, seg_end, nseg,
+                     clip, K, rank, keys, rnd, alive);
   return hipGetLastError();
 }
 
-hipError_t secagg_dequantize(const uint32_t* sum, float* out, long long n, float scale, int K, float divisor,
-                             hipStream_t st) {
-  long long b = (n + 255) / 256;
-  if (b > 8192) b = 8192;
-  if (b < 1) b = 1;
-  hipLaunchKernelGGL(secagg_unmask_kernel, dim3((int)b), dim3(256), 0, st, sum, out, n,
-                     1.f / (scale * divisor));
+hipError_t secagg_dequantize(const uint32_t* sum, float* out, long long n, const float* seg_scale,
+                             const long long* seg_end, int nseg, float divisor, hipStream_t st) {
+  if (nseg < 1) return hipErrorInvalidValue;
+  if (n == 0) return hipSuccess;
+  hipLaunchKernelGGL(secagg_unmask_kernel, dim3(grid_for(n)), dim3(256), 0, st, sum, out, n, seg_scale, seg_end,
+                     nseg, divisor);
   return hipGetLastError();
 }
 

@@ -98,6 +98,7 @@ class Plan {
     clear_graphs();
     if (fork_) hipEventDestroy(fork_);
     if (join_) hipEventDestroy(join_);
+    if (mark_) hipEventDestroy(mark_);
     if (side_) hipStreamDestroy(side_);
   }
 
@@ -131,10 +132,21 @@ class Plan {
 
   int size() const { return (int)ops_.size(); }
 
-  void run(int begin, int end, uintptr_t stream) {
+  // join=false (direct runs only): the side lane is NOT joined back at the end of the range; a
+  // consumer that needs the range's side-lane work (a gradient bucket's all-reduce) waits for it
+  // with wait_side() on its own stream, and the main lane keeps going.  The next joined range
+  // (or capture) joins everything.
+  void run(int begin, int end, uintptr_t stream, bool join) {
     hipStream_t st = reinterpret_cast<hipStream_t>(stream);
     if (end < 0 || end > (int)ops_.size()) end = (int)ops_.size();
-    issue(begin, end, st);
+    issue(begin, end, st, join);
+  }
+
+  // make `stream` wait for every side-lane op issued so far (event record on the side lane)
+  void wait_side(uintptr_t stream) {
+    if (!side_) return;
+    check(hipEventRecord(mark_, side_), "hipEventRecord(mark)");
+    check(hipStreamWaitEvent(reinterpret_cast<hipStream_t>(stream), mark_, 0), "hipStreamWaitEvent(mark)");
   }
 
   int lane(int idx) const { return ops_.at(idx).lane; }
@@ -195,6 +207,7 @@ class Plan {
     check(hipStreamCreateWithPriority(&side_, hipStreamNonBlocking, prio), "hipStreamCreate(side)");
     check(hipEventCreateWithFlags(&fork_, hipEventDisableTiming), "hipEventCreate(fork)");
     check(hipEventCreateWithFlags(&join_, hipEventDisableTiming), "hipEventCreate(join)");
+    check(hipEventCreateWithFlags(&mark_, hipEventDisableTiming), "hipEventCreate(mark)");
   }
 
   // issue ops[begin:end): lane-0 ops on `st`; lane-1 ops are queued and issued on the side
@@ -203,7 +216,7 @@ class Plan {
   // precede the fork, and the lowering guarantees no later main op overwrites a side op's
   // inputs, so deferring is safe) — and one join at the end.  Batching keeps the host API calls
   // per step low: with direct (non-graph) issue the backward is otherwise host-bound.
-  void issue(int begin, int end, hipStream_t st) {
+  void issue(int begin, int end, hipStream_t st, bool join = true) {
     bool side_used = false;
     std::vector<int> pending;
     int main_since = 0;
@@ -227,9 +240,12 @@ class Plan {
       }
     }
     flush();
-    if (side_used) {
+    if ((side_used || side_open_) && join) {
       check(hipEventRecord(join_, side_), "hipEventRecord(join)");
       check(hipStreamWaitEvent(st, join_, 0), "hipStreamWaitEvent(join)");
+      side_open_ = false;
+    } else if (side_used) {
+      side_open_ = true;
     }
   }
 
@@ -317,7 +333,8 @@ class Plan {
   std::vector<Op> ops_;
   hipStream_t side_ = nullptr;
   int side_flush_ = 1;
-  hipEvent_t fork_ = nullptr, join_ = nullptr;
+  hipEvent_t fork_ = nullptr, join_ = nullptr, mark_ = nullptr;
+  bool side_open_ = false;  // side-lane work issued by a join=false run, not yet joined
   std::vector<hipGraph_t> graphs_;
   std::vector<hipGraphExec_t> execs_;
 };
@@ -385,18 +402,21 @@ bool py_halo_ok(py::bytes payload) {
 }
 int py_pick_splits(int M, int K, int Cout) { return wgrad_pick_splits(M, K, Cout); }
 
-void py_secagg_mask(uintptr_t x, uintptr_t out, long long n, float scale, float clip, int nclients,
-                    int rank, unsigned long long seed, unsigned long long round_, unsigned long long alive,
-                    uintptr_t stream) {
-  check(secagg_quantize_mask(reinterpret_cast<const float*>(x), reinterpret_cast<uint32_t*>(out), n, scale, clip,
-                             nclients, rank, seed, round_, alive, reinterpret_cast<hipStream_t>(stream)),
+void py_secagg_mask(uintptr_t x, uintptr_t out, long long n, uintptr_t seg_scale, uintptr_t seg_end, int nseg,
+                    float clip, int nclients, int rank, uintptr_t keys, unsigned long long round_,
+                    unsigned long long alive, uintptr_t stream) {
+  check(secagg_quantize_mask(reinterpret_cast<const float*>(x), reinterpret_cast<uint32_t*>(out), n,
+                             reinterpret_cast<const float*>(seg_scale), reinterpret_cast<const long long*>(seg_end),
+                             nseg, clip, nclients, rank, reinterpret_cast<const uint32_t*>(keys), round_, alive,
+                             reinterpret_cast<hipStream_t>(stream)),
         "secagg_quantize_mask");
 }
 
-void py_secagg_unmask(uintptr_t sum, uintptr_t out, long long n, float scale, int nclients, float divisor,
-                      uintptr_t stream) {
-  check(secagg_dequantize(reinterpret_cast<const uint32_t*>(sum), reinterpret_cast<float*>(out), n, scale,
-                          nclients, divisor, reinterpret_cast<hipStream_t>(stream)),
+void py_secagg_unmask(uintptr_t sum, uintptr_t out, long long n, uintptr_t seg_scale, uintptr_t seg_end, int nseg,
+                      float divisor, uintptr_t stream) {
+  check(secagg_dequantize(reinterpret_cast<const uint32_t*>(sum), reinterpret_cast<float*>(out), n,
+                          reinterpret_cast<const float*>(seg_scale), reinterpret_cast<const long long*>(seg_end),
+                          nseg, divisor, reinterpret_cast<hipStream_t>(stream)),
         "secagg_dequantize");
 }
 
@@ -423,7 +443,8 @@ PYBIND11_MODULE(_idc_native, m) {
       .def("kind", &Plan::kind)
       .def("payload", &Plan::payload)
       .def("size", &Plan::size)
-      .def("run", &Plan::run)
+      .def("run", &Plan::run, py::arg("begin"), py::arg("end"), py::arg("stream"), py::arg("join") = true)
+      .def("wait_side", &Plan::wait_side)
       .def("capture", &Plan::capture)
       .def("launch", &Plan::launch)
       .def("clear_graphs", &Plan::clear_graphs)

@@ -44,6 +44,9 @@ def main(argv=None):
     f.add_argument("--config")
     f.add_argument("--synthetic", action="store_true")
     f.add_argument("--arch", default=None)
+    f.add_argument("--secure-agg", default=None, choices=[None, "mask"],
+                   help="masked aggregation of the weighted deltas (secure FedAvg)")
+    f.add_argument("--no-resume", action="store_true", help="ignore {path}/fed_state/state.pt")
     s = sub.add_parser("secure", help="secure federated learning (secure_fed_model.py)")
     s.add_argument("path")
     s.add_argument("rounds", type=int)
@@ -82,6 +85,10 @@ def main(argv=None):
             kw["synthetic"] = True
         if a.arch:
             kw["arch"] = a.arch
+        if a.secure_agg:
+            kw["secure_aggregation"] = a.secure_agg
+        if a.no_resume:
+            kw["resume"] = False
         if "input_shape" in kw:
             kw["input_shape"] = tuple(kw["input_shape"])
         run_fedavg(FedConfig(**kw))

@@ -125,6 +125,7 @@ class BatchedDataset:
         self._epoch = 0
         self.device = None       # prefetch_to(): batches are delivered on this device
         self._prefetcher = None
+        self._prefetcher_bs = None
 
     def prefetch_to(self, device) -> "BatchedDataset":
         """Deliver batches as ``device`` tensors through the native pinned-memory prefetcher
@@ -159,20 +160,30 @@ class BatchedDataset:
         self._epoch += 1
         return np.concatenate(parts) if len(parts) > 1 else parts[0]
 
+    def shard(self, rank: int, world: int) -> "RankShard":
+        """Data-parallel view: every rank draws the SAME global batch order (same seed and
+        epoch) and takes its own contiguous ``batch_size / world`` rows of each global batch in
+        INDEX space, so a rank only gathers and stages its own images (no replicated global batch
+        sliced after the copy).  A trailing partial global batch is dropped under data
+        parallelism (static per-rank shapes; its rows would not split evenly)."""
+        return RankShard(self, rank, world)
+
     def __iter__(self) -> Iterator[Tuple[torch.Tensor, torch.Tensor]]:
-        order = self.epoch_order()
-        bs = self.batch_size
+        yield from self._iter_order(self.epoch_order(), self.batch_size, self.drop_remainder)
+
+    def _iter_order(self, order: np.ndarray, bs: int, drop_remainder: bool):
         n = order.shape[0]
-        stop = n - (n % bs) if self.drop_remainder else n
+        stop = n - (n % bs) if drop_remainder else n
         x, y = self.ds.x, self.ds.y
         on_dev = isinstance(x, torch.Tensor) and x.is_cuda
         if isinstance(x, np.ndarray) and isinstance(y, np.ndarray) and stop > 0:
             from . import native
             if native.available():
-                if self._prefetcher is None:
+                if self._prefetcher is None or self._prefetcher_bs != bs:
                     self._prefetcher = native.PrefetchIterator(x, y, bs, device=self.device)
-                yield from self._prefetcher.epoch(order[:stop] if self.drop_remainder else order,
-                                                  self.drop_remainder)
+                    self._prefetcher_bs = bs
+                yield from self._prefetcher.epoch(order[:stop] if drop_remainder else order,
+                                                  drop_remainder)
                 return
         for s in range(0, stop, bs):
             idx = order[s:s + bs]
@@ -183,6 +194,31 @@ class BatchedDataset:
                 xb = x[idx] if isinstance(x, np.ndarray) else x[torch.as_tensor(idx)]
                 yb = y[idx] if isinstance(y, np.ndarray) else y[torch.as_tensor(idx)]
                 yield torch.as_tensor(xb), torch.as_tensor(yb)
+
+
+class RankShard:
+    """``BatchedDataset.shard``: rank ``rank``'s rows of every global batch."""
+
+    def __init__(self, data: BatchedDataset, rank: int, world: int):
+        if data.batch_size % world:
+            raise ValueError(f"global batch {data.batch_size} does not split over {world} replicas")
+        self.data, self.rank, self.world = data, rank, world
+        self.per = data.batch_size // world
+
+    def __len__(self):
+        return len(self.data.ds) * self.data.repeat // self.data.batch_size
+
+    def prefetch_to(self, device):
+        self.data.prefetch_to(device)
+        return self
+
+    def rank_order(self, order: np.ndarray) -> np.ndarray:
+        gb = self.data.batch_size
+        nb = order.shape[0] // gb
+        return order[:nb * gb].reshape(nb, gb)[:, self.rank * self.per:(self.rank + 1) * self.per].reshape(-1)
+
+    def __iter__(self):
+        yield from self.data._iter_order(self.rank_order(self.data.epoch_order()), self.per, True)
 
 
 def to_float_images(x: torch.Tensor) -> torch.Tensor:

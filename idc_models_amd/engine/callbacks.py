@@ -22,6 +22,7 @@ class Callback:
     def on_epoch_begin(self, epoch, logs=None): ...
     def on_epoch_end(self, epoch, logs=None): ...
     def on_train_batch_end(self, step, logs=None): ...
+    def on_epoch_train_end(self, epoch, logs=None): ...  # training batches done, before validation
 
 
 class History(Callback):
@@ -61,6 +62,45 @@ class ModelCheckpoint(Callback):
             self.model.save_checkpoint(path)
         if self.verbose:
             print(f"\nEpoch {epoch + 1:05d}: saving model to {path}")
+
+
+class ThroughputMeter(Callback):
+    """Training throughput of ``fit`` (the reference times whole fits with ``Timer``,
+    ``dist_model_tf_vgg.py:135-138``; this separates the training epochs from validation):
+    device-synchronised wall time of each epoch's training batches and images/sec of this rank
+    (``images`` counts the rows this process trained on)."""
+
+    def __init__(self):
+        self.epoch_seconds: List[float] = []
+        self.epoch_images: List[int] = []
+        self._t0 = 0.0
+        self._n = 0
+
+    @staticmethod
+    def _sync():
+        import torch
+        if torch.cuda.is_available() and torch.cuda.is_initialized():
+            torch.cuda.synchronize()
+
+    def on_epoch_begin(self, epoch, logs=None):
+        self._sync()
+        self._t0 = time.perf_counter()
+        self._n = 0
+
+    def on_train_batch_end(self, step, logs=None):
+        self._n += int((logs or {}).get("size", 0))
+
+    def on_epoch_train_end(self, epoch, logs=None):
+        self._sync()
+        self.epoch_seconds.append(time.perf_counter() - self._t0)
+        self.epoch_images.append(self._n)
+
+    def images_per_sec(self, skip_first: bool = True) -> float:
+        """Images/sec of this rank over the recorded epochs (the first one, which may build and
+        tune programs, excluded when there are others)."""
+        k = 1 if (skip_first and len(self.epoch_seconds) > 1) else 0
+        t = sum(self.epoch_seconds[k:])
+        return sum(self.epoch_images[k:]) / t if t > 0 else 0.0
 
 
 class JSONLLogger(Callback):

@@ -218,7 +218,7 @@ class Model:
             for m in ms[1:]:
                 m.update(logits, yd)
             if callbacks is not None:
-                callbacks.on_train_batch_end(step)
+                callbacks.on_train_batch_end(step, {"size": int(logits.shape[0])})
         self.strategy.reduce_metrics(ms)
         return {m.name: m.result() for m in ms}
 
@@ -232,6 +232,7 @@ class Model:
         for epoch in range(initial_epoch, epochs):
             cbs.on_epoch_begin(epoch)
             logs = self._run_epoch(x, steps_per_epoch, True, cbs)
+            cbs.on_epoch_train_end(epoch, logs)
             self.strategy.sync_bn_stats(self)
             if validation_data is not None:
                 vlogs = self.evaluate(validation_data, steps=validation_steps, verbose=0,
@@ -291,12 +292,15 @@ class Model:
             self.impl.sync_to_module()
         save_weights(self.net, path)
 
-    def load_weights(self, path: str) -> None:
+    def load_weights(self, path: str, strict: bool = False) -> List[str]:
+        """Load Keras-layout weights by name; returns the model weights the file did not hold
+        (``strict=True`` raises instead).  Under data parallelism rank 0's values win."""
         from ..ckpt import load_weights
-        load_weights(self.net, path)
+        missing = load_weights(self.net, path, strict=strict)
         self.strategy.broadcast_module(self.net)
         if self.impl is not None:
             self.impl.sync_from_module()
+        return missing
 
     def save_checkpoint(self, path: str, extra: Optional[dict] = None) -> None:
         from ..ckpt import save_checkpoint

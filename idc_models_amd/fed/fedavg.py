@@ -16,6 +16,13 @@ MI355X mapping: clients are assigned round-robin to ranks (one
 each rank trains its clients back to back on ONE compiled model (the client's weights/optimizer
 state are swapped into the flat arena — a device memcpy, no re-lowering); the per-rank partial
 ``[sum n_k*delta_k | sum n_k | metric sums]`` is combined with ONE packed all-reduce over RCCL.
+
+``secure_aggregation="mask"`` (north-star config #5, secure FedAvg): each client's example-weighted
+delta ``n_k * delta_k`` is quantised (one fixed-point scale per tensor) and masked with pairwise
+Diffie-Hellman-keyed Philox masks (``secagg.MaskedAggregator``); the masks cancel in the int32
+all-reduce, so the server learns only ``sum_k n_k * delta_k`` (example counts and metric sums stay
+in the clear, as TFF reports them).  A client whose update is non-finite still takes part in the
+masking with a zero vector and weight 0, so its peers' masks cancel.
 """
 from __future__ import annotations
 
@@ -55,6 +62,49 @@ def state_with_new_model_weights(state: ServerState, trainable_weights, non_trai
     return ServerState(ModelWeights(tw, nw), state.round_num, state.optimizer_state)
 
 
+def broadcast_server_state(state: ServerState, src: int = 0) -> ServerState:
+    """Make every rank's server state rank ``src``'s (one process per GPU: the server model must
+    be identical everywhere before clients start from it)."""
+    if comm.world_size() > 1:
+        for t in list(state.model.trainable) + list(state.model.non_trainable):
+            comm.broadcast_(t, src)
+        rn = torch.tensor([state.round_num], dtype=torch.int64,
+                          device=state.model.trainable[0].device if state.model.trainable else "cpu")
+        comm.broadcast_(rn, src)
+        state.round_num = int(rn.item())
+    return state
+
+
+def save_server_state(state: ServerState, path: str, extra: Optional[dict] = None) -> None:
+    """Federated resume point (SURVEY §5 checkpoint/resume): server model, round counter, server
+    optimizer state and the host RNG; written to a temporary file and renamed into place."""
+    import os
+    d = os.path.dirname(path)
+    if d:
+        os.makedirs(d, exist_ok=True)
+    blob = {"trainable": [t.detach().cpu() for t in state.model.trainable],
+            "non_trainable": [t.detach().cpu() for t in state.model.non_trainable],
+            "round_num": int(state.round_num),
+            "optimizer_state": {k: v.detach().cpu() for k, v in state.optimizer_state.items()
+                                if isinstance(v, torch.Tensor)},
+            "rng_cpu": torch.get_rng_state(),
+            "extra": {k: v for k, v in (extra or {}).items() if isinstance(v, (int, float, str, bool))}}
+    tmp = f"{path}.tmp"
+    torch.save(blob, tmp)
+    os.replace(tmp, path)
+
+
+def load_server_state(path: str, device=None) -> ServerState:
+    blob = torch.load(path, map_location="cpu", weights_only=True)
+    dev = torch.device(device) if device is not None else torch.device("cpu")
+    state = ServerState(ModelWeights([t.to(dev) for t in blob["trainable"]],
+                                     [t.to(dev) for t in blob["non_trainable"]]),
+                        int(blob["round_num"]), {k: v.to(dev) for k, v in blob.get("optimizer_state", {}).items()})
+    if "rng_cpu" in blob:
+        torch.set_rng_state(blob["rng_cpu"])
+    return state
+
+
 def assign_clients(num_clients: int, rank: int, world: int) -> List[int]:
     """ClientScheduler: client k -> rank k % world (8 train clients <-> 8 GPUs)."""
     return [k for k in range(num_clients) if k % world == rank]
@@ -63,7 +113,8 @@ def assign_clients(num_clients: int, rank: int, world: int) -> List[int]:
 class FedAvgProcess:
     def __init__(self, model_fn: Callable, client_optimizer_fn: Callable,
                  server_optimizer_fn: Optional[Callable] = None, average_bn_stats: bool = False,
-                 local_epochs: int = 1, loss="binary_crossentropy", metrics=("binary_accuracy",)):
+                 local_epochs: int = 1, loss="binary_crossentropy", metrics=("binary_accuracy",),
+                 secure_aggregation: Optional[str] = None):
         self.model_fn = model_fn
         self.client_optimizer_fn = client_optimizer_fn
         self.server_lr = 1.0
@@ -75,6 +126,10 @@ class FedAvgProcess:
         self.loss = loss
         self.metric_names = list(metrics)
         self._worker = None
+        if secure_aggregation not in (None, "none", "mask"):
+            raise ValueError(f"unknown secure aggregation mode {secure_aggregation!r}")
+        self.secure = secure_aggregation == "mask"
+        self._agg = None
 
     # -------------------------------------------------------------- worker model
     def worker(self):
@@ -92,7 +147,8 @@ class FedAvgProcess:
     def initialize(self) -> ServerState:
         m = self.worker()
         tr, ntr = self._tensors(m)
-        return ServerState(ModelWeights([t.detach().clone() for t in tr], [t.detach().clone() for t in ntr]))
+        state = ServerState(ModelWeights([t.detach().clone() for t in tr], [t.detach().clone() for t in ntr]))
+        return broadcast_server_state(state)
 
     def _load(self, m, weights: ModelWeights):
         _load_into(m, weights)
@@ -103,10 +159,12 @@ class FedAvgProcess:
         all) — absent clients simply carry no weight, as in TFF's sampled rounds."""
         m = self.worker()
         rank, world = comm.rank(), comm.world_size()
-        mine = assign_clients(len(federated_train_data), rank, world)
-        if participating is not None:
-            keep = set(int(k) for k in participating)
-            mine = [k for k in mine if k in keep]
+        K = len(federated_train_data)
+        mine = assign_clients(K, rank, world)
+        parts = sorted(int(k) for k in participating) if participating is not None else list(range(K))
+        keep = set(parts)
+        mine = [k for k in mine if k in keep]
+        masked = {}  # secure mode: client -> n_k * [delta | bn stats]
         dev = state.model.trainable[0].device if state.model.trainable else m.device
         flat_server = torch.cat([w.reshape(-1) for w in state.model.trainable]).to(m.device)
         delta_sum = torch.zeros_like(flat_server)
@@ -125,23 +183,43 @@ class FedAvgProcess:
             tr, ntr = self._tensors(m)
             flat = torch.cat([t.detach().reshape(-1) for t in tr])
             delta = flat - flat_server
-            if not bool(torch.isfinite(delta).all()):
+            finite = bool(torch.isfinite(delta).all())
+            if self.secure:
+                v = [n_k * delta] + ([n_k * torch.cat([t.detach().reshape(-1) for t in ntr])]
+                                     if ntr_sum is not None else [])
+                masked[k] = torch.cat(v) if finite else torch.zeros(sum(x.numel() for x in v), device=m.device)
+            if not finite:
                 continue  # TFF: non-finite client update gets weight 0
-            delta_sum += n_k * delta
-            if ntr_sum is not None:
-                ntr_sum += n_k * torch.cat([t.detach().reshape(-1) for t in ntr])
+            if not self.secure:
+                delta_sum += n_k * delta
+                if ntr_sum is not None:
+                    ntr_sum += n_k * torch.cat([t.detach().reshape(-1) for t in ntr])
             n_sum += n_k
             logs = {k2: v[-1] for k2, v in h.history.items()}
             met[0] += n_k * logs.get("loss", 0.0)
             for i, name in enumerate(self.metric_names):
                 met[1 + i] += n_k * logs.get(name if name in logs else "accuracy", 0.0)
-        # one packed all-reduce of [delta sums | bn sums | n | metrics]
-        parts = [delta_sum, n_sum, met] + ([ntr_sum] if ntr_sum is not None else [])
+        if self.secure:
+            # the weighted deltas cross ranks only masked; counts and metrics in the clear
+            if self._agg is None or self._agg.K != K:
+                from .secagg import MaskedAggregator
+                self._agg = MaskedAggregator(K, assign_clients(K, rank, world), m.device)
+            sizes = [w.numel() for w in state.model.trainable]
+            if ntr_sum is not None:
+                sizes += [w.numel() for w in state.model.non_trainable]
+            s = self._agg.masked_sum(masked, sizes, state.round_num, parts)
+            delta_sum.copy_(s[:delta_sum.numel()])
+            if ntr_sum is not None:
+                ntr_sum.copy_(s[delta_sum.numel():])
+            clear = [n_sum, met]
+        else:
+            clear = [delta_sum, n_sum, met] + ([ntr_sum] if ntr_sum is not None else [])
+        # one packed all-reduce of [delta sums | bn sums | n | metrics] (clear parts)
         if world > 1:
-            flatp = torch.cat([p.reshape(-1).float() for p in parts])
+            flatp = torch.cat([p.reshape(-1).float() for p in clear])
             comm.all_reduce_(flatp)
             off = 0
-            for p in parts:  # copy back IN PLACE (n_sum/met are float64 accumulators)
+            for p in clear:  # copy back IN PLACE (n_sum/met are float64 accumulators)
                 p.copy_(flatp[off:off + p.numel()].view(p.shape).to(p.dtype))
                 off += p.numel()
         total = float(n_sum.item())

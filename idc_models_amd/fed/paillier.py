@@ -149,6 +149,14 @@ def decrypt_vector(priv: PrivateKey, cts: List[int], scale: float, divisor: floa
     return [priv.decrypt(c) / scale / divisor for c in cts]
 
 
+def native_powm(base: int, exp: int, mod: int) -> int:
+    """base^exp mod mod on GMP (the Diffie-Hellman key agreement of fed/keyagree.py)."""
+    nat = _native()
+    if nat is None or not hasattr(nat, "powm"):
+        raise ImportError("native GMP module not built")
+    return int.from_bytes(nat.powm(_be(base % mod) or b"\0", _be(exp) or b"\0", _be(mod)), "big")
+
+
 def sum_ciphertexts(pub: PublicKey, vectors: List[List[int]]) -> List[int]:
     out = list(vectors[0])
     for v in vectors[1:]:

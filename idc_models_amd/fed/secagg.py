@@ -4,12 +4,15 @@ Reference: ``secure_fed_model.py:79,109-168`` — one global Paillier keypair, e
 the first ``int(n_tensors*percent)`` weight tensors element-wise, the server averages ciphertexts
 homomorphically, every client decrypts (quirk Q13: every client can decrypt everything).
 
-Here: each client quantises its weights to fixed point (int32 two's complement),
-adds pairwise Philox masks ``+m_ij`` / ``-m_ij`` for every other client, and the masked vectors
-are summed with ONE integer all-reduce (RCCL over xGMI; uint32/int32 sums wrap mod 2^32).  The
-masks cancel exactly, so the result equals the plain fixed-point sum BIT-EXACTLY, while any single
-masked vector is uniformly random.  ``percent`` keeps its meaning: the fraction of weight tensors
-that are protected (the rest are averaged in the clear, as the reference does).
+Here: each client quantises its weights to fixed point (int32 two's complement,
+one power-of-two scale per protected tensor), adds pairwise Philox masks ``+m_ij`` / ``-m_ij`` for
+every other participant, and the masked vectors are summed with ONE integer all-reduce (RCCL over
+xGMI; int32 sums wrap mod 2^32).  The masks cancel exactly, so the result equals the plain
+fixed-point sum BIT-EXACTLY, while any single masked vector is uniformly random.  The pair keys come
+from a Diffie-Hellman agreement between the two clients (``keyagree.py``): the aggregator, which
+sees only public keys and masked vectors, cannot regenerate any mask.  ``percent`` keeps its
+meaning: the fraction of weight tensors that are protected (the rest are averaged in the clear,
+as the reference does).
 
 GPU: native kernel (``csrc/kernels/secagg.hip``).  CPU: the identical Philox in numpy, so both
 paths produce the same bits.
@@ -41,15 +44,13 @@ def _philox_np(c0, c1, c2, c3, k0, k1):
     return c0.astype(np.uint32)
 
 
-def _pair_keys(seed: int, lo: int, hi: int):
-    k0 = (seed & MASK32) ^ ((lo * 0x9E3779B1) & MASK32)
-    k1 = ((seed >> 32) & MASK32) ^ ((hi * 0x85EBCA77) & MASK32)
-    return k0, k1
+def segment_ends(sizes) -> np.ndarray:
+    """Exclusive end offsets of consecutive segments (one per protected tensor)."""
+    return np.cumsum(np.asarray(list(sizes), dtype=np.int64)).astype(np.int64)
 
 
-def _quantize(x: torch.Tensor, scale: float, clip: float) -> torch.Tensor:
-    v = torch.clamp(x.float() * scale, -clip, clip)
-    return torch.round(v).to(torch.int32)
+def _seg_index(n: int, seg_end: np.ndarray) -> np.ndarray:
+    return np.searchsorted(seg_end, np.arange(n, dtype=np.int64), side="right")
 
 
 def default_clip(nclients: int) -> float:
@@ -66,27 +67,49 @@ def _alive_mask(nclients: int, participants) -> int:
     return m
 
 
-def mask_quantize(x: torch.Tensor, scale: float, nclients: int, rank: int, seed: int, round_: int,
-                  clip: float = None, participants=None) -> torch.Tensor:
-    """Fixed-point quantise ``x`` and add this client's pairwise masks -> int32 tensor.
+def _key_table(nclients: int, keys) -> np.ndarray:
+    t = np.zeros(2 * max(nclients, 1), dtype=np.uint32)
+    for j, (k0, k1) in (keys or {}).items():
+        t[2 * int(j)], t[2 * int(j) + 1] = k0 & MASK32, k1 & MASK32
+    return t
 
-    ``participants``: the clients taking part in this round (default: all).  Masks are only
-    exchanged between participants, so when a client drops out before masking the round is
-    re-keyed among the survivors and their masks still cancel exactly."""
+
+def mask_quantize(x: torch.Tensor, scales, seg_end, nclients: int, rank: int, keys, round_: int,
+                  clip: float = None, participants=None) -> torch.Tensor:
+    """Fixed-point quantise ``x`` (segment s scaled by ``scales[s]``) and add this client's
+    pairwise masks -> int32 tensor.  ``keys``: {peer client -> (k0, k1)} pair keys of this round
+    (``keyagree.ClientKeys.round_keys``).  ``participants``: the clients taking part (default all);
+    masks are only exchanged between participants, so a round re-keyed after a dropout still
+    cancels exactly."""
     if nclients > 64:
         raise ValueError("secure aggregation supports at most 64 clients per round")
     clip = default_clip(nclients) if clip is None else clip
     alive = _alive_mask(nclients, participants)
+    for j in range(nclients):
+        if j != rank and (alive >> j) & 1 and j not in (keys or {}):
+            raise ValueError(f"no pair key with participant {j}")
     x = x.reshape(-1).contiguous().float()
     n = x.numel()
+    scales = np.asarray(scales, dtype=np.float32)
+    seg_end = np.asarray(seg_end, dtype=np.int64)
+    if n and int(seg_end[-1]) != n:
+        raise ValueError("segments do not cover the vector")
+    table = _key_table(nclients, keys)
     if x.is_cuda:
         from ..ops import _native as nat
-        out = torch.empty(n, dtype=torch.int32, device=x.device)
-        nat.require().secagg_mask(x.data_ptr(), out.data_ptr(), n, float(scale), float(clip), int(nclients),
-                                  int(rank), int(seed) & ((1 << 64) - 1), int(round_), alive,
+        dev = x.device
+        out = torch.empty(n, dtype=torch.int32, device=dev)
+        sc = torch.from_numpy(scales).to(dev)
+        se = torch.from_numpy(seg_end).to(dev)
+        kt = torch.from_numpy(table.view(np.int32)).to(dev)
+        nat.require().secagg_mask(x.data_ptr(), out.data_ptr(), n, sc.data_ptr(), se.data_ptr(), len(seg_end),
+                                  float(clip), int(nclients), int(rank), kt.data_ptr(), int(round_), alive,
                                   nat.stream_handle())
+        torch.cuda.current_stream().synchronize()  # the small tables above are freed on return
         return out
-    q = _quantize(x, scale, clip).numpy().view(np.uint32).astype(np.uint64)
+    sidx = _seg_index(n, seg_end)
+    v = torch.clamp(x * torch.from_numpy(scales[sidx]), -clip, clip)
+    q = torch.round(v).to(torch.int32).numpy().view(np.uint32).astype(np.uint64)
     idx = np.arange(n, dtype=np.uint64)
     c0 = idx & np.uint64(MASK32)
     c1 = idx >> np.uint64(32)
@@ -94,31 +117,109 @@ def mask_quantize(x: torch.Tensor, scale: float, nclients: int, rank: int, seed:
     for j in range(nclients):
         if j == rank or not (alive >> j) & 1:
             continue
-        lo, hi = min(j, rank), max(j, rank)
-        k0, k1 = _pair_keys(int(seed), lo, hi)
-        m = _philox_np(c0, c1, round_ & MASK32, (round_ >> 32) & MASK32, k0, k1).astype(np.uint64)
-        acc = (acc + m) if rank == lo else (acc + (np.uint64(1 << 32) - m))
+        m = _philox_np(c0, c1, round_ & MASK32, (round_ >> 32) & MASK32, int(table[2 * j]),
+                       int(table[2 * j + 1])).astype(np.uint64)
+        acc = (acc + m) if rank < j else (acc + (np.uint64(1 << 32) - m))
         acc &= np.uint64(MASK32)
     return torch.from_numpy(acc.astype(np.uint32).view(np.int32).copy())
 
 
-def unmask_mean(total: torch.Tensor, scale: float, nclients: int, divisor: float) -> torch.Tensor:
-    """Masked int32 SUM over all clients -> float mean (sum / divisor)."""
+def unmask(total: torch.Tensor, scales, seg_end, divisor: float = 1.0) -> torch.Tensor:
+    """Masked int32 SUM over all participants -> float (sum / divisor), per-segment scale."""
     total = total.reshape(-1).contiguous()
     if total.dtype != torch.int32:
         total = total.view(torch.int32) if total.element_size() == 4 else total.to(torch.int32)
+    scales = np.asarray(scales, dtype=np.float32)
+    seg_end = np.asarray(seg_end, dtype=np.int64)
+    n = total.numel()
     if total.is_cuda:
         from ..ops import _native as nat
-        out = torch.empty(total.numel(), dtype=torch.float32, device=total.device)
-        nat.require().secagg_unmask(total.data_ptr(), out.data_ptr(), total.numel(), float(scale), int(nclients),
-                                    float(divisor), nat.stream_handle())
+        dev = total.device
+        out = torch.empty(n, dtype=torch.float32, device=dev)
+        sc = torch.from_numpy(scales).to(dev)
+        se = torch.from_numpy(seg_end).to(dev)
+        nat.require().secagg_unmask(total.data_ptr(), out.data_ptr(), n, sc.data_ptr(), se.data_ptr(),
+                                    len(seg_end), float(divisor), nat.stream_handle())
+        torch.cuda.current_stream().synchronize()
         return out
-    return total.float() / (scale * divisor)
+    sidx = _seg_index(n, seg_end)
+    return total.float() / (torch.from_numpy(scales[sidx]) * divisor)
 
 
-def choose_scale(max_abs: float, nclients: int, headroom: float = 2.0) -> float:
-    """Largest power-of-two scale with K * max|x| * scale < 2^31 (with headroom)."""
-    if max_abs <= 0:
-        return float(2 ** 16)
-    s = (2 ** 31 - 1) / (nclients * max_abs * headroom)
-    return float(2 ** int(np.floor(np.log2(max(s, 1.0)))))
+def choose_scales(max_abs, nclients: int, headroom: float = 2.0) -> np.ndarray:
+    """Per segment: the largest power-of-two scale with K * max|x| * scale < 2^31 (with headroom),
+    so each protected tensor keeps the resolution its own range allows."""
+    m = np.asarray(max_abs, dtype=np.float64).reshape(-1)
+    out = np.empty(m.shape, dtype=np.float32)
+    for i, v in enumerate(m):
+        if not np.isfinite(v):
+            raise ValueError("non-finite value in a protected tensor")
+        if v <= 0:
+            out[i] = 2.0 ** 16
+            continue
+        s = (2 ** 31 - 1) / (nclients * v * headroom)
+        out[i] = 2.0 ** int(np.floor(np.log2(max(s, 1.0))))
+    return out
+
+
+class MaskedAggregator:
+    """Secure SUM over K clients spread over the ranks (one process per GPU).
+
+    Each client owned by this rank holds a Diffie-Hellman key pair (``keyagree.ClientKeys``); the
+    public values are exchanged once (the only thing any party learns about another's keys).
+    ``masked_sum`` quantises every local client's vector with per-segment scales agreed through a
+    MAX all-reduce of the segment ranges, masks it with its pair keys of the round, adds the local
+    clients' masked vectors, and combines the ranks with ONE int32 SUM all-reduce — the only
+    protected data that crosses a process boundary is masked."""
+
+    def __init__(self, num_clients: int, my_clients, device):
+        from ..parallel import comm
+        from .keyagree import NBYTES, ClientKeys
+        self.K = int(num_clients)
+        self.device = torch.device(device)
+        self.keys = {int(k): ClientKeys(int(k)) for k in my_clients}
+        pub = torch.zeros(self.K, NBYTES, dtype=torch.int64)
+        for k, ck in self.keys.items():
+            pub[k] = torch.tensor(list(ck.public.to_bytes(NBYTES, "big")), dtype=torch.int64)
+        if comm.world_size() > 1:
+            pub = pub.to(self.device)
+            comm.all_reduce_(pub)  # every client's row is filled by exactly one rank
+            pub = pub.cpu()
+        self.publics = {k: int.from_bytes(bytes(pub[k].to(torch.uint8).tolist()), "big") for k in range(self.K)}
+        self.last_timings = {}
+
+    def masked_sum(self, vecs, sizes, round_: int, participants=None, printer=None) -> torch.Tensor:
+        """vecs: {client -> flat float tensor (segments ``sizes``)} for this rank's participating
+        clients.  Returns the float SUM over all participating clients (every rank gets it)."""
+        import time
+        from ..parallel import comm
+        from ..utils.timer import Timer
+        parts = sorted(int(k) for k in (participants if participants is not None else range(self.K)))
+        dev = self.device
+        n = int(sum(sizes))
+        seg_end = segment_ends(sizes)
+        mx = torch.zeros(len(sizes), dtype=torch.float32, device=dev)
+        for v in vecs.values():
+            segs = torch.split(v.reshape(-1).to(dev).float().abs(), list(sizes))
+            mx = torch.maximum(mx, torch.stack([s.max() if s.numel() else s.new_zeros(()) for s in segs]))
+        if comm.world_size() > 1:
+            import torch.distributed as dist
+            comm.all_reduce_(mx, op=dist.ReduceOp.MAX)
+        scales = choose_scales(mx.cpu().numpy(), self.K)
+        total = torch.zeros(n, dtype=torch.int64, device=dev)
+        for k, v in sorted(vecs.items()):
+            with Timer(f"Encryption for client {k}", printer):
+                keys = self.keys[k].round_keys(self.publics, round_, parts)
+                masked = mask_quantize(v.reshape(-1).to(dev), scales, seg_end, self.K, k, keys, round_,
+                                       participants=parts)
+                total = (total + masked.to(dev).to(torch.int64)) % (1 << 32)
+        t32 = torch.where(total >= (1 << 31), total - (1 << 32), total).to(torch.int32)
+        comm.all_reduce_(t32)  # int32 SUM wraps mod 2^32 on RCCL / gloo
+        t0 = time.perf_counter()
+        out = unmask(t32, scales, seg_end, 1.0).to(dev)
+        dt = time.perf_counter() - t0
+        if printer is not None:
+            for k in sorted(vecs):  # every client runs the same unmasking of the same sum
+                printer(f"Decryption for client {k} took {dt} seconds")
+        self.last_scales = scales
+        return out

@@ -9,9 +9,11 @@ Reference ``secure_fed_model.py:101-236``:
 * client 0 evaluates on the global test set -> (loss, accuracy, AUC).
 
 Protection modes:
-* ``"mask"`` (default, north star): fixed-point quantisation + pairwise Philox masks on the GPU,
-  summed with one int32 all-reduce over RCCL (wraps mod 2^32, masks cancel exactly);
-* ``"paillier"``: the reference's homomorphic scheme (pure-Python Paillier, CPU; parity mode);
+* ``"mask"`` (default, north star): fixed-point quantisation (one scale per protected tensor) +
+  pairwise Philox masks on the GPU keyed by Diffie-Hellman pair secrets (``keyagree.py``: the
+  aggregator sees only public keys and masked vectors), summed with one int32 all-reduce over RCCL
+  (wraps mod 2^32, masks cancel exactly);
+* ``"paillier"``: the reference's homomorphic scheme (3072-bit keys as ``phe``; GMP, CPU; parity);
 * ``"none"``: plain averaging (``percent == 0`` in the reference).
 
 MI355X mapping: clients are spread round-robin over the ranks; a rank holds its clients' states
@@ -38,7 +40,7 @@ class ClientState:
 
 class SecureFederatedProcess:
     def __init__(self, model_fn: Callable, client_data: Sequence[Tuple], percent: float = 0.0,
-                 mode: str = "mask", epochs: int = 5, seed: int = 0, paillier_bits: int = 1024,
+                 mode: str = "mask", epochs: int = 5, seed: int = 0, paillier_bits: int = 3072,
                  verbose: int = 0, timer_printer=print):
         self.model_fn = model_fn
         self.client_data = list(client_data)
@@ -66,6 +68,8 @@ class SecureFederatedProcess:
         if self.mode == "paillier":
             from .paillier import generate_paillier_keypair
             self.pub, self.priv = generate_paillier_keypair(paillier_bits)
+        elif self.mode == "mask":
+            self.agg = secagg.MaskedAggregator(self.K, self.mine, self.m.device)
 
     # ------------------------------------------------------------------ state swapping
     def _set(self, weights: List[torch.Tensor]):
@@ -127,9 +131,9 @@ class SecureFederatedProcess:
         plain_mean = plain_sum / n_alive
         prot_mean = torch.zeros(sum(prot_sizes), device=dev)
         if n_prot:
-            with Timer("Encryption/aggregation", self.printer if self.verbose else None):
+            with Timer("Secure aggregation", self.printer if self.verbose else None):
                 if self.mode == "mask":
-                    prot_mean = self._masked_mean(n_prot, sum(prot_sizes), dev, mine)
+                    prot_mean = self._masked_mean(prot_sizes, dev, mine)
                 elif self.mode == "paillier":
                     prot_mean = self._paillier_mean(n_prot, dev, mine)
                 else:
@@ -146,31 +150,30 @@ class SecureFederatedProcess:
             off += n
         return out
 
-    def _masked_mean(self, n_prot: int, n: int, dev, mine) -> torch.Tensor:
+    def _masked_mean(self, prot_sizes, dev, mine) -> torch.Tensor:
+        n_prot = len(prot_sizes)
         vecs = {k: torch.cat([w.reshape(-1).to(dev) for w in self.states[k].weights[:n_prot]]) for k in mine}
-        mx = max([float(v.abs().max()) for v in vecs.values()] or [0.0])
-        mx = comm.all_reduce_max(mx, dev) if self.world > 1 else mx
-        scale = secagg.choose_scale(mx, self.K)
-        total = torch.zeros(n, dtype=torch.int64, device=dev)
-        for k, v in vecs.items():
-            masked = secagg.mask_quantize(v, scale, self.K, k, seed=self.seed + 7919, round_=self.round,
-                                          participants=self.alive)
-            total = (total + masked.to(dev).to(torch.int64)) % (1 << 32)
-        t32 = torch.where(total >= (1 << 31), total - (1 << 32), total).to(torch.int32)
-        comm.all_reduce_(t32)  # int32 SUM wraps mod 2^32 on RCCL / gloo
-        return secagg.unmask_mean(t32, scale, self.K, float(len(self.alive))).to(dev)
+        s = self.agg.masked_sum(vecs, prot_sizes, self.round, self.alive,
+                                printer=self.printer if self.verbose else None)
+        return s / float(len(self.alive))
 
     def _paillier_mean(self, n_prot: int, dev, mine) -> torch.Tensor:
+        from ..utils.timer import Timer
         from .paillier import decrypt_vector, encrypt_vector, sum_ciphertexts
         if self.world > 1:
             raise NotImplementedError("Paillier parity mode runs single-process (as the reference)")
         scale = float(2 ** 24)
+        pr = self.printer if self.verbose else None
         cts = []
-        for k in mine:
-            v = torch.cat([w.reshape(-1).float().cpu() for w in self.states[k].weights[:n_prot]])
-            cts.append(encrypt_vector(self.pub, v.tolist(), scale))
+        for k in mine:  # secure_fed_model.py:137: Timer("Encryption for client i")
+            with Timer(f"Encryption for client {k}", pr):
+                v = torch.cat([w.reshape(-1).float().cpu() for w in self.states[k].weights[:n_prot]])
+                cts.append(encrypt_vector(self.pub, v.tolist(), scale))
         summed = sum_ciphertexts(self.pub, cts)
-        mean = decrypt_vector(self.priv, summed, scale, float(len(self.alive)))
+        mean = None
+        for k in mine:  # secure_fed_model.py:145: every client decrypts the aggregate
+            with Timer(f"Decryption for client {k}", pr):
+                mean = decrypt_vector(self.priv, summed, scale, float(len(self.alive)))
         return torch.tensor(mean, dtype=torch.float32, device=dev)
 
     def run_round(self, test_data=None, dropped=()):

@@ -185,6 +185,8 @@ class MirroredStrategy(Strategy):
     def distribute(self, data):
         if self.world == 1:
             return data
+        if hasattr(data, "shard"):  # BatchedDataset: shard the index order, not the images
+            return data.shard(self.rank, self.world)
         return _ShardedBatches(data, self.rank, self.world)
 
 
@@ -207,7 +209,10 @@ class CentralStorageStrategy(MirroredStrategy):
 
 
 class _ShardedBatches:
-    """Rank ``r`` takes its contiguous slice of every global batch."""
+    """Fallback for arbitrary iterables of global batches: rank ``r`` takes its contiguous slice
+    of every batch.  Uneven batches are split as evenly as possible (the first ``b % world``
+    ranks get one extra row); a batch with fewer rows than replicas ends the epoch on every
+    rank alike (every rank sees the same batch sizes, so they stay in step)."""
 
     def __init__(self, data, rank, world):
         self.data, self.rank, self.world = data, rank, world
@@ -218,11 +223,12 @@ class _ShardedBatches:
     def __iter__(self):
         for x, y in self.data:
             b = x.shape[0]
-            per = b // self.world
-            if per == 0:
-                raise ValueError(f"global batch {b} smaller than {self.world} replicas")
-            lo = self.rank * per
-            yield x[lo:lo + per], y[lo:lo + per]
+            if b < self.world:
+                return
+            per, extra = divmod(b, self.world)
+            lo = self.rank * per + min(self.rank, extra)
+            hi = lo + per + (1 if self.rank < extra else 0)
+            yield x[lo:hi], y[lo:hi]
 
 
 def _all_layers(net):

@@ -22,8 +22,8 @@ import torch
 from ..data import (contiguous_clients, idc_dataset, prepare_for_training, shard_clients,
                     synthetic_dataset, train_test_clients)
 from ..engine import Model, ModelCheckpoint, RMSprop
-from ..fed import (build_federated_averaging_process, build_federated_evaluation,
-                   state_with_new_model_weights)
+from ..fed import (broadcast_server_state, build_federated_averaging_process, build_federated_evaluation,
+                   load_server_state, save_server_state, state_with_new_model_weights)
 from ..fed.secure import SecureFederatedProcess
 from ..models import build_model
 from ..parallel import OneDeviceStrategy, comm
@@ -55,6 +55,8 @@ class FedConfig:
     average_bn_stats: bool = False
     seed: int = 0
     backend: str = "auto"
+    secure_aggregation: Optional[str] = None  # "mask": config #5 secure FedAvg
+    resume: bool = True                       # continue from {path}/fed_state/state.pt if present
 
 
 def _fed_data(cfg: FedConfig):
@@ -82,15 +84,22 @@ def run_fedavg(cfg: FedConfig, printer=print):
                 backend=cfg.backend)
     if os.path.exists(ckpt):
         printer("Loading pretrained model")
-        pre.load_weights(ckpt)
-    else:
+        pre.load_weights(ckpt, strict=True)  # a stale checkpoint of another arch must not load silently
+    elif comm.rank() == 0:
+        # one central pre-training (rank 0), not one per rank: the fused kernels are not bitwise
+        # reproducible, so per-rank runs would start the federation from different servers
         tr = prepare_for_training(labeled.take(train_size), cfg.batch_size, seed=cfg.seed)
         va = prepare_for_training(labeled.skip(train_size).take(cfg.dataset_size - train_size),
                                   cfg.batch_size, seed=cfg.seed + 1)
         pre.evaluate(va, steps=20)
-        with Timer("Pre-training", printer if comm.rank() == 0 else None):
+        with Timer("Pre-training", printer):
             pre.fit(tr, epochs=cfg.pretrain_epochs, validation_data=va, validation_steps=20,
-                    callbacks=[ModelCheckpoint(ckpt, save_weights_only=True, rank=comm.rank())], verbose=0)
+                    callbacks=[ModelCheckpoint(ckpt, save_weights_only=True, rank=0)], verbose=0)
+    if comm.world_size() > 1:
+        pre.impl.sync_to_module()
+        for t in pre.net.weight_tensors():  # rank 0's pre-trained (or loaded) model everywhere
+            comm.broadcast_(t.data, 0)
+        pre.impl.sync_from_module()
     net.base.trainable = True
     for layer in net.base.layers[:cfg.fine_tune_at]:
         layer.trainable = False
@@ -109,23 +118,32 @@ def run_fedavg(cfg: FedConfig, printer=print):
 
     fed_avg = build_federated_averaging_process(
         model_fn, client_optimizer_fn=lambda: RMSprop(cfg.base_learning_rate / 10),
-        average_bn_stats=cfg.average_bn_stats, metrics=("binary_accuracy",))
+        average_bn_stats=cfg.average_bn_stats, metrics=("binary_accuracy",),
+        secure_aggregation=cfg.secure_aggregation)
     evaluation = build_federated_evaluation(model_fn, metrics=("binary_accuracy",))
     results = []
     printer("Starting federated training")
+    state_path = os.path.join(cfg.path, "fed_state", "state.pt")
     with Timer("Federated training", printer if comm.rank() == 0 else None):
         state = fed_avg.initialize()
-        state = state_with_new_model_weights(
-            state, [t.detach() for t in pre.net.trainable_weights],
-            [t.detach() for t in pre.net.non_trainable_weights])
+        if cfg.resume and os.path.exists(state_path):
+            state = load_server_state(state_path, state.model.trainable[0].device)
+            if comm.rank() == 0:
+                printer(f"Resuming federated training at round {state.round_num}")
+        else:
+            state = state_with_new_model_weights(
+                state, [t.detach() for t in pre.net.trainable_weights],
+                [t.detach() for t in pre.net.non_trainable_weights])
+        state = broadcast_server_state(state)
         init_metrics = evaluation(state.model, fed_test)
         if comm.rank() == 0:
             printer("Initial model: {0:f} \n".format(init_metrics["binary_accuracy"]))
-        for r in range(cfg.rounds):
+        for r in range(state.round_num, cfg.rounds):
             state, train_metrics = fed_avg.next(state, fed_train)
             test_metrics = evaluation(state.model, fed_test)
             results.append((r, train_metrics, test_metrics))
             if comm.rank() == 0:
+                save_server_state(state, state_path)
                 printer("{0:2d}, {1:f}, {2:f}, {3:f}, {4:f} \n".format(
                     r, train_metrics["binary_accuracy"], train_metrics["loss"],
                     test_metrics["binary_accuracy"], test_metrics["loss"]))

@@ -155,6 +155,7 @@ class FusedProgram:
         # under rocprofv3 kernel tracing
         main_prio = -1 if os.environ.get("IDC_MAIN_PRIO", "normal") == "high" else 0
         self.stream = torch.cuda.Stream(device=model.device, priority=main_prio)
+        self.comm_stream = torch.cuda.Stream(device=model.device)  # issues the gradient all-reduces
         # initial bf16 weight casts (all convs, frozen ones included)
         if b.cast_all_n:
             cast = nat.load().Plan()
@@ -185,7 +186,9 @@ class FusedProgram:
             with torch.cuda.stream(self.stream):
                 self._cast_all_plan.run(0, -1, self._sh())
 
-    def run_range(self, lo: int, hi: int, graph: Optional[bool] = None):
+    def run_range(self, lo: int, hi: int, graph: Optional[bool] = None, join: bool = True):
+        """Issue ops [lo, hi).  ``join=False`` (direct issue only) leaves the side lane running
+        past the end of the range: use ``side_ready_on`` to order a consumer after it."""
         if hi <= lo:
             return
         if graph is None:
@@ -197,7 +200,12 @@ class FusedProgram:
                 self.graphs[(lo, hi)] = g
             self.plan.launch(g, self._sh())
         else:
-            self.plan.run(lo, hi, self._sh())
+            self.plan.run(lo, hi, self._sh(), join)
+
+    def side_ready_on(self, stream: torch.cuda.Stream):
+        """``stream`` waits for the main lane so far AND every side-lane op issued so far."""
+        stream.wait_stream(self.stream)
+        self.plan.wait_side(stream.cuda_stream)
 
     def _graph_for(self, lo: int) -> bool:
         for name, (a, b) in self.seg.items():
@@ -302,19 +310,26 @@ class FusedStep:
             lo, hi = p.seg["bwd"]
             bucketer = strategy.bucketer(m.arena) if world > 1 else None
             if bucketer is not None and p.bwd_marks:
-                # backward in bucket-aligned segments: launch each bucket's all-reduce as soon
-                # as its gradients are final, while the remaining backward keeps the GPU busy
+                # backward in bucket-aligned segments: each bucket's all-reduce is issued from
+                # the comm stream as soon as its gradients are final — the comm stream waits for
+                # the main lane AND the side-lane weight gradients issued so far, while the main
+                # lane itself runs on without joining the side lane (plan.cpp run(join=False))
+                graphed = p.use_graphs and "bwd" in p.graph_segments
+                cs = p.comm_stream
                 pos = lo
                 for mark, low_param in p.bwd_marks:
                     if mark <= pos:
                         continue
-                    p.run_range(pos, mark)
+                    p.run_range(pos, mark, join=graphed)
                     pos = mark
-                    with torch.cuda.stream(p.stream), trace.range("allreduce:from_param%d" % low_param):
+                    p.side_ready_on(cs)
+                    with torch.cuda.stream(cs), trace.range("allreduce:from_param%d" % low_param):
                         bucketer.launch_range(low_param, None)
                 p.run_range(pos, hi)
-                with torch.cuda.stream(p.stream):
+                cs.wait_stream(p.stream)
+                with torch.cuda.stream(cs):
                     bucketer.finish()
+                p.stream.wait_stream(cs)
             else:
                 p.run_range(lo, hi)
                 if bucketer is not None:

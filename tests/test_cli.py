@@ -37,6 +37,23 @@ def test_fed_pretrain_checkpoint_then_rounds(tmp_path, capsys):
     assert "Loading pretrained model" in capsys.readouterr().out
 
 
+def test_fed_resume_and_secure_aggregation(tmp_path, capsys):
+    """Federated resume (server state + round counter + RNG saved every round) and the masked
+    weighted-delta aggregation through the CLI: a 1-round run, then a 2-round run continues at
+    round 1 instead of starting over."""
+    cfg = _cfg(tmp_path, "f.yaml", dict(dataset_size=200, batch_size=20, pretrain_epochs=1,
+                                        input_shape=[32, 32, 3], arch="mobilenetv2"))
+    assert main(["fed", str(tmp_path), "1", "iid", "--synthetic", "--secure-agg", "mask", "--config", cfg]) == 0
+    out = capsys.readouterr().out
+    assert " 0, " in out and os.path.exists(tmp_path / "fed_state" / "state.pt")
+    assert main(["fed", str(tmp_path), "2", "iid", "--synthetic", "--secure-agg", "mask", "--config", cfg]) == 0
+    out = capsys.readouterr().out
+    assert "Resuming federated training at round 1" in out
+    assert " 1, " in out and " 0, " not in out
+    from idc_models_amd.fed import load_server_state
+    assert load_server_state(str(tmp_path / "fed_state" / "state.pt")).round_num == 2
+
+
 @pytest.mark.parametrize("mode", ["mask", "none"])
 def test_secure_round(tmp_path, capsys, mode):
     cfg = _cfg(tmp_path, "s.yaml", dict(dataset_size=200, epochs=1))

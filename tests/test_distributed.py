@@ -171,3 +171,38 @@ def test_secure_masked_aggregation_two_ranks():
         plain = np.mean([allw[k][i] for k in range(4)], axis=0)
         np.testing.assert_array_equal(a, avg1[i])
         np.testing.assert_allclose(a, plain, atol=1e-6)
+
+
+def _secure_fedavg_run():
+    from idc_models_amd.data import contiguous_clients, synthetic_dataset
+    from idc_models_amd.engine import Model, RMSprop
+    from idc_models_amd.fed import build_federated_averaging_process
+    from idc_models_amd.models import build_model
+    from idc_models_amd.parallel import OneDeviceStrategy
+    ds = synthetic_dataset(120, (10, 10, 3), seed=4, signal=30.0)
+    clients = [c.batch(10) for c in contiguous_clients(ds, 4, 30)]
+
+    def model_fn():
+        return Model(_nodrop(build_model("tinycnn", seed=5)), OneDeviceStrategy("cpu"))
+
+    proc = build_federated_averaging_process(model_fn, lambda: RMSprop(1e-2), secure_aggregation="mask")
+    state = proc.initialize()
+    state, tm = proc.next(state, clients)
+    return [t.numpy().copy() for t in state.model.trainable], dict(tm)
+
+
+def _secure_fedavg_worker(rank, world):
+    return _secure_fedavg_run()
+
+
+def test_secure_fedavg_two_ranks_equals_single_process():
+    """Masked weighted-delta FedAvg over 2 gloo ranks (clients 0,2 | 1,3; the int32 masked sums and
+    the public keys cross ranks) equals the single-process masked run and matches it bit for bit
+    across the two ranks."""
+    single = _secure_fedavg_run()
+    res = spawn(_secure_fedavg_worker, 2)
+    for a, b, c in zip(res[0][0], res[1][0], single[0]):
+        np.testing.assert_array_equal(a, b)
+        np.testing.assert_allclose(a, c, rtol=1e-5, atol=1e-6)
+    for k in single[1]:
+        assert res[0][1][k] == pytest.approx(single[1][k], rel=1e-5)

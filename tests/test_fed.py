@@ -8,36 +8,119 @@ from idc_models_amd.fed.paillier import (decrypt_vector, encrypt_vector, generat
                                          sum_ciphertexts)
 
 
+def _keys(K, round_=5, participants=None):
+    from idc_models_amd.fed.keyagree import ClientKeys
+    ks = {k: ClientKeys(k) for k in range(K)}
+    pubs = {k: ks[k].public for k in range(K)}
+    parts = list(range(K)) if participants is None else list(participants)
+    return ks, pubs, {k: ks[k].round_keys(pubs, round_, parts) for k in parts}
+
+
 @pytest.mark.parametrize("K", [2, 3, 8])
 def test_pairwise_masks_cancel_exactly(K):
     rng = np.random.default_rng(K)
-    xs = [torch.tensor(rng.normal(size=1000).astype(np.float32)) for _ in range(K)]
-    scale = secagg.choose_scale(max(float(x.abs().max()) for x in xs), K)
+    sizes = [700, 300]  # two protected tensors with their own fixed-point scales
+    xs = [torch.tensor(np.concatenate([rng.normal(size=700), 50 * rng.normal(size=300)]).astype(np.float32))
+          for _ in range(K)]
+    seg = secagg.segment_ends(sizes)
+    mx = [max(float(x[:700].abs().max()) for x in xs), max(float(x[700:].abs().max()) for x in xs)]
+    scales = secagg.choose_scales(mx, K)
+    assert scales[0] > scales[1]  # the small-range tensor gets the finer scale
+    _, _, rk = _keys(K)
     total = np.zeros(1000, np.uint64)
     masked = []
     for k, x in enumerate(xs):
-        m = secagg.mask_quantize(x, scale, K, k, seed=123, round_=5)
+        m = secagg.mask_quantize(x, scales, seg, K, k, rk[k], round_=5)
         masked.append(m)
         total = (total + m.numpy().view(np.uint32).astype(np.uint64)) & np.uint64(0xFFFFFFFF)
     t32 = torch.from_numpy(total.astype(np.uint32).view(np.int32).copy())
-    mean = secagg.unmask_mean(t32, scale, K, float(K))
-    isum = sum(torch.round(x * scale).to(torch.int64) for x in xs)
+    mean = secagg.unmask(t32, scales, seg, float(K))
+    sc = torch.from_numpy(np.repeat(scales, sizes))
+    isum = sum(torch.round(x * sc).to(torch.int64) for x in xs)
     assert torch.equal(t32.to(torch.int64), isum)  # masks cancel: the exact fixed-point sum
-    plain = isum.to(torch.int32).float() / (scale * K)
+    plain = isum.to(torch.int32).float() / (sc * K)
     assert torch.equal(mean, plain)  # bit-exact vs the unmasked fixed-point mean
-    assert torch.allclose(mean, torch.stack(xs).mean(0), atol=1.0 / scale)
+    assert torch.allclose(mean, torch.stack(xs).mean(0), atol=float(1.0 / scales.min()))
     # a single masked vector carries no usable signal about its input
-    q0 = torch.round(xs[0] * scale).to(torch.int64)
+    q0 = torch.round(xs[0] * sc).to(torch.int64)
     corr = np.corrcoef(masked[0].numpy().astype(np.float64), q0.numpy().astype(np.float64))[0, 1]
     assert abs(corr) < 0.1
 
 
 def test_masks_change_every_round_and_pair():
     x = torch.zeros(64)
-    a = secagg.mask_quantize(x, 1.0, 3, 0, 1, 0)
-    b = secagg.mask_quantize(x, 1.0, 3, 0, 1, 1)
-    c = secagg.mask_quantize(x, 1.0, 3, 1, 1, 0)
+    seg = secagg.segment_ends([64])
+    ks, pubs, rk = _keys(3, round_=0)
+    a = secagg.mask_quantize(x, [1.0], seg, 3, 0, rk[0], 0)
+    b = secagg.mask_quantize(x, [1.0], seg, 3, 0, ks[0].round_keys(pubs, 1, range(3)), 1)
+    c = secagg.mask_quantize(x, [1.0], seg, 3, 1, rk[1], 0)
     assert not torch.equal(a, b) and not torch.equal(a, c)
+
+
+def test_aggregator_view_does_not_determine_masks():
+    """Pair keys come from Diffie-Hellman secrets: both endpoints derive the same key, the masks
+    still cancel, but nothing the aggregator holds (public keys, masked vectors, indices, round,
+    configuration seeds) reproduces a client's mask — and the same public configuration with fresh
+    private keys yields unrelated masks."""
+    from idc_models_amd.fed import keyagree
+    K, n, rnd = 3, 256, 4
+    seg = secagg.segment_ends([n])
+    zero = torch.zeros(n)
+    ks, pubs, rk = _keys(K, rnd)
+    assert rk[0][1] == rk[1][0] and rk[1][2] == rk[2][1]  # S_ij = S_ji
+    masks = [secagg.mask_quantize(zero, [1.0], seg, K, k, rk[k], rnd) for k in range(K)]  # x=0: pure masks
+    assert int(sum(m.to(torch.int64) for m in masks).remainder(1 << 32).abs().sum()) == 0
+    # candidate keys an aggregator could derive from its view
+    cands = []
+    for seed in (0, 7919, 1234):  # the old public-seed derivation
+        for lo, hi in ((0, 1), (0, 2)):
+            cands.append(((seed & 0xFFFFFFFF) ^ ((lo * 0x9E3779B1) & 0xFFFFFFFF),
+                          ((seed >> 32) & 0xFFFFFFFF) ^ ((hi * 0x85EBCA77) & 0xFFFFFFFF)))
+    cands.append(keyagree.pair_mask_key(pubs[0] * pubs[1] % keyagree.P, rnd, 0, 1))
+    cands.append(keyagree.pair_mask_key(pubs[0] ^ pubs[1], rnd, 0, 1))
+    for c1 in cands:
+        for c2 in cands:
+            guess = secagg.mask_quantize(zero, [1.0], seg, K, 0, {1: c1, 2: c2}, rnd)
+            assert not torch.equal(guess, masks[0])
+    # same public configuration, fresh private keys: unrelated masks (not a function of it)
+    _, _, rk2 = _keys(K, rnd)
+    again = secagg.mask_quantize(zero, [1.0], seg, K, 0, rk2[0], rnd)
+    assert not torch.equal(again, masks[0])
+    assert (again == masks[0]).float().mean() < 0.01
+    # degenerate / out-of-subgroup public values are refused
+    for bad in (0, 1, keyagree.P - 1, keyagree.P):
+        with pytest.raises(ValueError):
+            keyagree.check_public(bad)
+    nonres = next(g for g in range(3, 50) if pow(g, keyagree.Q, keyagree.P) != 1)
+    with pytest.raises(ValueError):
+        keyagree.check_public(nonres)
+
+
+def test_per_tensor_scales_keep_small_tensor_resolution():
+    """One global scale chosen from the largest protected value (a BN moving variance of ~1e4)
+    leaves a small conv kernel a few quantisation steps; per-tensor scales keep its resolution."""
+    K = 4
+    rng = np.random.default_rng(0)
+    small = [rng.normal(scale=1e-3, size=512).astype(np.float32) for _ in range(K)]
+    big = [np.abs(rng.normal(scale=1e4, size=64)).astype(np.float32) for _ in range(K)]
+    xs = [torch.tensor(np.concatenate([a, b])) for a, b in zip(small, big)]
+    sizes = [512, 64]
+    seg = secagg.segment_ends(sizes)
+    _, _, rk = _keys(K)
+    ref = torch.stack(xs).mean(0)
+
+    def run(scales):
+        tot = sum(secagg.mask_quantize(x, scales, seg, K, k, rk[k], 5).to(torch.int64) for k, x in enumerate(xs))
+        t = tot.remainder(1 << 32)
+        t32 = torch.where(t >= (1 << 31), t - (1 << 32), t).to(torch.int32)
+        return secagg.unmask(t32, scales, seg, float(K))
+
+    per = run(secagg.choose_scales([max(np.abs(a).max() for a in small), max(b.max() for b in big)], K))
+    glob = secagg.choose_scales([max(b.max() for b in big)], K)[0]
+    one = run([glob, glob])
+    e_per = float((per[:512] - ref[:512]).abs().max())
+    e_one = float((one[:512] - ref[:512]).abs().max())
+    assert e_per < 1e-7 < e_one and e_per * 1000 < e_one
 
 
 def test_philox_known_answer():
@@ -111,6 +194,41 @@ def test_fedavg_skips_non_finite_client():
     m.fit = fit
     new, _ = proc.next(state, clients)
     assert all(torch.isfinite(w).all() for w in new.model.trainable)
+
+
+def test_fedavg_secure_mask_equals_plain_weighted_mean():
+    """Secure FedAvg (config #5): masked example-weighted deltas sum to the plain FedAvg update
+    within the per-tensor fixed-point resolution; a non-finite client still takes part in the
+    masking (zero vector, weight 0) so the others' masks cancel."""
+    from idc_models_amd.engine import RMSprop
+    from idc_models_amd.fed import build_federated_averaging_process
+    plain, clients, model_fn = _tiny_fed()
+    sec = build_federated_averaging_process(model_fn, lambda: RMSprop(1e-2), secure_aggregation="mask")
+    s0 = plain.initialize()
+    s1 = sec.initialize()
+    for a, b in zip(s0.model.trainable, s1.model.trainable):
+        b.copy_(a)
+    n0, m0 = plain.next(s0, clients)
+    n1, m1 = sec.next(s1, clients)
+    for a, b in zip(n0.model.trainable, n1.model.trainable):
+        assert torch.allclose(a, b, atol=1e-6), float((a - b).abs().max())
+    assert m0 == pytest.approx(m1)
+    # a poisoned client: weight 0 in both, masks still cancel
+    w = sec.worker()
+    orig = w.fit
+    calls = {"n": 0}
+
+    def fit(ds, **kw):
+        calls["n"] += 1
+        h = orig(ds, **kw)
+        if calls["n"] == 1:
+            with torch.no_grad():
+                w.net.trainable_weights[0].fill_(float("inf"))
+        return h
+
+    w.fit = fit
+    n2, _ = sec.next(n1, clients)
+    assert all(torch.isfinite(t).all() for t in n2.model.trainable)
 
 
 def test_state_with_new_model_weights_shape_check():
@@ -195,6 +313,8 @@ def test_secure_aggregation_survives_client_dropout(mode):
     # without re-keying the dropped client's masks would not cancel: check that it matters
     from idc_models_amd.fed import secagg
     x = torch.ones(16)
-    full = [secagg.mask_quantize(x, 1.0, 4, k, 1, 0) for k in (0, 1, 3)]
+    ks, pubs, _ = _keys(4, 0)
+    seg = secagg.segment_ends([16])
+    full = [secagg.mask_quantize(x, [1.0], seg, 4, k, ks[k].round_keys(pubs, 0, range(4)), 0) for k in (0, 1, 3)]
     s = sum(t.to(torch.int64) for t in full) % (1 << 32)
     assert not torch.equal(s, torch.full((16,), 3, dtype=torch.int64))

@@ -396,22 +396,28 @@ def test_rmsprop_kernel_matches_keras_formula():
 
 
 def test_secagg_masks_cancel_exactly():
-    from idc_models_amd.fed.secagg import mask_quantize, unmask_mean
-    K, n = 5, 10007
+    from idc_models_amd.fed.keyagree import ClientKeys
+    from idc_models_amd.fed.secagg import mask_quantize, segment_ends, unmask
+    K, sizes = 5, [10000, 7]
+    n = sum(sizes)
+    seg = segment_ends(sizes)
+    scales = [2.0 ** 16, 2.0 ** 10]
+    ks = {k: ClientKeys(k) for k in range(K)}
+    pubs = {k: ks[k].public for k in range(K)}
+    rk = {k: ks[k].round_keys(pubs, 7, range(K)) for k in range(K)}
     xs = [torch.randn(n, device=DEV) for _ in range(K)]
-    scale = 2.0 ** 16
-    masked = [mask_quantize(x, scale, K, r, seed=1234, round_=7) for r, x in enumerate(xs)]
+    masked = [mask_quantize(x, scales, seg, K, r, rk[r], round_=7) for r, x in enumerate(xs)]
     total = torch.zeros(n, dtype=torch.int64, device=DEV)
     for m in masked:
         total = (total + m.to(torch.int64)) % (1 << 32)
-    s32 = total.to(torch.int64)
-    s32 = torch.where(s32 >= (1 << 31), s32 - (1 << 32), s32).to(torch.int32)
-    plain = sum(torch.round(x * scale).to(torch.int64) for x in xs)
+    s32 = torch.where(total >= (1 << 31), total - (1 << 32), total).to(torch.int32)
+    sc = torch.tensor([scales[0]] * sizes[0] + [scales[1]] * sizes[1], device=DEV)
+    plain = sum(torch.round(x * sc).to(torch.int64) for x in xs)
     assert torch.equal(s32.to(torch.int64), plain)
-    mean = unmask_mean(s32, scale, K, K)
-    assert torch.allclose(mean, sum(xs) / K, atol=K / scale)
+    mean = unmask(s32, scales, seg, K)
+    assert torch.allclose(mean, sum(xs) / K, atol=K / min(scales))
     # CPU numpy Philox produces the same bits as the GPU kernel
-    cpu = mask_quantize(xs[1].cpu(), scale, K, 1, seed=1234, round_=7)
+    cpu = mask_quantize(xs[1].cpu(), scales, seg, K, 1, rk[1], round_=7)
     assert torch.equal(cpu, masked[1].cpu())
 
 
