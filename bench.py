@@ -46,6 +46,78 @@ def stock_img_s_per_gpu(model: str):
     return max(vals) if vals else None
 
 
+def fed_bench(args):
+    """Configs #4 / #5: FedAvg rounds (MobileNetV2) or secure-aggregation FedAvg rounds (DenseNet-121)
+    with ``--clients`` simulated clients spread over the ranks (one process per GPU), each holding
+    ``--client-size`` synthetic 50x50x3 patches trained for one local epoch at ``--client-batch``
+    (``fed_model.py:47-61``: 3,000 examples per client, batch 32).  One untimed warm-up round, then
+    ``--rounds`` timed rounds between barrier + synchronize; max over ranks."""
+    import torch
+    import torch.distributed as dist
+
+    from idc_models_amd.data import contiguous_clients, synthetic_dataset
+    from idc_models_amd.engine import Model, RMSprop
+    from idc_models_amd.fed import build_federated_averaging_process
+    from idc_models_amd.models import build_model
+    from idc_models_amd.parallel import OneDeviceStrategy, comm
+
+    rank, world, local = comm.init_process_group()
+    dev = torch.device("cuda", local)
+    torch.cuda.set_device(dev)
+    # config #4 backbone MobileNetV2, config #5 DenseNet-121 (--model overrides for fedavg only)
+    arch = "densenet121" if args.mode == "secure" else (
+        "mobilenetv2" if args.model == "densenet121" else args.model)
+    base = build_model(arch, None, 1, seed=1234)
+    mine = [k for k in range(args.clients) if k % world == rank]
+    ds = synthetic_dataset(args.client_size * len(mine), (50, 50, 3), 2, seed=100 + rank)
+    parts = contiguous_clients(ds, len(mine), args.client_size)
+    clients = [None] * args.clients  # only this rank's clients are materialised
+    for k, c in zip(mine, parts):
+        clients[k] = c.batch(args.client_batch, True, 1000, True, seed=k)
+
+    import copy
+
+    def model_fn():
+        return Model(copy.deepcopy(base), OneDeviceStrategy(dev))
+
+    proc = build_federated_averaging_process(
+        model_fn, lambda: RMSprop(1e-4), average_bn_stats=True, backend=args.backend,
+        secure_aggregation="mask" if args.mode == "secure" else None)
+    state = proc.initialize()
+    state, _ = proc.next(state, clients)  # warm-up: builds and tunes the client program
+    torch.cuda.synchronize(dev)
+    comm.barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.rounds):
+        state, metrics = proc.next(state, clients)
+    torch.cuda.synchronize(dev)
+    comm.barrier()
+    dt = time.perf_counter() - t0
+    dt = comm.all_reduce_max(dt, dev) if world > 1 else dt
+    spr = dt / args.rounds
+    imgs = args.clients * (args.client_size // args.client_batch) * args.client_batch
+    if rank == 0:
+        print(json.dumps({
+            "metric": ("seconds/round FedAvg MobileNetV2" if args.mode == "fedavg"
+                       else "seconds/round secure-aggregation FedAvg DenseNet-121") +
+                      f" 50x50x3, {args.clients} clients x {args.client_size} examples, batch {args.client_batch}",
+            "value": round(spr, 4), "unit": "seconds/round", "n_gpus": world, "steps": args.rounds,
+            "warmup": 1, "higher_is_better": False, "scaling": "strong", "vs_baseline": None,
+            "dtype": "bf16", "data": "synthetic uint8 50x50x3 patches, random-init weights",
+            "client_images_per_sec": round(imgs / spr, 1),
+            "train_loss": round(float(metrics["loss"]), 5),
+            "config": {"model": arch, "clients": args.clients, "client_size": args.client_size,
+                       "client_batch": args.client_batch, "local_epochs": 1,
+                       "client_optimizer": "RMSprop(lr=1e-4)", "server_optimizer": "SGD(lr=1.0)",
+                       "aggregation": "DH-keyed additive masks, int32 all-reduce" if args.mode == "secure"
+                       else "example-weighted mean, packed all-reduce",
+                       "parallelism": f"clients over {world} rank(s)", "backend": args.backend,
+                       "comm_backend": dist.get_backend() if world > 1 else None},
+        }), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -61,7 +133,15 @@ def main():
     # statistics; 0.99^320 = 0.04
     ap.add_argument("--fit-steps", type=int, default=20, help="global batches per fit epoch (0: skip fit/AUC)")
     ap.add_argument("--fit-epochs", type=int, default=16)
+    ap.add_argument("--mode", default="train", choices=["train", "fedavg", "secure"],
+                    help="train: the headline DP step; fedavg / secure: north-star configs #4 / #5")
+    ap.add_argument("--clients", type=int, default=8)
+    ap.add_argument("--client-size", type=int, default=3000)
+    ap.add_argument("--client-batch", type=int, default=32)
+    ap.add_argument("--rounds", type=int, default=3)
     args = ap.parse_args()
+    if args.mode != "train":
+        return fed_bench(args)
 
     import torch
     import torch.distributed as dist

@@ -68,6 +68,7 @@ __global__ __launch_bounds__(256) void conv_igemm_kernel(ConvArgs a) {
   constexpr int TM = WTM / 16, TN = WTN / 16;
   constexpr int A_ELEMS = C::A_ELEMS, B_ELEMS = C::B_ELEMS, CS_LD = C::CS_LD;
   static_assert(TM >= 1 && TN >= 1, "bad wave tile");
+  static_assert(C::MAIN >= 8 * BN * 4, "statistics partials alias the staging tile");
   static_assert(NT % CPR == 0, "chunk mapping");
 
   extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -585,12 +586,22 @@ __global__ __launch_bounds__(256) void conv_igemm_kernel(ConvArgs a) {
   if (want_stats) {
     wave_reduce_chunks<CPB>(psum);
     wave_reduce_chunks<CPB>(psq);
-    if ((tid & 63) < CPB && (tid & ~63) < WTM * CPB) {
+    // per-wave partials -> fixed-order sum over the 4 waves (no LDS float atomics: the block's
+    // statistics are bitwise reproducible; the staging tile's LDS is free after the last pass)
+    __syncthreads();
+    float* s_part = reinterpret_cast<float*>(smem);  // [4 waves][2][BN]
+    if ((tid & 63) < CPB) {
+      const bool part = (tid & ~63) < WTM * CPB;
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
-        atomicAdd(&s_sum[my_c8 * 8 + j], psum[j]);
-        atomicAdd(&s_sq[my_c8 * 8 + j], psq[j]);
+        s_part[wid * 2 * BN + my_c8 * 8 + j] = part ? psum[j] : 0.f;
+        s_part[wid * 2 * BN + BN + my_c8 * 8 + j] = part ? psq[j] : 0.f;
       }
+    }
+    __syncthreads();
+    for (int j = tid; j < BN; j += NT) {
+      s_sum[j] = ((s_part[j] + s_part[2 * BN + j]) + s_part[4 * BN + j]) + s_part[6 * BN + j];
+      s_sq[j] = ((s_part[BN + j] + s_part[3 * BN + j]) + s_part[5 * BN + j]) + s_part[7 * BN + j];
     }
     __syncthreads();
     const size_t so = EPI == 0 ? (size_t)(mt % stat_slots(a.stats_slots)) * 2 * a.stats_ld

@@ -18,9 +18,17 @@ struct WgradArgs {
   // backward pending affine on G (common.h BwdAff; gpro.mode != 0 selects it): the staged
   // gradient is A*g + B*x + C, x read from gpro.x at the same pixel and output channel
   BwdAff gpro;
+  // deterministic mode: with `part` set, pixel-slice z stores its partial dW (fp32, dW layout)
+  // to part[z * numel(dW) + i] instead of adding atomically; wgrad_reduce then sums the slices
+  // in a fixed order (csrc/kernels/conv_wgrad.hip)
+  float* part;
+  long long part_floats;  // capacity, checked at launch
 };
 
 hipError_t conv_wgrad(WgradArgs a, int splits, bool g_f32, hipStream_t st);
+// dw[i] += sum_{z < splits} part[z * n + i], in slice order
+hipError_t wgrad_reduce(const float* part, float* dw, long long n, int splits, hipStream_t st);
+int wgrad_effective_splits(const WgradArgs& a, int splits);
 int wgrad_pick_splits(int M, int K, int Cout);
 
 }  // namespace idc

@@ -266,8 +266,29 @@ __global__ __launch_bounds__(256) void conv_wgrad_kernel(WgradArgs a) {
       if (c >= a.cin_real) continue;
       kdst = rs * a.cin_real + c;
     }
-    atomicAdd(&a.dw[(size_t)kdst * a.Cout + co], Cs[row * CS_LD + col] * a.scale);
+    const float v = Cs[row * CS_LD + col] * a.scale;
+    if (a.part) a.part[(size_t)blockIdx.z * ((size_t)a.KH * a.KW * (a.cin_real ? a.cin_real : a.Cin) * a.Cout) +
+                       (size_t)kdst * a.Cout + co] = v;
+    else atomicAdd(&a.dw[(size_t)kdst * a.Cout + co], v);
   }
+}
+
+__global__ __launch_bounds__(256) void wgrad_reduce_kernel(const float* __restrict__ part, float* __restrict__ dw,
+                                                           long long n, int splits) {
+  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n; i += (long long)gridDim.x * blockDim.x) {
+    float s = 0.f;
+    for (int z = 0; z < splits; ++z) s += part[(size_t)z * n + i];
+    dw[i] += s;
+  }
+}
+
+hipError_t wgrad_reduce(const float* part, float* dw, long long n, int splits, hipStream_t st) {
+  if (n <= 0) return hipSuccess;
+  if (part == nullptr || dw == nullptr || splits < 1) return hipErrorInvalidValue;
+  long long b = (n + 255) / 256;
+  if (b > 4096) b = 4096;
+  hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((int)b), dim3(256), 0, st, part, dw, n, splits);
+  return hipGetLastError();
 }
 
 template <int BKR, int BC, int BP, int WM, int WN>
@@ -307,9 +328,22 @@ hipError_t conv_wgrad(WgradArgs a, int splits, bool g_f32, hipStream_t st) {
   per = (per + bp - 1) / bp * bp;
   splits = (M + per - 1) / per;
   a.pix_per_split = per;
+  if (a.part) {  // the partial slab must hold every slice
+    const long long n = (long long)a.KH * a.KW * (a.cin_real ? a.cin_real : a.Cin) * a.Cout;
+    if ((long long)splits * n > a.part_floats) return hipErrorInvalidValue;
+  }
   if (a.Cout <= 32) return launch_wg<128, 32, 32, 4, 1>(a, is1x1, g_f32, pro, splits, st);
   if (a.Cout <= 64) return launch_wg<128, 64, 32, 2, 2>(a, is1x1, g_f32, pro, splits, st);
   return launch_wg<64, 128, 32, 2, 2>(a, is1x1, g_f32, pro, splits, st);
+}
+
+int wgrad_effective_splits(const WgradArgs& a, int splits) {
+  const int M = a.N * a.Ho * a.Wo;
+  if (splits < 1) splits = 1;
+  const int bp = wgrad_bp(a.Cout);
+  int per = (M + splits - 1) / splits;
+  per = (per + bp - 1) / bp * bp;
+  return (M + per - 1) / per;
 }
 
 int wgrad_pick_splits(int M, int K, int Cout) {

@@ -88,6 +88,7 @@ struct HeadBwdArgs {
   int N, HW, C, U;
   float* dw; float* db;   // grads (accumulate)
   float* dA; int ldda;    // [N*HW, C] fp32 output: dfeat/HW broadcast
+  int det;                // deterministic mode: one block row, one add per dW / db element
 };
 
 struct CastEntry {
@@ -125,5 +126,8 @@ hipError_t bn_apply(const bf16_t* x, int ldx, BnArgs bn, const bf16_t* res, int 
 // into one array (BatchNorm gamma/beta gradients in the parameter-gradient arena)
 hipError_t slot_collapse(const float* src, float* dst, const float* src2, float* dst2, int slots,
                          int ld, int C, hipStream_t st);
+// workgroups of the row-streaming kernels (pool / BN-reduce / BN-apply) for M rows of C channels,
+// `per_thread_rows` rows per thread: one statistics slot per workgroup in the deterministic mode
+int rows_grid(int M, int C, int per_thread_rows);
 
 }  // namespace idc

@@ -697,44 +697,50 @@ __global__ __launch_bounds__(256) void head_bwd_kernel(HeadBwdArgs a) {
   __shared__ float s_dw[4][64][17];
   __shared__ float s_dl[HB][16];
   const int c0 = blockIdx.x * 64;
-  const int n0 = blockIdx.y * HB;
   const int cl = threadIdx.x & 63, grp = threadIdx.x >> 6;
   const int c = c0 + cl;
   const bool cok = c < a.C;
-  for (int i = threadIdx.x; i < HB * a.U; i += blockDim.x) {
-    const int n = n0 + i / a.U;
-    s_dl[i / a.U][i % a.U] = n < a.N ? a.dlogits[n * a.U + i % a.U] : 0.f;
-  }
   float wc[16];
 #pragma unroll
   for (int u = 0; u < 16; ++u) wc[u] = (cok && u < a.U) ? a.w[(size_t)c * a.U + u] : 0.f;
-  __syncthreads();
-  float acc[16];
+  float acc[16], accb = 0.f;
 #pragma unroll
   for (int u = 0; u < 16; ++u) acc[u] = 0.f;
   const float inv_hw = 1.f / (float)a.HW;
   constexpr int PER = HB / 4;
-  float f[PER];
-#pragma unroll
-  for (int k = 0; k < PER; ++k) {
-    const int n = n0 + grp * PER + k;
-    f[k] = (cok && n < a.N) ? a.feats[(size_t)n * a.C + c] : 0.f;
-  }
-#pragma unroll
-  for (int k = 0; k < PER; ++k) {
-    const int nl = grp * PER + k, n = n0 + nl;
-    float df = 0.f;
-#pragma unroll
-    for (int u = 0; u < 16; ++u) {
-      const float dl = u < a.U ? s_dl[nl][u] : 0.f;
-      acc[u] += f[k] * dl;
-      df += dl * wc[u];
+  // chunks of HB samples, strided over gridDim.y (gridDim.y == 1 in the deterministic mode: every
+  // dW / db element then receives exactly one add)
+  for (int n0 = blockIdx.y * HB; n0 < a.N; n0 += gridDim.y * HB) {
+    __syncthreads();  // s_dl of the previous chunk fully consumed
+    for (int i = threadIdx.x; i < HB * a.U; i += blockDim.x) {
+      const int n = n0 + i / a.U;
+      s_dl[i / a.U][i % a.U] = n < a.N ? a.dlogits[n * a.U + i % a.U] : 0.f;
     }
-    if (a.dA && cok && n < a.N) {
-      const float v = df * inv_hw;
-      float* dst = a.dA + (size_t)n * a.HW * a.ldda + c;
-      for (int p = 0; p < a.HW; ++p) dst[(size_t)p * a.ldda] = v;
+    __syncthreads();
+    float f[PER];
+#pragma unroll
+    for (int k = 0; k < PER; ++k) {
+      const int n = n0 + grp * PER + k;
+      f[k] = (cok && n < a.N) ? a.feats[(size_t)n * a.C + c] : 0.f;
     }
+#pragma unroll
+    for (int k = 0; k < PER; ++k) {
+      const int nl = grp * PER + k, n = n0 + nl;
+      float df = 0.f;
+#pragma unroll
+      for (int u = 0; u < 16; ++u) {
+        const float dl = u < a.U ? s_dl[nl][u] : 0.f;
+        acc[u] += f[k] * dl;
+        df += dl * wc[u];
+      }
+      if (a.dA && cok && n < a.N) {
+        const float v = df * inv_hw;
+        float* dst = a.dA + (size_t)n * a.HW * a.ldda + c;
+        for (int p = 0; p < a.HW; ++p) dst[(size_t)p * a.ldda] = v;
+      }
+    }
+    if (blockIdx.x == 0 && threadIdx.x < a.U)
+      for (int k = 0; k < HB; ++k) accb += s_dl[k][threadIdx.x];
   }
 #pragma unroll
   for (int u = 0; u < 16; ++u)
@@ -743,17 +749,13 @@ __global__ __launch_bounds__(256) void head_bwd_kernel(HeadBwdArgs a) {
   if (grp == 0 && cok)
     for (int u = 0; u < a.U; ++u)
       atomicAdd(&a.dw[(size_t)c * a.U + u], s_dw[0][cl][u] + s_dw[1][cl][u] + s_dw[2][cl][u] + s_dw[3][cl][u]);
-  if (blockIdx.x == 0 && threadIdx.x < a.U && a.db) {
-    float sdb = 0.f;
-    for (int k = 0; k < HB; ++k) sdb += s_dl[k][threadIdx.x];
-    atomicAdd(&a.db[threadIdx.x], sdb);
-  }
+  if (blockIdx.x == 0 && threadIdx.x < a.U && a.db) atomicAdd(&a.db[threadIdx.x], accb);
 }
 
 hipError_t head_bwd(const HeadBwdArgs& a, hipStream_t st) {
   if (a.U > 16) return hipErrorInvalidValue;
   constexpr int HB = 16;
-  dim3 grid((a.C + 63) / 64, (a.N + HB - 1) / HB);
+  dim3 grid((a.C + 63) / 64, a.det ? 1 : (a.N + HB - 1) / HB);
   hipLaunchKernelGGL(head_bwd_kernel<HB>, grid, dim3(256), 0, st, a);
   return hipGetLastError();
 }
@@ -1035,17 +1037,34 @@ hipError_t bn_apply(const bf16_t* x, int ldx, BnArgs bn, const bf16_t* res, int 
 }
 
 // ------------------------------------------------------------------------------------------
+// Fixed-order slot reduction: a block owns 32 channels; thread (ty, tx) sums slots ty, ty+8, ...
+// of channel tx, then the 8 partials are added in ty order — the same bits every run (the
+// deterministic mode folds every producer's per-workgroup slots through here).
 __global__ __launch_bounds__(256) void slot_collapse_kernel(const float* src, float* dst, const float* src2,
                                                             float* dst2, int slots, int ld, int C) {
-  const int c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= C) return;
+  __shared__ float sa[8][33], sb[8][33];
+  const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;
+  const int c = blockIdx.x * 32 + tx;
   float a = 0.f, b = 0.f;
-  for (int s = 0; s < slots; ++s) {
-    a += src[(size_t)s * ld + c];
-    if (src2) b += src2[(size_t)s * ld + c];
+  if (c < C) {
+    for (int s = ty; s < slots; s += 8) {
+      a += src[(size_t)s * ld + c];
+      if (src2) b += src2[(size_t)s * ld + c];
+    }
   }
-  dst[c] += a;
-  if (dst2) dst2[c] += b;
+  sa[ty][tx] = a;
+  sb[ty][tx] = b;
+  __syncthreads();
+  if (ty == 0 && c < C) {
+    float ta = 0.f, tb = 0.f;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      ta += sa[k][tx];
+      tb += sb[k][tx];
+    }
+    dst[c] += ta;
+    if (dst2) dst2[c] += tb;
+  }
 }
 
 hipError_t slot_collapse(const float* src, float* dst, const float* src2, float* dst2, int slots, int ld,
@@ -1053,9 +1072,11 @@ hipError_t slot_collapse(const float* src, float* dst, const float* src2, float*
   if (C <= 0) return hipSuccess;
   if (src == nullptr || dst == nullptr || (src2 == nullptr) != (dst2 == nullptr) || slots < 1 || ld < C)
     return hipErrorInvalidValue;
-  hipLaunchKernelGGL(slot_collapse_kernel, dim3((C + 255) / 256), dim3(256), 0, st, src, dst, src2, dst2, slots,
+  hipLaunchKernelGGL(slot_collapse_kernel, dim3((C + 31) / 32), dim3(256), 0, st, src, dst, src2, dst2, slots,
                      ld, C);
   return hipGetLastError();
 }
+
+int rows_grid(int M, int C, int per_thread_rows) { return grid_rows(M, C, per_thread_rows); }
 
 }  // namespace idc

@@ -257,7 +257,15 @@ class Plan {
         check(conv_igemm(a, op.i[0], op.i[1] != 0, st), "conv_igemm");
         break;
       }
-      case OP_WGRAD: check(conv_wgrad(as<WgradArgs>(op), op.i[0], op.i[1] != 0, st), "conv_wgrad"); break;
+      case OP_WGRAD: {
+        const WgradArgs& a = as<WgradArgs>(op);
+        check(conv_wgrad(a, op.i[0], op.i[1] != 0, st), "conv_wgrad");
+        if (a.part) {  // deterministic mode: fixed-order sum of the per-slice partials
+          const long long n = (long long)a.KH * a.KW * (a.cin_real ? a.cin_real : a.Cin) * a.Cout;
+          check(wgrad_reduce(a.part, a.dw, n, wgrad_effective_splits(a, op.i[0]), st), "wgrad_reduce");
+        }
+        break;
+      }
       case OP_BN_BWD_APPLY: check(bn_bwd_apply(as<BnBwdApplyArgs>(op), st), "bn_bwd_apply"); break;
       case OP_BN_BWD_REDUCE: check(bn_bwd_reduce(as<BnBwdReduceArgs>(op), st), "bn_bwd_reduce"); break;
       case OP_MAXPOOL: check(maxpool_fwd(as<PoolArgs>(op), st), "maxpool_fwd"); break;
@@ -388,6 +396,8 @@ py::dict struct_sizes() {
   d["PoolBwdArgs.dx_f32"] = offsetof(PoolBwdArgs, dx_f32);
   d["BwdAff.fold_sumx"] = offsetof(BwdAff, fold_sumx);
   d["ConvArgs.aout"] = offsetof(ConvArgs, aout);
+  d["WgradArgs.part_floats"] = offsetof(WgradArgs, part_floats);
+  d["HeadBwdArgs.det"] = offsetof(HeadBwdArgs, det);
   return d;
 }
 
@@ -401,6 +411,14 @@ bool py_halo_ok(py::bytes payload) {
   return conv3x3_halo_ok(a);
 }
 int py_pick_splits(int M, int K, int Cout) { return wgrad_pick_splits(M, K, Cout); }
+
+int py_effective_splits(py::bytes payload, int splits) {
+  std::string s = payload;
+  if (s.size() != sizeof(WgradArgs)) throw std::runtime_error("WgradArgs size mismatch");
+  WgradArgs a;
+  std::memcpy(&a, s.data(), sizeof(a));
+  return wgrad_effective_splits(a, splits);
+}
 
 void py_secagg_mask(uintptr_t x, uintptr_t out, long long n, uintptr_t seg_scale, uintptr_t seg_end, int nseg,
                     float clip, int nclients, int rank, uintptr_t keys, unsigned long long round_,
@@ -457,6 +475,8 @@ PYBIND11_MODULE(_idc_native, m) {
   m.def("dw_wgrad_ws_floats", &dwconv_wgrad_ws_floats);
   m.attr("TILE_HALO") = TILE_HALO;
   m.def("pick_splits", &py_pick_splits);
+  m.def("effective_splits", &py_effective_splits);
+  m.def("rows_grid", &rows_grid);
   m.def("num_tiles", &conv_num_tiles);
   m.def("tile_bm", &conv_tile_bm);
   m.def("tile_bn", &conv_tile_bn);

@@ -114,7 +114,7 @@ class FedAvgProcess:
     def __init__(self, model_fn: Callable, client_optimizer_fn: Callable,
                  server_optimizer_fn: Optional[Callable] = None, average_bn_stats: bool = False,
                  local_epochs: int = 1, loss="binary_crossentropy", metrics=("binary_accuracy",),
-                 secure_aggregation: Optional[str] = None):
+                 secure_aggregation: Optional[str] = None, backend: str = "auto"):
         self.model_fn = model_fn
         self.client_optimizer_fn = client_optimizer_fn
         self.server_lr = 1.0
@@ -130,12 +130,13 @@ class FedAvgProcess:
             raise ValueError(f"unknown secure aggregation mode {secure_aggregation!r}")
         self.secure = secure_aggregation == "mask"
         self._agg = None
+        self.backend = backend
 
     # -------------------------------------------------------------- worker model
     def worker(self):
         if self._worker is None:
             m = self.model_fn()
-            m.compile(self.client_optimizer_fn(), self.loss, list(self.metric_names))
+            m.compile(self.client_optimizer_fn(), self.loss, list(self.metric_names), backend=self.backend)
             self._worker = m
         return self._worker
 

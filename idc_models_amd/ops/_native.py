@@ -54,7 +54,7 @@ class WgradArgs(C.Structure):
                 ("g", vp), ("ldg", ci), ("Ho", ci), ("Wo", ci), ("Cout", ci),
                 ("KH", ci), ("KW", ci), ("SH", ci), ("SW", ci), ("PT", ci), ("PL", ci),
                 ("pro", BnArgs), ("dw", vp), ("scale", cf), ("cin_real", ci), ("pix_per_split", ci),
-                ("gpro", BwdAff)]
+                ("gpro", BwdAff), ("part", vp), ("part_floats", cll)]
 
 
 class BnBwdApplyArgs(C.Structure):
@@ -98,7 +98,7 @@ class HeadArgs(C.Structure):
 
 class HeadBwdArgs(C.Structure):
     _fields_ = [("feats", vp), ("dlogits", vp), ("w", vp), ("N", ci), ("HW", ci), ("C", ci),
-                ("U", ci), ("dw", vp), ("db", vp), ("dA", vp), ("ldda", ci)]
+                ("U", ci), ("dw", vp), ("db", vp), ("dA", vp), ("ldda", ci), ("det", ci)]
 
 
 class CastEntry(C.Structure):
@@ -152,7 +152,8 @@ def _verify(ext):
               "ConvArgs.gsum_ld": ConvArgs.gsum_ld.offset, "BnArgs.slots": BnArgs.slots.offset,
               "DwArgs.gsum_ld": DwArgs.gsum_ld.offset, "ConvArgs.bepi": ConvArgs.bepi.offset,
               "WgradArgs.gpro": WgradArgs.gpro.offset, "PoolBwdArgs.dx_f32": PoolBwdArgs.dx_f32.offset,
-              "BwdAff.fold_sumx": BwdAff.fold_sumx.offset, "ConvArgs.aout": ConvArgs.aout.offset}
+              "BwdAff.fold_sumx": BwdAff.fold_sumx.offset, "ConvArgs.aout": ConvArgs.aout.offset,
+              "WgradArgs.part_floats": WgradArgs.part_floats.offset, "HeadBwdArgs.det": HeadBwdArgs.det.offset}
     for k, v in checks.items():
         if sizes[k] != v:
             raise RuntimeError(f"native struct field {k}: ctypes offset {v} != C++ {sizes[k]}")

@@ -141,12 +141,18 @@ class Builder:
         # statistics slots (stat_slots_for); IDC_STAT_SLOTS=0 restores single-copy reductions
         self.stat_slots_on = os.environ.get("IDC_STAT_SLOTS", "1") != "0"
         self.pending_sums: List["BNRef"] = []  # BatchNorms whose gradient slot copies await a fold
+        # IDC_DETERMINISTIC=1: every float reduction has a fixed order (see _det_* below); the
+        # same program on the same inputs then produces the same bits run after run
+        self.det = os.environ.get("IDC_DETERMINISTIC", "0") == "1"
+        self._post: List[tuple] = []  # collapse ops queued to follow the next emitted op
+        self._wslab: Dict[int, torch.Tensor] = {}  # det wgrad partial slabs, one per lane
         self.guards: List[tuple] = []
         self.splitk_slab: Optional[torch.Tensor] = None
         self.tickets: List[torch.Tensor] = []
         self.bwd_marks: List[Tuple[int, int]] = []  # (op index, lowest arena param index ready)
         # stats arena is allocated lazily with a generous capacity; views are handed out in order
-        self._stats_cap = 1 << 20
+        # (the deterministic mode's per-workgroup private slots need ~10-40x more)
+        self._stats_cap = (1 << 25) if self.det else (1 << 20)
         self.stats_arena = torch.zeros(self._stats_cap, dtype=F32, device=device)
 
     # ------------------------------------------------------------------ allocation
@@ -187,10 +193,10 @@ class Builder:
         return v
 
     def stats(self, ld: int, count: int) -> Stats:
-        slots = stat_slots_for(count) if self.stat_slots_on else 1
+        slots = stat_slots_for(count) if (self.stat_slots_on and not self.det) else 1
         return Stats(self._stats_floats(2 * ld * slots), ld, count, slots)
 
-    def grad_sums(self, bn: Optional["BNRef"], rows: int):
+    def grad_sums(self, bn: Optional["BNRef"], rows: int, grid: int = 0):
         """(gsum, gsumx, slots, ld) for the producer of a BatchNorm backward's reductions
         (sum dZ -> d beta, sum dZ*xhat -> d gamma).  With several row blocks the producer adds
         into slot copies in the stats arena and ``finish_grad_sums`` folds them into the gradient
@@ -199,6 +205,11 @@ class Builder:
             return 0, 0, 1, 0
         if getattr(bn, "gsums", None) is not None:
             raise RuntimeError(f"{bn.layer.name}: a second BatchNorm-backward reduction producer")
+        if self.det:
+            # the producer's workgroup w adds only into its private slot w; a fixed-order collapse
+            # into d beta / d gamma follows it; consumers read the collapsed sums
+            bn.gsums = (bn.dbeta.data_ptr(), bn.dgamma.data_ptr(), 1, 0)
+            return self._det_gsum_slots(bn.C, max(int(grid), 1), bn.dbeta.data_ptr(), bn.dgamma.data_ptr())
         S = stat_slots_for(rows) if self.stat_slots_on else 1
         if S == 1:
             bn.gsums = (bn.dbeta.data_ptr(), bn.dgamma.data_ptr(), 1, 0)
@@ -238,6 +249,37 @@ class Builder:
         raw = nat.raw(payload) if payload is not None else b""
         self.ops.append((self.segment, kind, raw, list(ints), list(floats), list(longs),
                          [int(p) for p in ptrs], lane if self.side_lane else 0))
+        post, self._post = self._post, []
+        for k2, i2, p2 in post:  # deterministic-mode collapses of this op's private slots
+            self.ops.append((self.segment, k2, b"", list(i2), [], [], [int(q) for q in p2],
+                             lane if self.side_lane else 0))
+
+    # ------------------------------------------------------------------ deterministic mode
+    def _det_gsum_slots(self, C: int, S: int, dst: int, dst2: int = 0):
+        """A private [S][C] pair of slot arrays (gsum, gsumx layout: stride C) for one producer
+        whose workgroup w adds only into slot w (single adder per address: exact on the zeroed
+        stats arena), and the fixed-order collapse into dst/dst2 queued behind it.
+        Returns (gsum, gsumx, slots, ld) for the kernel arguments."""
+        raw = self._stats_floats(2 * S * C)
+        r1 = raw.data_ptr()
+        r2 = r1 + 4 * S * C if dst2 else 0
+        self._post.append((nat.OP_COLLAPSE, (S, C, C), (r1, dst, r2, dst2)))
+        return r1, r2, S, C
+
+    def _det_stats_slots(self, C: int, S: int, final: "Stats", off: int):
+        """Forward statistics form: private [S][2][C] slots, collapsed into ``final`` at channel
+        offset ``off``.  Returns (stats_out, stats_ld, stats_off, stats_slots)."""
+        raw = self._stats_floats(2 * S * C).data_ptr()
+        fin = final.ptr + 4 * off
+        self._post.append((nat.OP_COLLAPSE, (S, 2 * C, C), (raw, fin, raw + 4 * C, fin + 4 * final.ld)))
+        return raw, C, 0, S
+
+    @staticmethod
+    def _conv_row_tiles(M: int) -> int:
+        return -(-M // 64)  # the most row tiles any conv tile shape (BM >= 64) produces
+
+    def _rows_grid(self, M: int, C: int, per: int) -> int:
+        return int(nat.load().rows_grid(int(M), int(C), int(per)))
 
     def mark_grads_ready(self, params):
         """Backward has finished producing the grads of ``params`` (for DP bucket overlap)."""
@@ -404,13 +446,16 @@ class Builder:
         a.bias = nat.ptr(bias)
         a.epi_act = epi_act
         a.out_mode = out_mode
+        M = x.N * y.H * y.W
         if stats is not None:
             a.stats_out, a.stats_ld, a.stats_off = stats.ptr, stats.ld, stats_off
             a.stats_slots = stats.slots
+            if self.det:
+                a.stats_out, a.stats_ld, a.stats_off, a.stats_slots = self._det_stats_slots(
+                    y.C, self._conv_row_tiles(M), stats, stats_off)
         a.mbn = act_only(0)
         if bpro is not None:
             a.bpro = bpro
-        M = x.N * y.H * y.W
         if tile < 0:
             tile = self._default_tile(a, M, y.C)
         self._splitk(a, M, y.C)
@@ -483,7 +528,13 @@ class Builder:
             a.mx, a.ldmx = mx.ptr, mx.ld
             a.mbn = mbn
             if gbn is not None:
-                a.gsum, a.gsumx, a.gsum_slots, a.gsum_ld = self.grad_sums(gbn, dx.M)
+                a.gsum, a.gsumx, a.gsum_slots, a.gsum_ld = self.grad_sums(gbn, dx.M, self._conv_row_tiles(dx.M))
+            elif self.det and (gsum is not None or gsumx is not None):
+                a.gsum, a.gsumx, a.gsum_slots, a.gsum_ld = self._det_gsum_slots(
+                    dx.C, self._conv_row_tiles(dx.M), nat.ptr(gsum) if gsum is not None else nat.ptr(gsumx),
+                    nat.ptr(gsumx) if (gsum is not None and gsumx is not None) else 0)
+                if gsum is None:
+                    a.gsum, a.gsumx = 0, a.gsum
             else:
                 a.gsum, a.gsumx = nat.ptr(gsum), nat.ptr(gsumx)
         else:
@@ -526,6 +577,16 @@ class Builder:
         a.cin_real = cin_real
         if splits < 0:
             splits = nat.load().pick_splits(g.M, kh * kw * x.C, g.C)
+        if self.det:
+            # per-slice partials + a fixed-order reduce instead of float atomics (plan.cpp OP_WGRAD);
+            # one slab per lane, reused by that lane's wgrads (a lane runs them one after another)
+            ln = lane if self.side_lane else 0
+            need = int(nat.load().effective_splits(nat.raw(a), splits)) * dw.numel()
+            slab = self._wslab.get(ln)
+            if slab is None or slab.numel() < need:
+                slab = self.alloc((max(need, 2 * (slab.numel() if slab is not None else 0)),), F32)
+                self._wslab[ln] = slab
+            a.part, a.part_floats = slab.data_ptr(), slab.numel()
         self.emit(nat.OP_WGRAD, a, ints=(splits, 1 if g.is_f32 else 0), lane=lane)
 
     def bn_bwd_apply(self, dz: Tensor4, x: Tensor4, bn: BNRef, dst: Tensor4, accumulate: bool):
@@ -558,7 +619,7 @@ class Builder:
         a.bn = bn.args()
         a.dz, a.lddz = dz.ptr, dz.ld
         a.dz_f32 = 1 if dz.is_f32 else 0
-        a.gsum, a.gsumx, a.gsum_slots, a.gsum_ld = self.grad_sums(bn, x.M)
+        a.gsum, a.gsumx, a.gsum_slots, a.gsum_ld = self.grad_sums(bn, x.M, self._rows_grid(x.M, x.C, 4) if self.det else 0)
         a.M, a.C = x.M, x.C
         self.emit(nat.OP_BN_BWD_REDUCE, a)
         self.finish_grad_sums(bn)
@@ -576,6 +637,9 @@ class Builder:
         if stats is not None:
             a.stats, a.stats_ld, a.stats_off = stats.ptr, stats.ld, stats_off
             a.stats_slots = stats.slots
+            if self.det:
+                a.stats, a.stats_ld, a.stats_off, a.stats_slots = self._det_stats_slots(
+                    x.C, self._rows_grid(x.N * y.H * y.W, x.C, 1), stats, stats_off)
         self.emit(nat.OP_MAXPOOL if is_max else nat.OP_AVGPOOL, a)
 
     def pool_bwd(self, dy: Tensor4, dx: Tensor4, *, k, s, pt=0, pl=0, is_max=True, argmax=None,
@@ -597,7 +661,8 @@ class Builder:
             a.x, a.ldx = x.ptr, x.ld
             a.bn = bn.args() if bn is not None else act_only(act)
             if bn is not None:
-                a.gsum, a.gsumx, a.gsum_slots, a.gsum_ld = self.grad_sums(bn, dx.M)
+                grid = self._rows_grid(dx.M, dx.C, 4 if k <= s else 2) if self.det else 0
+                a.gsum, a.gsumx, a.gsum_slots, a.gsum_ld = self.grad_sums(bn, dx.M, grid)
         else:
             a.bn = act_only(0)
         a.dx, a.lddx = dx.ptr, dx.ld
@@ -608,6 +673,7 @@ class Builder:
     def bn_apply(self, x: Tensor4, bn: "BNRef", y: Tensor4, *, act: Optional[int] = None,
                  res: Optional[Tensor4] = None, stats: Optional[Stats] = None):
         """Materialise y = act(BN(x)) [+ res] (bf16), optionally reducing y's statistics."""
+        self._no_det("bn_apply")
         args = bn.args()
         if act is not None:
             args.act = act
@@ -627,8 +693,14 @@ class Builder:
         a.KH, a.KW, a.S, a.PT, a.PL, a.Ho, a.Wo = kh, kw, stride, pads[0], pads[1], Ho, Wo
         return a
 
+    def _no_det(self, what: str):
+        if self.det:
+            raise NotImplementedError(f"IDC_DETERMINISTIC: {what} has no fixed-order reduction yet "
+                                      "(covered: VGG16 and the DenseNet family)")
+
     def dwconv(self, x: Tensor4, layer, y: Tensor4, *, stride=1, pads=(1, 1), pro=None,
                stats: Optional[Stats] = None):
+        self._no_det("depthwise conv")
         a = self._dw_args(x, layer, y.H, y.W, stride, pads, pro)
         a.y, a.ldy = y.ptr, y.ld
         if stats is not None:

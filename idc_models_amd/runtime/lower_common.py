@@ -97,6 +97,7 @@ def emit_head_bwd(b: Builder, feat: Tensor4, dense, U: int, io: HeadIO, need_dA:
         a.dA, a.ldda = b.alloc((feat.N * feat.H * feat.W * feat.C,), F32).data_ptr(), feat.C
     else:
         a.dA, a.ldda = dA.ptr, dA.ld
+    a.det = 1 if b.det else 0
     b.emit(nat.OP_HEAD_BWD, a)
     if train_head:
         b.mark_grads_ready([dense.kernel] + ([dense.bias] if dense.use_bias else []))

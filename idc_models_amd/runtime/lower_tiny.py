@@ -22,6 +22,7 @@ def tiny_supported(net) -> bool:
 
 
 def lower_tiny(b: Builder, net, U: int, input_dtype):
+    b._no_det("the tiny-CNN MLP head")
     by_class = {}
     for l in net.layers:
         by_class.setdefault(l.keras_class, []).append(l)

@@ -48,6 +48,8 @@ def lower_vgg(b: Builder, net, U: int, input_dtype):
 
     b.segment = "bwd"
     b.memset(b.arena.grad)
+    if b.det:  # the deterministic mode's private bias-gradient slots live in the stats arena
+        b.memset(b.stats_arena)
     need = fz.any()
     dA = emit_head_bwd(b, cur, dense, U, io, need_dA=need)
     if not need:
@@ -99,6 +101,8 @@ def _pool_bwd_relu(b: Builder, dy, dx, argmax, x, gbias):
     a.bn = nat.bn_args(mode=0, act=RELU)
     a.gsum = nat.ptr(gbias)
     a.gsumx = 0
+    if b.det and gbias is not None:  # one private slot per workgroup + fixed-order collapse
+        a.gsum, _, a.gsum_slots, a.gsum_ld = b._det_gsum_slots(dx.C, b._rows_grid(dx.M, dx.C, 4), gbias.data_ptr())
     a.dx, a.lddx = dx.ptr, dx.ld
     a.is_avg = 0
     b.emit(nat.OP_POOL_BWD, a)

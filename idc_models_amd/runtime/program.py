@@ -165,7 +165,9 @@ class FusedProgram:
         else:
             self._cast_all_plan = None
         self.recast_all()
-        if os.environ.get("IDC_AUTOTUNE", "1") != "0":
+        # autotuning picks tiles by timing, which may differ from run to run: a deterministic
+        # program keeps the fixed default tiles (and no split-K)
+        if os.environ.get("IDC_AUTOTUNE", "1") != "0" and not b.det:
             from .autotune import autotune_plan
             halo = ()
             if "fwd" in self.seg and os.environ.get("IDC_HALO_FWD", "0") == "1":

@@ -28,6 +28,7 @@ def run_case(arch, kind, per=None):
     # program then differ by float-atomic summation order amplified through 120 BatchNorms, so
     # the comparison uses 32 per rank (as the fine-tune GPU test does)
     per = per or (32 if arch.startswith("densenet") else 8)
+    # (under IDC_DETERMINISTIC=1 the comparison is exact at any batch)
     import torch.distributed as dist
     from idc_models_amd.engine import Model, RMSprop
     from idc_models_amd.models import build_model
@@ -69,8 +70,13 @@ def run_case(arch, kind, per=None):
         d, e = red.double(), tot.double()
         out["grad_cos"] = float(d @ e / (d.norm() * e.norm() + 1e-30))
         out["grad_rel_err"] = float((d - e).norm() / (e.norm() + 1e-30))
-        tol = (0.999, 0.05) if arch.startswith("vgg") else (0.99, 0.15)
-        out["ok"] = bool(same == 0.0 and out["grad_cos"] > tol[0] and out["grad_rel_err"] < tol[1])
+        if os.environ.get("IDC_DETERMINISTIC") == "1":
+            # fixed-order reductions: each rank's shard gradient is the single-process one to the
+            # bit, and a two-rank sum is exactly g0 + g1
+            out["ok"] = bool(same == 0.0 and out["grad_rel_err"] == 0.0)
+        else:
+            tol = (0.999, 0.05) if arch.startswith("vgg") else (0.99, 0.15)
+            out["ok"] = bool(same == 0.0 and out["grad_cos"] > tol[0] and out["grad_rel_err"] < tol[1])
         print("DPCASE " + json.dumps(out), flush=True)
     m.impl.close()
     dist.barrier()

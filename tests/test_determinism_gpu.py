@@ -1,0 +1,54 @@
+"""IDC_DETERMINISTIC=1 (SURVEY §5 race detection / reproducibility): every float reduction of the
+fused step has a fixed order — per-workgroup private statistic slots collapsed in order, per-slice
+weight-gradient partials reduced in order, no LDS float atomics, fixed tiles — so the same program
+on the same inputs gives the same bits.  Checked against the eager fp32 reference as well, so the
+deterministic kernels are also correct ones.  Reference: ``dist_model_tf_dense.py:131-144``."""
+import copy
+
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+DEV = torch.device("cuda", 0)
+
+
+def _model(arch, seed=0):
+    from idc_models_amd.engine import Model, RMSprop
+    from idc_models_amd.models import build_model
+    net = build_model(arch, None, num_outputs=1, seed=seed)
+    ref = copy.deepcopy(net).to(DEV)
+    m = Model(net, device=DEV)
+    m.compile(RMSprop(1e-3), "binary_crossentropy", [], backend="fused")
+    return m, ref
+
+
+@pytest.mark.parametrize("arch,B", [("densenet121", 64), ("vgg16", 32)])
+def test_deterministic_mode_is_bitwise_reproducible(monkeypatch, arch, B):
+    monkeypatch.setenv("IDC_DETERMINISTIC", "1")
+    g = torch.Generator().manual_seed(3)
+    H = 50
+    x = torch.randint(0, 256, (B, H, H, 3), generator=g, dtype=torch.uint8)
+    y = torch.randint(0, 2, (B,), generator=g)
+    m1, ref = _model(arch)
+    p = m1.impl._prog(B, True, torch.uint8)
+    grads = []
+    for _ in range(2):  # the same program twice
+        m1.impl._stage_inputs(p, x, y)
+        p.run_segment("fwd")
+        p.run_segment("bwd")
+        torch.cuda.synchronize()
+        grads.append(m1.arena.grad.clone())
+    assert torch.equal(grads[0], grads[1])
+    # and still the right gradients: per parameter vs the eager fp32 reference, within the bf16
+    # autocast precision floor (the same criterion as the non-deterministic fused tests)
+    from tests.test_fused_gpu import _check
+    _check(m1, ref, x, y)
+    # two independent models / programs, two full training steps each: identical weights
+    m2, _ = _model(arch)
+    for _ in range(2):
+        m1.impl.train_step(x, y)
+        m2.impl.train_step(x, y)
+    torch.cuda.synchronize()
+    for a, b in zip(m1.net.trainable_weights, m2.net.trainable_weights):
+        assert torch.equal(a, b)

@@ -23,8 +23,9 @@ def _free_port():
 
 @pytest.mark.timeout(600)
 def test_fused_data_parallel_two_ranks_on_one_gpu(tmp_path):
+    # deterministic reductions: the DP gradient must equal the single-process shard sum EXACTLY
     env = dict(os.environ, IDC_AUTOTUNE="0", HSA_ENABLE_IPC_MODE_LEGACY="0", OMP_NUM_THREADS="4",
-               PYTHONUNBUFFERED="1")
+               PYTHONUNBUFFERED="1", IDC_DETERMINISTIC="1")
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
            "--master-addr", "127.0.0.1", "--master-port", str(_free_port()),
            os.path.join(ROOT, "tests", "dp_worker.py"),
