@@ -132,7 +132,7 @@ def main():
     # mostly at their init after a few dozen steps (0.99^36 = 0.70), so a short fit evaluates stale
     # statistics; 0.99^320 = 0.04
     ap.add_argument("--fit-steps", type=int, default=20, help="global batches per fit epoch (0: skip fit/AUC)")
-    ap.add_argument("--fit-epochs", type=int, default=16)
+    ap.add_argument("--fit-epochs", type=int, default=48)
     ap.add_argument("--mode", default="train", choices=["train", "fedavg", "secure"],
                     help="train: the headline DP step; fedavg / secure: north-star configs #4 / #5")
     ap.add_argument("--clients", type=int, default=8)
@@ -203,7 +203,7 @@ def main():
 
     # ---- after the timed region: fit() throughput and held-out validation AUC ----------------
     fit_ips = val_auc = val_acc = None
-    if args.fit_steps > 0:
+    if args.fit_steps > 0 and args.fit_epochs > 0:
         gb = args.batch * world
         train = synthetic_dataset(gb * args.fit_steps, (H, W, C), 2, seed=11)
         held = synthetic_dataset(max(gb * 2, 1024), (H, W, C), 2, seed=12)
