@@ -121,6 +121,24 @@ __device__ __forceinline__ int xcd_remap(int bid, int nblocks) {
   return base + bid / nx;
 }
 
+// Kernel arguments reach the waves through the scalar cache, one 64-B line per miss, and the
+// compiler loads each field where it is first used (then waits for it).  The conv / wgrad / pool
+// descriptors are 300-650 B and are read in several phases (prologue tables, K loop, epilogue,
+// statistics), so each phase paid a dependent miss on the kernarg segment: with kernargs moved to
+// host memory (HIP_FORCE_DEV_KERNARG=0) a small backward conv took +6 us, i.e. several serial
+// misses per launch.  Touching every line once at entry, all loads in flight together, turns
+// those into one round trip that overlaps the first tile loads.
+template <int BYTES>
+__device__ __forceinline__ void prefetch_kernargs() {
+  const unsigned* p = (const unsigned*)__builtin_amdgcn_kernarg_segment_ptr();
+  constexpr int L = (BYTES + 63) / 64;
+  unsigned v[L];
+#pragma unroll
+  for (int i = 0; i < L; ++i) v[i] = p[i * 16];
+#pragma unroll
+  for (int i = 0; i < L; ++i) asm volatile("" ::"s"(v[i]));
+}
+
 // BatchNorm descriptor shared by every kernel that applies a BN affine (+activation) to an
 // operand on the fly ("pending BN").  mode 1: batch statistics from `stats` ([sum|sumsq] over
 // `count` samples); mode 2: inference (moving statistics).  mode 0: identity (act only).
@@ -396,6 +414,61 @@ __device__ __forceinline__ void bwd_aff_table(const BwdAff& b, int c0, int n, in
     sB[i] = Bc;
     sC[i] = -g * rstd * sd - Bc * mean;
   }
+}
+
+// Batched table inputs for launches whose statistics have at most 4 slot copies (every layer with
+// <= 16K rows: DenseNet stages 2-4).  The general table builders above branch on the runtime slot
+// count and wait for each array's loads before the next array's are issued, so a backward conv
+// with a pending-affine prologue and an epilogue BatchNorm paid three to four dependent memory
+// round trips before its K loop (tools/micro/conv_phases.hip: ~6k shader cycles for the prologue
+// table alone).  Here every load of every table a thread builds is issued first (4 clamped slot
+// loads per array, unconditional), then everything is combined: one round trip.
+struct Raw4 {
+  float a0[4], a1[4];
+};
+__device__ __forceinline__ void load4(const float* p0, const float* p1, int S, size_t stride, int c, Raw4& r) {
+#pragma unroll
+  for (int s = 0; s < 4; ++s) {
+    const size_t o = (size_t)(s < S ? s : S - 1) * stride + c;
+    r.a0[s] = p0[o];
+    r.a1[s] = p1[o];
+  }
+}
+__device__ __forceinline__ void sum4(const Raw4& r, int S, float& v0, float& v1) {
+  v0 = r.a0[0];
+  v1 = r.a1[0];
+#pragma unroll
+  for (int s = 1; s < 4; ++s) {
+    v0 += s < S ? r.a0[s] : 0.f;
+    v1 += s < S ? r.a1[s] : 0.f;
+  }
+}
+__device__ __forceinline__ bool bn_slots4(const BnArgs& b) { return b.mode != 1 || stat_slots(b.slots) <= 4; }
+__device__ __forceinline__ bool bwd_aff_slots4(const BwdAff& b) {
+  return b.mode == 0 || b.bn.mode != 1 || (stat_slots(b.bn.slots) <= 4 && stat_slots(b.gsum_slots) <= 4);
+}
+
+// raw inputs of one channel of a BwdAff table (training-mode BatchNorm, <= 4 slots)
+struct BwdAffRaw {
+  Raw4 st, gs;
+  float g;
+};
+__device__ __forceinline__ void bwd_aff_load(const BwdAff& b, int c, BwdAffRaw& r) {
+  load4(b.bn.stats, b.bn.stats + b.bn.C, stat_slots(b.bn.slots), 2 * (size_t)b.bn.C, c, r.st);
+  load4(b.gsum, b.gsumx, stat_slots(b.gsum_slots), (size_t)b.gsum_ld, c, r.gs);
+  r.g = b.bn.gamma ? b.bn.gamma[c] : 1.f;
+}
+__device__ __forceinline__ void bwd_aff_finish(const BwdAff& b, const BwdAffRaw& r, float& A, float& B, float& C) {
+  float m0, m1, q0, q1;
+  sum4(r.st, stat_slots(b.bn.slots), m0, m1);
+  sum4(r.gs, stat_slots(b.gsum_slots), q0, q1);
+  const float mean = m0 * b.bn.inv_count;
+  const float var = fmaxf(m1 * b.bn.inv_count - mean * mean, 0.f);
+  const float rstd = rsqrtf(var + b.bn.eps);
+  const float Bc = -r.g * rstd * rstd * (q1 * b.inv_n);
+  A = b.unit_alpha ? 1.f : r.g * rstd;
+  B = Bc;
+  C = -r.g * rstd * (q0 * b.inv_n) - Bc * mean;
 }
 
 // d beta / d gamma of the BatchNorm: sum of the slot copies, once per step, spread over the

@@ -34,6 +34,11 @@
 #include "common.h"
 #include "conv_igemm.h"
 
+// phase timestamps for tools/micro/conv_phases.hip (compiled out everywhere else)
+#ifndef IDC_PHASE_STAMP
+#define IDC_PHASE_STAMP(i)
+#endif
+
 namespace idc {
 
 template <int BK>
@@ -51,8 +56,17 @@ struct IgemmCfg {
   static constexpr int A_ELEMS = BM * BK, B_ELEMS = BN * BK;
   static constexpr int STAGE_BYTES = 2 * (A_ELEMS + B_ELEMS) * 2;
   static constexpr int CS_LD = BN + 4;
-  static constexpr int EPI_BYTES = WTM * CS_LD * 4;  // one wave-row of the tile per pass
-  static constexpr int MAIN = STAGE_BYTES > EPI_BYTES ? STAGE_BYTES : EPI_BYTES;
+  // epilogue staging: the whole fp32 tile in one pass when it fits the staging buffers (or 20 KB),
+  // else one wave-row of the tile per pass
+  static constexpr int FULL_BYTES = BM * CS_LD * 4;
+  static constexpr int NPASS = FULL_BYTES <= (STAGE_BYTES > 20480 ? STAGE_BYTES : 20480) ? 1 : WM;
+  static constexpr int PROWS = BM / NPASS;
+  static constexpr int EPI_BYTES = PROWS * CS_LD * 4;
+  // statistics: every thread's 16 partials, transposed reduction (row stride 20 floats)
+  static constexpr int RED_LD = 20;
+  static constexpr int RED_BYTES = NT * RED_LD * 4;
+  static constexpr int MAIN0 = STAGE_BYTES > EPI_BYTES ? STAGE_BYTES : EPI_BYTES;
+  static constexpr int MAIN = MAIN0 > RED_BYTES ? MAIN0 : RED_BYTES;
   static int smem_bytes(int cpro) {
     int t = (cpro + 3) / 4 * 4;
     return MAIN + 3 * t * 4 + 10 * BN * 4;
@@ -61,6 +75,8 @@ struct IgemmCfg {
 
 template <int BM, int BN, int BK, int WM, int WN, bool IS1X1, typename TA, int PRO, int EPI>
 __global__ __launch_bounds__(256) void conv_igemm_kernel(ConvArgs a) {
+  IDC_PHASE_STAMP(0);
+  prefetch_kernargs<sizeof(ConvArgs)>();
   using C = IgemmCfg<BM, BN, BK, WM, WN>;
   constexpr int NT = C::NT, CPR = C::CPR, WTM = C::WTM, WTN = C::WTN;
   constexpr int NA = (BM * CPR + NT - 1) / NT;  // A chunks per thread
@@ -68,8 +84,9 @@ __global__ __launch_bounds__(256) void conv_igemm_kernel(ConvArgs a) {
   constexpr int TM = WTM / 16, TN = WTN / 16;
   constexpr int A_ELEMS = C::A_ELEMS, B_ELEMS = C::B_ELEMS, CS_LD = C::CS_LD;
   static_assert(TM >= 1 && TN >= 1, "bad wave tile");
-  static_assert(C::MAIN >= 8 * BN * 4, "statistics partials alias the staging tile");
+  static_assert(NT / (2 * BN) <= 4 && NT % (2 * BN) == 0, "statistics reducer layout");
   static_assert(NT % CPR == 0, "chunk mapping");
+  static_assert(BN <= NT, "one epilogue channel per thread in the table builders");
 
   extern __shared__ __attribute__((aligned(16))) char smem[];
   bf16_t* As = reinterpret_cast<bf16_t*>(smem);
@@ -297,48 +314,111 @@ __global__ __launch_bounds__(256) void conv_igemm_kernel(ConvArgs a) {
   load_tile(st0);
   advance_k();
   load_tile(st1);
+  IDC_PHASE_STAMP(1);
   // ---- prologue tables ----
   if constexpr (PRO == 1) bn_coeff_table<NT>(a.pro, a.Cin, s_scale, s_shift);
-  if constexpr (PRO == 2) {
-    bwd_aff_table<NT>(a.bpro, 0, a.Cin, a.Cin, s_scale, s_shift, s_third);
-    bwd_aff_fold<NT>(a.bpro);
+  // backward tables (pending-affine prologue, epilogue BatchNorm, epilogue pending affine): one
+  // batched round trip when every statistic has <= 4 slot copies (common.h "Batched table inputs")
+  bool batched = false;
+  if constexpr (PRO == 2 || EPI >= 1) {
+    batched = (PRO != 2 || (a.Cin <= NT && (!a.bpro.mode || (a.bpro.bn.mode == 1 && bwd_aff_slots4(a.bpro))))) &&
+              (EPI != 2 || !a.bepi.mode || (a.bepi.bn.mode == 1 && bwd_aff_slots4(a.bepi))) &&
+              (EPI < 1 || bn_slots4(a.mbn));
   }
-  if constexpr (EPI == 2) bwd_aff_table<NT>(a.bepi, n0, BN, a.Cout, s_pa, s_pb, s_pc);
-  if constexpr (EPI >= 1) {
-    for (int j = tid; j < BN; j += NT) {
-      int c = n0 + j;
-      float sc = 1.f, sh = 0.f, mean = 0.f, rstd = 1.f;
-      if (c < a.Cout && a.mbn.mode) {
-        bn_mean_rstd(a.mbn, c, mean, rstd);
-        const float g = a.mbn.gamma ? a.mbn.gamma[c] : 1.f;
-        const float be = a.mbn.beta ? a.mbn.beta[c] : 0.f;
-        sc = g * rstd;
-        sh = be - mean * sc;
+  if (batched) {
+    const int cp = tid < a.Cin ? tid : 0;           // PRO 2 channel of this thread
+    const int ce = n0 + tid < a.Cout ? n0 + tid : 0;  // epilogue channel (BN <= NT)
+    BwdAffRaw rp, re2;
+    Raw4 rm;
+    float mg = 1.f, mb = 0.f;
+    if constexpr (PRO == 2) {
+      if (a.bpro.mode) bwd_aff_load(a.bpro, cp, rp);
+    }
+    if constexpr (EPI == 2) {
+      if (a.bepi.mode) bwd_aff_load(a.bepi, ce, re2);
+    }
+    if constexpr (EPI >= 1) {
+      if (a.mbn.mode == 1) load4(a.mbn.stats, a.mbn.stats + a.mbn.C, stat_slots(a.mbn.slots), 2 * (size_t)a.mbn.C, ce, rm);
+      else if (a.mbn.mode == 2) { rm.a0[0] = a.mbn.mmean[ce]; rm.a1[0] = a.mbn.mvar[ce]; }
+      if (a.mbn.mode) {
+        mg = a.mbn.gamma ? a.mbn.gamma[ce] : 1.f;
+        mb = a.mbn.beta ? a.mbn.beta[ce] : 0.f;
       }
-      s_e0[j] = sc; s_e1[j] = sh; s_e2[j] = mean; s_e3[j] = rstd;
+    }
+    if constexpr (PRO == 2) {
+      if (tid < a.Cin) {
+        float A = 1.f, B = 0.f, Cc = 0.f;
+        if (a.bpro.mode) bwd_aff_finish(a.bpro, rp, A, B, Cc);
+        s_scale[tid] = A; s_shift[tid] = B; s_third[tid] = Cc;
+      }
+    }
+    if (tid < BN) {
+      if constexpr (EPI == 2) {
+        float A = 1.f, B = 0.f, Cc = 0.f;
+        if (a.bepi.mode && n0 + tid < a.Cout) bwd_aff_finish(a.bepi, re2, A, B, Cc);
+        s_pa[tid] = A; s_pb[tid] = B; s_pc[tid] = Cc;
+      }
+      if constexpr (EPI >= 1) {
+        float sc = 1.f, sh = 0.f, mean = 0.f, rstd = 1.f;
+        if (n0 + tid < a.Cout && a.mbn.mode) {
+          float v0, v1 = rm.a1[0];
+          if (a.mbn.mode == 1) {
+            sum4(rm, stat_slots(a.mbn.slots), v0, v1);
+            mean = v0 * a.mbn.inv_count;
+            v1 = fmaxf(v1 * a.mbn.inv_count - mean * mean, 0.f);
+          } else {
+            mean = rm.a0[0];
+          }
+          rstd = rsqrtf(v1 + a.mbn.eps);
+          sc = mg * rstd;
+          sh = mb - mean * sc;
+        }
+        s_e0[tid] = sc; s_e1[tid] = sh; s_e2[tid] = mean; s_e3[tid] = rstd;
+      }
+    }
+  } else {
+    if constexpr (PRO == 2) bwd_aff_table<NT>(a.bpro, 0, a.Cin, a.Cin, s_scale, s_shift, s_third);
+    IDC_PHASE_STAMP(2);
+    if constexpr (EPI == 2) bwd_aff_table<NT>(a.bepi, n0, BN, a.Cout, s_pa, s_pb, s_pc);
+    IDC_PHASE_STAMP(3);
+    if constexpr (EPI >= 1) {
+      for (int j = tid; j < BN; j += NT) {
+        int c = n0 + j;
+        float sc = 1.f, sh = 0.f, mean = 0.f, rstd = 1.f;
+        if (c < a.Cout && a.mbn.mode) {
+          bn_mean_rstd(a.mbn, c, mean, rstd);
+          const float g = a.mbn.gamma ? a.mbn.gamma[c] : 1.f;
+          const float be = a.mbn.beta ? a.mbn.beta[c] : 0.f;
+          sc = g * rstd;
+          sh = be - mean * sc;
+        }
+        s_e0[j] = sc; s_e1[j] = sh; s_e2[j] = mean; s_e3[j] = rstd;
+      }
     }
   }
-  for (int j = tid; j < BN; j += NT) { s_sum[j] = 0.f; s_sq[j] = 0.f; }
+  if constexpr (PRO == 2) bwd_aff_fold<NT>(a.bpro);
+  IDC_PHASE_STAMP(4);
 
   // Epilogue operands (the forward input x for the activation mask / x-hat, and the old fp32
   // accumulator of epilogue 2) do not depend on the GEMM: issue them now, youngest of all, so
   // their memory latency hides under the K loop instead of adding a dependent round trip after
   // it (the small late-stage GEMMs are latency chains).  Up to 4 chunks per thread.
   constexpr int CPB = BN / 8;
-  constexpr int EPI_IT = (WTM * CPB + NT - 1) / NT;
-  constexpr bool EPF = (EPI >= 1) && (WM * EPI_IT <= 4);
-  constexpr int NEP = EPF ? WM * EPI_IT : 1;
+  constexpr int NPASS = C::NPASS, PROWS = C::PROWS;
+  constexpr int EPI_IT = (PROWS * CPB + NT - 1) / NT;
+  constexpr bool EPF = (EPI >= 1) && (NPASS * EPI_IT <= 4);
+  constexpr int NEP = EPF ? NPASS * EPI_IT : 1;
   uint4 ep_x[NEP];
   float4 ep_o0[EPI == 2 ? NEP : 1], ep_o1[EPI == 2 ? NEP : 1];
   if constexpr (EPF) {
 #pragma unroll
-    for (int pass = 0; pass < WM; ++pass)
+    for (int pass = 0; pass < NPASS; ++pass)
 #pragma unroll
       for (int it = 0; it < EPI_IT; ++it) {
         const int idx = tid + it * NT;
         const int lrow = idx / CPB, c8 = idx % CPB;
-        const int m = m0 + pass * WTM + lrow, n = n0 + c8 * 8;
-        const bool ok = idx < WTM * CPB && m < M && n < a.Cout;
+        const int m = m0 + pass * PROWS + lrow, n = n0 + c8 * 8;
+        const bool ok = idx < PROWS * CPB && m < M && n < a.Cout;
         const size_t mm = ok ? (size_t)m : 0, nn = ok ? (size_t)n : 0;
         ep_x[pass * EPI_IT + it] = *reinterpret_cast<const uint4*>(a.mx + mm * a.ldmx + nn);
         if constexpr (EPI == 2) {
@@ -349,9 +429,11 @@ __global__ __launch_bounds__(256) void conv_igemm_kernel(ConvArgs a) {
       }
   }
 
+  IDC_PHASE_STAMP(5);
   __syncthreads();  // prologue tables visible
   store_tile(st0, 0);
   __syncthreads();
+  IDC_PHASE_STAMP(6);
 
   const int frow = lane & 15;
   const int fk = lane >> 4;
@@ -404,6 +486,7 @@ __global__ __launch_bounds__(256) void conv_igemm_kernel(ConvArgs a) {
     compute(0);  // odd tile count: the last tile sits in LDS0
     __syncthreads();  // the epilogue's fp32 staging tile aliases LDS0
   }
+  IDC_PHASE_STAMP(7);
 
   // ---- split-K: publish this slice's partial tile; the last arriver of the tile reduces ------
   // (guide §5 "In-launch split-K reduction": plain stores -> every wave vmcnt(0) -> barrier ->
@@ -465,34 +548,35 @@ __global__ __launch_bounds__(256) void conv_igemm_kernel(ConvArgs a) {
     }
   }
 
-  // ---- epilogue: WM passes, each stages one wave-row (WTM x BN) of fp32 results in LDS ------
+  // ---- epilogue: NPASS passes, each stages PROWS x BN fp32 results in LDS -------------------
   const bool want_stats = (EPI >= 1) || (a.stats_out != nullptr);
   float psum[8], psq[8];
 #pragma unroll
   for (int j = 0; j < 8; ++j) { psum[j] = 0.f; psq[j] = 0.f; }
-  const int my_c8 = tid % CPB;
 
 #pragma unroll
-  for (int pass = 0; pass < WM; ++pass) {
+  for (int pass = 0; pass < NPASS; ++pass) {
     if (pass) __syncthreads();
-    if (wr == pass) {
+    if (pass == 0) IDC_PHASE_STAMP(11);
+    if ((wr * WTM) / PROWS == pass) {
 #pragma unroll
       for (int i = 0; i < TM; ++i)
 #pragma unroll
         for (int j = 0; j < TN; ++j) {
           int col = wc * WTN + j * 16 + (lane & 15);
-          int rbase = i * 16 + (lane >> 4) * 4;
+          int rbase = (wr * WTM) % PROWS + i * 16 + (lane >> 4) * 4;
 #pragma unroll
           for (int r = 0; r < 4; ++r) Cs[(rbase + r) * CS_LD + col] = acc[i][j][r];
         }
     }
     __syncthreads();
+    if (pass == 0) IDC_PHASE_STAMP(12);
 #pragma unroll
     for (int it = 0; it < EPI_IT; ++it) {
       const int idx = tid + it * NT;
-      if (idx >= WTM * CPB) break;
+      if (idx >= PROWS * CPB) break;
       int lrow = idx / CPB, c8 = idx % CPB;
-      int m = m0 + pass * WTM + lrow, n = n0 + c8 * 8;
+      int m = m0 + pass * PROWS + lrow, n = n0 + c8 * 8;
       if (m >= M || n >= a.Cout) continue;
       float v[8];
       const float4 lo = *reinterpret_cast<const float4*>(&Cs[lrow * CS_LD + c8 * 8]);
@@ -583,41 +667,46 @@ __global__ __launch_bounds__(256) void conv_igemm_kernel(ConvArgs a) {
       }
     }
   }
+  IDC_PHASE_STAMP(8);
   if (want_stats) {
-    wave_reduce_chunks<CPB>(psum);
-    wave_reduce_chunks<CPB>(psq);
-    // per-wave partials -> fixed-order sum over the 4 waves (no LDS float atomics: the block's
-    // statistics are bitwise reproducible; the staging tile's LDS is free after the last pass)
+    // transposed reduction: every thread's 16 partials (its chunk's 8 column sums and sums of
+    // squares) to LDS, then Q = NT/(2*BN) threads per output sum 16 contributions each in a fixed
+    // order and combine over their quad with DPP; deterministic, two barriers, no shuffles
+    __syncthreads();  // the staging tile is dead
+    IDC_PHASE_STAMP(13);
+    float* s_red = reinterpret_cast<float*>(smem);
+    {
+      float4* d = reinterpret_cast<float4*>(s_red + tid * C::RED_LD);
+      d[0] = make_float4(psum[0], psum[1], psum[2], psum[3]);
+      d[1] = make_float4(psum[4], psum[5], psum[6], psum[7]);
+      d[2] = make_float4(psq[0], psq[1], psq[2], psq[3]);
+      d[3] = make_float4(psq[4], psq[5], psq[6], psq[7]);
+    }
     __syncthreads();
-    float* s_part = reinterpret_cast<float*>(smem);  // [4 waves][2][BN]
-    if ((tid & 63) < CPB) {
-      const bool part = (tid & ~63) < WTM * CPB;
+    IDC_PHASE_STAMP(14);
+    constexpr int Q = NT / (2 * BN);
+    const int o = tid / Q, q = tid % Q;
+    const int kind = o / BN, col = o % BN;
+    const int base = (col >> 3) * C::RED_LD + kind * 8 + (col & 7);
+    float v = 0.f;
 #pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        s_part[wid * 2 * BN + my_c8 * 8 + j] = part ? psum[j] : 0.f;
-        s_part[wid * 2 * BN + BN + my_c8 * 8 + j] = part ? psq[j] : 0.f;
-      }
-    }
-    __syncthreads();
-    for (int j = tid; j < BN; j += NT) {
-      s_sum[j] = ((s_part[j] + s_part[2 * BN + j]) + s_part[4 * BN + j]) + s_part[6 * BN + j];
-      s_sq[j] = ((s_part[BN + j] + s_part[3 * BN + j]) + s_part[5 * BN + j]) + s_part[7 * BN + j];
-    }
-    __syncthreads();
-    const size_t so = EPI == 0 ? (size_t)(mt % stat_slots(a.stats_slots)) * 2 * a.stats_ld
-                               : (size_t)(mt % stat_slots(a.gsum_slots)) * a.gsum_ld;
-    for (int j = tid; j < BN; j += NT) {
-      int c = n0 + j;
-      if (c >= a.Cout) continue;
+    for (int i = 0; i < 16; ++i) v += s_red[base + (i * Q + q) * CPB * C::RED_LD];
+    if constexpr (Q >= 2) v += __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0xB1, 0xF, 0xF, true));
+    if constexpr (Q >= 4) v += __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0x4E, 0xF, 0xF, true));
+    IDC_PHASE_STAMP(9);
+    const int c = n0 + col;
+    if (q == 0 && c < a.Cout) {
       if constexpr (EPI == 0) {
-        atomicAdd(&a.stats_out[so + a.stats_off + c], s_sum[j]);
-        atomicAdd(&a.stats_out[so + a.stats_ld + a.stats_off + c], s_sq[j]);
+        const size_t so = (size_t)(mt % stat_slots(a.stats_slots)) * 2 * a.stats_ld;
+        atomicAdd(&a.stats_out[so + (kind ? a.stats_ld : 0) + a.stats_off + c], v);
       } else {
-        if (a.gsum) atomicAdd(&a.gsum[so + c], s_sum[j]);
-        if (a.gsumx) atomicAdd(&a.gsumx[so + c], s_sq[j]);
+        const size_t so = (size_t)(mt % stat_slots(a.gsum_slots)) * a.gsum_ld;
+        float* g = kind ? a.gsumx : a.gsum;
+        if (g) atomicAdd(&g[so + c], v);
       }
     }
   }
+  IDC_PHASE_STAMP(10);
 }
 
 // ----------------------------------------------------------------------------------------------

@@ -62,6 +62,7 @@ __device__ __forceinline__ v8bf tr_frag(const bf16_t* tile, int col_base, int la
 
 template <int BKR, int BC, int BP_, int WM, int WN, bool IS1X1, typename TG, int PRO, int GPRO>
 __global__ __launch_bounds__(256) void conv_wgrad_kernel(WgradArgs a) {
+  prefetch_kernargs<sizeof(WgradArgs)>();
   using C = WgCfg<BKR, BC, BP_>;
   constexpr int NT = C::NT, BP = C::BP;
   constexpr int WTM = BKR / WM, WTN = BC / WN;

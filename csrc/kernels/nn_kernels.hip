@@ -136,6 +136,7 @@ __device__ __forceinline__ void chunk_reduce(const ChunkMap& cm, int C, const fl
 // the destination type / accumulate mode as template parameters so the loop is branch-free.
 template <bool F32, bool ACC>
 __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(BnBwdApplyArgs a) {
+  prefetch_kernargs<sizeof(BnBwdApplyArgs)>();
   constexpr int RU = 4;
   extern __shared__ float sh[];
   float* sA = sh;
@@ -280,6 +281,7 @@ hipError_t bn_bwd_apply(const BnBwdApplyArgs& a, hipStream_t st) {
 
 // ------------------------------------------------------------------------------------------
 __global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(BnBwdReduceArgs a) {
+  prefetch_kernargs<sizeof(BnBwdReduceArgs)>();
   extern __shared__ float sh[];
   float* s_sc = sh;
   float* s_sh = sh + a.C;
@@ -333,6 +335,7 @@ hipError_t bn_bwd_reduce(const BnBwdReduceArgs& a, hipStream_t st) {
 // ------------------------------------------------------------------------------------------
 template <bool IS_MAX, int K>
 __global__ __launch_bounds__(256) void pool_fwd_kernel(PoolArgs a) {
+  prefetch_kernargs<sizeof(PoolArgs)>();
   extern __shared__ float sh[];
   float* s_sc = sh;
   float* s_sh = sh + a.C;
@@ -443,6 +446,7 @@ hipError_t avgpool_fwd(const PoolArgs& a, hipStream_t st) { return pool_fwd<fals
 // rows (every window's dy / argmax, and x) before any arithmetic.
 template <int WIN, int RU>
 __global__ __launch_bounds__(256) void pool_bwd_kernel(PoolBwdArgs a) {
+  prefetch_kernargs<sizeof(PoolBwdArgs)>();
   extern __shared__ float sh[];
   float* s_sc = sh;
   float* s_sh = sh + a.C;
@@ -622,6 +626,7 @@ hipError_t bn_update_moving(const BnMovingDesc* d, int n, int maxC, hipStream_t 
 // ------------------------------------------------------------------------------------------
 // head forward: one block per sample
 __global__ __launch_bounds__(256) void head_fwd_kernel(HeadArgs a) {
+  prefetch_kernargs<sizeof(HeadArgs)>();
   extern __shared__ float sh[];
   float* s_feat = sh;            // [C]
   float* s_red = sh + a.C;       // [U][4 waves]
@@ -694,6 +699,7 @@ hipError_t head_fwd(const HeadArgs& a, hipStream_t st) {
 // form — left 16 blocks looping over all 256 samples: ~50 us for a 1 us job.)
 template <int HB>
 __global__ __launch_bounds__(256) void head_bwd_kernel(HeadBwdArgs a) {
+  prefetch_kernargs<sizeof(HeadBwdArgs)>();
   __shared__ float s_dw[4][64][17];
   __shared__ float s_dl[HB][16];
   const int c0 = blockIdx.x * 64;

@@ -94,7 +94,6 @@ const T& as(const Op& op) {
 class Plan {
  public:
   ~Plan() {
-    if (std::getenv("IDC_PLAN_LEAK")) return;  // debugging aid: never release HIP objects
     clear_graphs();
     if (fork_) hipEventDestroy(fork_);
     if (join_) hipEventDestroy(join_);

@@ -22,9 +22,6 @@ from ..utils import trace
 from .builder import Builder
 
 
-_GRAVEYARD = []  # IDC_KEEP_BUFFERS=1 (debugging aid): never free a program's device buffers
-
-
 def _lowering_for(net):
     from ..models import Sequential
     from ..models.densenet import DenseNet
@@ -77,8 +74,6 @@ class FusedProgram:
             b.segment = "bwd"
             b.flush_grad_sums()
         self.b = b
-        if os.environ.get("IDC_KEEP_BUFFERS") == "1":
-            _GRAVEYARD.append(b.keep)
         self.xin = b.xin
         self.io = b.io
         b.finalize_casts()
