@@ -468,23 +468,46 @@ __global__ __launch_bounds__(256) void conv_igemm_kernel(ConvArgs a) {
   // writes land in a buffer that is never read again).  Conditional load/store pairs made the
   // waitcnt pass drain vmcnt(0) at the loop back-edge, serialising the prefetch.
   int kt = 0;
-  for (; kt + 2 <= nk; kt += 2) {
-    // even step: compute LDS0 (tile kt), st1 holds kt+1, reload st0 with kt+2
+  if (nk >= 4) {
+    for (; kt + 2 <= nk; kt += 2) {
+      // even step: compute LDS0 (tile kt), st1 holds kt+1, reload st0 with kt+2
+      advance_k();
+      load_tile(st0);
+      compute(0);
+      store_tile(st1, 1);
+      __syncthreads();
+      // odd step: compute LDS1 (tile kt+1), st0 holds kt+2, reload st1 with kt+3
+      advance_k();
+      load_tile(st1);
+      compute(1);
+      store_tile(st0, 0);
+      __syncthreads();
+    }
+    if (kt < nk) {
+      compute(0);  // odd tile count: the last tile sits in LDS0
+      __syncthreads();  // the epilogue's fp32 staging tile aliases LDS0
+    }
+  } else if (nk == 3) {
+    // short K (the small late layers): straight-line, no load issued or waited for past the end
     advance_k();
     load_tile(st0);
     compute(0);
     store_tile(st1, 1);
     __syncthreads();
-    // odd step: compute LDS1 (tile kt+1), st0 holds kt+2, reload st1 with kt+3
-    advance_k();
-    load_tile(st1);
     compute(1);
     store_tile(st0, 0);
     __syncthreads();
-  }
-  if (kt < nk) {
-    compute(0);  // odd tile count: the last tile sits in LDS0
-    __syncthreads();  // the epilogue's fp32 staging tile aliases LDS0
+    compute(0);
+    __syncthreads();
+  } else if (nk == 2) {
+    compute(0);
+    store_tile(st1, 1);
+    __syncthreads();
+    compute(1);
+    __syncthreads();
+  } else if (nk == 1) {
+    compute(0);
+    __syncthreads();
   }
   IDC_PHASE_STAMP(7);
 
@@ -553,6 +576,21 @@ __global__ __launch_bounds__(256) void conv_igemm_kernel(ConvArgs a) {
   float psum[8], psq[8];
 #pragma unroll
   for (int j = 0; j < 8; ++j) { psum[j] = 0.f; psq[j] = 0.f; }
+  // a thread's 8-channel chunk is the same in every pass (NT % CPB == 0): its per-channel
+  // epilogue coefficients (and bias) are read once into registers
+  const int my_c8 = tid % CPB;
+  float t_e0[8], t_e1[8], t_e2[8], t_e3[8], t_pb[8], t_pc[8], t_bias[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const int cj = my_c8 * 8 + j;
+    if constexpr (EPI >= 1) {
+      t_e0[j] = s_e0[cj]; t_e1[j] = s_e1[cj]; t_e2[j] = s_e2[cj]; t_e3[j] = s_e3[cj];
+    }
+    if constexpr (EPI == 2) {
+      t_pb[j] = s_pb[cj]; t_pc[j] = s_pc[cj];
+    }
+    if constexpr (EPI == 0) t_bias[j] = (a.bias && n0 + cj < a.Cout) ? a.bias[n0 + cj] : 0.f;
+  }
 
 #pragma unroll
   for (int pass = 0; pass < NPASS; ++pass) {
@@ -586,7 +624,7 @@ __global__ __launch_bounds__(256) void conv_igemm_kernel(ConvArgs a) {
       if constexpr (EPI == 0) {
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
-          float t = v[j] + (a.bias ? a.bias[n + j] : 0.f);
+          float t = v[j] + t_bias[j];
           v[j] = clampf(t, epi_lo, epi_hi);
         }
         if (a.out_mode == OUT_BF16) {
@@ -633,12 +671,11 @@ __global__ __launch_bounds__(256) void conv_igemm_kernel(ConvArgs a) {
         unpack8(xv, xf);
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
-          const int cj = c8 * 8 + j;
-          const float z = xf[j] * s_e0[cj] + s_e1[cj];
+          const float z = xf[j] * t_e0[j] + t_e1[j];
           const float d = (z > msk_lo && z < msk_hi) ? v[j] : 0.f;
           psum[j] += d;
-          psq[j] += d * (xf[j] - s_e2[cj]) * s_e3[cj];
-          o[j] = old[j] + fmaf(s_e0[cj], d, fmaf(s_pb[cj], xf[j], s_pc[cj]));
+          psq[j] += d * (xf[j] - t_e2[j]) * t_e3[j];
+          o[j] = old[j] + fmaf(t_e0[j], d, fmaf(t_pb[j], xf[j], t_pc[j]));
         }
         *reinterpret_cast<float4*>(yp) = make_float4(o[0], o[1], o[2], o[3]);
         *reinterpret_cast<float4*>(yp + 4) = make_float4(o[4], o[5], o[6], o[7]);
@@ -650,8 +687,7 @@ __global__ __launch_bounds__(256) void conv_igemm_kernel(ConvArgs a) {
         unpack8(xv, xf);
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
-          int cj = c8 * 8 + j;
-          float z = xf[j] * s_e0[cj] + s_e1[cj];
+          float z = xf[j] * t_e0[j] + t_e1[j];
           d[j] = (z > msk_lo && z < msk_hi) ? v[j] : 0.f;
         }
         uint4 p = pack8(d);
@@ -660,9 +696,8 @@ __global__ __launch_bounds__(256) void conv_igemm_kernel(ConvArgs a) {
         unpack8(p, r);
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
-          int cj = c8 * 8 + j;
           psum[j] += r[j];
-          psq[j] += r[j] * (xf[j] - s_e2[cj]) * s_e3[cj];
+          psq[j] += r[j] * (xf[j] - t_e2[j]) * t_e3[j];
         }
       }
     }

@@ -22,6 +22,9 @@ struct DwArgs {
   float* dw;
   float* ws;
   int stats_slots, gsum_slots, gsum_ld;  // statistics slots (common.h)
+  // bwd data / wgrad (3x3 only): dy is staged through the pending backward of the BatchNorm that
+  // follows this depthwise conv (common.h BwdAff; x = the raw depthwise output at dy's positions)
+  BwdAff dyaff;
 };
 
 long long dwconv_wgrad_ws_floats(long long M, int C, int taps);

@@ -216,13 +216,311 @@ __global__ __launch_bounds__(256) void dw_wgrad_kernel(DwArgs a) {
   for (int k = threadIdx.x; k < T * a.C; k += blockDim.x) atomicAdd(&a.dw[k], s_acc[k]);
 }
 
+// ---- 3x3 strip kernels -------------------------------------------------------------------
+// A thread owns one 8-channel chunk and a strip of P consecutive pixels along W: the 3 x
+// ((P-1)*S + 3) input vectors of the strip are loaded once and feed every output that reads
+// them (stride 1: 18 loads for 4 outputs instead of 36), the chunk's 9 taps and BN coefficients
+// sit in registers for the whole grid-stride loop, the pending BN + activation is a branch-free
+// clamp, and padding taps are masked after the activation (Keras pads the activated tensor).
+constexpr int kDwStrip = 4;
+
+template <int S>
+__global__ __launch_bounds__(256) void dw_fwd3_kernel(DwArgs a) {
+  constexpr int P = kDwStrip, NCOL = (P - 1) * S + 3;
+  extern __shared__ float sh[];
+  float* s_sc = sh;
+  float* s_sf = sh + a.C;
+  float* s_a = sh + 2 * a.C;
+  float* s_b = sh + 3 * a.C;
+  for (int c = threadIdx.x; c < a.C; c += blockDim.x) {
+    bn_coeffs(a.pro, c, s_sc[c], s_sf[c]);
+    s_a[c] = 0.f;
+    s_b[c] = 0.f;
+  }
+  __syncthreads();
+  Map8 mp(a.C);
+  const int WS = (a.Wo + P - 1) / P;
+  const int strips = a.N * a.Ho * WS;
+  if (mp.ty < mp.R) {
+    const int c = mp.tx * 8;
+    float wk[9][8], sc[8], sf[8];
+#pragma unroll
+    for (int t = 0; t < 9; ++t) {
+      const float4 w0 = *reinterpret_cast<const float4*>(a.w + (size_t)t * a.C + c);
+      const float4 w1 = *reinterpret_cast<const float4*>(a.w + (size_t)t * a.C + c + 4);
+      wk[t][0] = w0.x; wk[t][1] = w0.y; wk[t][2] = w0.z; wk[t][3] = w0.w;
+      wk[t][4] = w1.x; wk[t][5] = w1.y; wk[t][6] = w1.z; wk[t][7] = w1.w;
+    }
+#pragma unroll
+    for (int j = 0; j < 8; ++j) { sc[j] = s_sc[c + j]; sf[j] = s_sf[c + j]; }
+    const float lo = act_lo(a.pro.act), hi = act_hi(a.pro.act);
+    float ps[8] = {0}, pq[8] = {0};
+    for (int st = blockIdx.x * mp.R + mp.ty; st < strips; st += gridDim.x * mp.R) {
+      const int ws = st % WS, t = st / WS, ho = t % a.Ho, n = t / a.Ho;
+      const int wo0 = ws * P;
+      float acc[P][8];
+#pragma unroll
+      for (int p = 0; p < P; ++p)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) acc[p][j] = 0.f;
+#pragma unroll
+      for (int r = 0; r < 3; ++r) {
+        const int h = ho * S - a.PT + r;
+        const bool hv = (unsigned)h < (unsigned)a.H;
+        uint4 xv[NCOL];
+#pragma unroll
+        for (int q = 0; q < NCOL; ++q) {
+          const int w = wo0 * S - a.PL + q;
+          const bool v = hv && (unsigned)w < (unsigned)a.W;
+          const size_t pix = v ? ((size_t)(n * a.H + h) * a.W + w) : 0;
+          xv[q] = *reinterpret_cast<const uint4*>(a.x + pix * a.ldx + c);
+        }
+#pragma unroll
+        for (int q = 0; q < NCOL; ++q) {
+          const int w = wo0 * S - a.PL + q;
+          const float m = (hv && (unsigned)w < (unsigned)a.W) ? 1.f : 0.f;
+          float u[8];
+          unpack8(xv[q], u);
+#pragma unroll
+          for (int j = 0; j < 8; ++j) u[j] = fminf(fmaxf(fmaf(u[j], sc[j], sf[j]), lo), hi) * m;
+#pragma unroll
+          for (int p = 0; p < P; ++p) {
+            const int s = q - p * S;
+            if (s >= 0 && s < 3) {
+#pragma unroll
+              for (int j = 0; j < 8; ++j) acc[p][j] = fmaf(u[j], wk[r * 3 + s][j], acc[p][j]);
+            }
+          }
+        }
+      }
+      const size_t ob = (size_t)(n * a.Ho + ho) * a.Wo;
+#pragma unroll
+      for (int p = 0; p < P; ++p) {
+        if (wo0 + p >= a.Wo) break;
+        const uint4 pk = pack8(acc[p]);
+        *reinterpret_cast<uint4*>(a.y + (ob + wo0 + p) * a.ldy + c) = pk;
+        float r8[8];
+        unpack8(pk, r8);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) { ps[j] += r8[j]; pq[j] += r8[j] * r8[j]; }
+      }
+    }
+    if (a.stats) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) { atomicAdd(&s_a[c + j], ps[j]); atomicAdd(&s_b[c + j], pq[j]); }
+    }
+  }
+  if (a.stats) {
+    __syncthreads();
+    float* so = a.stats + (size_t)(blockIdx.x % stat_slots(a.stats_slots)) * 2 * a.stats_ld;
+    for (int c = threadIdx.x; c < a.C; c += blockDim.x) {
+      atomicAdd(&so[c], s_a[c]);
+      atomicAdd(&so[a.stats_ld + c], s_b[c]);
+    }
+  }
+}
+
+// backward data, stride 1: dx[h, w] = sum_{r,s} dy[h+PT-r, w+PL-s] * w[r, s]; a strip of P input
+// pixels reads P+2 dy columns per tap row.  Stride 2 gathers per pixel (the taps that hit an
+// output position depend on parity).  Epilogue: dZ = g * act'(bn(x)), sum dZ, sum dZ*xhat.
+// Stride 2 with left pad PL2 (0 or 1, Keras correct_pad): for a strip of P input pixels starting
+// at an even w0, dy column (w0 >> 1) - 1 + q feeds pixel p through tap s = p + PL2 + 2 - 2q, so
+// which (pixel, column) pairs meet is known at compile time; PL2 < 0 gathers per pixel.
+template <int S, int PL2, bool AFF>
+__global__ __launch_bounds__(256) void dw_bwd3_kernel(DwArgs a) {
+  constexpr bool STRIP = S == 1 || PL2 >= 0;
+  constexpr int P = STRIP ? kDwStrip : 1;
+  constexpr int NCOL = S == 1 ? P + 2 : (PL2 >= 0 ? (P + PL2 + 2) / 2 + 1 : 3);
+  extern __shared__ float sh[];
+  float* s_sc = sh;
+  float* s_sf = sh + a.C;
+  float* s_mu = sh + 2 * a.C;
+  float* s_rs = sh + 3 * a.C;
+  float* s_a = sh + 4 * a.C;
+  float* s_b = sh + 5 * a.C;
+  float* s_fA = sh + 6 * a.C;  // AFF: dy' = A*dy + B*x + C
+  float* s_fB = sh + 7 * a.C;
+  float* s_fC = sh + 8 * a.C;
+  const bool epi = !(a.pro.mode == 0 && a.pro.act == ACT_NONE);
+  for (int c = threadIdx.x; c < a.C; c += blockDim.x) {
+    bn_coeffs(a.pro, c, s_sc[c], s_sf[c]);
+    float mean = 0.f, rstd = 1.f;
+    if (a.pro.mode) bn_mean_rstd(a.pro, c, mean, rstd);
+    s_mu[c] = mean; s_rs[c] = rstd; s_a[c] = 0.f; s_b[c] = 0.f;
+  }
+  if constexpr (AFF) {
+    bwd_aff_table<256>(a.dyaff, 0, a.C, a.C, s_fA, s_fB, s_fC);
+    bwd_aff_fold<256>(a.dyaff);
+  }
+  __syncthreads();
+  Map8 mp(a.C);
+  const int WS = (a.W + P - 1) / P;
+  const int strips = a.N * a.H * WS;
+  if (mp.ty < mp.R) {
+    const int c = mp.tx * 8;
+    float wk[9][8], sc[8], sf[8], mu[8], rs[8], fA[8], fB[8], fC[8];
+#pragma unroll
+    for (int t = 0; t < 9; ++t) {
+      const float4 w0 = *reinterpret_cast<const float4*>(a.w + (size_t)t * a.C + c);
+      const float4 w1 = *reinterpret_cast<const float4*>(a.w + (size_t)t * a.C + c + 4);
+      wk[t][0] = w0.x; wk[t][1] = w0.y; wk[t][2] = w0.z; wk[t][3] = w0.w;
+      wk[t][4] = w1.x; wk[t][5] = w1.y; wk[t][6] = w1.z; wk[t][7] = w1.w;
+    }
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      sc[j] = s_sc[c + j]; sf[j] = s_sf[c + j]; mu[j] = s_mu[c + j]; rs[j] = s_rs[c + j];
+      if constexpr (AFF) { fA[j] = s_fA[c + j]; fB[j] = s_fB[c + j]; fC[j] = s_fC[c + j]; }
+    }
+    const float lo = act_lo(a.pro.act), hi = act_hi(a.pro.act);
+    float ps[8] = {0}, px[8] = {0};
+    for (int st = blockIdx.x * mp.R + mp.ty; st < strips; st += gridDim.x * mp.R) {
+      const int ws = st % WS, t = st / WS, h = t % a.H, n = t / a.H;
+      const int w0 = ws * P;
+      float g[P][8];
+#pragma unroll
+      for (int p = 0; p < P; ++p)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) g[p][j] = 0.f;
+#pragma unroll
+      for (int r = 0; r < 3; ++r) {
+        const int th = h + a.PT - r;
+        int ho;
+        bool hv;
+        if constexpr (S == 1) {
+          ho = th;
+          hv = (unsigned)th < (unsigned)a.Ho;
+        } else {
+          ho = th >> 1;
+          hv = th >= 0 && !(th & 1) && ho < a.Ho;
+        }
+        uint4 dv[NCOL], xv[AFF ? NCOL : 1];
+        float m[NCOL];
+#pragma unroll
+        for (int q = 0; q < NCOL; ++q) {
+          int wo;
+          bool v;
+          if constexpr (S == 1) {
+            wo = w0 + a.PL - 2 + q;  // column q feeds pixel p through tap s = p + 2 - q
+            v = hv && (unsigned)wo < (unsigned)a.Wo;
+          } else if constexpr (PL2 >= 0) {
+            wo = (w0 >> 1) - 1 + q;
+            v = hv && (unsigned)wo < (unsigned)a.Wo;
+          } else {
+            const int tw = w0 + a.PL - q;  // tap s = q
+            wo = tw >> 1;
+            v = hv && tw >= 0 && !(tw & 1) && wo < a.Wo;
+          }
+          m[q] = v ? 1.f : 0.f;
+          const size_t o = v ? ((size_t)(n * a.Ho + ho) * a.Wo + wo) : 0;
+          dv[q] = *reinterpret_cast<const uint4*>(a.dy + o * a.lddy + c);
+          if constexpr (AFF) xv[q] = *reinterpret_cast<const uint4*>(a.dyaff.x + o * a.dyaff.ldx + c);
+        }
+#pragma unroll
+        for (int q = 0; q < NCOL; ++q) {
+          float d[8];
+          unpack8(dv[q], d);
+          if constexpr (AFF) {
+            float xd[8];
+            unpack8(xv[q], xd);
+#pragma unroll
+            for (int j = 0; j < 8; ++j) d[j] = fmaf(fA[j], d[j], fmaf(fB[j], xd[j], fC[j]));
+          }
+#pragma unroll
+          for (int p = 0; p < P; ++p) {
+            const int s = S == 1 ? p + 2 - q : (PL2 >= 0 ? p + PL2 + 2 - 2 * q : q);
+            if (s >= 0 && s < 3) {
+#pragma unroll
+              for (int j = 0; j < 8; ++j) g[p][j] = fmaf(d[j] * m[q], wk[r * 3 + s][j], g[p][j]);
+            }
+          }
+        }
+      }
+      const size_t ib = (size_t)(n * a.H + h) * a.W;
+#pragma unroll
+      for (int p = 0; p < P; ++p) {
+        if (w0 + p >= a.W) break;
+        const size_t i = ib + w0 + p;
+        if (epi) {
+          float x[8];
+          unpack8(*reinterpret_cast<const uint4*>(a.x + i * a.ldx + c), x);
+#pragma unroll
+          for (int j = 0; j < 8; ++j) {
+            const float z = fmaf(x[j], sc[j], sf[j]);
+            g[p][j] = (z > lo && z < hi) ? g[p][j] : 0.f;
+          }
+          const uint4 pk = pack8(g[p]);
+          *reinterpret_cast<uint4*>(a.dx + i * a.lddx + c) = pk;
+          float r8[8];
+          unpack8(pk, r8);
+#pragma unroll
+          for (int j = 0; j < 8; ++j) { ps[j] += r8[j]; px[j] += r8[j] * (x[j] - mu[j]) * rs[j]; }
+        } else {
+          *reinterpret_cast<uint4*>(a.dx + i * a.lddx + c) = pack8(g[p]);
+        }
+      }
+    }
+    if (epi) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) { atomicAdd(&s_a[c + j], ps[j]); atomicAdd(&s_b[c + j], px[j]); }
+    }
+  }
+  if (epi) {
+    __syncthreads();
+    const size_t so = (size_t)(blockIdx.x % stat_slots(a.gsum_slots)) * a.gsum_ld;
+    for (int c = threadIdx.x; c < a.C; c += blockDim.x) {
+      if (a.gsum) atomicAdd(&a.gsum[so + c], s_a[c]);
+      if (a.gsumx) atomicAdd(&a.gsumx[so + c], s_b[c]);
+    }
+  }
+}
+
+namespace {
+// grid of a strip kernel: ~2 strips per thread row (amortises the per-thread tap registers)
+inline int strip_blocks(long long strips, int C) {
+  int C8 = C / 8, R = 256 / C8;
+  if (R < 1) R = 1;
+  long long b = (strips + 2LL * R - 1) / (2LL * R);
+  if (b > 4096) b = 4096;
+  return b < 1 ? 1 : (int)b;
+}
+}  // namespace
+
 hipError_t dwconv_fwd(const DwArgs& a, hipStream_t st) {
+  if (a.KH == 3 && a.KW == 3 && (a.S == 1 || a.S == 2) && a.C % 8 == 0 && a.C <= 2048) {
+    const long long strips = (long long)a.N * a.Ho * ((a.Wo + kDwStrip - 1) / kDwStrip);
+    if (a.S == 1)
+      hipLaunchKernelGGL(dw_fwd3_kernel<1>, dim3(strip_blocks(strips, a.C)), dim3(256), 4 * a.C * 4, st, a);
+    else
+      hipLaunchKernelGGL(dw_fwd3_kernel<2>, dim3(strip_blocks(strips, a.C)), dim3(256), 4 * a.C * 4, st, a);
+    return hipGetLastError();
+  }
   hipLaunchKernelGGL(dw_fwd_kernel, dim3(nblocks((long long)a.N * a.Ho * a.Wo, a.C, 4)), dim3(256), 4 * a.C * 4,
                      st, a);
   return hipGetLastError();
 }
 
 hipError_t dwconv_bwd_data(const DwArgs& a, hipStream_t st) {
+  const bool aff = a.dyaff.mode != 0;
+  if (a.KH == 3 && a.KW == 3 && (a.S == 1 || a.S == 2) && a.C % 8 == 0 && a.C <= 2048) {
+    const size_t shm = 9 * a.C * 4;
+    const long long strips4 = (long long)a.N * a.H * ((a.W + kDwStrip - 1) / kDwStrip);
+    const int g4 = strip_blocks(strips4, a.C), g1 = strip_blocks((long long)a.N * a.H * a.W, a.C);
+#define IDC_DWB(S_, PL_, G_)                                                                      \
+  if (aff) hipLaunchKernelGGL((dw_bwd3_kernel<S_, PL_, true>), dim3(G_), dim3(256), shm, st, a); \
+  else hipLaunchKernelGGL((dw_bwd3_kernel<S_, PL_, false>), dim3(G_), dim3(256), shm, st, a);
+    if (a.S == 1) {
+      IDC_DWB(1, -1, g4)
+    } else if (a.PL == 0) {
+      IDC_DWB(2, 0, g4)
+    } else if (a.PL == 1) {
+      IDC_DWB(2, 1, g4)
+    } else {
+      IDC_DWB(2, -1, g1)
+    }
+#undef IDC_DWB
+    return hipGetLastError();
+  }
+  if (aff) return hipErrorInvalidValue;  // the backward affine prologue is 3x3-only
   hipLaunchKernelGGL(dw_bwd_data_kernel, dim3(nblocks((long long)a.N * a.H * a.W, a.C, 4)), dim3(256),
                      6 * a.C * 4, st, a);
   return hipGetLastError();
@@ -236,12 +534,12 @@ hipError_t dwconv_bwd_data(const DwArgs& a, hipStream_t st) {
 // single-stage kernel's few long-running blocks (and the atomic alternative's contention on
 // 9*C addresses) made this the MobileNetV2 step's longest kernel.
 namespace {
-constexpr int kDwRowsPerThread = 4;
+constexpr int kDwRowsPerThread = 16;
 inline int dw_wgrad_blocks(long long M, int C) {
   int C8 = C / 8, R = 256 / C8;
   if (R < 1) R = 1;
   long long b = (M + (long long)R * kDwRowsPerThread - 1) / ((long long)R * kDwRowsPerThread);
-  if (b > 2048) b = 2048;
+  if (b > 1024) b = 1024;
   return b < 1 ? 1 : (int)b;
 }
 }  // namespace
@@ -314,20 +612,138 @@ __global__ __launch_bounds__(256) void dw_wgrad_part_kernel(DwArgs a, int rows_p
   for (int k = threadIdx.x; k < T * a.C; k += blockDim.x) out[k] = s_acc[k];
 }
 
+// 3x3 weight-gradient partials over strips of P output pixels: the strip's 3 x ((P-1)*S+3) input
+// vectors are loaded once and multiplied into every tap they meet (stride 1: 18 loads and 4 dy
+// loads per 4 outputs instead of 40); block b owns strips [b*spb, (b+1)*spb).
+template <int S, bool AFF>
+__global__ __launch_bounds__(256) void dw_wgrad3_part_kernel(DwArgs a, int spb) {
+  constexpr int P = kDwStrip, NCOL = (P - 1) * S + 3;
+  extern __shared__ float sh[];
+  float* s_sc = sh;
+  float* s_sf = sh + a.C;
+  float* s_fA = sh + 2 * a.C;   // AFF: dy' = A*dy + B*x + C
+  float* s_fB = sh + 3 * a.C;
+  float* s_fC = sh + 4 * a.C;
+  float* s_red = sh + 5 * a.C;  // [256 threads][3 taps][8]: one tap row per reduction round
+  for (int c = threadIdx.x; c < a.C; c += blockDim.x) bn_coeffs(a.pro, c, s_sc[c], s_sf[c]);
+  if constexpr (AFF) bwd_aff_table<256>(a.dyaff, 0, a.C, a.C, s_fA, s_fB, s_fC);
+  __syncthreads();
+  Map8 mp(a.C);
+  const int WS = (a.Wo + P - 1) / P;
+  const int strips = a.N * a.Ho * WS;
+  const int s0 = blockIdx.x * spb, s1 = min(strips, s0 + spb);
+  const float lo = act_lo(a.pro.act), hi = act_hi(a.pro.act);
+  float acc[9][8];
+#pragma unroll
+  for (int t = 0; t < 9; ++t)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc[t][j] = 0.f;
+  if (mp.ty < mp.R) {
+    const int c = mp.tx * 8;
+    float sc[8], sf[8], fA[8], fB[8], fC[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      sc[j] = s_sc[c + j]; sf[j] = s_sf[c + j];
+      if constexpr (AFF) { fA[j] = s_fA[c + j]; fB[j] = s_fB[c + j]; fC[j] = s_fC[c + j]; }
+    }
+    for (int st = s0 + mp.ty; st < s1; st += mp.R) {
+      const int ws = st % WS, t = st / WS, ho = t % a.Ho, n = t / a.Ho;
+      const int wo0 = ws * P;
+      float d[P][8];
+#pragma unroll
+      for (int p = 0; p < P; ++p) {
+        const bool v = wo0 + p < a.Wo;
+        const size_t o = v ? ((size_t)(n * a.Ho + ho) * a.Wo + wo0 + p) : 0;
+        unpack8(*reinterpret_cast<const uint4*>(a.dy + o * a.lddy + c), d[p]);
+        if constexpr (AFF) {
+          float xd[8];
+          unpack8(*reinterpret_cast<const uint4*>(a.dyaff.x + o * a.dyaff.ldx + c), xd);
+#pragma unroll
+          for (int j = 0; j < 8; ++j) d[p][j] = fmaf(fA[j], d[p][j], fmaf(fB[j], xd[j], fC[j]));
+        }
+        if (!v) {
+#pragma unroll
+          for (int j = 0; j < 8; ++j) d[p][j] = 0.f;
+        }
+      }
+#pragma unroll
+      for (int r = 0; r < 3; ++r) {
+        const int h = ho * S - a.PT + r;
+        const bool hv = (unsigned)h < (unsigned)a.H;
+        uint4 xv[NCOL];
+#pragma unroll
+        for (int q = 0; q < NCOL; ++q) {
+          const int w = wo0 * S - a.PL + q;
+          const bool v = hv && (unsigned)w < (unsigned)a.W;
+          const size_t pix = v ? ((size_t)(n * a.H + h) * a.W + w) : 0;
+          xv[q] = *reinterpret_cast<const uint4*>(a.x + pix * a.ldx + c);
+        }
+#pragma unroll
+        for (int q = 0; q < NCOL; ++q) {
+          const int w = wo0 * S - a.PL + q;
+          const float m = (hv && (unsigned)w < (unsigned)a.W) ? 1.f : 0.f;
+          float u[8];
+          unpack8(xv[q], u);
+#pragma unroll
+          for (int j = 0; j < 8; ++j) u[j] = fminf(fmaxf(fmaf(u[j], sc[j], sf[j]), lo), hi) * m;
+#pragma unroll
+          for (int p = 0; p < P; ++p) {
+            const int s = q - p * S;
+            if (s >= 0 && s < 3) {
+#pragma unroll
+              for (int j = 0; j < 8; ++j) acc[r * 3 + s][j] = fmaf(u[j], d[p][j], acc[r * 3 + s][j]);
+            }
+          }
+        }
+      }
+    }
+  }
+  // block reduction over the R thread rows of each chunk, one tap row (3 taps) per round:
+  // every thread's 24 partials to LDS, then each (tap, channel) output sums its R entries in
+  // order (the per-address LDS atomics this replaces serialised R-way on small C)
+  float* out = a.ws + (size_t)blockIdx.x * 9 * a.C;
+  const int C8 = a.C / 8;
+  const bool act = mp.ty < mp.R;
+#pragma unroll
+  for (int r = 0; r < 3; ++r) {
+    if (r) __syncthreads();
+    float4* d = reinterpret_cast<float4*>(s_red + threadIdx.x * 24);
+#pragma unroll
+    for (int s = 0; s < 3; ++s) {
+      const float* v = acc[r * 3 + s];
+      d[2 * s] = act ? make_float4(v[0], v[1], v[2], v[3]) : make_float4(0.f, 0.f, 0.f, 0.f);
+      d[2 * s + 1] = act ? make_float4(v[4], v[5], v[6], v[7]) : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+    __syncthreads();
+    for (int o = threadIdx.x; o < 3 * a.C; o += blockDim.x) {
+      const int s = o / a.C, c = o - s * a.C, tx = c >> 3, j = c & 7;
+      float sum = 0.f;
+      for (int ty = 0; ty < mp.R; ++ty) sum += s_red[(ty * C8 + tx) * 24 + s * 8 + j];
+      out[(r * 3 + s) * a.C + c] = sum;
+    }
+  }
+}
+
+// column sums of the per-block partials: blockIdx.y splits the blocks so the sum is spread over
+// many workgroups (a single pass per column was a few long latency chains on a handful of CUs)
 __global__ __launch_bounds__(256) void dw_wgrad_sum_kernel(const float* __restrict__ ws, int nblk, int n,
                                                            float* __restrict__ dw) {
   const int k = blockIdx.x * blockDim.x + threadIdx.x;
   if (k >= n) return;
+  const int per = (nblk + gridDim.y - 1) / gridDim.y;
+  const int b0 = blockIdx.y * per, b1 = min(nblk, b0 + per);
   float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
-  int b = 0;
-  for (; b + 4 <= nblk; b += 4) {
+  int b = b0;
+  for (; b + 4 <= b1; b += 4) {
     s0 += ws[(size_t)b * n + k];
     s1 += ws[(size_t)(b + 1) * n + k];
     s2 += ws[(size_t)(b + 2) * n + k];
     s3 += ws[(size_t)(b + 3) * n + k];
   }
-  for (; b < nblk; ++b) s0 += ws[(size_t)b * n + k];
-  dw[k] += (s0 + s1) + (s2 + s3);
+  for (; b < b1; ++b) s0 += ws[(size_t)b * n + k];
+  const float v = (s0 + s1) + (s2 + s3);
+  if (gridDim.y == 1) dw[k] += v;
+  else atomicAdd(&dw[k], v);
 }
 
 hipError_t dwconv_wgrad(const DwArgs& a, hipStream_t st) {
@@ -336,10 +752,30 @@ hipError_t dwconv_wgrad(const DwArgs& a, hipStream_t st) {
   const int T = a.KH * a.KW;
   if (a.ws) {
     const int nblk = dw_wgrad_blocks(Mo, a.C);
-    const int rpb = (int)((Mo + nblk - 1) / nblk);
-    hipLaunchKernelGGL(dw_wgrad_part_kernel, dim3(nblk), dim3(256), (2 + T) * a.C * 4, st, a, rpb);
+    const bool aff = a.dyaff.mode != 0;
+    if (a.KH == 3 && a.KW == 3 && (a.S == 1 || a.S == 2) && a.C % 8 == 0) {
+      const long long strips = (long long)a.N * a.Ho * ((a.Wo + kDwStrip - 1) / kDwStrip);
+      const int spb = (int)((strips + nblk - 1) / nblk);
+      const size_t shm = (5 * a.C + 256 * 24) * 4;
+      if (a.S == 1) {
+        if (aff) hipLaunchKernelGGL((dw_wgrad3_part_kernel<1, true>), dim3(nblk), dim3(256), shm, st, a, spb);
+        else hipLaunchKernelGGL((dw_wgrad3_part_kernel<1, false>), dim3(nblk), dim3(256), shm, st, a, spb);
+      } else {
+        if (aff) hipLaunchKernelGGL((dw_wgrad3_part_kernel<2, true>), dim3(nblk), dim3(256), shm, st, a, spb);
+        else hipLaunchKernelGGL((dw_wgrad3_part_kernel<2, false>), dim3(nblk), dim3(256), shm, st, a, spb);
+      }
+    } else if (aff) {
+      return hipErrorInvalidValue;
+    } else {
+      const int rpb = (int)((Mo + nblk - 1) / nblk);
+      hipLaunchKernelGGL(dw_wgrad_part_kernel, dim3(nblk), dim3(256), (2 + T) * a.C * 4, st, a, rpb);
+    }
     const int n = T * a.C;
-    hipLaunchKernelGGL(dw_wgrad_sum_kernel, dim3((n + 255) / 256), dim3(256), 0, st, a.ws, nblk, n, a.dw);
+    const int cols = (n + 255) / 256;
+    int split = (nblk + 31) / 32;  // ~32 partials per thread, enough workgroups to fill the chip
+    if (split > 64) split = 64;
+    if (split < 1) split = 1;
+    hipLaunchKernelGGL(dw_wgrad_sum_kernel, dim3(cols, split), dim3(256), 0, st, a.ws, nblk, n, a.dw);
     return hipGetLastError();
   }
   hipLaunchKernelGGL(dw_wgrad_kernel, dim3(nblocks(Mo, a.C, 32)), dim3(256), (2 + T) * a.C * 4, st, a);

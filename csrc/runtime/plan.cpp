@@ -397,6 +397,7 @@ py::dict struct_sizes() {
   d["ConvArgs.aout"] = offsetof(ConvArgs, aout);
   d["WgradArgs.part_floats"] = offsetof(WgradArgs, part_floats);
   d["HeadBwdArgs.det"] = offsetof(HeadBwdArgs, det);
+  d["DwArgs.dyaff"] = offsetof(DwArgs, dyaff);
   return d;
 }
 

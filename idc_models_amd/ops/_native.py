@@ -112,7 +112,7 @@ class DwArgs(C.Structure):
                 ("PL", ci), ("Ho", ci), ("Wo", ci), ("y", vp), ("ldy", ci), ("stats", vp),
                 ("stats_ld", ci), ("dy", vp), ("lddy", ci), ("dx", vp), ("lddx", ci),
                 ("gsum", vp), ("gsumx", vp), ("dw", vp), ("ws", vp), ("stats_slots", ci),
-                ("gsum_slots", ci), ("gsum_ld", ci)]
+                ("gsum_slots", ci), ("gsum_ld", ci), ("dyaff", BwdAff)]
 
 
 class Mlp2Args(C.Structure):
@@ -153,7 +153,8 @@ def _verify(ext):
               "DwArgs.gsum_ld": DwArgs.gsum_ld.offset, "ConvArgs.bepi": ConvArgs.bepi.offset,
               "WgradArgs.gpro": WgradArgs.gpro.offset, "PoolBwdArgs.dx_f32": PoolBwdArgs.dx_f32.offset,
               "BwdAff.fold_sumx": BwdAff.fold_sumx.offset, "ConvArgs.aout": ConvArgs.aout.offset,
-              "WgradArgs.part_floats": WgradArgs.part_floats.offset, "HeadBwdArgs.det": HeadBwdArgs.det.offset}
+              "WgradArgs.part_floats": WgradArgs.part_floats.offset, "HeadBwdArgs.det": HeadBwdArgs.det.offset,
+              "DwArgs.dyaff": DwArgs.dyaff.offset}
     for k, v in checks.items():
         if sizes[k] != v:
             raise RuntimeError(f"native struct field {k}: ctypes offset {v} != C++ {sizes[k]}")

@@ -708,10 +708,19 @@ class Builder:
             a.stats_slots = stats.slots
         self.emit(nat.OP_DW_FWD, a)
 
+    def _dw_dyaff(self, a: nat.DwArgs, layer, dyaff: Optional[nat.BwdAff]):
+        if dyaff is None:
+            return
+        if tuple(layer.kernel_size) != (3, 3) or a.S not in (1, 2) or a.C % 8 or a.C > 2048:
+            raise RuntimeError(f"{layer.name}: the depthwise backward-affine prologue is 3x3-only")
+        a.dyaff = dyaff
+
     def dw_bwd_data(self, x: Tensor4, layer, dy: Tensor4, dz: Tensor4, *, stride=1, pads=(1, 1),
-                    bn: Optional["BNRef"] = None):
-        """dz = (dy conv^T w) * act'(BN(x)), sums into bn's dbeta/dgamma (x = raw dw input)."""
+                    bn: Optional["BNRef"] = None, dyaff: Optional[nat.BwdAff] = None):
+        """dz = (dy conv^T w) * act'(BN(x)), sums into bn's dbeta/dgamma (x = raw dw input).
+        ``dyaff``: dy is staged through the pending backward of the BatchNorm after this conv."""
         a = self._dw_args(x, layer, dy.H, dy.W, stride, pads, bn.args() if bn is not None else None)
+        self._dw_dyaff(a, layer, dyaff)
         a.dy, a.lddy = dy.ptr, dy.ld
         a.dx, a.lddx = dz.ptr, dz.ld
         if bn is not None:
@@ -720,8 +729,9 @@ class Builder:
         self.finish_grad_sums(bn)
 
     def dw_wgrad(self, x: Tensor4, layer, dy: Tensor4, dw: torch.Tensor, *, stride=1, pads=(1, 1),
-                 pro=None, lane=0):
+                 pro=None, lane=0, dyaff: Optional[nat.BwdAff] = None):
         a = self._dw_args(x, layer, dy.H, dy.W, stride, pads, pro)
+        self._dw_dyaff(a, layer, dyaff)
         a.dy, a.lddy = dy.ptr, dy.ld
         a.dw = dw.data_ptr()
         kh, kw = layer.kernel_size

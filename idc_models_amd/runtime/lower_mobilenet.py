@@ -8,10 +8,13 @@ MI355X structure:
   apply the pending expand-BN + ReLU6 on load and reduce their own output statistics;
 * each block output ``BN_project(p) [+ residual]`` is materialised ONCE by ``bn_apply`` (it is the
   next block's expand input AND, for identity blocks, its residual);
-* backward mirrors it: BN backward of the project BN (reduce + apply), project dgrad with the
-  BN-backward epilogue through depthwise-BN + ReLU6, depthwise backward-data with the same
-  epilogue through expand-BN + ReLU6, expand dgrad ACCUMULATED into the residual gradient in
-  place (fp32), weight gradients on the side lane.
+* backward: every BatchNorm backward is reduced once by its producer and APPLIED BY ITS CONSUMERS
+  (common.h BwdAff: A*dZ + B*x + C staged while loading dZ) — the pointwise dgrads for the
+  Conv_1, project and expand BNs (they also write the staged operand for the side-lane weight
+  gradient); only the depthwise BN keeps an apply pass (its depthwise consumers re-read dZ ~4.5x,
+  so staging there costs more than the pass); the project dgrad's epilogue goes through
+  depthwise-BN + ReLU6, the depthwise backward-data epilogue through expand-BN + ReLU6, and the
+  expand dgrad ACCUMULATES into the fp32 residual gradient in place.
 Keras ``correct_pad`` asymmetric padding of stride-2 layers = top/left pad + implicit bottom/right.
 """
 from __future__ import annotations
@@ -126,16 +129,23 @@ def lower_mobilenet(b: Builder, net, U: int, input_dtype):
         b.mark_grads_ready([bn_c1.gamma, bn_c1.beta])
         return
     dc1 = b.nhwc(c1.N, c1.H, c1.W, c1.C)
-    b.bn_bwd_apply(zc, c1, bn_c1, dc1, accumulate=False)
-    b.mark_grads_ready([bn_c1.gamma, bn_c1.beta])
     h_last = blocks[-1]["h_out"]
+    if not fz.before(c1l):
+        b.bn_bwd_apply(zc, c1, bn_c1, dc1, accumulate=False)
+        b.mark_grads_ready([bn_c1.gamma, bn_c1.beta])
+        if fz.trainable(c1l):
+            b.wgrad(h_last, c1l, dc1, b.arena.grad_of(c1l.kernel), lane=1)
+        b.mark_grads_ready([c1l.kernel])
+        return
+    # the BatchNorm backward of Conv_1_bn is staged by its consumer: the dgrad applies
+    # A*dZ + B*x + C while loading dZ (and folds the BN's reductions), and writes the staged
+    # operand for the side-lane weight gradient (no separate apply pass)
+    G = b.nhwc(h_last.N, h_last.H, h_last.W, h_last.C, F32)
+    b.dgrad(zc, c1l, G, out_mode=nat.OUT_F32, bpro=b.bwd_aff(bn_c1, c1, fold=True), aout=dc1)
+    b.mark_grads_ready([bn_c1.gamma, bn_c1.beta])
     if fz.trainable(c1l):
         b.wgrad(h_last, c1l, dc1, b.arena.grad_of(c1l.kernel), lane=1)
     b.mark_grads_ready([c1l.kernel])
-    if not fz.before(c1l):
-        return
-    G = b.nhwc(h_last.N, h_last.H, h_last.W, h_last.C, F32)
-    b.dgrad(dc1, c1l, G, out_mode=nat.OUT_F32)
 
     for blk in reversed(blocks):
         p, bn_p, d, bn_d = blk["p"], blk["bn_p"], blk["d"], blk["bn_d"]
@@ -147,22 +157,31 @@ def lower_mobilenet(b: Builder, net, U: int, input_dtype):
             b.mark_grads_ready([bn_p.gamma, bn_p.beta])
             return
         dp = b.nhwc(p.N, p.H, p.W, p.C)
-        b.bn_bwd_apply(zp, p, bn_p, dp, accumulate=False)
+        if not fz.before(prj):
+            b.bn_bwd_apply(zp, p, bn_p, dp, accumulate=False)
+            b.mark_grads_ready([bn_p.gamma, bn_p.beta])
+            if fz.trainable(prj):
+                b.wgrad(d, prj, dp, b.arena.grad_of(prj.kernel), pro=bn_d.args(), lane=1)
+            b.mark_grads_ready([prj.kernel])
+            return
+        # project dgrad: prologue = project-BN backward, epilogue = backward through the
+        # depthwise BN + ReLU6 (dZ_d and its reductions); dp side output for the wgrad
+        zd = b.nhwc(d.N, d.H, d.W, d.C)
+        b.dgrad(zp, prj, zd, mx=d, mbn=bn_d.args(), gbn=bn_d, bpro=b.bwd_aff(bn_p, p, fold=True), aout=dp)
         b.mark_grads_ready([bn_p.gamma, bn_p.beta])
         if fz.trainable(prj):
             b.wgrad(d, prj, dp, b.arena.grad_of(prj.kernel), pro=bn_d.args(), lane=1)
         b.mark_grads_ready([prj.kernel])
-        if not fz.before(prj):
-            return
-        zd = b.nhwc(d.N, d.H, d.W, d.C)
-        b.dgrad(dp, prj, zd, mx=d, mbn=bn_d.args(), gbn=bn_d)
         if not fz.before(bn_d.layer):
             b.mark_grads_ready([bn_d.gamma, bn_d.beta])
             return
+        e, bn_in = blk["e"], blk["bn_in"]
+        # depthwise BN backward: materialised once (the depthwise kernels re-read dZ ~4.5x; staging
+        # the affine there re-reads the BN input as often and rebuilds the slot-summed A/B/C table
+        # in every workgroup, measured slower than this pass)
         dd = b.nhwc(d.N, d.H, d.W, d.C)
         b.bn_bwd_apply(zd, d, bn_d, dd, accumulate=False)
         b.mark_grads_ready([bn_d.gamma, bn_d.beta])
-        e, bn_in = blk["e"], blk["bn_in"]
         if fz.trainable(dwl):
             b.dw_wgrad(e, dwl, dd, b.arena.grad_of(dwl.depthwise_kernel), stride=blk["stride"],
                        pads=blk["pads"], pro=bn_in.args(), lane=1)
@@ -174,25 +193,30 @@ def lower_mobilenet(b: Builder, net, U: int, input_dtype):
         if not fz.before(bn_in.layer):
             b.mark_grads_ready([bn_in.gamma, bn_in.beta])
             return
-        de = b.nhwc(e.N, e.H, e.W, e.C)
-        b.bn_bwd_apply(ze, e, bn_in, de, accumulate=False)
-        b.mark_grads_ready([bn_in.gamma, bn_in.beta])
         ex = blk["ex"]
-        if ex is None:  # block 0: de is the gradient of the raw stem conv output
-            if fz.trainable(conv1):
-                b.wgrad(x8, conv1, de, b.arena.grad_of(conv1.kernel), stride=(2, 2), pads=stem_pads,
-                        cin_real=Cimg, lane=1)
-            b.mark_grads_ready([conv1.kernel])
+        de = b.nhwc(e.N, e.H, e.W, e.C)
+        if ex is None or not fz.before(ex):
+            b.bn_bwd_apply(ze, e, bn_in, de, accumulate=False)
+            b.mark_grads_ready([bn_in.gamma, bn_in.beta])
+            if ex is None:  # block 0: de is the gradient of the raw stem conv output
+                if fz.trainable(conv1):
+                    b.wgrad(x8, conv1, de, b.arena.grad_of(conv1.kernel), stride=(2, 2), pads=stem_pads,
+                            cin_real=Cimg, lane=1)
+                b.mark_grads_ready([conv1.kernel])
+            else:
+                if fz.trainable(ex):
+                    b.wgrad(blk["h_in"], ex, de, b.arena.grad_of(ex.kernel), lane=1)
+                b.mark_grads_ready([ex.kernel])
             return
         h_prev = blk["h_in"]
+        aff_in = b.bwd_aff(bn_in, e, fold=True)
+        if blk["residual"]:
+            # dL/dh_prev = G (identity shortcut) + expand^T de: accumulate into G in place
+            b.dgrad(ze, ex, G, out_mode=nat.OUT_F32_ACC, bpro=aff_in, aout=de)
+        else:
+            G = b.nhwc(h_prev.N, h_prev.H, h_prev.W, h_prev.C, F32)
+            b.dgrad(ze, ex, G, out_mode=nat.OUT_F32, bpro=aff_in, aout=de)
+        b.mark_grads_ready([bn_in.gamma, bn_in.beta])
         if fz.trainable(ex):
             b.wgrad(h_prev, ex, de, b.arena.grad_of(ex.kernel), lane=1)
         b.mark_grads_ready([ex.kernel])
-        if not fz.before(ex):
-            return
-        if blk["residual"]:
-            # dL/dh_prev = G (identity shortcut) + expand^T de: accumulate into G in place
-            b.dgrad(de, ex, G, out_mode=nat.OUT_F32_ACC)
-        else:
-            G = b.nhwc(h_prev.N, h_prev.H, h_prev.W, h_prev.C, F32)
-            b.dgrad(de, ex, G, out_mode=nat.OUT_F32)

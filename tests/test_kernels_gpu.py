@@ -361,9 +361,10 @@ def test_bn_stats(fn):
     assert relerr(st[96:], (x * x).sum((0, 1, 2))) < 1e-4
 
 
-@pytest.mark.parametrize("s,H,pads,ho", [(1, 13, (1, 1), 13), (2, 26, (0, 0), 13), (2, 13, (1, 1), 7)])
-def test_dwconv(fn, s, H, pads, ho):
-    N, C = 2, 96
+@pytest.mark.parametrize("s,H,pads,ho,C", [(1, 13, (1, 1), 13, 96), (2, 26, (0, 0), 13, 96), (2, 13, (1, 1), 7, 96),
+                                            (1, 4, (1, 1), 4, 384), (2, 4, (0, 0), 2, 960)])
+def test_dwconv(fn, s, H, pads, ho, C):
+    N = 2
     x = bf(torch.randn(N, H, H, C, device=DEV))
     k = torch.randn(3, 3, C, 1, device=DEV) * 0.3
     y = fn.dwconv(x.to(torch.bfloat16), k, stride=s, pads=pads, out_hw=(ho, ho))
