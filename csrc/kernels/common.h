@@ -154,7 +154,21 @@ struct BnArgs {
   int act;
   int C;                  // channels covered by stats/gamma (stats row length)
   int slots;              // mode 1: `stats` holds this many [sum|sumsq] copies (0/1: one), see below
+  const float* shift;     // mode 1 (nullable): per-channel shift K, stats hold sum(y-K), sum((y-K)^2)
 };
+
+// Shifted statistics.  Producers accumulate sum(y - K) and sum((y - K)^2) with a per-channel
+// shift K (the previous step's batch mean, updated after every backward by stats_shift_kernel),
+// so the variance sum((y-K)^2)/n - (sum(y-K)/n)^2 cancels only (mean - K)^2 instead of mean^2:
+// a channel with mean 50 and std 0.1 loses ~all of its fp32 variance in E[y^2] - E[y]^2 (the
+// 2500-sized sums round at ~1e-4 per add) but keeps it with K ~ 50.  K = 0 on the first step.
+__device__ __forceinline__ float bn_shift(const BnArgs& b, int c) { return b.shift ? b.shift[c] : 0.f; }
+__device__ __forceinline__ void shifted_mean_var(float k, float s0, float s1, float inv_n, float& mean,
+                                                 float& var) {
+  const float d = s0 * inv_n;
+  mean = k + d;
+  var = fmaxf(s1 * inv_n - d * d, 0.f);
+}
 
 // Statistics slots.  Per-channel sums are accumulated with global float atomics, which execute
 // at the memory side and serialise per ADDRESS (measured ~24 ns per add, tools/micro/
@@ -229,8 +243,7 @@ __device__ __forceinline__ void bn_coeffs(const BnArgs& b, int c, float& scale, 
   if (b.mode == 1) {
     float s0, s1;
     bn_slot_sums(b, c, s0, s1);
-    mean = s0 * b.inv_count;
-    var = fmaxf(s1 * b.inv_count - mean * mean, 0.f);
+    shifted_mean_var(bn_shift(b, c), s0, s1, b.inv_count, mean, var);
   } else {
     mean = b.mmean[c];
     var = b.mvar[c];
@@ -264,14 +277,14 @@ __device__ __forceinline__ void bn_coeff_table(const BnArgs& b, int C, float* s_
     slot_sums_1(p0, p1, S, stride, c, v0, v1);
     const float g = b.gamma ? b.gamma[c] : 1.f;
     const float be = b.beta ? b.beta[c] : 0.f;
-    const float mean = v0 * mul;
-    const float var = fmaxf(v1 * mul - mean * mean, 0.f);
+    float mean, var;
+    shifted_mean_var(bn_shift(b, c), v0, v1, mul, mean, var);
     const float rs = rsqrtf(var + b.eps);
     s_scale[c] = g * rs;
     s_shift[c] = be - mean * g * rs;
   }
   for (int base = 0; S == 1 && base < C; base += 4 * NT) {
-    float v0[4], v1[4], g[4], be[4];
+    float v0[4], v1[4], g[4], be[4], k[4];
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
       int c = base + u * NT + tid;
@@ -280,13 +293,14 @@ __device__ __forceinline__ void bn_coeff_table(const BnArgs& b, int C, float* s_
       v1[u] = p1[cc];
       g[u] = b.gamma ? b.gamma[cc] : 1.f;
       be[u] = b.beta ? b.beta[cc] : 0.f;
+      k[u] = b.mode == 1 ? bn_shift(b, cc) : 0.f;
     }
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
       int c = base + u * NT + tid;
       if (c >= C) break;
-      float mean = v0[u] * mul;
-      float var = b.mode == 1 ? fmaxf(v1[u] * mul - mean * mean, 0.f) : v1[u];
+      float mean = v0[u], var = v1[u];
+      if (b.mode == 1) shifted_mean_var(k[u], v0[u], v1[u], mul, mean, var);
       float sc = g[u] * rsqrtf(var + b.eps);
       s_scale[c] = sc;
       s_shift[c] = be[u] - mean * sc;
@@ -316,8 +330,8 @@ __device__ __forceinline__ void bn_full_table(const BnArgs& b, int C, float* s_s
     slot_sums_1(p0, p1, S, stride, c, v0, v1);
     const float g = b.gamma ? b.gamma[c] : 1.f;
     const float be = b.beta ? b.beta[c] : 0.f;
-    const float mean = v0 * mul;
-    const float var = fmaxf(v1 * mul - mean * mean, 0.f);
+    float mean, var;
+    shifted_mean_var(bn_shift(b, c), v0, v1, mul, mean, var);
     const float rs = rsqrtf(var + b.eps);
     s_sc[c] = g * rs;
     s_sh[c] = be - mean * g * rs;
@@ -325,7 +339,7 @@ __device__ __forceinline__ void bn_full_table(const BnArgs& b, int C, float* s_s
     s_rs[c] = rs;
   }
   for (int base = 0; S == 1 && base < C; base += 4 * NT) {
-    float v0[4], v1[4], g[4], be[4];
+    float v0[4], v1[4], g[4], be[4], k[4];
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
       int c = base + u * NT + tid;
@@ -334,13 +348,14 @@ __device__ __forceinline__ void bn_full_table(const BnArgs& b, int C, float* s_s
       v1[u] = p1[cc];
       g[u] = b.gamma ? b.gamma[cc] : 1.f;
       be[u] = b.beta ? b.beta[cc] : 0.f;
+      k[u] = b.mode == 1 ? bn_shift(b, cc) : 0.f;
     }
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
       int c = base + u * NT + tid;
       if (c >= C) break;
-      float mean = v0[u] * mul;
-      float var = b.mode == 1 ? fmaxf(v1[u] * mul - mean * mean, 0.f) : v1[u];
+      float mean = v0[u], var = v1[u];
+      if (b.mode == 1) shifted_mean_var(k[u], v0[u], v1[u], mul, mean, var);
       float rs = rsqrtf(var + b.eps);
       float sc = g[u] * rs;
       s_sc[c] = sc;
@@ -403,10 +418,7 @@ __device__ __forceinline__ void bwd_aff_table(const BwdAff& b, int c0, int n, in
       m1 = b.bn.mvar[c];
     }
     float mean = m0, var = m1;
-    if (b.bn.mode == 1) {
-      mean *= b.bn.inv_count;
-      var = fmaxf(var * b.bn.inv_count - mean * mean, 0.f);
-    }
+    if (b.bn.mode == 1) shifted_mean_var(bn_shift(b.bn, c), m0, m1, b.bn.inv_count, mean, var);
     const float rstd = rsqrtf(var + b.bn.eps);
     const float sd = q0 * b.inv_n, sdx = q1 * b.inv_n;
     const float Bc = -g * rstd * rstd * sdx;
@@ -451,19 +463,20 @@ __device__ __forceinline__ bool bwd_aff_slots4(const BwdAff& b) {
 // raw inputs of one channel of a BwdAff table (training-mode BatchNorm, <= 4 slots)
 struct BwdAffRaw {
   Raw4 st, gs;
-  float g;
+  float g, k;
 };
 __device__ __forceinline__ void bwd_aff_load(const BwdAff& b, int c, BwdAffRaw& r) {
   load4(b.bn.stats, b.bn.stats + b.bn.C, stat_slots(b.bn.slots), 2 * (size_t)b.bn.C, c, r.st);
   load4(b.gsum, b.gsumx, stat_slots(b.gsum_slots), (size_t)b.gsum_ld, c, r.gs);
   r.g = b.bn.gamma ? b.bn.gamma[c] : 1.f;
+  r.k = bn_shift(b.bn, c);
 }
 __device__ __forceinline__ void bwd_aff_finish(const BwdAff& b, const BwdAffRaw& r, float& A, float& B, float& C) {
   float m0, m1, q0, q1;
   sum4(r.st, stat_slots(b.bn.slots), m0, m1);
   sum4(r.gs, stat_slots(b.gsum_slots), q0, q1);
-  const float mean = m0 * b.bn.inv_count;
-  const float var = fmaxf(m1 * b.bn.inv_count - mean * mean, 0.f);
+  float mean, var;
+  shifted_mean_var(r.k, m0, m1, b.bn.inv_count, mean, var);
   const float rstd = rsqrtf(var + b.bn.eps);
   const float Bc = -r.g * rstd * rstd * (q1 * b.inv_n);
   A = b.unit_alpha ? 1.f : r.g * rstd;
@@ -504,8 +517,7 @@ __device__ __forceinline__ void bn_mean_rstd(const BnArgs& b, int c, float& mean
   if (b.mode == 1) {
     float s0, s1;
     bn_slot_sums(b, c, s0, s1);
-    mean = s0 * b.inv_count;
-    var = fmaxf(s1 * b.inv_count - mean * mean, 0.f);
+    shifted_mean_var(bn_shift(b, c), s0, s1, b.inv_count, mean, var);
   } else {
     mean = b.mmean[c];
     var = b.mvar[c];

@@ -204,6 +204,9 @@ __global__ __launch_bounds__(NT) void conv3x3_halo_kernel(ConvArgs a) {
 #pragma unroll
   for (int j = 0; j < 8; ++j) { psum[j] = 0.f; psq[j] = 0.f; }
   const int my_c8 = lane % CPB;
+  float t_k[8];  // statistics shift of this lane's chunk (common.h "Shifted statistics")
+#pragma unroll
+  for (int j = 0; j < 8; ++j) t_k[j] = (EPI == 0 && a.stats_shift) ? a.stats_shift[my_c8 * 8 + j] : 0.f;
   const float epi_lo = act_lo(a.epi_act), epi_hi = act_hi(a.epi_act);
   const float msk_lo = act_lo(a.mbn.act), msk_hi = act_hi(a.mbn.act);
   const size_t out_img = (size_t)img * g.npix;
@@ -239,7 +242,11 @@ __global__ __launch_bounds__(NT) void conv3x3_halo_kernel(ConvArgs a) {
           float rr[8];
           unpack8(pk, rr);
 #pragma unroll
-          for (int jj = 0; jj < 8; ++jj) { psum[jj] += rr[jj]; psq[jj] += rr[jj] * rr[jj]; }
+          for (int jj = 0; jj < 8; ++jj) {
+            const float dj = rr[jj] - t_k[jj];
+            psum[jj] += dj;
+            psq[jj] += dj * dj;
+          }
         } else {
           float xf[8], d[8];
           unpack8(*reinterpret_cast<const uint4*>(a.mx + m * a.ldmx + n), xf);

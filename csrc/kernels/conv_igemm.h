@@ -62,6 +62,9 @@ struct ConvArgs {
   // a plain bf16 gradient instead of redoing the affine on the fp32 / two-tensor form
   bf16_t* aout;
   int ldaout;
+  // epi 0 statistics shift of the output channels (pre-offset to output channel 0; nullable):
+  // the statistics accumulate y - K (common.h "Shifted statistics")
+  const float* stats_shift;
 };
 
 // tile TILE_HALO selects the one-image-per-workgroup direct 3x3 kernel (conv3x3_halo.hip)

@@ -163,8 +163,10 @@ __global__ __launch_bounds__(256) void conv_igemm_kernel(ConvArgs a) {
   const float epi_lo = act_lo(a.epi_act), epi_hi = act_hi(a.epi_act);
   const float msk_lo = act_lo(a.mbn.act), msk_hi = act_hi(a.mbn.act);
 
-  // two staging register sets: tile t+2 is loaded while tile t is computed and tile t+1 (already
-  // in registers) waits to be written to LDS, so each global load has two compute phases to land
+  // NS staging register sets, tile t in set t % NS: tile t+NS is issued while tile t is computed
+  // from LDS and tile t+1 waits in registers to be written, so each global load has NS-1 compute
+  // phases to land.  The small tiles (the DenseNet layers: a few MFMAs per K-step against a
+  // ~2k-cycle load latency) take 4 sets, the big ones 2 (register budget).
   struct Stage {
     uint4 ra[NA];
     uint4 rx[PRO == 2 ? NA : 1];
@@ -175,7 +177,10 @@ __global__ __launch_bounds__(256) void conv_igemm_kernel(ConvArgs a) {
     bool bvalid[NB];
     int kc, kr, ks;
   };
-  Stage st0, st1;
+  constexpr int STAGE_VGPR = NA * (sizeof(TA) == 4 ? 9 : 5) + (PRO == 2 ? NA * 5 : 0) + NB * 5;
+  constexpr int NS = 2;  // 4 sets measured slower: the small-tile K loop is issue-bound, not load-latency-bound
+  (void)STAGE_VGPR;
+  Stage st[NS];
 
   auto load_tile = [&](Stage& S) {
     uint4* ra = S.ra;
@@ -311,16 +316,20 @@ __global__ __launch_bounds__(256) void conv_igemm_kernel(ConvArgs a) {
   // the first two tiles are issued BEFORE the prologue tables are built: the tables' own global
   // loads (BN statistics, gamma, beta) then overlap the tile loads instead of adding a second
   // full memory latency in front of the K loop
-  load_tile(st0);
-  advance_k();
-  load_tile(st1);
+#pragma unroll
+  for (int s = 0; s < NS; ++s) {
+    if (s) advance_k();
+    load_tile(st[s]);
+  }
   IDC_PHASE_STAMP(1);
   // ---- prologue tables ----
   if constexpr (PRO == 1) bn_coeff_table<NT>(a.pro, a.Cin, s_scale, s_shift);
   // backward tables (pending-affine prologue, epilogue BatchNorm, epilogue pending affine): one
   // batched round trip when every statistic has <= 4 slot copies (common.h "Batched table inputs")
+  // (compiled into the small-accumulator tiles only: they are the ones small layers pick, and the
+  // extra live registers made the big tiles spill)
   bool batched = false;
-  if constexpr (PRO == 2 || EPI >= 1) {
+  if constexpr ((PRO == 2 || EPI >= 1) && TM * TN <= 8) {
     batched = (PRO != 2 || (a.Cin <= NT && (!a.bpro.mode || (a.bpro.bn.mode == 1 && bwd_aff_slots4(a.bpro))))) &&
               (EPI != 2 || !a.bepi.mode || (a.bepi.bn.mode == 1 && bwd_aff_slots4(a.bepi))) &&
               (EPI < 1 || bn_slots4(a.mbn));
@@ -330,7 +339,7 @@ __global__ __launch_bounds__(256) void conv_igemm_kernel(ConvArgs a) {
     const int ce = n0 + tid < a.Cout ? n0 + tid : 0;  // epilogue channel (BN <= NT)
     BwdAffRaw rp, re2;
     Raw4 rm;
-    float mg = 1.f, mb = 0.f;
+    float mg = 1.f, mb = 0.f, mk = 0.f;
     if constexpr (PRO == 2) {
       if (a.bpro.mode) bwd_aff_load(a.bpro, cp, rp);
     }
@@ -338,7 +347,10 @@ __global__ __launch_bounds__(256) void conv_igemm_kernel(ConvArgs a) {
       if (a.bepi.mode) bwd_aff_load(a.bepi, ce, re2);
     }
     if constexpr (EPI >= 1) {
-      if (a.mbn.mode == 1) load4(a.mbn.stats, a.mbn.stats + a.mbn.C, stat_slots(a.mbn.slots), 2 * (size_t)a.mbn.C, ce, rm);
+      if (a.mbn.mode == 1) {
+        load4(a.mbn.stats, a.mbn.stats + a.mbn.C, stat_slots(a.mbn.slots), 2 * (size_t)a.mbn.C, ce, rm);
+        mk = bn_shift(a.mbn, ce);
+      }
       else if (a.mbn.mode == 2) { rm.a0[0] = a.mbn.mmean[ce]; rm.a1[0] = a.mbn.mvar[ce]; }
       if (a.mbn.mode) {
         mg = a.mbn.gamma ? a.mbn.gamma[ce] : 1.f;
@@ -364,8 +376,7 @@ __global__ __launch_bounds__(256) void conv_igemm_kernel(ConvArgs a) {
           float v0, v1 = rm.a1[0];
           if (a.mbn.mode == 1) {
             sum4(rm, stat_slots(a.mbn.slots), v0, v1);
-            mean = v0 * a.mbn.inv_count;
-            v1 = fmaxf(v1 * a.mbn.inv_count - mean * mean, 0.f);
+            shifted_mean_var(mk, v0, v1, a.mbn.inv_count, mean, v1);
           } else {
             mean = rm.a0[0];
           }
@@ -431,7 +442,7 @@ __global__ __launch_bounds__(256) void conv_igemm_kernel(ConvArgs a) {
 
   IDC_PHASE_STAMP(5);
   __syncthreads();  // prologue tables visible
-  store_tile(st0, 0);
+  store_tile(st[0], 0);
   __syncthreads();
   IDC_PHASE_STAMP(6);
 
@@ -462,52 +473,23 @@ __global__ __launch_bounds__(256) void conv_igemm_kernel(ConvArgs a) {
     }
   };
 
-  // iteration kt: LDS[kt&1] holds tile kt, registers hold tile kt+1 (set (kt+1)&1);
-  // tile kt+2 is issued into the set that was written to LDS last iteration.
-  // Loads/stores are unconditional: tiles past the end are clamped + zero-filled (their LDS
-  // writes land in a buffer that is never read again).  Conditional load/store pairs made the
-  // waitcnt pass drain vmcnt(0) at the loop back-edge, serialising the prefetch.
-  int kt = 0;
-  if (nk >= 4) {
-    for (; kt + 2 <= nk; kt += 2) {
-      // even step: compute LDS0 (tile kt), st1 holds kt+1, reload st0 with kt+2
+  // step kt: LDS[kt&1] holds tile kt and sets (kt+1..kt+NS-1) % NS hold the next tiles; set
+  // kt % NS is free (tile kt was stored last step) and receives tile kt+NS.  Loads are
+  // unconditional (tiles past the end are clamped and zero-filled, never stored): conditional
+  // load/store pairs made the waitcnt pass drain vmcnt(0) at the back-edge.  Stores past the end
+  // are skipped, so no step waits for a load it does not use.  Every step ends with a barrier
+  // (the epilogue's fp32 staging tile aliases the LDS buffers).
+  for (int kb = 0; kb < nk; kb += NS) {
+#pragma unroll
+    for (int u = 0; u < NS; ++u) {
+      const int kt = kb + u;
+      if (kt >= nk) break;
       advance_k();
-      load_tile(st0);
-      compute(0);
-      store_tile(st1, 1);
-      __syncthreads();
-      // odd step: compute LDS1 (tile kt+1), st0 holds kt+2, reload st1 with kt+3
-      advance_k();
-      load_tile(st1);
-      compute(1);
-      store_tile(st0, 0);
+      load_tile(st[u]);
+      compute(u & 1);
+      if (kt + 1 < nk) store_tile(st[(u + 1) % NS], (u + 1) & 1);
       __syncthreads();
     }
-    if (kt < nk) {
-      compute(0);  // odd tile count: the last tile sits in LDS0
-      __syncthreads();  // the epilogue's fp32 staging tile aliases LDS0
-    }
-  } else if (nk == 3) {
-    // short K (the small late layers): straight-line, no load issued or waited for past the end
-    advance_k();
-    load_tile(st0);
-    compute(0);
-    store_tile(st1, 1);
-    __syncthreads();
-    compute(1);
-    store_tile(st0, 0);
-    __syncthreads();
-    compute(0);
-    __syncthreads();
-  } else if (nk == 2) {
-    compute(0);
-    store_tile(st1, 1);
-    __syncthreads();
-    compute(1);
-    __syncthreads();
-  } else if (nk == 1) {
-    compute(0);
-    __syncthreads();
   }
   IDC_PHASE_STAMP(7);
 
@@ -576,12 +558,19 @@ __global__ __launch_bounds__(256) void conv_igemm_kernel(ConvArgs a) {
   float psum[8], psq[8];
 #pragma unroll
   for (int j = 0; j < 8; ++j) { psum[j] = 0.f; psq[j] = 0.f; }
-  // a thread's 8-channel chunk is the same in every pass (NT % CPB == 0): its per-channel
-  // epilogue coefficients (and bias) are read once into registers
+  // a thread's 8-channel chunk is the same in every pass (NT % CPB == 0): on the small tiles its
+  // per-channel epilogue coefficients (and bias) are read once into registers; the big tiles
+  // keep their accumulators live across passes and read them from LDS per element instead
+  constexpr bool HOIST = TM * TN <= 8;
   const int my_c8 = tid % CPB;
-  float t_e0[8], t_e1[8], t_e2[8], t_e3[8], t_pb[8], t_pc[8], t_bias[8];
+  float t_e0[8], t_e1[8], t_e2[8], t_e3[8], t_pb[8], t_pc[8], t_bias[8], t_k[8];
 #pragma unroll
   for (int j = 0; j < 8; ++j) {
+    const int c = n0 + my_c8 * 8 + j;
+    t_k[j] = (EPI == 0 && a.stats_shift && c < a.Cout) ? a.stats_shift[c] : 0.f;
+  }
+#pragma unroll
+  for (int j = 0; j < 8 && HOIST; ++j) {
     const int cj = my_c8 * 8 + j;
     if constexpr (EPI >= 1) {
       t_e0[j] = s_e0[cj]; t_e1[j] = s_e1[cj]; t_e2[j] = s_e2[cj]; t_e3[j] = s_e3[cj];
@@ -624,7 +613,7 @@ __global__ __launch_bounds__(256) void conv_igemm_kernel(ConvArgs a) {
       if constexpr (EPI == 0) {
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
-          float t = v[j] + t_bias[j];
+          float t = v[j] + (HOIST ? t_bias[j] : (a.bias ? a.bias[n + j] : 0.f));
           v[j] = clampf(t, epi_lo, epi_hi);
         }
         if (a.out_mode == OUT_BF16) {
@@ -634,7 +623,11 @@ __global__ __launch_bounds__(256) void conv_igemm_kernel(ConvArgs a) {
             float r[8];
             unpack8(p, r);
 #pragma unroll
-            for (int j = 0; j < 8; ++j) { psum[j] += r[j]; psq[j] += r[j] * r[j]; }
+            for (int j = 0; j < 8; ++j) {
+              const float dj = r[j] - t_k[j];
+              psum[j] += dj;
+              psq[j] += dj * dj;
+            }
           }
         } else {
           float* yp = reinterpret_cast<float*>(a.y) + (size_t)m * a.ldy + n;
@@ -648,7 +641,11 @@ __global__ __launch_bounds__(256) void conv_igemm_kernel(ConvArgs a) {
           *reinterpret_cast<float4*>(yp + 4) = make_float4(v[4], v[5], v[6], v[7]);
           if (want_stats) {
 #pragma unroll
-            for (int j = 0; j < 8; ++j) { psum[j] += v[j]; psq[j] += v[j] * v[j]; }
+            for (int j = 0; j < 8; ++j) {
+              const float dj = v[j] - t_k[j];
+              psum[j] += dj;
+              psq[j] += dj * dj;
+            }
           }
         }
       } else if constexpr (EPI == 2) {
@@ -671,11 +668,15 @@ __global__ __launch_bounds__(256) void conv_igemm_kernel(ConvArgs a) {
         unpack8(xv, xf);
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
-          const float z = xf[j] * t_e0[j] + t_e1[j];
+          const int cj = c8 * 8 + j;
+          const float e0 = HOIST ? t_e0[j] : s_e0[cj], e1 = HOIST ? t_e1[j] : s_e1[cj];
+          const float e2 = HOIST ? t_e2[j] : s_e2[cj], e3 = HOIST ? t_e3[j] : s_e3[cj];
+          const float pb = HOIST ? t_pb[j] : s_pb[cj], pc = HOIST ? t_pc[j] : s_pc[cj];
+          const float z = xf[j] * e0 + e1;
           const float d = (z > msk_lo && z < msk_hi) ? v[j] : 0.f;
           psum[j] += d;
-          psq[j] += d * (xf[j] - t_e2[j]) * t_e3[j];
-          o[j] = old[j] + fmaf(t_e0[j], d, fmaf(t_pb[j], xf[j], t_pc[j]));
+          psq[j] += d * (xf[j] - e2) * e3;
+          o[j] = old[j] + fmaf(e0, d, fmaf(pb, xf[j], pc));
         }
         *reinterpret_cast<float4*>(yp) = make_float4(o[0], o[1], o[2], o[3]);
         *reinterpret_cast<float4*>(yp + 4) = make_float4(o[4], o[5], o[6], o[7]);
@@ -687,7 +688,8 @@ __global__ __launch_bounds__(256) void conv_igemm_kernel(ConvArgs a) {
         unpack8(xv, xf);
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
-          float z = xf[j] * t_e0[j] + t_e1[j];
+          const int cj = c8 * 8 + j;
+          float z = xf[j] * (HOIST ? t_e0[j] : s_e0[cj]) + (HOIST ? t_e1[j] : s_e1[cj]);
           d[j] = (z > msk_lo && z < msk_hi) ? v[j] : 0.f;
         }
         uint4 p = pack8(d);
@@ -696,8 +698,9 @@ __global__ __launch_bounds__(256) void conv_igemm_kernel(ConvArgs a) {
         unpack8(p, r);
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
+          const int cj = c8 * 8 + j;
           psum[j] += r[j];
-          psq[j] += r[j] * (xf[j] - t_e2[j]) * t_e3[j];
+          psq[j] += r[j] * (xf[j] - (HOIST ? t_e2[j] : s_e2[cj])) * (HOIST ? t_e3[j] : s_e3[cj]);
         }
       }
     }

@@ -25,6 +25,8 @@ struct DwArgs {
   // bwd data / wgrad (3x3 only): dy is staged through the pending backward of the BatchNorm that
   // follows this depthwise conv (common.h BwdAff; x = the raw depthwise output at dy's positions)
   BwdAff dyaff;
+  // fwd statistics shift per channel (nullable, common.h "Shifted statistics")
+  const float* stats_shift;
 };
 
 long long dwconv_wgrad_ws_floats(long long M, int C, int taps);

@@ -75,7 +75,11 @@ __global__ __launch_bounds__(256) void dw_fwd_kernel(DwArgs a) {
       if (a.stats) {
         unpack8(p, acc);
 #pragma unroll
-        for (int j = 0; j < 8; ++j) { ps[j] += acc[j]; pq[j] += acc[j] * acc[j]; }
+        for (int j = 0; j < 8; ++j) {
+          const float dj = acc[j] - (a.stats_shift ? a.stats_shift[c + j] : 0.f);
+          ps[j] += dj;
+          pq[j] += dj * dj;
+        }
       }
     }
     if (a.stats) {
@@ -254,7 +258,9 @@ __global__ __launch_bounds__(256) void dw_fwd3_kernel(DwArgs a) {
 #pragma unroll
     for (int j = 0; j < 8; ++j) { sc[j] = s_sc[c + j]; sf[j] = s_sf[c + j]; }
     const float lo = act_lo(a.pro.act), hi = act_hi(a.pro.act);
-    float ps[8] = {0}, pq[8] = {0};
+    float ps[8] = {0}, pq[8] = {0}, kk[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) kk[j] = a.stats_shift ? a.stats_shift[c + j] : 0.f;
     for (int st = blockIdx.x * mp.R + mp.ty; st < strips; st += gridDim.x * mp.R) {
       const int ws = st % WS, t = st / WS, ho = t % a.Ho, n = t / a.Ho;
       const int wo0 = ws * P;
@@ -302,7 +308,11 @@ __global__ __launch_bounds__(256) void dw_fwd3_kernel(DwArgs a) {
         float r8[8];
         unpack8(pk, r8);
 #pragma unroll
-        for (int j = 0; j < 8; ++j) { ps[j] += r8[j]; pq[j] += r8[j] * r8[j]; }
+        for (int j = 0; j < 8; ++j) {
+          const float dj = r8[j] - kk[j];
+          ps[j] += dj;
+          pq[j] += dj * dj;
+        }
       }
     }
     if (a.stats) {

@@ -42,6 +42,7 @@ struct PoolArgs {
   uint8_t* argmax;     // [N*Ho*Wo*C] (max pool)
   float* stats; int stats_ld; int stats_off;  // output statistics (optional)
   int stats_slots;
+  const float* stats_shift;  // shift of the output channels (pre-offset to output channel 0)
 };
 
 struct PoolBwdArgs {
@@ -66,7 +67,15 @@ struct BnMovingDesc {
   float* mmean; float* mvar; float momentum;
   int ld;  // statistics row length (sumsq of channel c at stats[ld + c])
   int slots;  // statistics slot copies (stride 2*ld)
+  const float* shift;  // per-channel statistics shift (nullable, common.h "Shifted statistics")
 };
+
+// one statistics array whose shift is advanced to this step's batch mean (stats_shift)
+struct ShiftDesc {
+  const float* stats; float* shift;
+  int ld; int slots; float inv_count; int pad;
+};
+hipError_t stats_shift(const ShiftDesc* d, int n, int maxC, hipStream_t st);
 
 struct HeadArgs {
   const bf16_t* x; int ldx;  // [N*HW, C]

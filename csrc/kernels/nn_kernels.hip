@@ -81,7 +81,12 @@ inline int grid_rows(int M, int C, int per_thread_rows = 4) {
   int C8 = C / 8;
   int R = 256 / C8;
   if (R < 1) R = 1;
-  long long blocks = ((long long)M + (long long)R * per_thread_rows - 1) / ((long long)R * per_thread_rows);
+  const long long full = ((long long)M + (long long)R * per_thread_rows - 1) / ((long long)R * per_thread_rows);
+  // every workgroup first builds its BatchNorm tables (slot-summed statistics: dependent memory
+  // round trips of a few us) and then grid-strides over rows: a grid sized for one pass of
+  // per_thread_rows rows ran the prologue per ~64 rows (the stem max-pool backward: 2500
+  // workgroups, 151 us).  Keep at most max(512, full/8) workgroups (>= 2 per CU).
+  long long blocks = full < 512 ? full : (full + 7) / 8 > 512 ? (full + 7) / 8 : 512;
   if (blocks > 4096) blocks = 4096;
   if (blocks < 1) blocks = 1;
   return (int)blocks;
@@ -177,13 +182,14 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(BnBwdApplyArgs a) {
   // ones (large maps, <= 512 channels): one channel per batch, its 2*(SS+SG) loads in flight
   const int per = (SG == 1 && SS == 1) ? 4 : 1;
   for (int base = 0; base < a.C; base += per * 256) {
-    float m0[4], m1[4], g[4], q0[4], q1[4];
+    float m0[4], m1[4], g[4], q0[4], q1[4], k[4];
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
       if (u >= per) break;
       const int c = base + u * 256 + threadIdx.x;
       const int cc = c < a.C ? c : 0;
       g[u] = a.bn.gamma[cc];
+      k[u] = batch_mode ? bn_shift(a.bn, cc) : 0.f;
       if (batch_mode) {
         if (SS == 1) {
           m0[u] = a.bn.stats[cc];
@@ -208,10 +214,7 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(BnBwdApplyArgs a) {
       const int c = base + u * 256 + threadIdx.x;
       if (u >= per || c >= a.C) break;
       float mean = m0[u], var = m1[u];
-      if (batch_mode) {
-        mean *= a.bn.inv_count;
-        var = fmaxf(var * a.bn.inv_count - mean * mean, 0.f);
-      }
+      if (batch_mode) shifted_mean_var(k[u], m0[u], m1[u], a.bn.inv_count, mean, var);
       const float rstd = rsqrtf(var + a.bn.eps);
       if (blockIdx.x == 0 && a.fold_sum) {  // d beta / d gamma into the gradient arena
         a.fold_sum[c] += q0[u];
@@ -350,6 +353,9 @@ __global__ __launch_bounds__(256) void pool_fwd_kernel(PoolArgs a) {
   const bool ident = (a.pro.mode == 0 && a.pro.act == ACT_NONE);
   if (cm.active()) {
     const int c = cm.tx * 8;
+    float kk[8];  // statistics shift of this thread's chunk
+#pragma unroll
+    for (int j = 0; j < 8; ++j) kk[j] = a.stats_shift ? a.stats_shift[c + j] : 0.f;
     for (int o = blockIdx.x * cm.R + cm.ty; o < Mo; o += gridDim.x * cm.R) {
       int wo = o % a.Wo, t = o / a.Wo, ho = t % a.Ho, n = t / a.Ho;
       float best[8], sum[8];
@@ -414,7 +420,11 @@ __global__ __launch_bounds__(256) void pool_fwd_kernel(PoolArgs a) {
       if (a.stats) {
         unpack8(p, out);
 #pragma unroll
-        for (int j = 0; j < 8; ++j) { ps[j] += out[j]; pq[j] += out[j] * out[j]; }
+        for (int j = 0; j < 8; ++j) {
+          const float dj = out[j] - kk[j];
+          ps[j] += dj;
+          pq[j] += dj * dj;
+        }
       }
     }
   }
@@ -609,11 +619,31 @@ __global__ void bn_update_moving_kernel(const BnMovingDesc* d, int n) {
       s0 += b.stats[(size_t)s * 2 * b.ld + c];
       s1 += b.stats[(size_t)s * 2 * b.ld + b.ld + c];
     }
-    float mean = s0 * b.inv_count;
-    float var = fmaxf(s1 * b.inv_count - mean * mean, 0.f) * b.unbias;
+    float mean, var;
+    shifted_mean_var(b.shift ? b.shift[c] : 0.f, s0, s1, b.inv_count, mean, var);
+    var *= b.unbias;
     b.mmean[c] = b.momentum * b.mmean[c] + (1.f - b.momentum) * mean;
     b.mvar[c] = b.momentum * b.mvar[c] + (1.f - b.momentum) * var;
   }
+}
+
+// after the backward: every statistics array's shift becomes this step's batch mean (the next
+// step's producers accumulate around it, common.h "Shifted statistics")
+__global__ void stats_shift_kernel(const ShiftDesc* d, int n) {
+  const ShiftDesc& b = d[blockIdx.y];
+  for (int c = blockIdx.x * blockDim.x + threadIdx.x; c < b.ld; c += gridDim.x * blockDim.x) {
+    float s0 = 0.f;
+    for (int s = 0; s < stat_slots(b.slots); ++s) s0 += b.stats[(size_t)s * 2 * b.ld + c];
+    // a non-finite batch (a step the non-finite guard skips) keeps the old shift
+    const float k = b.shift[c] + s0 * b.inv_count;
+    if (isfinite(k)) b.shift[c] = k;
+  }
+}
+
+hipError_t stats_shift(const ShiftDesc* d, int n, int maxC, hipStream_t st) {
+  if (n == 0) return hipSuccess;
+  hipLaunchKernelGGL(stats_shift_kernel, dim3((maxC + 255) / 256, n), dim3(256), 0, st, d, n);
+  return hipGetLastError();
 }
 
 hipError_t bn_update_moving(const BnMovingDesc* d, int n, int maxC, hipStream_t st) {

@@ -69,6 +69,7 @@ enum OpKind : int {
   OP_MLP_BWD = 22,
   OP_MLP_STEP = 23,
   OP_COLLAPSE = 24,
+  OP_STATS_SHIFT = 25,
 };
 
 struct Op {
@@ -188,9 +189,9 @@ class Plan {
                                   "pool_bwd", "bn_moving", "head_fwd", "head_bwd", "rmsprop", "cast",
                                   "input", "memset", "bn_stats", "bn_apply", "dw_fwd", "dw_bwd_data",
                                   "dw_wgrad", "copy", "finite_check", "mlp_fwd", "mlp_bwd", "mlp_step",
-                                  "collapse"};
+                                  "collapse", "stats_shift"};
     int k = ops_.at(idx).kind;
-    return (k >= 0 && k < 25) ? names[k] : "?";
+    return (k >= 0 && k < 26) ? names[k] : "?";
   }
 
  private:
@@ -328,6 +329,9 @@ class Plan {
                             op.i[1], op.i[2], st),
               "slot_collapse");
         break;
+      case OP_STATS_SHIFT:
+        check(stats_shift(reinterpret_cast<const ShiftDesc*>(op.p[0]), op.i[0], op.i[1], st), "stats_shift");
+        break;
       case OP_COPY:
         check(hipMemcpyAsync(reinterpret_cast<void*>(op.p[0]), reinterpret_cast<const void*>(op.p[1]),
                              (size_t)op.l[0], hipMemcpyDeviceToDevice, st),
@@ -375,6 +379,12 @@ py::dict struct_sizes() {
   d["PoolArgs"] = sizeof(PoolArgs);
   d["PoolBwdArgs"] = sizeof(PoolBwdArgs);
   d["BnMovingDesc"] = sizeof(BnMovingDesc);
+  d["ShiftDesc"] = sizeof(ShiftDesc);
+  d["BnArgs.shift"] = offsetof(BnArgs, shift);
+  d["ConvArgs.stats_shift"] = offsetof(ConvArgs, stats_shift);
+  d["PoolArgs.stats_shift"] = offsetof(PoolArgs, stats_shift);
+  d["DwArgs.stats_shift"] = offsetof(DwArgs, stats_shift);
+  d["BnMovingDesc.shift"] = offsetof(BnMovingDesc, shift);
   d["HeadArgs"] = sizeof(HeadArgs);
   d["HeadBwdArgs"] = sizeof(HeadBwdArgs);
   d["CastEntry"] = sizeof(CastEntry);

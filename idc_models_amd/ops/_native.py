@@ -27,7 +27,8 @@ cll = C.c_longlong
 
 class BnArgs(C.Structure):
     _fields_ = [("stats", vp), ("gamma", vp), ("beta", vp), ("mmean", vp), ("mvar", vp),
-                ("inv_count", cf), ("eps", cf), ("mode", ci), ("act", ci), ("C", ci), ("slots", ci)]
+                ("inv_count", cf), ("eps", cf), ("mode", ci), ("act", ci), ("C", ci), ("slots", ci),
+                ("shift", vp)]
 
 
 class BwdAff(C.Structure):
@@ -46,7 +47,7 @@ class ConvArgs(C.Structure):
                 ("mx", vp), ("ldmx", ci), ("mbn", BnArgs), ("gsum", vp), ("gsumx", vp),
                 ("slab", vp), ("tickets", vp), ("slab_floats", cll), ("tickets_n", ci),
                 ("ksplit", ci), ("stats_slots", ci), ("gsum_slots", ci), ("gsum_ld", ci),
-                ("bpro", BwdAff), ("bepi", BwdAff), ("aout", vp), ("ldaout", ci)]
+                ("bpro", BwdAff), ("bepi", BwdAff), ("aout", vp), ("ldaout", ci), ("stats_shift", vp)]
 
 
 class WgradArgs(C.Structure):
@@ -74,7 +75,7 @@ class PoolArgs(C.Structure):
     _fields_ = [("x", vp), ("ldx", ci), ("N", ci), ("H", ci), ("W", ci), ("C", ci),
                 ("pro", BnArgs), ("k", ci), ("s", ci), ("pt", ci), ("pl", ci), ("Ho", ci),
                 ("Wo", ci), ("y", vp), ("ldy", ci), ("argmax", vp), ("stats", vp),
-                ("stats_ld", ci), ("stats_off", ci), ("stats_slots", ci)]
+                ("stats_ld", ci), ("stats_off", ci), ("stats_slots", ci), ("stats_shift", vp)]
 
 
 class PoolBwdArgs(C.Structure):
@@ -87,7 +88,11 @@ class PoolBwdArgs(C.Structure):
 
 class BnMovingDesc(C.Structure):
     _fields_ = [("stats", vp), ("C", ci), ("inv_count", cf), ("unbias", cf), ("mmean", vp),
-                ("mvar", vp), ("momentum", cf), ("ld", ci), ("slots", ci)]
+                ("mvar", vp), ("momentum", cf), ("ld", ci), ("slots", ci), ("shift", vp)]
+
+
+class ShiftDesc(C.Structure):
+    _fields_ = [("stats", vp), ("shift", vp), ("ld", ci), ("slots", ci), ("inv_count", cf), ("pad", ci)]
 
 
 class HeadArgs(C.Structure):
@@ -112,7 +117,7 @@ class DwArgs(C.Structure):
                 ("PL", ci), ("Ho", ci), ("Wo", ci), ("y", vp), ("ldy", ci), ("stats", vp),
                 ("stats_ld", ci), ("dy", vp), ("lddy", ci), ("dx", vp), ("lddx", ci),
                 ("gsum", vp), ("gsumx", vp), ("dw", vp), ("ws", vp), ("stats_slots", ci),
-                ("gsum_slots", ci), ("gsum_ld", ci), ("dyaff", BwdAff)]
+                ("gsum_slots", ci), ("gsum_ld", ci), ("dyaff", BwdAff), ("stats_shift", vp)]
 
 
 class Mlp2Args(C.Structure):
@@ -127,13 +132,13 @@ _STRUCTS = {"BnArgs": BnArgs, "BwdAff": BwdAff, "ConvArgs": ConvArgs, "WgradArgs
             "BnBwdApplyArgs": BnBwdApplyArgs, "BnBwdReduceArgs": BnBwdReduceArgs,
             "PoolArgs": PoolArgs, "PoolBwdArgs": PoolBwdArgs, "BnMovingDesc": BnMovingDesc,
             "HeadArgs": HeadArgs, "HeadBwdArgs": HeadBwdArgs, "CastEntry": CastEntry,
-            "DwArgs": DwArgs, "Mlp2Args": Mlp2Args}
+            "DwArgs": DwArgs, "Mlp2Args": Mlp2Args, "ShiftDesc": ShiftDesc}
 
 # op kinds (csrc/runtime/plan.cpp)
 OP_CONV, OP_WGRAD, OP_BN_BWD_APPLY, OP_BN_BWD_REDUCE, OP_MAXPOOL, OP_AVGPOOL, OP_POOL_BWD = range(7)
 OP_BN_MOVING, OP_HEAD_FWD, OP_HEAD_BWD, OP_RMSPROP, OP_CAST, OP_INPUT, OP_MEMSET = range(7, 14)
 OP_BN_STATS, OP_BN_APPLY, OP_DW_FWD, OP_DW_BWD_DATA, OP_DW_WGRAD, OP_COPY, OP_FINITE_CHECK = range(14, 21)
-OP_MLP_FWD, OP_MLP_BWD, OP_MLP_STEP, OP_COLLAPSE = range(21, 25)
+OP_MLP_FWD, OP_MLP_BWD, OP_MLP_STEP, OP_COLLAPSE, OP_STATS_SHIFT = range(21, 26)
 
 ACT = {None: 0, "none": 0, "linear": 0, "relu": 1, "relu6": 2}
 OUT_BF16, OUT_F32, OUT_F32_ACC = 0, 1, 2
@@ -154,7 +159,11 @@ def _verify(ext):
               "WgradArgs.gpro": WgradArgs.gpro.offset, "PoolBwdArgs.dx_f32": PoolBwdArgs.dx_f32.offset,
               "BwdAff.fold_sumx": BwdAff.fold_sumx.offset, "ConvArgs.aout": ConvArgs.aout.offset,
               "WgradArgs.part_floats": WgradArgs.part_floats.offset, "HeadBwdArgs.det": HeadBwdArgs.det.offset,
-              "DwArgs.dyaff": DwArgs.dyaff.offset}
+              "DwArgs.dyaff": DwArgs.dyaff.offset, "BnArgs.shift": BnArgs.shift.offset,
+              "ConvArgs.stats_shift": ConvArgs.stats_shift.offset,
+              "PoolArgs.stats_shift": PoolArgs.stats_shift.offset,
+              "DwArgs.stats_shift": DwArgs.stats_shift.offset,
+              "BnMovingDesc.shift": BnMovingDesc.shift.offset}
     for k, v in checks.items():
         if sizes[k] != v:
             raise RuntimeError(f"native struct field {k}: ctypes offset {v} != C++ {sizes[k]}")
@@ -217,9 +226,10 @@ def raw(struct) -> bytes:
 
 
 def bn_args(stats=None, gamma=None, beta=None, mmean=None, mvar=None, count=1, eps=1e-3,
-            mode=0, act=0, C_=0, slots=1) -> BnArgs:
+            mode=0, act=0, C_=0, slots=1, shift=None) -> BnArgs:
     b = BnArgs()
     b.stats, b.gamma, b.beta = ptr(stats), ptr(gamma), ptr(beta)
+    b.shift = ptr(shift)
     b.mmean, b.mvar = ptr(mmean), ptr(mvar)
     b.inv_count = 1.0 / float(max(count, 1))
     b.eps = float(eps)

@@ -33,6 +33,7 @@ class BN:
     mode: int = 1
     act: int = 0
     ld: Optional[int] = None
+    shift: Optional[torch.Tensor] = None  # statistics shift K (stats hold sums of y - K)
 
     def args(self) -> nat.BnArgs:
         if self.stats is None and self.mean is None:
@@ -41,7 +42,7 @@ class BN:
         return nat.bn_args(stats=self.stats, gamma=self.gamma, beta=self.beta, mmean=self.mean,
                            mvar=self.var, count=self.count, eps=self.eps,
                            mode=self.mode if self.stats is not None or self.mode == 2 else 2,
-                           act=self.act, C_=C)
+                           act=self.act, C_=C, shift=self.shift)
 
 
 def _ident():
@@ -89,9 +90,10 @@ def conv2d(x: torch.Tensor, kernel_hwio: torch.Tensor, stride=(1, 1), pads=(0, 0
            out_hw: Optional[Tuple[int, int]] = None, pro: Optional[BN] = None,
            bias: Optional[torch.Tensor] = None, act: int = 0, out_f32: bool = False,
            stats: Optional[torch.Tensor] = None, tile: int = -1,
-           w_layout: Optional[torch.Tensor] = None, ksplit: int = 1) -> torch.Tensor:
+           w_layout: Optional[torch.Tensor] = None, ksplit: int = 1,
+           stats_shift: Optional[torch.Tensor] = None) -> torch.Tensor:
     """y = act(conv(pro(x)) + bias); x NHWC (bf16 or fp32), Cin % 8 == 0.  Optional output
-    statistics [sum|sumsq] accumulated into ``stats``."""
+    statistics [sum|sumsq] accumulated into ``stats`` (sums of y - ``stats_shift`` when given)."""
     N, H, W, Cin = x.shape
     kh, kw, kcin, cout = kernel_hwio.shape
     if out_hw is None:
@@ -115,6 +117,7 @@ def conv2d(x: torch.Tensor, kernel_hwio: torch.Tensor, stride=(1, 1), pads=(0, 0
     a.out_mode = nat.OUT_F32 if out_f32 else nat.OUT_BF16
     if stats is not None:
         a.stats_out, a.stats_ld, a.stats_off = stats.data_ptr(), cout, 0
+        a.stats_shift = nat.ptr(stats_shift)
     a.mbn = _ident()
     keep = _splitk_args(a, N * Ho * Wo, cout, ksplit, tile)
     nat.require().conv(nat.raw(a), tile, 1 if x.dtype == torch.float32 else 0, nat.stream_handle())
@@ -352,3 +355,22 @@ def dwconv_bwd(x, kernel, dy, stride=1, pads=(1, 1), pro: Optional[BN] = None, g
     _plan1(nat.OP_DW_BWD_DATA, a)
     _plan1(nat.OP_DW_WGRAD, a)
     return dx, dw
+
+
+def bn_moments(stats: torch.Tensor, count: int, shift: Optional[torch.Tensor] = None):
+    """(mean, unbiased variance) per channel as the BatchNorm consumers compute them from
+    [sum|sumsq] statistics (with ``shift``: sums of y - K), read out through the moving-statistics
+    kernel at momentum 0."""
+    C = stats.numel() // 2
+    mean = torch.zeros(C, dtype=torch.float32, device=stats.device)
+    var = torch.zeros_like(mean)
+    d = nat.BnMovingDesc()
+    d.stats, d.C, d.ld, d.slots = stats.data_ptr(), C, C, 1
+    d.inv_count = 1.0 / float(count)
+    d.unbias = count / max(count - 1, 1)
+    d.mmean, d.mvar, d.momentum = mean.data_ptr(), var.data_ptr(), 0.0
+    d.shift = nat.ptr(shift)
+    dev = torch.frombuffer(bytearray(bytes(d)), dtype=torch.uint8).to(stats.device)
+    _plan1(nat.OP_BN_MOVING, ints=(1, C), ptrs=(dev.data_ptr(),))
+    torch.cuda.synchronize()
+    return mean, var

@@ -75,6 +75,13 @@ class Stats:
     ld: int
     count: int
     slots: int = 1
+    # per-channel shift K (persistent across steps, NOT in the zeroed arena): the producers
+    # accumulate y - K, and K advances to the batch mean after every backward (common.h
+    # "Shifted statistics")
+    shift: Optional[torch.Tensor] = None
+
+    def shift_ptr(self, off: int = 0) -> int:
+        return self.shift.data_ptr() + 4 * off if self.shift is not None else 0
 
     @property
     def ptr(self):
@@ -106,7 +113,8 @@ class BNRef:
                            mmean=self.layer.moving_mean, mvar=self.layer.moving_variance,
                            count=st.count if st is not None else 1, eps=self.layer.epsilon,
                            mode=self.mode, act=self.act, C_=st.ld if st is not None else self.C,
-                           slots=st.slots if (st is not None and self.mode == 1) else 1)
+                           slots=st.slots if (st is not None and self.mode == 1) else 1,
+                           shift=st.shift if (st is not None and self.mode == 1) else None)
 
 
 def act_only(act: int) -> nat.BnArgs:
@@ -154,6 +162,9 @@ class Builder:
         # (the deterministic mode's per-workgroup private slots need ~10-40x more)
         self._stats_cap = (1 << 25) if self.det else (1 << 20)
         self.stats_arena = torch.zeros(self._stats_cap, dtype=F32, device=device)
+        self.all_stats: List[Stats] = []
+        # shifted statistics (IDC_STATS_SHIFT=0: plain E[y^2] - E[y]^2, for comparisons)
+        self.shift_stats = os.environ.get("IDC_STATS_SHIFT", "1") != "0"
 
     # ------------------------------------------------------------------ allocation
     def alloc(self, shape, dtype=BF16) -> torch.Tensor:
@@ -194,7 +205,29 @@ class Builder:
 
     def stats(self, ld: int, count: int) -> Stats:
         slots = stat_slots_for(count) if (self.stat_slots_on and not self.det) else 1
-        return Stats(self._stats_floats(2 * ld * slots), ld, count, slots)
+        st = Stats(self._stats_floats(2 * ld * slots), ld, count, slots,
+                   self.alloc((ld,), F32) if self.shift_stats else None)
+        self.all_stats.append(st)
+        return st
+
+    def emit_stats_shift(self):
+        """After the last consumer of this step's statistics: every shifted statistics array's K
+        becomes its batch mean (the next step's producers accumulate around it).  Issued as the
+        LAST side-lane op: side-lane weight gradients read the statistics (and K) in their
+        prologues, and the final side batch is forked after every main-lane op (plan.cpp issue),
+        so it runs after the consumers of both lanes."""
+        descs = [st for st in self.all_stats if st.shift is not None]
+        if not descs:
+            return
+        arr = (nat.ShiftDesc * len(descs))()
+        for d, st in zip(arr, descs):
+            d.stats, d.shift, d.ld, d.slots = st.ptr, st.shift.data_ptr(), st.ld, st.slots
+            d.inv_count = 1.0 / float(max(st.count, 1))
+        host = torch.frombuffer(bytearray(C.string_at(C.addressof(arr), C.sizeof(arr))), dtype=torch.uint8)
+        dev = host.to(self.device)
+        self.keep.append(dev)
+        self.emit(nat.OP_STATS_SHIFT, ints=(len(descs), max(st.ld for st in descs)), ptrs=(dev.data_ptr(),),
+                  lane=1 if self.side_lane else 0)
 
     def grad_sums(self, bn: Optional["BNRef"], rows: int, grid: int = 0):
         """(gsum, gsumx, slots, ld) for the producer of a BatchNorm backward's reductions
@@ -380,6 +413,7 @@ class Builder:
         d.mmean = bn.layer.moving_mean.data_ptr()
         d.mvar = bn.layer.moving_variance.data_ptr()
         d.momentum = bn.layer.momentum
+        d.shift = st.shift_ptr()
         self.moving.append(d)
 
     # ------------------------------------------------------------------ kernels
@@ -400,7 +434,7 @@ class Builder:
             return (v or 0) + off if v else 0
 
         bna.stats, bna.gamma, bna.beta = sh(bna.stats), sh(bna.gamma), sh(bna.beta)
-        bna.mmean, bna.mvar = sh(bna.mmean), sh(bna.mvar)
+        bna.mmean, bna.mvar, bna.shift = sh(bna.mmean), sh(bna.mvar), sh(bna.shift)
         a.bn = bna
         if bn.mode == 1:
             if getattr(bn, "gsums", None) is None:
@@ -450,6 +484,7 @@ class Builder:
         if stats is not None:
             a.stats_out, a.stats_ld, a.stats_off = stats.ptr, stats.ld, stats_off
             a.stats_slots = stats.slots
+            a.stats_shift = stats.shift_ptr(stats_off)
             if self.det:
                 a.stats_out, a.stats_ld, a.stats_off, a.stats_slots = self._det_stats_slots(
                     y.C, self._conv_row_tiles(M), stats, stats_off)
@@ -637,6 +672,7 @@ class Builder:
         if stats is not None:
             a.stats, a.stats_ld, a.stats_off = stats.ptr, stats.ld, stats_off
             a.stats_slots = stats.slots
+            a.stats_shift = stats.shift_ptr(stats_off)
             if self.det:
                 a.stats, a.stats_ld, a.stats_off, a.stats_slots = self._det_stats_slots(
                     x.C, self._rows_grid(x.N * y.H * y.W, x.C, 1), stats, stats_off)
@@ -674,6 +710,9 @@ class Builder:
                  res: Optional[Tensor4] = None, stats: Optional[Stats] = None):
         """Materialise y = act(BN(x)) [+ res] (bf16), optionally reducing y's statistics."""
         self._no_det("bn_apply")
+        if stats is not None and stats.shift is not None:
+            raise NotImplementedError("bn_apply statistics are not shifted; allocate them with "
+                                      "IDC_STATS_SHIFT=0 or reduce through a conv epilogue")
         args = bn.args()
         if act is not None:
             args.act = act
@@ -706,6 +745,7 @@ class Builder:
         if stats is not None:
             a.stats, a.stats_ld = stats.ptr, stats.ld
             a.stats_slots = stats.slots
+            a.stats_shift = stats.shift_ptr()
         self.emit(nat.OP_DW_FWD, a)
 
     def _dw_dyaff(self, a: nat.DwArgs, layer, dyaff: Optional[nat.BwdAff]):

@@ -73,6 +73,10 @@ class FusedProgram:
         if b.pending_sums:  # BatchNorm gradient slot copies no apply kernel folded
             b.segment = "bwd"
             b.flush_grad_sums()
+        if training and b.ops:
+            # statistics shifts advance after the step's last statistics consumer
+            b.segment = b.ops[-1][0]
+            b.emit_stats_shift()
         self.b = b
         self.xin = b.xin
         self.io = b.io
@@ -182,6 +186,13 @@ class FusedProgram:
         if self._cast_all_plan is not None:
             with torch.cuda.stream(self.stream):
                 self._cast_all_plan.run(0, -1, self._sh())
+
+    def reset_stats_shift(self):
+        """Zero every statistics shift (the state the first step starts from): comparisons that
+        replay one program on several inputs as if each were a first step use it."""
+        for st in self.b.all_stats:
+            if st.shift is not None:
+                st.shift.zero_()
 
     def run_range(self, lo: int, hi: int, graph: Optional[bool] = None, join: bool = True):
         """Issue ops [lo, hi).  ``join=False`` (direct issue only) leaves the side lane running

@@ -61,6 +61,7 @@ def run_case(arch, kind, per=None):
         p = ref.impl._prog(per, True, torch.uint8)
         tot = torch.zeros_like(red)
         for r in range(world):
+            p.reset_stats_shift()  # each rank's shard as a first step (statistics shift K = 0)
             ref.impl._stage_inputs(p, x[r * per:(r + 1) * per], y[r * per:(r + 1) * per])
             p.run_segment("fwd")
             p.run_segment("bwd")

@@ -33,7 +33,8 @@ def test_deterministic_mode_is_bitwise_reproducible(monkeypatch, arch, B):
     m1, ref = _model(arch)
     p = m1.impl._prog(B, True, torch.uint8)
     grads = []
-    for _ in range(2):  # the same program twice
+    for _ in range(2):  # the same program twice, from the same state (statistics shift K = 0)
+        p.reset_stats_shift()
         m1.impl._stage_inputs(p, x, y)
         p.run_segment("fwd")
         p.run_segment("bwd")
@@ -46,6 +47,7 @@ def test_deterministic_mode_is_bitwise_reproducible(monkeypatch, arch, B):
     _check(m1, ref, x, y)
     # two independent models / programs, two full training steps each: identical weights
     m2, _ = _model(arch)
+    p.reset_stats_shift()  # m1's program already ran steps: start both from the same state
     for _ in range(2):
         m1.impl.train_step(x, y)
         m2.impl.train_step(x, y)

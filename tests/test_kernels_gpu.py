@@ -567,3 +567,30 @@ def test_bn_bwd_reduce_f32_scaled_output(fn):
     dZ = dy * (z > 0).float()
     assert relerr(a, k["A"] * dZ) < 1e-2
     assert relerr(gs, dZ.sum((0, 1, 2))) < 1e-2
+
+
+def test_bn_statistics_shifted_large_mean(fn):
+    """Offset-heavy activations (VERDICT: mean 50, std 0.1): the conv epilogue's fp32 statistics
+    cancel catastrophically in E[y^2] - E[y]^2, while statistics shifted by K (the previous step's
+    batch mean, common.h "Shifted statistics") give the variance to fp64 accuracy."""
+    g = torch.Generator(device="cpu").manual_seed(5)
+    N, H, Cin, Cout = 16, 16, 64, 64          # 4096 rows
+    x = (1.0 + 0.015 * torch.randn(N, H, H, Cin, generator=g)).to(DEV).to(torch.bfloat16)
+    k = torch.full((1, 1, Cin, Cout), 25.0 / 32.0, device=DEV)  # exact in bf16: y = 0.78125 * sum(x)
+    k[0, 0, :, 1::2] *= 0.5                                    # second mean level (~25) on odd channels
+    M = N * H * H
+    s0 = torch.zeros(2 * Cout, device=DEV)
+    y = fn.conv2d(x, k, out_f32=True, stats=s0)
+    yr = y.reshape(M, Cout).double()
+    mref, vref = yr.mean(0), yr.var(0)                         # unbiased, as the kernel reports
+    assert float(mref[0]) == pytest.approx(50.0, rel=0.02) and float(vref[0].sqrt()) < 0.2
+    m0, v0 = fn.bn_moments(s0, M)                              # K = 0: plain fp32 sums
+    K = m0.clone()                                             # the shift the next step would use
+    s1 = torch.zeros(2 * Cout, device=DEV)
+    fn.conv2d(x, k, out_f32=True, stats=s1, stats_shift=K)
+    m1, v1 = fn.bn_moments(s1, M, shift=K)
+    err0 = float(((v0.double() - vref) / vref).abs().max())
+    err1 = float(((v1.double() - vref) / vref).abs().max())
+    assert float(((m1.double() - mref) / mref).abs().max()) < 1e-5
+    assert err1 < 2e-3, err1
+    assert err0 > 10 * err1, (err0, err1)                      # what the shift buys
