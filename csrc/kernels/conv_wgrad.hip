@@ -12,6 +12,8 @@
 // so tiles are staged [pixel][column] in LDS and read transposed with ds_read_b64_tr_b16
 // (guide §5.5 T10); the XOR swizzles below were brute-force checked conflict-free for those
 // reads and for the ds_write_b128 staging stores.
+#include <cstdlib>
+
 #include "common.h"
 #include "conv_wgrad.h"
 
@@ -274,6 +276,193 @@ __global__ __launch_bounds__(256) void conv_wgrad_kernel(WgradArgs a) {
   }
 }
 
+// ----------------------------------------------------------------------------------------------
+// Direct 3x3 weight gradient for SMALL images (DenseNet growth convs: 3x3 / s1 / 'same',
+// Cout = 32, on 13x13, 6x6 and 3x3 maps).  As a pixel-split GEMM (conv_wgrad_kernel) these take
+// 20-50 us on the side lane: 32-pixel K steps of 4 MFMAs per wave, each behind a global load
+// round trip, plus ~100 fp32 atomics per dW element from the pixel slices.  Here a workgroup owns
+// a run of whole images and 64 input channels and keeps the full 9 x 64 x 32 dW partial in
+// registers (wave w: channels 16w..16w+15, all 9 taps, both 16-column halves of Cout):
+//
+//   * a pass stages P images as one stacked halo tile X[(img, h+1, w+1)][c] (BN + act applied,
+//     zero padding AFTER the activation, Keras semantics) and G[(img, h, w)][co] in the SAME
+//     padded (H+2)x(W+2) row space, so for tap (r, s) the im2col operand of output position q is
+//     simply row q + r*(W+2) + s of X: every tap is a shifted window, no gather, no im2col;
+//   * dW[tap][c][co] += sum_q X[q + off(tap)][c] * G[q][co] over q = pixel rows of the pass, in
+//     32-row chunks with v_mfma_f32_16x16x32_bf16; both operands are read transposed from their
+//     [row][column] LDS images with ds_read_b64_tr_b16 (tr_frag above), the G fragments once per
+//     chunk for all 9 taps;
+//   * positions outside an image (the W+2 padding columns, the rows between stacked images) have
+//     G = 0, so they add nothing; the next pass's loads are in flight during the MFMAs;
+//   * at the end, one fp32 atomic per dW element per workgroup (or a plain store into the
+//     deterministic mode's per-group partial slab).
+// Reference hot loop: the Conv2D gradient of dist_model_tf_dense.py:131-150 (DenseNet-121).
+namespace {
+constexpr int WH_CB = 64;        // input channels per workgroup
+constexpr int WH_MAXPIX = 256;   // valid pixels staged per pass (<= 8 X / 4 G chunks per thread)
+constexpr int WH_XROWB = WH_CB * 2;  // 128 B per X row
+constexpr int WH_GROWB = 32 * 2;     // 64 B per G row
+
+struct WhGeom {
+  int Hp, Wp, RI, P, q_max, qpad, xrows, grows;
+  size_t x_bytes, g_bytes;
+};
+
+__host__ __device__ inline WhGeom wh_geom(int H, int W, int ipw) {
+  WhGeom g;
+  g.Hp = H + 2;
+  g.Wp = W + 2;
+  g.RI = g.Hp * g.Wp;
+  int p = WH_MAXPIX / (H * W);
+  const int p_lds = (56 * 1024) / (g.RI * WH_XROWB);  // X tile budget
+  if (p > p_lds) p = p_lds;
+  if (p > ipw) p = ipw;
+  g.P = p < 1 ? 1 : p;
+  g.q_max = (g.P - 1) * g.RI + (H - 1) * g.Wp + W;  // one past the last valid output row
+  g.qpad = (g.q_max + 31) / 32 * 32;
+  const int need_x = g.qpad + 2 * g.Wp + 2;          // rows the shifted windows touch
+  g.xrows = need_x > g.P * g.RI ? need_x : g.P * g.RI;
+  g.grows = g.qpad;
+  g.x_bytes = (size_t)g.xrows * WH_XROWB;
+  g.g_bytes = (size_t)g.grows * WH_GROWB;
+  return g;
+}
+}  // namespace
+
+__global__ __launch_bounds__(256) void wgrad3x3_img_kernel(WgradArgs a, int ipw) {
+  prefetch_kernargs<sizeof(WgradArgs)>();
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int H = a.H, W = a.W;
+  const WhGeom geo = wh_geom(H, W, ipw);
+  bf16_t* Xs = reinterpret_cast<bf16_t*>(smem);
+  bf16_t* Gs = reinterpret_cast<bf16_t*>(smem + geo.x_bytes);
+  float* s_scale = reinterpret_cast<float*>(smem + geo.x_bytes + geo.g_bytes);
+  float* s_shift = s_scale + a.Cin;
+
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int c0 = blockIdx.y * WH_CB;
+  const int img_beg = blockIdx.x * ipw;
+  const int img_end = min(a.N, img_beg + ipw);
+  const int HW = H * W, Wp = geo.Wp, RI = geo.RI, P = geo.P;
+
+  // zero both tiles once: padding rows / columns are never written afterwards
+  {
+    uint4* z = reinterpret_cast<uint4*>(smem);
+    const int n16 = (int)((geo.x_bytes + geo.g_bytes) / 16);
+    for (int i = tid; i < n16; i += 256) z[i] = make_uint4(0, 0, 0, 0);
+  }
+  bn_coeff_table<256>(a.pro, a.Cin, s_scale, s_shift);
+  const float lo = act_lo(a.pro.act), hi = act_hi(a.pro.act);
+
+  const bf16_t* __restrict__ X = a.x;
+  const bf16_t* __restrict__ G = reinterpret_cast<const bf16_t*>(a.g);
+  uint4 rx[8], rg[4];
+
+  // chunk i of a pass: X chunk e = tid + 256*i -> (pixel e/8, channel chunk e%8);
+  //                    G chunk e = tid + 256*i -> (pixel e/4, column chunk e%4)
+  auto load = [&](int ib) {
+    const int np = min(P, img_end - ib) * HW;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const int e = tid + 256 * i, px = e >> 3, ch = e & 7;
+      const bool ok = px < np;
+      const size_t pix = (size_t)ib * HW + (ok ? px : 0);
+      rx[i] = *reinterpret_cast<const uint4*>(X + pix * a.ldx + c0 + ch * 8);
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int e = tid + 256 * i, px = e >> 2, ch = e & 3;
+      const bool ok = px < np;
+      const size_t pix = (size_t)ib * HW + (ok ? px : 0);
+      rg[i] = *reinterpret_cast<const uint4*>(G + pix * a.ldg + ch * 8);
+    }
+  };
+  auto store = [&](int ib) {
+    const int nimg = min(P, img_end - ib);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const int e = tid + 256 * i, px = e >> 3, ch = e & 7;
+      if (px >= nimg * HW) continue;  // rows of absent images keep stale finite values (G = 0 there)
+      const int im = px / HW, r = px - im * HW, h = r / W, w = r - h * W;
+      const int row = im * RI + (h + 1) * Wp + (w + 1);
+      float f[8];
+      unpack8(rx[i], f);
+      affine_act8(f, s_scale + c0 + ch * 8, s_shift + c0 + ch * 8, lo, hi);
+      *reinterpret_cast<uint4*>(Xs + row * WH_CB + wswz<WH_XROWB>(row, ch) * 8) = pack8(f);
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int e = tid + 256 * i, px = e >> 2, ch = e & 3;
+      if (px >= P * HW) continue;
+      const int im = px / HW, r = px - im * HW, h = r / W, w = r - h * W;
+      const int row = im * RI + h * Wp + w;
+      const uint4 v = px < nimg * HW ? rg[i] : make_uint4(0, 0, 0, 0);  // absent images: G = 0
+      *reinterpret_cast<uint4*>(Gs + row * 32 + wswz<WH_GROWB>(row, ch) * 8) = v;
+    }
+  };
+
+  v4f acc[9][2];
+#pragma unroll
+  for (int t = 0; t < 9; ++t) acc[t][0] = acc[t][1] = (v4f){0.f, 0.f, 0.f, 0.f};
+
+  if (img_beg < img_end) load(img_beg);
+  __syncthreads();  // zero fill + coefficient table
+  for (int ib = img_beg; ib < img_end; ib += P) {
+    store(ib);
+    __syncthreads();
+    if (ib + P < img_end) load(ib + P);  // next pass in flight under the MFMAs
+    const int nq = geo.qpad / 32;
+    for (int qc = 0; qc < nq; ++qc) {
+      const int q0 = qc * 32;
+      const v8bf g0 = tr_frag<WH_GROWB>(Gs, 0, lane, q0);
+      const v8bf g1 = tr_frag<WH_GROWB>(Gs, 16, lane, q0);
+#pragma unroll
+      for (int t = 0; t < 9; ++t) {
+        const int off = (t / 3) * Wp + (t % 3);
+        const v8bf xf = tr_frag<WH_XROWB>(Xs, wid * 16, lane, q0 + off);
+        acc[t][0] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(xf, g0, acc[t][0], 0, 0, 0);
+        acc[t][1] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(xf, g1, acc[t][1], 0, 0, 0);
+      }
+    }
+    __syncthreads();  // LDS reads done before the next pass overwrites the tiles
+  }
+
+  // epilogue: C[row = channel, col = co]; row = (lane>>4)*4 + r, col = lane&15 (+16 for half 1)
+  const long long n_dw = 9LL * a.Cin * 32;
+#pragma unroll
+  for (int t = 0; t < 9; ++t)
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int c = c0 + wid * 16 + (lane >> 4) * 4 + r;
+        const int co = j * 16 + (lane & 15);
+        const size_t k = (size_t)t * a.Cin + c;
+        const float v = acc[t][j][r] * a.scale;
+        if (a.part) a.part[(size_t)blockIdx.x * n_dw + k * 32 + co] = v;
+        else atomicAdd(&a.dw[k * 32 + co], v);
+      }
+}
+
+// the direct small-image path applies (and then `splits` counts image groups): 3x3 / s1 / pad 1,
+// Cout 32, bf16 G without a pending affine, Cin a multiple of 64, maps of at most 16x16
+static bool wgrad_halo_ok(const WgradArgs& a, bool g_f32) {
+  static const bool on = [] {
+    const char* e = std::getenv("IDC_WG_HALO");
+    return !(e && e[0] == '0');
+  }();
+  return on && !g_f32 && a.KH == 3 && a.KW == 3 && a.SH == 1 && a.SW == 1 && a.PT == 1 && a.PL == 1 &&
+         a.Ho == a.H && a.Wo == a.W && a.Cout == 32 && a.Cin % WH_CB == 0 && a.gpro.mode == 0 &&
+         (a.cin_real == 0 || a.cin_real == a.Cin) && a.H <= 16 && a.W <= 16 && a.H * a.W >= 4 &&
+         a.ldx % 8 == 0 && a.ldg % 8 == 0;
+}
+
+static int wgrad_halo_groups(const WgradArgs& a, int splits) {
+  int g = splits < 1 ? 1 : (splits > a.N ? a.N : splits);
+  const int ipw = (a.N + g - 1) / g;
+  return (a.N + ipw - 1) / ipw;
+}
+
 __global__ __launch_bounds__(256) void wgrad_reduce_kernel(const float* __restrict__ part, float* __restrict__ dw,
                                                            long long n, int splits) {
   for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n; i += (long long)gridDim.x * blockDim.x) {
@@ -320,6 +509,15 @@ static hipError_t launch_wg(const WgradArgs& a, bool is1x1, bool g_f32, int pro,
 static int wgrad_bp(int) { return 32; }
 
 hipError_t conv_wgrad(WgradArgs a, int splits, bool g_f32, hipStream_t st) {
+  if (wgrad_halo_ok(a, g_f32)) {
+    const int groups = wgrad_halo_groups(a, splits);
+    const int ipw = (a.N + groups - 1) / groups;
+    if (a.part && (long long)groups * 9 * a.Cin * 32 > a.part_floats) return hipErrorInvalidValue;
+    const WhGeom geo = wh_geom(a.H, a.W, ipw);
+    const size_t shm = geo.x_bytes + geo.g_bytes + 2 * (size_t)a.Cin * 4;
+    hipLaunchKernelGGL(wgrad3x3_img_kernel, dim3(groups, a.Cin / WH_CB), dim3(256), shm, st, a, ipw);
+    return hipGetLastError();
+  }
   const bool is1x1 = a.KH == 1 && a.KW == 1 && a.SH == 1 && a.SW == 1 && a.PT == 0 && a.PL == 0;
   const int pro = (a.pro.mode != 0 || a.pro.act != ACT_NONE) ? 1 : 0;
   const int M = a.N * a.Ho * a.Wo;
@@ -339,6 +537,7 @@ hipError_t conv_wgrad(WgradArgs a, int splits, bool g_f32, hipStream_t st) {
 }
 
 int wgrad_effective_splits(const WgradArgs& a, int splits) {
+  if (wgrad_halo_ok(a, false)) return wgrad_halo_groups(a, splits);
   const int M = a.N * a.Ho * a.Wo;
   if (splits < 1) splits = 1;
   const int bp = wgrad_bp(a.Cout);

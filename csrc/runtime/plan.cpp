@@ -177,11 +177,132 @@ class Plan {
     check(hipGraphLaunch(execs_.at(gid), reinterpret_cast<hipStream_t>(stream)), "hipGraphLaunch");
   }
 
+  // Two-lane graphs.  A single captured graph with fork/join edges is executed by ROCm without
+  // the side lane's concurrency (measured slower than direct issue on the DenseNet backward), and
+  // direct issue of ~250 launches leaves the small-kernel backward host-bound (issue gaps).  So a
+  // range with side-lane ops becomes TWO graphs: the main lane's ops, with an external event
+  // record node at every fork point, and the side lane's batches, each behind an external event
+  // wait node on its fork event.  launch_dual() launches the main graph first and then the side
+  // graph on the side stream, from this thread: HIP enqueues a graph's nodes during
+  // hipGraphLaunch, so every wait node refers to the record of the same launch.
+  int capture_dual(int begin, int end, uintptr_t stream) {
+    hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+    if (end < 0 || end > (int)ops_.size()) end = (int)ops_.size();
+    ensure_side();
+    Dual d;
+    std::vector<std::vector<int>> batches;
+    auto abort_capture = [](hipStream_t s) {
+      hipGraph_t g = nullptr;
+      hipStreamEndCapture(s, &g);
+      if (g) hipGraphDestroy(g);
+    };
+    check(hipStreamBeginCapture(st, hipStreamCaptureModeThreadLocal), "hipStreamBeginCapture(main)");
+    try {
+      std::vector<int> pending;
+      int main_since = 0;
+      auto flush = [&]() {
+        if (pending.empty()) return;
+        hipEvent_t e = nullptr;
+        check(hipEventCreateWithFlags(&e, hipEventDisableTiming), "hipEventCreate(dual)");
+        d.evs.push_back(e);
+        add_event_node(st, e, /*record=*/true);
+        batches.push_back(pending);
+        pending.clear();
+      };
+      for (int k = begin; k < end; ++k) {
+        const Op& op = ops_[k];
+        if (op.lane == 1) {
+          if (pending.empty()) main_since = 0;
+          pending.push_back(k);
+        } else {
+          exec(op, st);
+          if (!pending.empty() && ++main_since >= side_flush_) flush();
+        }
+      }
+      flush();
+    } catch (...) {
+      abort_capture(st);
+      for (auto e : d.evs) hipEventDestroy(e);
+      throw;
+    }
+    check(hipStreamEndCapture(st, &d.gm), "hipStreamEndCapture(main)");
+    check(hipGraphInstantiate(&d.main, d.gm, nullptr, nullptr, 0), "hipGraphInstantiate(main)");
+    if (!batches.empty()) {
+      check(hipStreamBeginCapture(side_, hipStreamCaptureModeThreadLocal), "hipStreamBeginCapture(side)");
+      try {
+        for (size_t b = 0; b < batches.size(); ++b) {
+          add_event_node(side_, d.evs[b], /*record=*/false);
+          for (int k : batches[b]) exec(ops_[k], side_);
+        }
+      } catch (...) {
+        abort_capture(side_);
+        throw;
+      }
+      check(hipStreamEndCapture(side_, &d.gs), "hipStreamEndCapture(side)");
+      check(hipGraphInstantiate(&d.side, d.gs, nullptr, nullptr, 0), "hipGraphInstantiate(side)");
+    }
+    duals_.push_back(std::move(d));
+    return (int)duals_.size() - 1;
+  }
+
+  // join=false: the side graph keeps running past the range (see run()); wait_side() orders a
+  // consumer after it and the next joined range joins it
+  void launch_dual(int id, uintptr_t stream, bool join) {
+    hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+    const Dual& d = duals_.at(id);
+    check(hipGraphLaunch(d.main, st), "hipGraphLaunch(main)");
+    if (d.side) check(hipGraphLaunch(d.side, side_), "hipGraphLaunch(side)");
+    if ((d.side || side_open_) && join) {
+      check(hipEventRecord(join_, side_), "hipEventRecord(join)");
+      check(hipStreamWaitEvent(st, join_, 0), "hipStreamWaitEvent(join)");
+      side_open_ = false;
+    } else if (d.side) {
+      side_open_ = true;
+    }
+  }
+
+  // Add an event record (leaf) or wait node to the graph `st` is capturing, after the nodes
+  // captured so far (hipEventRecordWithFlags(External) is rejected under capture on this ROCm).
+  // A wait node becomes the dependency of everything captured after it.
+  static void add_event_node(hipStream_t st, hipEvent_t e, bool record) {
+    hipStreamCaptureStatus status;
+    unsigned long long id = 0;
+    hipGraph_t g = nullptr;
+    const hipGraphNode_t* deps = nullptr;
+    size_t ndeps = 0;
+    check(hipStreamGetCaptureInfo_v2(st, &status, &id, &g, &deps, &ndeps), "hipStreamGetCaptureInfo_v2");
+    if (status != hipStreamCaptureStatusActive || g == nullptr) throw std::runtime_error("add_event_node: not capturing");
+    std::vector<hipGraphNode_t> dv(deps, deps + ndeps);
+    hipGraphNode_t n = nullptr;
+    if (record) {
+      check(hipGraphAddEventRecordNode(&n, g, dv.data(), dv.size(), e), "hipGraphAddEventRecordNode");
+    } else {
+      check(hipGraphAddEventWaitNode(&n, g, dv.data(), dv.size(), e), "hipGraphAddEventWaitNode");
+      check(hipStreamUpdateCaptureDependencies(st, &n, 1, hipStreamSetCaptureDependencies),
+            "hipStreamUpdateCaptureDependencies");
+    }
+  }
+
+  bool has_side(int begin, int end) const {
+    if (end < 0 || end > (int)ops_.size()) end = (int)ops_.size();
+    for (int k = begin; k < end; ++k)
+      if (ops_[k].lane == 1) return true;
+    return false;
+  }
+
   void clear_graphs() {
     for (auto e : execs_) hipGraphExecDestroy(e);
     for (auto g : graphs_) hipGraphDestroy(g);
     execs_.clear();
     graphs_.clear();
+    for (auto& d : duals_) {
+      if (d.main) hipGraphExecDestroy(d.main);
+      if (d.side) hipGraphExecDestroy(d.side);
+      if (d.gm) hipGraphDestroy(d.gm);
+      if (d.gs) hipGraphDestroy(d.gs);
+      for (auto e : d.evs) hipEventDestroy(e);
+    }
+    duals_.clear();
   }
 
   std::string describe(int idx) const {
@@ -348,6 +469,12 @@ class Plan {
   bool side_open_ = false;  // side-lane work issued by a join=false run, not yet joined
   std::vector<hipGraph_t> graphs_;
   std::vector<hipGraphExec_t> execs_;
+  struct Dual {
+    hipGraph_t gm = nullptr, gs = nullptr;
+    hipGraphExec_t main = nullptr, side = nullptr;
+    std::vector<hipEvent_t> evs;  // one external fork event per side batch
+  };
+  std::vector<Dual> duals_;
 };
 
 // direct (non-plan) entry points, used by the op-level python API and tests
@@ -475,6 +602,9 @@ PYBIND11_MODULE(_idc_native, m) {
       .def("wait_side", &Plan::wait_side)
       .def("capture", &Plan::capture)
       .def("launch", &Plan::launch)
+      .def("capture_dual", &Plan::capture_dual)
+      .def("launch_dual", &Plan::launch_dual)
+      .def("has_side", &Plan::has_side)
       .def("clear_graphs", &Plan::clear_graphs)
       .def("describe", &Plan::describe);
   m.def("conv", &py_conv);

@@ -143,10 +143,14 @@ class FusedProgram:
         if cur is not None:
             self.seg[cur] = (start, op_index)
         self.use_graphs = use_graphs and os.environ.get("IDC_NO_GRAPHS", "0") != "1"
-        # Which segments replay as HIP graphs.  The backward is issued directly by default: its
-        # side-lane weight-gradient kernels overlap the dgrad chain on a second stream, which
-        # ROCm's graph executor serialises (measured: 6.5 ms direct vs 7.8 ms graph per step).
-        self.graph_segments = set(os.environ.get("IDC_GRAPH_SEGMENTS", "fwd,opt").split(","))
+        # Which segments replay as HIP graphs.  The backward is issued directly by default: one
+        # captured fork/join graph loses the side lane's concurrency under ROCm's graph executor
+        # (4.93 vs 4.45 ms/step direct on DenseNet-121), and the opt-in IDC_DUAL_GRAPH=1 (main-
+        # and side-lane graphs joined by event nodes, plan.cpp capture_dual) is exact but slower
+        # still (6.1 ms/step: ROCm runs graphs holding event nodes node by node)
+        self.dual_graphs = os.environ.get("IDC_DUAL_GRAPH", "0") == "1"
+        default_graphs = "fwd,bwd,opt" if self.dual_graphs else "fwd,opt"
+        self.graph_segments = set(os.environ.get("IDC_GRAPH_SEGMENTS", default_graphs).split(","))
         self.graphs: Dict[Tuple[int, int], int] = {}
         self.grad_scale = grad_scale
         # stream priorities are opt-in (IDC_MAIN_PRIO=high, IDC_SIDE_PRIO=low in plan.cpp): measured
@@ -201,7 +205,14 @@ class FusedProgram:
             return
         if graph is None:
             graph = self.use_graphs and self._graph_for(lo)
-        if graph:
+        if graph and self.dual_graphs and self.plan.has_side(lo, hi):
+            # main-lane and side-lane graphs joined by external events (plan.cpp capture_dual)
+            g = self.graphs.get(("dual", lo, hi))
+            if g is None:
+                g = self.plan.capture_dual(lo, hi, self._sh())
+                self.graphs[("dual", lo, hi)] = g
+            self.plan.launch_dual(g, self._sh(), join)
+        elif graph:
             g = self.graphs.get((lo, hi))
             if g is None:
                 g = self.plan.capture(lo, hi, self._sh())
@@ -322,13 +333,12 @@ class FusedStep:
                 # the comm stream as soon as its gradients are final — the comm stream waits for
                 # the main lane AND the side-lane weight gradients issued so far, while the main
                 # lane itself runs on without joining the side lane (plan.cpp run(join=False))
-                graphed = p.use_graphs and "bwd" in p.graph_segments
                 cs = p.comm_stream
                 pos = lo
                 for mark, low_param in p.bwd_marks:
                     if mark <= pos:
                         continue
-                    p.run_range(pos, mark, join=graphed)
+                    p.run_range(pos, mark, join=False)
                     pos = mark
                     p.side_ready_on(cs)
                     with torch.cuda.stream(cs), trace.range("allreduce:from_param%d" % low_param):

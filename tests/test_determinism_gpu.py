@@ -54,3 +54,32 @@ def test_deterministic_mode_is_bitwise_reproducible(monkeypatch, arch, B):
     torch.cuda.synchronize()
     for a, b in zip(m1.net.trainable_weights, m2.net.trainable_weights):
         assert torch.equal(a, b)
+
+
+@pytest.mark.parametrize("arch,B", [("densenet121", 64), ("vgg16", 32)])
+def test_dual_graph_backward_matches_direct_issue(monkeypatch, arch, B):
+    """The backward replayed as two graphs (main lane + side lane joined by external events,
+    plan.cpp capture_dual) must order every weight-gradient kernel after the dgrad that stages
+    its operand: under IDC_DETERMINISTIC=1 it gives the same bits as direct issue, step after step
+    (a side-lane kernel that ran early would read the previous step's gradients)."""
+    monkeypatch.setenv("IDC_DETERMINISTIC", "1")
+    g = torch.Generator().manual_seed(5)
+    xs = [torch.randint(0, 256, (B, 50, 50, 3), generator=g, dtype=torch.uint8) for _ in range(3)]
+    ys = [torch.randint(0, 2, (B,), generator=g) for _ in range(3)]
+    monkeypatch.setenv("IDC_DUAL_GRAPH", "1")
+    m1, _ = _model(arch)
+    p1 = m1.impl._prog(B, True, torch.uint8)
+    assert "bwd" in p1.graph_segments and p1.dual_graphs
+    monkeypatch.setenv("IDC_DUAL_GRAPH", "0")
+    monkeypatch.setenv("IDC_GRAPH_SEGMENTS", "fwd,opt")
+    m2, _ = _model(arch)
+    p2 = m2.impl._prog(B, True, torch.uint8)
+    assert "bwd" not in p2.graph_segments
+    for x, y in zip(xs, ys):
+        m1.impl.train_step(x, y)
+        m2.impl.train_step(x, y)
+    torch.cuda.synchronize()
+    assert any(k[0] == "dual" for k in p1.graphs if isinstance(k, tuple) and len(k) == 3)
+    assert torch.equal(m1.arena.grad, m2.arena.grad)
+    for a, b in zip(m1.net.trainable_weights, m2.net.trainable_weights):
+        assert torch.equal(a, b)

@@ -594,3 +594,38 @@ def test_bn_statistics_shifted_large_mean(fn):
     assert float(((m1.double() - mref) / mref).abs().max()) < 1e-5
     assert err1 < 2e-3, err1
     assert err0 > 10 * err1, (err0, err1)                      # what the shift buys
+
+
+@pytest.mark.parametrize("N,H,Cin,xpad,gpad,splits", [
+    (8, 13, 128, 0, 0, -1),     # stage 1 (one image per pass), default groups
+    (37, 6, 128, 64, 32, 5),    # stage 2: stacked images, channel slices, partial last pass
+    (50, 3, 128, 0, 0, 7),      # stage 3: many images per pass
+    (16, 3, 192, 32, 0, 1),     # one group, 3 channel blocks
+])
+def test_wgrad3x3_small_image_path(fn, N, H, Cin, xpad, gpad, splits):
+    """conv_wgrad.hip wgrad3x3_img_kernel (3x3 s1 'same', Cout 32, small maps): whole images per
+    workgroup, shifted-window operands, BN+ReLU prologue; channel slices of wider buffers."""
+    from idc_models_amd.ops import _native as nat
+    Cout = 32
+    xfull = bf(torch.randn(N, H, H, Cin + xpad, device=DEV) * 2 + 0.5)
+    t = xfull[..., :Cin]
+    st = torch.cat([t.sum((0, 1, 2)), (t * t).sum((0, 1, 2))])
+    g, b = torch.rand(Cin, device=DEV) + 0.5, torch.randn(Cin, device=DEV) * 0.1
+    gfull = bf(torch.randn(N, H, H, Cout + gpad, device=DEV))
+    dy = gfull[..., :Cout]
+    cnt = N * H * H
+    bn = fn.BN(stats=st, gamma=g, beta=b, count=cnt, eps=1e-3, act=1)
+    out = torch.zeros((3, 3, Cin, Cout), dtype=torch.float32, device=DEV)
+    xb, gb = xfull.to(torch.bfloat16).contiguous(), gfull.to(torch.bfloat16).contiguous()
+    a = nat.WgradArgs()
+    a.x, a.N, a.H, a.W, a.Cin, a.ldx = xb.data_ptr(), N, H, H, Cin, Cin + xpad
+    a.g, a.ldg = gb.data_ptr(), Cout + gpad
+    a.Ho, a.Wo, a.Cout = H, H, Cout
+    a.KH, a.KW, a.SH, a.SW, a.PT, a.PL = 3, 3, 1, 1, 1, 1
+    a.pro = bn.args()
+    a.dw, a.scale = out.data_ptr(), 1.0
+    nat.require().wgrad(nat.raw(a), splits, 0, nat.stream_handle())
+    act = bf(bn_ref(t, st, g, b, cnt, 1e-3, 1))
+    ref = torch.nn.grad.conv2d_weight(act.permute(0, 3, 1, 2), (Cout, Cin, 3, 3), dy.permute(0, 3, 1, 2),
+                                      padding=1).permute(2, 3, 1, 0)
+    assert relerr(out, ref) < 1e-2
