@@ -26,6 +26,7 @@ from __future__ import annotations
 
 import argparse
 import json
+import math
 import os
 import sys
 import time
@@ -128,11 +129,15 @@ def main():
     ap.add_argument("--lr", type=float, default=1e-4)
     ap.add_argument("--no-graphs", action="store_true")
     ap.add_argument("--backend", default="fused")
+    ap.add_argument("--device", default="cuda", choices=["cuda", "cpu"],
+                    help="cpu: config #1 (MobileNetV2 on CPU, world_size 1, eager backend)")
     # ~320 fit steps: Keras BatchNorm momentum 0.99 leaves the inference-mode moving statistics
     # mostly at their init after a few dozen steps (0.99^36 = 0.70), so a short fit evaluates stale
     # statistics; 0.99^320 = 0.04
     ap.add_argument("--fit-steps", type=int, default=20, help="global batches per fit epoch (0: skip fit/AUC)")
-    ap.add_argument("--fit-epochs", type=int, default=48)
+    ap.add_argument("--fit-epochs", type=int, default=None,
+                    help="default: enough epochs for the BatchNorm moving statistics to forget their "
+                         "Keras init (momentum^updates < 1e-2), at least 48")
     ap.add_argument("--mode", default="train", choices=["train", "fedavg", "secure"],
                     help="train: the headline DP step; fedavg / secure: north-star configs #4 / #5")
     ap.add_argument("--clients", type=int, default=8)
@@ -160,6 +165,9 @@ def main():
         strategy = MirroredStrategy(backend="gloo", device="cuda:0")
     elif world > 1:
         strategy = MirroredStrategy()
+    elif args.device == "cpu":
+        strategy = OneDeviceStrategy("cpu")
+        args.backend = "eager"
     else:
         strategy = OneDeviceStrategy("cuda:0")
     rank = strategy.rank
@@ -183,17 +191,22 @@ def main():
     y = torch.randint(0, 2, (args.batch,), generator=g).to(dev)
 
     step = model.impl.train_step
+
+    def sync():
+        if dev.type == "cuda":
+            torch.cuda.synchronize(dev)
+
     for _ in range(args.warmup):
         loss, _ = step(x, y)
-    torch.cuda.synchronize(dev)
+    sync()
     barrier()
-    torch.cuda.synchronize(dev)
+    sync()
     t0 = time.perf_counter()
     for _ in range(args.steps):
         loss, _ = step(x, y)
-    torch.cuda.synchronize(dev)
+    sync()
     barrier()
-    torch.cuda.synchronize(dev)
+    sync()
     dt = time.perf_counter() - t0
     dt = all_reduce_max(dt, dev) if world > 1 else dt
     ms = dt / args.steps * 1e3
@@ -203,6 +216,13 @@ def main():
 
     # ---- after the timed region: fit() throughput and held-out validation AUC ----------------
     fit_ips = val_auc = val_acc = None
+    if args.fit_epochs is None:
+        # evaluate() uses the moving statistics (Keras inference BN): with MobileNetV2's momentum
+        # 0.999 they keep 38% of their init after 960 updates and the held-out output collapses to
+        # a constant, in the eager reference backend as much as in the fused one
+        moms = [l.momentum for l in net.base.layers if getattr(l, "keras_class", "") == "BatchNormalization"]
+        need = math.ceil(math.log(1e-2) / math.log(max(moms))) if moms else 0
+        args.fit_epochs = max(48, math.ceil(need / max(args.fit_steps, 1)))
     if args.fit_steps > 0 and args.fit_epochs > 0:
         gb = args.batch * world
         train = synthetic_dataset(gb * args.fit_steps, (H, W, C), 2, seed=11)
@@ -224,14 +244,14 @@ def main():
             if args.model == "densenet121" else f"images/sec (whole node) {args.model} 50x50x3",
             "value": round(value, 1),
             "unit": "images/sec",
-            "n_gpus": world,
+            "n_gpus": world if dev.type == "cuda" else 0,
             "steps": args.steps,
             "warmup": args.warmup,
             "ms_per_step": round(ms, 3),
             "higher_is_better": True,
             "scaling": "weak",
-            "vs_baseline": round(value / (base * world), 3) if base else None,
-            "dtype": "bf16",
+            "vs_baseline": round(value / (base * world), 3) if base and dev.type == "cuda" else None,
+            "dtype": "bf16" if dev.type == "cuda" else "fp32",
             "data": "synthetic uint8 50x50x3 patches, random-init weights",
             "val_auc": round(val_auc, 4) if val_auc is not None else None,
             "val_accuracy": round(val_acc, 4) if val_acc is not None else None,

@@ -508,6 +508,21 @@ static hipError_t launch_wg(const WgradArgs& a, bool is1x1, bool g_f32, int pro,
 // workgroups per CU, and these kernels are latency-bound, not MFMA-bound)
 static int wgrad_bp(int) { return 32; }
 
+// 128x128 tiles (64x64 per wave: 16 MFMAs per 32-pixel step against 8 transposed fragment
+// reads, vs 8 against 6 for 32x64) for wide layers over few pixels (K >= 512, Cout >= 128,
+// M <= 16384: the DenseNet stage-3/4 1x1 wgrads, half the workgroups and dW atomics).  Measured
+// slower on VGG's large-M layers (3.73 vs 3.32 ms/step), so those keep 64x128.  IDC_WG_BIG=0: off
+static bool wgrad_big_on() {
+  static const bool on = [] {
+    const char* e = std::getenv("IDC_WG_BIG");
+    return !(e && e[0] == '0');
+  }();
+  return on;
+}
+static bool wgrad_big_tile(const WgradArgs& a) {
+  return wgrad_big_on() && a.Cout >= 128 && a.KH * a.KW * a.Cin >= 512 && a.N * a.Ho * a.Wo <= 16384;
+}
+
 hipError_t conv_wgrad(WgradArgs a, int splits, bool g_f32, hipStream_t st) {
   if (wgrad_halo_ok(a, g_f32)) {
     const int groups = wgrad_halo_groups(a, splits);
@@ -533,6 +548,7 @@ hipError_t conv_wgrad(WgradArgs a, int splits, bool g_f32, hipStream_t st) {
   }
   if (a.Cout <= 32) return launch_wg<128, 32, 32, 4, 1>(a, is1x1, g_f32, pro, splits, st);
   if (a.Cout <= 64) return launch_wg<128, 64, 32, 2, 2>(a, is1x1, g_f32, pro, splits, st);
+  if (wgrad_big_tile(a)) return launch_wg<128, 128, 32, 2, 2>(a, is1x1, g_f32, pro, splits, st);
   return launch_wg<64, 128, 32, 2, 2>(a, is1x1, g_f32, pro, splits, st);
 }
 
@@ -550,6 +566,7 @@ int wgrad_pick_splits(int M, int K, int Cout) {
   int tiles;
   if (Cout <= 32) tiles = ((K + 127) / 128) * ((Cout + 31) / 32);
   else if (Cout <= 64) tiles = ((K + 127) / 128) * ((Cout + 63) / 64);
+  else if (wgrad_big_on() && Cout >= 128 && K >= 512 && M <= 16384) tiles = ((K + 127) / 128) * ((Cout + 127) / 128);
   else tiles = ((K + 63) / 64) * ((Cout + 127) / 128);
   int target = 512;  // ~2 blocks per CU
   int s = (target + tiles - 1) / tiles;

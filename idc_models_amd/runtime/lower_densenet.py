@@ -19,6 +19,8 @@ MI355X-specific structure:
 """
 from __future__ import annotations
 
+import os
+
 import torch
 
 from ..ops import _native as nat
@@ -220,6 +222,10 @@ def lower_densenet(b: Builder, net, U: int, input_dtype):
     b.pool_bwd(dbuf.slice(0, 64), zs, k=3, s=2, pt=1, pl=1, is_max=True, argmax=argmax, x=ys,
                bn=bn_stem, dyaff=b.bwd_aff(pend, st0["buf"].slice(0, 64), unit_alpha=True, fold=True))
     if fz.trainable(conv1):
+        # the stem wgrad consumes the LAST main-lane op's output, so it can never overlap the
+        # dgrad chain; on the main lane it starts at once and overlaps the side lane's backlog of
+        # stage-1 weight gradients instead of queueing behind it (IDC_STEM_SIDE=1: side lane)
+        stem_lane = 1 if os.environ.get("IDC_STEM_SIDE", "0") == "1" else 0
         b.wgrad(x8, conv1, zs, b.arena.grad_of(conv1.kernel), stride=(2, 2), pads=(3, 3),
-                cin_real=Cimg, lane=1, gpro=b.bwd_aff(bn_stem, ys))
+                cin_real=Cimg, lane=stem_lane, gpro=b.bwd_aff(bn_stem, ys))
     b.mark_grads_ready([conv1.kernel, bn_stem.gamma, bn_stem.beta] + pend_params())

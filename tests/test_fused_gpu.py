@@ -237,3 +237,39 @@ def test_fused_matches_eager_at_bench_batch(arch):
     autotuner's split-K choices and the full-size workspaces — not only the small test batches."""
     m, ref, x, y = _setup(arch, 256)
     _check(m, ref, x, y)
+
+
+@pytest.mark.parametrize("arch", ["mobilenetv2", "densenet121"])
+def test_moving_statistics_match_eager_every_bn(arch):
+    """Every BatchNorm's moving-statistics update after one fused training step implies the same
+    batch mean / variance as the eager reference's update (moving = m*momentum + batch*(1-m), so
+    the batch statistic is recovered from the delta; comparing the moving values themselves would
+    hide a wrong update under the 0.99 momentum)."""
+    m, ref, x, y = _setup(arch, 64)
+    ref16 = copy.deepcopy(ref)
+    bns = [l for l in m.net.base.layers if l.keras_class == "BatchNormalization"]
+    rbns = {l.name: l for l in ref.base.layers if l.keras_class == "BatchNormalization"}
+    r16 = {l.name: l for l in ref16.base.layers if l.keras_class == "BatchNormalization"}
+    m0 = {l.name: (l.moving_mean.clone(), l.moving_variance.clone()) for l in bns}
+    m.impl.train_step(x, y)
+    torch.cuda.synchronize()
+    for net, bf16 in ((ref, False), (ref16, True)):
+        net.train()
+        with torch.no_grad(), torch.autocast("cuda", dtype=torch.bfloat16, enabled=bf16):
+            net(x.to(DEV).float() / 255.0)
+
+    def implied(layer, name):  # the batch mean / variance the update used
+        mom = layer.momentum
+        mm0, mv0 = m0[name]
+        return (layer.moving_mean - mom * mm0) / (1 - mom), (layer.moving_variance - mom * mv0) / (1 - mom)
+
+    bad = []
+    for l in bns:
+        (fm, fv), (rm, rv), (hm, hv) = implied(l, l.name), implied(rbns[l.name], l.name), implied(r16[l.name], l.name)
+        sd = rv.clamp_min(0).sqrt() + 1e-3
+        em, em16 = ((fm - rm).abs() / sd).max().item(), ((hm - rm).abs() / sd).max().item()
+        ev, ev16 = [((v - rv).abs() / (rv.abs() + 1e-3)).max().item() for v in (fv, hv)]
+        # within the bf16 precision floor: 2x eager-autocast's own deviation from fp32 + 0.05
+        if em > 2 * em16 + 0.05 or ev > 2 * ev16 + 0.05:
+            bad.append((l.name, round(em, 3), round(em16, 3), round(ev, 3), round(ev16, 3)))
+    assert not bad, bad[:12]

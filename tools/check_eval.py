@@ -19,6 +19,7 @@ def main():
     ap.add_argument("--batch", type=int, default=64)
     ap.add_argument("--epochs", type=int, default=3)
     ap.add_argument("--lr", type=float, default=1e-4)
+    ap.add_argument("--train-backend", default="fused", choices=["fused", "eager"])
     a = ap.parse_args()
     from idc_models_amd.data import synthetic_dataset
     from idc_models_amd.engine import Model, RMSprop
@@ -26,7 +27,7 @@ def main():
     dev = torch.device("cuda", 0)
     net = build_model(a.model, num_outputs=1, seed=0)
     m = Model(net, device=dev)
-    m.compile(RMSprop(a.lr), "binary_crossentropy", ["accuracy", "auc"], backend="fused")
+    m.compile(RMSprop(a.lr), "binary_crossentropy", ["accuracy", "auc"], backend=a.train_backend)
     tr = synthetic_dataset(a.batch * 16, net.input_shape, 2, seed=11)
     te = synthetic_dataset(512, net.input_shape, 2, seed=12)
     h = m.fit(tr.batch(a.batch, True, 1000, True, seed=1), epochs=a.epochs, verbose=1,
@@ -43,6 +44,8 @@ def main():
     print("eval logits eager", le.reshape(-1)[:8].tolist())
     # run-to-run variability of the fused training step at this batch: the same program, the same
     # weights and inputs, gradients of two back-to-back fwd+bwd runs
+    if a.train_backend != "fused":
+        return
     p = m.impl._prog(xb.shape[0], True, torch.uint8)
     gs = []
     for _ in range(2):
