@@ -510,12 +510,13 @@ static int wgrad_bp(int) { return 32; }
 
 // 128x128 tiles (64x64 per wave: 16 MFMAs per 32-pixel step against 8 transposed fragment
 // reads, vs 8 against 6 for 32x64) for wide layers over few pixels (K >= 512, Cout >= 128,
-// M <= 16384: the DenseNet stage-3/4 1x1 wgrads, half the workgroups and dW atomics).  Measured
-// slower on VGG's large-M layers (3.73 vs 3.32 ms/step), so those keep 64x128.  IDC_WG_BIG=0: off
+// M <= 16384).  Opt-in (IDC_WG_BIG=1): measured slower on VGG16 (3.12 vs 3.02 ms/step, blocks
+// 4-5) and neutral on DenseNet-121 (4.34-4.44 both ways) — these loops are load-latency bound,
+// and the bigger tile halves the workgroups that hide it.
 static bool wgrad_big_on() {
   static const bool on = [] {
     const char* e = std::getenv("IDC_WG_BIG");
-    return !(e && e[0] == '0');
+    return e && e[0] == '1';
   }();
   return on;
 }
