@@ -69,6 +69,13 @@ struct ConvArgs {
 
 // tile TILE_HALO selects the one-image-per-workgroup direct 3x3 kernel (conv3x3_halo.hip)
 constexpr int TILE_HALO = 100;
+// tiles TILE_BIG128 / TILE_BIG256 select the 256 x {128, 256} global_load_lds kernel for plain
+// wide layers (conv_big.hip)
+constexpr int TILE_BIG128 = 101;
+constexpr int TILE_BIG256 = 102;
+constexpr int TILE_BIG64 = 103;
+bool conv_big_ok(const ConvArgs& a, bool a_f32);
+hipError_t conv_big(const ConvArgs& a, int bn, bool a_f32, hipStream_t st);
 hipError_t conv_igemm(const ConvArgs& a, int tile, bool a_f32, hipStream_t st);
 bool conv3x3_halo_ok(const ConvArgs& a);
 hipError_t conv3x3_halo(const ConvArgs& a, bool a_f32, hipStream_t st);

@@ -547,6 +547,13 @@ bool py_halo_ok(py::bytes payload) {
   std::memcpy(&a, s.data(), sizeof(a));
   return conv3x3_halo_ok(a);
 }
+bool py_big_ok(py::bytes payload, int a_f32) {
+  std::string s = payload;
+  if (s.size() != sizeof(ConvArgs)) throw std::runtime_error("ConvArgs size mismatch");
+  ConvArgs a;
+  std::memcpy(&a, s.data(), sizeof(a));
+  return conv_big_ok(a, a_f32 != 0);
+}
 int py_pick_splits(int M, int K, int Cout) { return wgrad_pick_splits(M, K, Cout); }
 
 int py_effective_splits(py::bytes payload, int splits) {
@@ -614,6 +621,10 @@ PYBIND11_MODULE(_idc_native, m) {
   m.def("halo_ok", &py_halo_ok);
   m.def("dw_wgrad_ws_floats", &dwconv_wgrad_ws_floats);
   m.attr("TILE_HALO") = TILE_HALO;
+  m.def("big_ok", &py_big_ok);
+  m.attr("TILE_BIG128") = TILE_BIG128;
+  m.attr("TILE_BIG256") = TILE_BIG256;
+  m.attr("TILE_BIG64") = TILE_BIG64;
   m.def("pick_splits", &py_pick_splits);
   m.def("effective_splits", &py_effective_splits);
   m.def("rows_grid", &rows_grid);

@@ -66,7 +66,7 @@ def _time_op(plan, i, stream, reps=4) -> float:
     return e0.elapsed_time(e1) / reps
 
 
-def _conv_candidates(ext, M: int, cout: int, payload: bytes = None, halo: bool = False):
+def _conv_candidates(ext, M: int, cout: int, payload: bytes = None, halo: bool = False, a_f32: int = 0):
     ntile = ext.num_tiles()
     cap = 32 if cout <= 32 else (64 if cout <= 64 else 128)
     out = []
@@ -79,6 +79,12 @@ def _conv_candidates(ext, M: int, cout: int, payload: bytes = None, halo: bool =
         out.append(t)
     if payload is not None and (halo or os.environ.get("IDC_HALO", "0") == "1") and ext.halo_ok(payload):
         out.append(ext.TILE_HALO)
+    # 256 x {128, 256} global_load_lds tiles for plain wide layers (conv_big.hip), when they
+    # still make >= 128 workgroups
+    if payload is not None and os.environ.get("IDC_CONV_BIG", "1") != "0" and ext.big_ok(payload, a_f32):
+        for t, bn in ((ext.TILE_BIG128, 128), (ext.TILE_BIG256, 256)):
+            if cout >= bn and -(-M // 256) * -(-cout // bn) >= 128:
+                out.append(t)
     return out
 
 
@@ -121,12 +127,12 @@ def autotune_plan(plan, stream, verbose: bool = False, reset_tickets=None, slab_
             if best is None:
                 times = {}
                 plan.set_int(i, 2, 1)
-                for t in _conv_candidates(ext, M, a.Cout, plan.payload(i), i in halo_ops) or [ext.pick_tile(M, a.Cout)]:
+                for t in _conv_candidates(ext, M, a.Cout, plan.payload(i), i in halo_ops, f32) or [ext.pick_tile(M, a.Cout)]:
                     plan.set_int(i, 0, t)
                     times[(t, 1)] = _time_op(plan, i, stream)
                 if a.slab and a.tickets and reset_tickets is not None and \
                         os.environ.get("IDC_SPLITK", "1") != "0":
-                    top = sorted((v, t) for (t, s), v in times.items() if t != ext.TILE_HALO)[:3]
+                    top = sorted((v, t) for (t, s), v in times.items() if t < ext.num_tiles())[:3]
                     for _, t in top:
                         for s in _splits_for(ext, a, t, M, slab_floats):
                             plan.set_int(i, 0, t)

@@ -629,3 +629,31 @@ def test_wgrad3x3_small_image_path(fn, N, H, Cin, xpad, gpad, splits):
     ref = torch.nn.grad.conv2d_weight(act.permute(0, 3, 1, 2), (Cout, Cin, 3, 3), dy.permute(0, 3, 1, 2),
                                       padding=1).permute(2, 3, 1, 0)
     assert relerr(out, ref) < 1e-2
+
+
+@pytest.mark.parametrize("big", ["TILE_BIG64", "TILE_BIG128", "TILE_BIG256"])
+@pytest.mark.parametrize("N,H,Cin,Cout", [(8, 25, 64, 256), (32, 12, 256, 256), (128, 6, 512, 512), (9, 25, 128, 384),
+                                          (3, 50, 64, 64)])
+def test_conv_big_tile_fwd_and_dgrad(fn, big, N, H, Cin, Cout):
+    """conv_big.hip (256 x {128, 256} tiles, global_load_lds staging, source-side swizzle): the
+    VGG forward (bias + ReLU epilogue) and data gradient (ReLU mask from the saved input, bias
+    gradient of the producer) against fp32 PyTorch; M tails (N*H*W not a multiple of 256), image
+    padding rows and Cout tails (384 with 256-wide tiles)."""
+    from idc_models_amd.ops import _native as nat
+    t = getattr(nat.load(), big)
+    x = bf(torch.relu(torch.randn(N, H, H, Cin, device=DEV)))
+    w = bf(torch.randn(3, 3, Cin, Cout, device=DEV) * (2.0 / (9 * Cin)) ** 0.5)
+    bias = torch.randn(Cout, device=DEV) * 0.1
+    y = fn.conv2d(x.to(torch.bfloat16), w, pads=(1, 1), bias=bias, act=1, tile=t)
+    ref = ref_conv(x, w, 1, (1, 1, 1, 1), bias, act=1)
+    assert relerr(y.float(), ref) < 1e-2
+    # data gradient through this conv into its ReLU input x (the previous conv's output)
+    dy = bf(torch.randn(N, H, H, Cout, device=DEV))
+    gsum = torch.zeros(Cin, device=DEV)
+    dz = fn.conv2d_dgrad(dy.to(torch.bfloat16), w, (H, H), pads=(1, 1), mx=x.to(torch.bfloat16),
+                         mbn=fn.BN(act=1), gsum=gsum, tile=t)
+    dA = torch.nn.grad.conv2d_input((N, Cin, H, H), w.permute(3, 2, 0, 1), dy.permute(0, 3, 1, 2),
+                                    padding=1).permute(0, 2, 3, 1)
+    dZ = dA * (x > 0).float()
+    assert relerr(dz.float(), dZ) < 1e-2
+    assert relerr(gsum, dZ.sum((0, 1, 2))) < 1e-2
