@@ -37,7 +37,7 @@ __device__ __attribute__((aligned(16))) uint4 g_zero_src[8];  // zero-initialise
 
 typedef __attribute__((address_space(3))) void lds_void_t;
 
-template <int BN, int WM_, int WN_>
+template <int BN, int WM_, int WN_, int NBUF_>
 struct BigCfg {
   static constexpr int WM = WM_, WN = WN_, NW = WM * WN;
   static constexpr int BM = 256, BK = 64, NT = NW * 64;
@@ -45,9 +45,9 @@ struct BigCfg {
   static constexpr int TM = WTM / 16, TN = WTN / 16;
   static constexpr int A_ELEMS = BM * BK, B_ELEMS = BN * BK;
   static constexpr int BUF_ELEMS = A_ELEMS + B_ELEMS;
-  // LDS buffers: 2 (3 — two tiles in flight across each barrier — measured 1-3% slower on the
-  // VGG layers: 144 KB of LDS per workgroup)
-  static constexpr int NBUF = 2;
+  // LDS buffers: 2, or 3 (two tiles in flight across each barrier: the few-workgroup, deep-K
+  // layers whose K step is load-latency bound; 1-3% slower on the large-M ones)
+  static constexpr int NBUF = NBUF_;
   static constexpr int LDS_MAIN = NBUF * BUF_ELEMS * 2;
   static constexpr int NGA = BM * (BK / 8) / NT;  // glds per thread per tile (A)
   static constexpr int NGB = BN * (BK / 8) / NT;  // (B)
@@ -60,10 +60,10 @@ __device__ __forceinline__ int bswz(int row, int chunk) { return chunk ^ (row & 
 
 }  // namespace
 
-template <int BN, int WM, int WN, int EPI>
+template <int BN, int WM, int WN, int NBUF_, int EPI>
 __global__ __launch_bounds__(WM * WN * 64) void conv_big_kernel(ConvArgs a) {
   prefetch_kernargs<sizeof(ConvArgs)>();
-  using C = BigCfg<BN, WM, WN>;
+  using C = BigCfg<BN, WM, WN, NBUF_>;
   constexpr int NW = C::NW;
   constexpr int BM = C::BM, BK = C::BK, TM = C::TM, TN = C::TN, WTN = C::WTN;
   constexpr int NGA = C::NGA, NGB = C::NGB;
@@ -76,10 +76,16 @@ __global__ __launch_bounds__(WM * WN * 64) void conv_big_kernel(ConvArgs a) {
   const int K = a.KH * a.KW * a.Cin;
   const int ntiles = (a.Cout + BN - 1) / BN;
   const int mtiles = (M + BM - 1) / BM;
-  const int bid = xcd_remap(blockIdx.x, mtiles * ntiles);
-  const int mt = bid / ntiles, nt = bid % ntiles;
+  const int nsplit = a.ksplit > 1 ? a.ksplit : 1;
+  // split-K (the under-filled small-M layers): the slices of a tile are consecutive ids
+  const int bid = xcd_remap(blockIdx.x, mtiles * ntiles * nsplit);
+  const int tile = bid / nsplit, slice = bid - tile * nsplit;
+  const int mt = tile / ntiles, nt = tile % ntiles;
   const int m0 = mt * BM, n0 = nt * BN;
-  const int nk = K / BK;
+  const int nk_all = K / BK;
+  const int per_slice = (nk_all + nsplit - 1) / nsplit;
+  const int kb = slice * per_slice;
+  const int nk = max(0, min(nk_all, kb + per_slice) - kb);
 
   // ---- per-thread source rows (fixed for the whole K loop) ----------------------------------
   // wave instruction j covers rows (j*NW + wid)*8 .. +8; lane -> row + lane/8, LDS chunk lane%8
@@ -103,7 +109,7 @@ __global__ __launch_bounds__(WM * WN * 64) void conv_big_kernel(ConvArgs a) {
   const uint4* zsrc = g_zero_src;
 
   auto issue = [&](int kt, int buf) {
-    const int k0 = kt * BK;
+    const int k0 = (kb + kt) * BK;
     const int rs = k0 / a.Cin, c0 = k0 - rs * a.Cin;
     const int kr = rs / a.KW, ks = rs - kr * a.KW;
     bf16_t* As = lds + buf * C::BUF_ELEMS;
@@ -132,7 +138,7 @@ __global__ __launch_bounds__(WM * WN * 64) void conv_big_kernel(ConvArgs a) {
 
   const int frow = lane & 15, fk = lane >> 4;
   constexpr int NBUF = C::NBUF, NG = NGA + NGB;
-  issue(0, 0);
+  if (nk > 0) issue(0, 0);
   if (NBUF == 3 && nk > 1) issue(1, 1);
   for (int kt = 0; kt < nk; ++kt) {
     // tile kt must have landed; the loads of the NBUF-2 tiles after it stay in flight
@@ -169,6 +175,55 @@ __global__ __launch_bounds__(WM * WN * 64) void conv_big_kernel(ConvArgs a) {
     }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();  // buffer kt % NBUF free for tile kt + NBUF
+  }
+
+  // ---- split-K: publish this slice's partial tile; the tile's last arriver sums them ---------
+  // (the protocol of conv_igemm_impl.h: plain stores -> vmcnt(0) -> barrier -> lane 0 agent
+  //  release + relaxed ticket (modulo nsplit) -> the last arriver acquires and reads)
+  if (nsplit > 1) {
+    constexpr int NF = TM * TN;
+    float4* slab = reinterpret_cast<float4*>(a.slab) + (size_t)tile * nsplit * NF * C::NT;
+    {
+      float4* mine = slab + (size_t)slice * NF * C::NT;
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+          mine[(i * TN + j) * C::NT + tid] = make_float4(acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    int* s_flag = reinterpret_cast<int*>(smem);
+    if (tid == 0) {
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      const unsigned prev =
+          __hip_atomic_fetch_add(&a.tickets[tile], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      const int last = (prev % (unsigned)nsplit) == (unsigned)(nsplit - 1);
+      if (last) {
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      }
+      s_flag[0] = last;
+    }
+    __syncthreads();
+    const int last = s_flag[0];
+    __syncthreads();  // the epilogue reuses this LDS
+    if (!last) return;
+    for (int sl = 0; sl < nsplit; ++sl) {
+      if (sl == slice) continue;
+      const float4* o = slab + (size_t)sl * NF * C::NT;
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j) {
+          const float4 q = o[(i * TN + j) * C::NT + tid];
+          acc[i][j][0] += q.x;
+          acc[i][j][1] += q.y;
+          acc[i][j][2] += q.z;
+          acc[i][j][3] += q.w;
+        }
+    }
   }
 
   // ---- epilogue: each wave stages 16 rows of its sub-tile at a time -------------------------
@@ -246,34 +301,37 @@ __global__ __launch_bounds__(WM * WN * 64) void conv_big_kernel(ConvArgs a) {
 }
 
 bool conv_big_ok(const ConvArgs& a, bool a_f32) {
-  if (a_f32 || a.ksplit > 1) return false;
+  if (a_f32) return false;
   if (a.pro.mode != 0 || a.pro.act != ACT_NONE || a.bpro.mode != 0) return false;
   if ((a.Cin % 64) || (a.ldx % 8) || (a.ldy % 8) || (a.Cout % 8)) return false;
-  if ((long long)a.N * a.Ho * a.Wo < 4096) return false;
   if (a.epi_mode == 0) return a.out_mode == OUT_BF16 && a.stats_out == nullptr;
   if (a.epi_mode == 1)
     return a.mbn.mode == 0 && a.gsumx == nullptr && a.mx != nullptr && (a.ldmx % 8) == 0;
   return false;
 }
 
-template <int BN, int WM, int WN>
+template <int BN, int WM, int WN, int NBUF>
 static hipError_t big_launch(const ConvArgs& a, hipStream_t st) {
-  using C = BigCfg<BN, WM, WN>;
+  using C = BigCfg<BN, WM, WN, NBUF>;
   const int M = a.N * a.Ho * a.Wo;
-  const int grid = ((M + C::BM - 1) / C::BM) * ((a.Cout + BN - 1) / BN);
+  const int tiles = ((M + C::BM - 1) / C::BM) * ((a.Cout + BN - 1) / BN);
+  const int ks = a.ksplit > 1 ? a.ksplit : 1;
+  if (ks > 1 && ((long long)tiles * ks * C::BM * BN > a.slab_floats || tiles > a.tickets_n)) return hipErrorInvalidValue;
+  const int grid = tiles * ks;
   if (grid == 0) return hipSuccess;
   if (a.epi_mode == 0)
-    hipLaunchKernelGGL((conv_big_kernel<BN, WM, WN, 0>), dim3(grid), dim3(C::NT), C::LDS_BYTES, st, a);
+    hipLaunchKernelGGL((conv_big_kernel<BN, WM, WN, NBUF, 0>), dim3(grid), dim3(C::NT), C::LDS_BYTES, st, a);
   else
-    hipLaunchKernelGGL((conv_big_kernel<BN, WM, WN, 1>), dim3(grid), dim3(C::NT), C::LDS_BYTES, st, a);
+    hipLaunchKernelGGL((conv_big_kernel<BN, WM, WN, NBUF, 1>), dim3(grid), dim3(C::NT), C::LDS_BYTES, st, a);
   return hipGetLastError();
 }
 
 hipError_t conv_big(const ConvArgs& a, int bn, bool a_f32, hipStream_t st) {
   if (!conv_big_ok(a, a_f32)) return hipErrorInvalidValue;
-  if (bn == 256) return big_launch<256, 2, 4>(a, st);
-  if (bn == 128) return big_launch<128, 2, 4>(a, st);
-  return big_launch<64, 4, 1>(a, st);  // 4 waves of 64 x 64
+  if (bn == 256) return big_launch<256, 2, 4, 2>(a, st);
+  if (bn == 128) return big_launch<128, 2, 4, 2>(a, st);
+  if (bn == -128) return big_launch<128, 2, 4, 3>(a, st);  // three buffers
+  return big_launch<64, 4, 1, 2>(a, st);  // 4 waves of 64 x 64
 }
 
 }  // namespace idc

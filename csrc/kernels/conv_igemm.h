@@ -74,6 +74,7 @@ constexpr int TILE_HALO = 100;
 constexpr int TILE_BIG128 = 101;
 constexpr int TILE_BIG256 = 102;
 constexpr int TILE_BIG64 = 103;
+constexpr int TILE_BIG128D = 104;  // 256 x 128 with three LDS buffers
 bool conv_big_ok(const ConvArgs& a, bool a_f32);
 hipError_t conv_big(const ConvArgs& a, int bn, bool a_f32, hipStream_t st);
 hipError_t conv_igemm(const ConvArgs& a, int tile, bool a_f32, hipStream_t st);

@@ -28,7 +28,7 @@ int conv_tile_bn(int t) { return kTiles[t].bn; }
 
 hipError_t conv_igemm(const ConvArgs& a, int tile, bool a_f32, hipStream_t st) {
   if (tile < 0 || (tile >= conv_num_tiles() && tile != TILE_HALO && tile != TILE_BIG128 && tile != TILE_BIG256 &&
-                   tile != TILE_BIG64))
+                   tile != TILE_BIG64 && tile != TILE_BIG128D))
     return hipErrorInvalidValue;
   const bool is1x1 = a.KH == 1 && a.KW == 1 && a.SH == 1 && a.SW == 1 && a.PT == 0 && a.PL == 0;
   const int pro = a.bpro.mode != 0 ? 2 : (a.pro.mode != 0 || a.pro.act != ACT_NONE) ? 1 : 0;
@@ -37,8 +37,9 @@ hipError_t conv_igemm(const ConvArgs& a, int tile, bool a_f32, hipStream_t st) {
   if (pro == 2 && (a.bpro.x == nullptr || (a.bpro.ldx % 8) || a.bpro.bn.gamma == nullptr)) return hipErrorInvalidValue;
   if (epi == 2 && a.mx == nullptr) return hipErrorInvalidValue;
   if (a.ksplit > 1 && (a.slab == nullptr || a.tickets == nullptr)) return hipErrorInvalidValue;
-  if (tile == TILE_BIG128 || tile == TILE_BIG256 || tile == TILE_BIG64)
-    return conv_big(a, tile == TILE_BIG256 ? 256 : tile == TILE_BIG128 ? 128 : 64, a_f32, st);
+  if (tile == TILE_BIG128 || tile == TILE_BIG256 || tile == TILE_BIG64 || tile == TILE_BIG128D)
+    return conv_big(a, tile == TILE_BIG256 ? 256 : tile == TILE_BIG128 ? 128 : tile == TILE_BIG128D ? -128 : 64,
+                    a_f32, st);
   if (tile == TILE_HALO) {
     if (a.ksplit > 1 || pro == 2 || epi == 2) return hipErrorInvalidValue;
     return conv3x3_halo(a, a_f32, st);

@@ -625,6 +625,7 @@ PYBIND11_MODULE(_idc_native, m) {
   m.attr("TILE_BIG128") = TILE_BIG128;
   m.attr("TILE_BIG256") = TILE_BIG256;
   m.attr("TILE_BIG64") = TILE_BIG64;
+  m.attr("TILE_BIG128D") = TILE_BIG128D;
   m.def("pick_splits", &py_pick_splits);
   m.def("effective_splits", &py_effective_splits);
   m.def("rows_grid", &rows_grid);

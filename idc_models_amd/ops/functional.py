@@ -133,7 +133,10 @@ def _splitk_args(a, M: int, cout: int, ksplit: int, tile: int):
     ext = nat.require()
     if tile < 0:
         tile = ext.pick_tile(M, cout)
-    bm, bn = ext.tile_bm(tile), ext.tile_bn(tile)
+    if tile in (ext.TILE_BIG128, ext.TILE_BIG128D, ext.TILE_BIG256):
+        bm, bn = 256, (256 if tile == ext.TILE_BIG256 else 128)
+    else:
+        bm, bn = ext.tile_bm(tile), ext.tile_bn(tile)
     tiles = -(-M // bm) * -(-cout // bn)
     slab = torch.empty(tiles * ksplit * bm * bn, dtype=torch.float32, device="cuda")
     tickets = torch.zeros(tiles, dtype=torch.int32, device="cuda")

@@ -82,22 +82,39 @@ def _conv_candidates(ext, M: int, cout: int, payload: bytes = None, halo: bool =
     # 256 x {128, 256} global_load_lds tiles for plain wide layers (conv_big.hip), when they
     # still make >= 128 workgroups
     if payload is not None and os.environ.get("IDC_CONV_BIG", "1") != "0" and ext.big_ok(payload, a_f32):
-        for t, bn in ((ext.TILE_BIG128, 128), (ext.TILE_BIG256, 256)):
-            if cout >= bn and -(-M // 256) * -(-cout // bn) >= 128:
+        for t, bn in ((ext.TILE_BIG128, 128), (ext.TILE_BIG128D, 128), (ext.TILE_BIG256, 256)):
+            if cout >= bn and -(-M // 256) * -(-cout // bn) >= 8:
                 out.append(t)
     return out
+
+
+def _tile_shape(ext, t: int):
+    """(BM, BN, BK) of conv tile ``t``; None for the halo kernel (no split-K)."""
+    if t in (ext.TILE_BIG128, ext.TILE_BIG128D):
+        return 256, 128, 64
+    if t == ext.TILE_BIG256:
+        return 256, 256, 64
+    if t >= ext.num_tiles():
+        return None
+    bk = 256 if t >= 17 else (128 if t >= 12 else (64 if t >= 5 else 32))
+    return ext.tile_bm(t), ext.tile_bn(t), bk
 
 
 def _splits_for(ext, a, t: int, M: int, slab_floats: int):
     """Feasible split-K factors for conv tile ``t``: the partial slabs must fit the workspace, each
     slice must keep >= 2 K-steps, and only grids that leave the GPU under-filled are split."""
-    bm, bn = ext.tile_bm(t), ext.tile_bn(t)
+    shape = _tile_shape(ext, t)
+    if shape is None:
+        return []
+    bm, bn, bk = shape
     tiles = -(-M // bm) * -(-a.Cout // bn)
     if tiles >= 256:
         return []
     K = a.KH * a.KW * a.Cin
-    bk = 256 if t >= 17 else (128 if t >= 12 else (64 if t >= 5 else 32))
     nk = -(-K // bk)
+    if bm == 256:  # conv_big.hip: one workgroup per CU, so the split grid must fit 256 CUs
+        return [s for s in (2, 3, 4, 6, 8) if tiles * s <= 256 and tiles * s * bm * bn <= slab_floats
+                and nk >= 4 * s]
     return [s for s in (2, 4, 8) if tiles * s * bm * bn <= slab_floats and nk >= 2 * s]
 
 
@@ -132,7 +149,10 @@ def autotune_plan(plan, stream, verbose: bool = False, reset_tickets=None, slab_
                     times[(t, 1)] = _time_op(plan, i, stream)
                 if a.slab and a.tickets and reset_tickets is not None and \
                         os.environ.get("IDC_SPLITK", "1") != "0":
-                    top = sorted((v, t) for (t, s), v in times.items() if t < ext.num_tiles())[:3]
+                    top = sorted((v, t) for (t, s), v in times.items() if _tile_shape(ext, t))[:3]
+                    # the 256-row tiles are under-filled exactly where split-K pays: always try them
+                    top += [(v, t) for (t, s), v in times.items()
+                            if _tile_shape(ext, t) and _tile_shape(ext, t)[0] == 256 and (v, t) not in top]
                     for _, t in top:
                         for s in _splits_for(ext, a, t, M, slab_floats):
                             plan.set_int(i, 0, t)

@@ -498,7 +498,7 @@ class Builder:
 
     # split-K workspace (conv_igemm.h): one fp32 partial-tile slab shared by every main-lane conv
     # (they run one after another on the plan stream) and one ticket array per op
-    SLAB_FLOATS = 4 << 20
+    SLAB_FLOATS = 16 << 20  # 64 MB: room for 256x256 big-tile partials (conv_big.hip)
 
     def _splitk(self, a, M: int, cout: int):
         if self.splitk_slab is None:

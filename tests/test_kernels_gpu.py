@@ -631,7 +631,7 @@ def test_wgrad3x3_small_image_path(fn, N, H, Cin, xpad, gpad, splits):
     assert relerr(out, ref) < 1e-2
 
 
-@pytest.mark.parametrize("big", ["TILE_BIG64", "TILE_BIG128", "TILE_BIG256"])
+@pytest.mark.parametrize("big", ["TILE_BIG64", "TILE_BIG128", "TILE_BIG128D", "TILE_BIG256"])
 @pytest.mark.parametrize("N,H,Cin,Cout", [(8, 25, 64, 256), (32, 12, 256, 256), (128, 6, 512, 512), (9, 25, 128, 384),
                                           (3, 50, 64, 64)])
 def test_conv_big_tile_fwd_and_dgrad(fn, big, N, H, Cin, Cout):
@@ -652,6 +652,32 @@ def test_conv_big_tile_fwd_and_dgrad(fn, big, N, H, Cin, Cout):
     gsum = torch.zeros(Cin, device=DEV)
     dz = fn.conv2d_dgrad(dy.to(torch.bfloat16), w, (H, H), pads=(1, 1), mx=x.to(torch.bfloat16),
                          mbn=fn.BN(act=1), gsum=gsum, tile=t)
+    dA = torch.nn.grad.conv2d_input((N, Cin, H, H), w.permute(3, 2, 0, 1), dy.permute(0, 3, 1, 2),
+                                    padding=1).permute(0, 2, 3, 1)
+    dZ = dA * (x > 0).float()
+    assert relerr(dz.float(), dZ) < 1e-2
+    assert relerr(gsum, dZ.sum((0, 1, 2))) < 1e-2
+
+
+@pytest.mark.parametrize("big,ks", [("TILE_BIG128", 3), ("TILE_BIG256", 2), ("TILE_BIG128", 8), ("TILE_BIG128D", 4),
+                                    ("TILE_BIG128D", 1)])
+def test_conv_big_tile_split_k(fn, big, ks):
+    """conv_big.hip in-launch split-K (VGG block 5: M = 2304, K = 4608): partial tiles in the
+    slab, modulo tickets, the last arriver runs the epilogue; twice in a row (tickets carry over)."""
+    from idc_models_amd.ops import _native as nat
+    t = getattr(nat.load(), big)
+    N, H, Cin, Cout = 256, 3, 512, 512
+    x = bf(torch.relu(torch.randn(N, H, H, Cin, device=DEV)))
+    w = bf(torch.randn(3, 3, Cin, Cout, device=DEV) * (2.0 / (9 * Cin)) ** 0.5)
+    bias = torch.randn(Cout, device=DEV) * 0.1
+    ref = ref_conv(x, w, 1, (1, 1, 1, 1), bias, act=1)
+    for _ in range(2):
+        y = fn.conv2d(x.to(torch.bfloat16), w, pads=(1, 1), bias=bias, act=1, tile=t, ksplit=ks)
+        assert relerr(y.float(), ref) < 1e-2
+    dy = bf(torch.randn(N, H, H, Cout, device=DEV))
+    gsum = torch.zeros(Cin, device=DEV)
+    dz = fn.conv2d_dgrad(dy.to(torch.bfloat16), w, (H, H), pads=(1, 1), mx=x.to(torch.bfloat16),
+                         mbn=fn.BN(act=1), gsum=gsum, tile=t, ksplit=ks)
     dA = torch.nn.grad.conv2d_input((N, Cin, H, H), w.permute(3, 2, 0, 1), dy.permute(0, 3, 1, 2),
                                     padding=1).permute(0, 2, 3, 1)
     dZ = dA * (x > 0).float()
