@@ -154,6 +154,35 @@ __global__ __launch_bounds__(WM * WN * 64) void conv_big_kernel(ConvArgs a) {
     __builtin_amdgcn_s_barrier();  // every wave's tile-kt DMA is visible
     const bf16_t* As = lds + (kt % NBUF) * C::BUF_ELEMS;
     const bf16_t* Bs = As + C::A_ELEMS;
+    // 256x128 tiles read every fragment of the K step up front (both 32-deep halves, distinct
+    // registers), then issue the MFMAs: hipcc otherwise recycles two fragment registers, which
+    // serialises each ds_read behind the MFMAs of the previous pair (read -> lgkmcnt(0) -> 4
+    // MFMAs -> read ...).  256x256 tiles have no registers for that (it spills) and keep the
+    // per-half order.
+    if constexpr (TN <= 2) {
+    v8bf af[BK / 32][TM], bfr[BK / 32][TN];
+#pragma unroll
+    for (int q = 0; q < BK / 32; ++q) {
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        const int row = wc * WTN + j * 16 + frow;
+        bfr[q][j] = *reinterpret_cast<const v8bf*>(Bs + row * BK + bswz(row, q * 4 + fk) * 8);
+      }
+#pragma unroll
+      for (int i = 0; i < TM; ++i) {
+        const int row = wr * C::WTM + i * 16 + frow;
+        af[q][i] = *reinterpret_cast<const v8bf*>(As + row * BK + bswz(row, q * 4 + fk) * 8);
+      }
+    }
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int q = 0; q < BK / 32; ++q)
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[q][i], bfr[q][j], acc[i][j], 0, 0, 0);
+    } else {
 #pragma unroll
     for (int q = 0; q < BK / 32; ++q) {
       v8bf af[TM], bfr[TN];
@@ -172,6 +201,7 @@ __global__ __launch_bounds__(WM * WN * 64) void conv_big_kernel(ConvArgs a) {
 #pragma unroll
         for (int j = 0; j < TN; ++j)
           acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+    }
     }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();  // buffer kt % NBUF free for tile kt + NBUF
