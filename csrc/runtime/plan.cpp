@@ -150,7 +150,9 @@ class Plan {
   }
 
   int lane(int idx) const { return ops_.at(idx).lane; }
-  void set_side_flush(int n) { side_flush_ = n < 1 ? 1 : n; }
+  // n main ops between a side batch's first member and its fork; 0: fork at once (the side op
+  // starts when the main ops issued before it finish, not one main op later)
+  void set_side_flush(int n) { side_flush_ = n < 0 ? 0 : n; }
 
   int capture(int begin, int end, uintptr_t stream) {
     hipStream_t st = reinterpret_cast<hipStream_t>(stream);
@@ -214,6 +216,7 @@ class Plan {
         if (op.lane == 1) {
           if (pending.empty()) main_since = 0;
           pending.push_back(k);
+          if (side_flush_ == 0) flush();
         } else {
           exec(op, st);
           if (!pending.empty() && ++main_since >= side_flush_) flush();
@@ -355,6 +358,7 @@ class Plan {
       if (op.lane == 1) {
         if (pending.empty()) main_since = 0;
         pending.push_back(k);
+        if (side_flush_ == 0) flush();
       } else {
         exec(op, st);
         if (!pending.empty() && ++main_since >= side_flush_) flush();

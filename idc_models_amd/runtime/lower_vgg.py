@@ -74,7 +74,9 @@ def lower_vgg(b: Builder, net, U: int, input_dtype):
             g, masked = dx, True
         else:
             if fz.trainable(l):
-                b.wgrad(x, l, g, ar.grad_of(l.kernel), pads=(1, 1), lane=1)  # inputs never reused
+                # inputs never reused; the first conv's wgrad consumes the LAST dgrad's output and
+                # runs on the main lane, next to the side lane's backlog (lower_densenet stem)
+                b.wgrad(x, l, g, ar.grad_of(l.kernel), pads=(1, 1), lane=0 if i == 0 else 1)
                 b.mark_grads_ready([l.kernel, l.bias])
             if not fz.before(l):
                 return
