@@ -186,6 +186,8 @@ def autotune_plan(plan, stream, verbose: bool = False, reset_tickets=None, slab_
                 for s in cands:
                     plan.set_int(i, 0, s)
                     times[s] = _time_op(plan, i, stream)
+                # the isolated optimum: biasing wgrad splits either way (fewest / most slices
+                # within 10-50% of it) measured 1-23% slower steps on DenseNet-121 and VGG16
                 best = min(times, key=times.get)
                 _CACHE[key] = best
                 if verbose:
