@@ -17,6 +17,8 @@
 //   cast_weights   fp32 Keras HWIO master -> bf16 kernel layouts (fwd + flipped dgrad), one launch
 //   input_stage    uint8/fp32 NHWC images -> bf16 NHWC padded to 8 channels
 #include "common.h"
+#include <cstdlib>
+
 #include "nn_kernels.h"
 
 namespace idc {
@@ -595,8 +597,69 @@ __global__ __launch_bounds__(256) void pool_bwd_kernel(PoolBwdArgs a) {
   }
 }
 
+// Scatter-form backward of a NON-overlapping max pool (k == s, no padding) with no epilogue: the
+// VGG16 pools, whose dy arrives already masked (dZ) from the next dgrad's epilogue.  One thread
+// per (pooled pixel, 8-channel chunk) reads dy and the argmax bytes ONCE and writes the k x k
+// window's chunks (the selected value or 0); the gather form re-reads both for every input pixel
+// (k^2 times).  Input rows / columns past the last window (floor pooling, 25 -> 12) get zeros
+// from the threads of the last window row / column.
+__global__ __launch_bounds__(256) void pool_bwd_scatter_kernel(PoolBwdArgs a) {
+  const int C8 = a.C / 8, k = a.k;
+  const long long total = (long long)a.N * a.Ho * a.Wo * C8;
+  const uint4 zero = make_uint4(0, 0, 0, 0);
+  for (long long idx = (long long)blockIdx.x * blockDim.x + threadIdx.x; idx < total;
+       idx += (long long)gridDim.x * blockDim.x) {
+    const int c = (int)(idx % C8) * 8;
+    long long p = idx / C8;
+    const int wo = (int)(p % a.Wo);
+    p /= a.Wo;
+    const int ho = (int)(p % a.Ho);
+    const int n = (int)(p / a.Ho);
+    const size_t o = ((size_t)n * a.Ho + ho) * a.Wo + wo;
+    float d[8];
+    load8(a.dy, a.dy_f32, o * a.lddy + c, d);
+    const uint2 am = *reinterpret_cast<const uint2*>(a.argmax + o * a.C + c);
+    const int h0 = ho * k, w0 = wo * k;
+    const int h1 = ho == a.Ho - 1 ? a.H : h0 + k;  // last window row also clears the uncovered rows
+    const int w1 = wo == a.Wo - 1 ? a.W : w0 + k;
+    for (int h = h0; h < h1; ++h)
+      for (int w = w0; w < w1; ++w) {
+        uint4 v = zero;
+        if (h < h0 + k && w < w0 + k) {
+          const uint8_t pos = (uint8_t)((h - h0) * k + (w - w0));
+          float g[8];
+#pragma unroll
+          for (int j = 0; j < 8; ++j) {
+            const uint32_t word = j < 4 ? am.x : am.y;
+            g[j] = (uint8_t)(word >> (8 * (j & 3))) == pos ? d[j] : 0.f;
+          }
+          v = pack8(g);
+        }
+        *reinterpret_cast<uint4*>(a.dx + ((size_t)(n * a.H + h) * a.W + w) * a.lddx + c) = v;
+      }
+  }
+}
+
+static bool pool_bwd_scatter_ok(const PoolBwdArgs& a) {
+  static const bool on = [] {
+    const char* e = std::getenv("IDC_POOL_SCATTER");
+    return !(e && e[0] == '0');
+  }();
+  return on && !a.is_avg && a.k == a.s && a.pt == 0 && a.pl == 0 && a.bn.mode == 0 && a.bn.act == ACT_NONE &&
+         a.dyaff.mode == 0 && !a.dx_f32 && (a.C % 8) == 0 && (a.lddx % 8) == 0 && (a.lddy % 8) == 0 &&
+         a.Ho * a.k <= a.H && a.Wo * a.k <= a.W && a.k * a.k <= 255;
+}
+
 hipError_t pool_bwd(const PoolBwdArgs& a, hipStream_t st) {
   if (a.dx_f32 && !(a.bn.mode != 0 || a.bn.act != ACT_NONE)) return hipErrorInvalidValue;
+  if (pool_bwd_scatter_ok(a)) {
+    const long long total = (long long)a.N * a.Ho * a.Wo * (a.C / 8);
+    long long blocks = (total + 255) / 256;
+    if (blocks > 8192) blocks = 8192;
+    if (blocks < 1) return hipSuccess;
+    hipLaunchKernelGGL(pool_bwd_scatter_kernel, dim3((int)blocks), dim3(256), 0, st, a);
+    return hipGetLastError();
+  }
   if (a.dyaff.mode != 0 && (a.dyaff.x == nullptr || (a.dyaff.ldx % 8))) return hipErrorInvalidValue;
   const size_t shm = (9 * a.C + 2 * 256 * 8) * 4;
   const int M = a.N * a.H * a.W;

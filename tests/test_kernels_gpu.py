@@ -683,3 +683,23 @@ def test_conv_big_tile_split_k(fn, big, ks):
     dZ = dA * (x > 0).float()
     assert relerr(dz.float(), dZ) < 1e-2
     assert relerr(gsum, dZ.sum((0, 1, 2))) < 1e-2
+
+
+@pytest.mark.parametrize("N,H,C", [(4, 50, 64), (3, 25, 128), (2, 13, 256), (5, 6, 512)])
+def test_maxpool_bwd_scatter_form(fn, N, H, C):
+    """nn_kernels.hip pool_bwd_scatter_kernel (2x2 s2 max pool, no epilogue: the VGG16 pools): each
+    pooled element lands on the window position its argmax names, everything else is zero,
+    including the row / column floor pooling drops (odd H); the forward matches torch."""
+    x = bf(torch.randn(N, H, H, C, device=DEV))
+    p, am = fn.pool2d(x.to(torch.bfloat16), 2, 2, is_max=True)
+    ref = F.max_pool2d(x.permute(0, 3, 1, 2), 2, 2).permute(0, 2, 3, 1)
+    assert torch.equal(p.float(), ref)
+    Ho = H // 2
+    dy = bf(torch.randn(N, Ho, Ho, C, device=DEV))
+    dx = fn.pool2d_bwd(dy.to(torch.bfloat16), (N, H, H, C), 2, 2, is_max=True, argmax=am)
+    a = am.view(N, Ho, Ho, C).long()
+    exp = torch.zeros(N, H, H, C, device=DEV)
+    for dh in range(2):
+        for dw in range(2):
+            exp[:, dh:2 * Ho:2, dw:2 * Ho:2, :] = torch.where(a == dh * 2 + dw, dy, torch.zeros_like(dy))
+    assert torch.equal(dx.float(), exp)
