@@ -597,67 +597,140 @@ __global__ __launch_bounds__(256) void pool_bwd_kernel(PoolBwdArgs a) {
   }
 }
 
-// Scatter-form backward of a NON-overlapping max pool (k == s, no padding) with no epilogue: the
-// VGG16 pools, whose dy arrives already masked (dZ) from the next dgrad's epilogue.  One thread
-// per (pooled pixel, 8-channel chunk) reads dy and the argmax bytes ONCE and writes the k x k
-// window's chunks (the selected value or 0); the gather form re-reads both for every input pixel
-// (k^2 times).  Input rows / columns past the last window (floor pooling, 25 -> 12) get zeros
-// from the threads of the last window row / column.
+// Scatter-form backward of a NON-overlapping pool (k == s, no padding): one thread per (pooled
+// pixel, 8-channel chunk) reads dy (and the argmax bytes) ONCE and writes the k x k window's
+// chunks; the gather form re-reads them for every input pixel (k^2 times).  Input rows / columns
+// past the last window (floor pooling, 25 -> 12) are written as zero gradients by the threads of
+// the last window row / column.  EPI: the backward of the pending BN+act that fed the pool, per
+// input pixel (dZ = g * act'(bn(x)), sums of dZ and dZ*xhat, fp32 gamma*rstd*dZ or bf16 dZ),
+// exactly as the gather form.  Used for the VGG16 max pools (no epilogue) and the DenseNet
+// transition average pools (BN epilogue, fp32 concat-gradient output).
+template <bool AVG, bool EPI>
 __global__ __launch_bounds__(256) void pool_bwd_scatter_kernel(PoolBwdArgs a) {
-  const int C8 = a.C / 8, k = a.k;
-  const long long total = (long long)a.N * a.Ho * a.Wo * C8;
-  const uint4 zero = make_uint4(0, 0, 0, 0);
-  for (long long idx = (long long)blockIdx.x * blockDim.x + threadIdx.x; idx < total;
-       idx += (long long)gridDim.x * blockDim.x) {
-    const int c = (int)(idx % C8) * 8;
-    long long p = idx / C8;
-    const int wo = (int)(p % a.Wo);
-    p /= a.Wo;
-    const int ho = (int)(p % a.Ho);
-    const int n = (int)(p / a.Ho);
-    const size_t o = ((size_t)n * a.Ho + ho) * a.Wo + wo;
-    float d[8];
-    load8(a.dy, a.dy_f32, o * a.lddy + c, d);
-    const uint2 am = *reinterpret_cast<const uint2*>(a.argmax + o * a.C + c);
-    const int h0 = ho * k, w0 = wo * k;
-    const int h1 = ho == a.Ho - 1 ? a.H : h0 + k;  // last window row also clears the uncovered rows
-    const int w1 = wo == a.Wo - 1 ? a.W : w0 + k;
-    for (int h = h0; h < h1; ++h)
-      for (int w = w0; w < w1; ++w) {
-        uint4 v = zero;
-        if (h < h0 + k && w < w0 + k) {
-          const uint8_t pos = (uint8_t)((h - h0) * k + (w - w0));
+  prefetch_kernargs<sizeof(PoolBwdArgs)>();
+  extern __shared__ float sh[];
+  float* s_sc = sh;
+  float* s_sh = sh + a.C;
+  float* s_mu = sh + 2 * a.C;
+  float* s_rs = sh + 3 * a.C;
+  float* s_a = sh + 4 * a.C;
+  float* s_b = sh + 5 * a.C;
+  float* s_tmp = sh + 9 * a.C;
+  if constexpr (EPI) {
+    bn_full_table<256>(a.bn, a.C, s_sc, s_sh, s_mu, s_rs);
+    __syncthreads();
+  }
+  const bool sums = EPI && (a.gsum || a.gsumx);
+  ChunkMap cm(a.C);
+  const int k = a.k;
+  const float inv = 1.f / (float)(k * k);
+  const float lo = act_lo(a.bn.act), hi = act_hi(a.bn.act);
+  const long long Np = (long long)a.N * a.Ho * a.Wo;
+  float ps[8] = {0, 0, 0, 0, 0, 0, 0, 0}, px[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  if (cm.active()) {
+    const int c = cm.tx * 8;
+    for (long long pp = (long long)blockIdx.x * cm.R + cm.ty; pp < Np; pp += (long long)gridDim.x * cm.R) {
+      const int wo = (int)(pp % a.Wo);
+      const long long t = pp / a.Wo;
+      const int ho = (int)(t % a.Ho);
+      const int n = (int)(t / a.Ho);
+      float d[8];
+      load8(a.dy, a.dy_f32, (size_t)pp * a.lddy + c, d);
+      uint2 am = make_uint2(0, 0);
+      if constexpr (!AVG) am = *reinterpret_cast<const uint2*>(a.argmax + (size_t)pp * a.C + c);
+      const int h0 = ho * k, w0 = wo * k;
+      const int h1 = ho == a.Ho - 1 ? a.H : h0 + k;  // the last window row also clears dropped rows
+      const int w1 = wo == a.Wo - 1 ? a.W : w0 + k;
+      for (int h = h0; h < h1; ++h)
+        for (int w = w0; w < w1; ++w) {
+          const size_t pix = (size_t)(n * a.H + h) * a.W + w;
+          const bool in = h < h0 + k && w < w0 + k;
           float g[8];
+          const uint8_t pos = (uint8_t)((h - h0) * k + (w - w0));
 #pragma unroll
           for (int j = 0; j < 8; ++j) {
-            const uint32_t word = j < 4 ? am.x : am.y;
-            g[j] = (uint8_t)(word >> (8 * (j & 3))) == pos ? d[j] : 0.f;
+            if constexpr (AVG) {
+              g[j] = in ? d[j] * inv : 0.f;
+            } else {
+              const uint32_t word = j < 4 ? am.x : am.y;
+              g[j] = (in && (uint8_t)(word >> (8 * (j & 3))) == pos) ? d[j] : 0.f;
+            }
           }
-          v = pack8(g);
+          if constexpr (EPI) {
+            float x[8];
+            unpack8(*reinterpret_cast<const uint4*>(a.x + pix * a.ldx + c), x);
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+              const float z = x[j] * s_sc[c + j] + s_sh[c + j];
+              g[j] = (z > lo && z < hi) ? g[j] : 0.f;
+            }
+            if (a.dx_f32) {
+              float o[8];
+#pragma unroll
+              for (int j = 0; j < 8; ++j) {
+                o[j] = s_sc[c + j] * g[j];
+                ps[j] += g[j];
+                px[j] += g[j] * (x[j] - s_mu[c + j]) * s_rs[c + j];
+              }
+              float* q = reinterpret_cast<float*>(a.dx) + pix * a.lddx + c;
+              *reinterpret_cast<float4*>(q) = make_float4(o[0], o[1], o[2], o[3]);
+              *reinterpret_cast<float4*>(q + 4) = make_float4(o[4], o[5], o[6], o[7]);
+            } else {
+              const uint4 pk = pack8(g);
+              *reinterpret_cast<uint4*>(a.dx + pix * a.lddx + c) = pk;
+              unpack8(pk, g);  // reduce exactly what was stored
+#pragma unroll
+              for (int j = 0; j < 8; ++j) {
+                ps[j] += g[j];
+                px[j] += g[j] * (x[j] - s_mu[c + j]) * s_rs[c + j];
+              }
+            }
+          } else {
+            *reinterpret_cast<uint4*>(a.dx + pix * a.lddx + c) = pack8(g);
+          }
         }
-        *reinterpret_cast<uint4*>(a.dx + ((size_t)(n * a.H + h) * a.W + w) * a.lddx + c) = v;
-      }
+    }
+  }
+  if (sums) {
+    chunk_reduce(cm, a.C, ps, px, s_tmp, s_a, s_b);
+    flush_sums(s_a, s_b, a.C, slot_ptr(a.gsum, a.gsum_slots, a.gsum_ld),
+               slot_ptr(a.gsumx, a.gsum_slots, a.gsum_ld));
   }
 }
 
+// the scatter form applies: k == s without padding, no dy affine, whole windows inside the image,
+// a channel count whose 8-chunks tile the 256-thread block (ChunkMap), and — with BN sums — the
+// normal statistics slots (the deterministic mode sizes one private slot per gather workgroup)
 static bool pool_bwd_scatter_ok(const PoolBwdArgs& a) {
   static const bool on = [] {
     const char* e = std::getenv("IDC_POOL_SCATTER");
     return !(e && e[0] == '0');
   }();
-  return on && !a.is_avg && a.k == a.s && a.pt == 0 && a.pl == 0 && a.bn.mode == 0 && a.bn.act == ACT_NONE &&
-         a.dyaff.mode == 0 && !a.dx_f32 && (a.C % 8) == 0 && (a.lddx % 8) == 0 && (a.lddy % 8) == 0 &&
-         a.Ho * a.k <= a.H && a.Wo * a.k <= a.W && a.k * a.k <= 255;
+  const bool epi = a.bn.mode != 0 || a.bn.act != ACT_NONE;
+  const int C8 = a.C / 8;
+  return on && a.k == a.s && a.pt == 0 && a.pl == 0 && a.dyaff.mode == 0 && (a.C % 8) == 0 && C8 <= 256 &&
+         (256 % C8) == 0 && (a.lddx % 8) == 0 && (a.lddy % 8) == 0 && (!epi || (a.ldx % 8) == 0) &&
+         a.Ho * a.k <= a.H && a.Wo * a.k <= a.W && a.k * a.k <= 255 && (a.dx_f32 ? epi : true) &&
+         (!epi || !(a.gsum || a.gsumx) || a.gsum_slots <= MAX_STAT_SLOTS);
 }
 
 hipError_t pool_bwd(const PoolBwdArgs& a, hipStream_t st) {
   if (a.dx_f32 && !(a.bn.mode != 0 || a.bn.act != ACT_NONE)) return hipErrorInvalidValue;
   if (pool_bwd_scatter_ok(a)) {
-    const long long total = (long long)a.N * a.Ho * a.Wo * (a.C / 8);
-    long long blocks = (total + 255) / 256;
-    if (blocks > 8192) blocks = 8192;
+    const long long Np = (long long)a.N * a.Ho * a.Wo;
+    const int R = 256 / (a.C / 8);
+    long long blocks = (Np + R - 1) / R;
+    if (blocks > 4096) blocks = 4096;
     if (blocks < 1) return hipSuccess;
-    hipLaunchKernelGGL(pool_bwd_scatter_kernel, dim3((int)blocks), dim3(256), 0, st, a);
+    const bool epi = a.bn.mode != 0 || a.bn.act != ACT_NONE;
+    const size_t shm_s = epi ? (9 * (size_t)a.C + 2 * 256 * 8) * 4 : 0;
+    if (a.is_avg) {
+      if (epi) hipLaunchKernelGGL((pool_bwd_scatter_kernel<true, true>), dim3((int)blocks), dim3(256), shm_s, st, a);
+      else hipLaunchKernelGGL((pool_bwd_scatter_kernel<true, false>), dim3((int)blocks), dim3(256), shm_s, st, a);
+    } else {
+      if (epi) hipLaunchKernelGGL((pool_bwd_scatter_kernel<false, true>), dim3((int)blocks), dim3(256), shm_s, st, a);
+      else hipLaunchKernelGGL((pool_bwd_scatter_kernel<false, false>), dim3((int)blocks), dim3(256), shm_s, st, a);
+    }
     return hipGetLastError();
   }
   if (a.dyaff.mode != 0 && (a.dyaff.x == nullptr || (a.dyaff.ldx % 8))) return hipErrorInvalidValue;

@@ -703,3 +703,37 @@ def test_maxpool_bwd_scatter_form(fn, N, H, C):
         for dw in range(2):
             exp[:, dh:2 * Ho:2, dw:2 * Ho:2, :] = torch.where(a == dh * 2 + dw, dy, torch.zeros_like(dy))
     assert torch.equal(dx.float(), exp)
+
+
+@pytest.mark.parametrize("H", [12, 13])
+def test_avgpool_bwd_scatter_bn_epilogue_f32(fn, H):
+    """The DenseNet transition pool backward through the scatter form: 2x2 average pool, BN+ReLU
+    backward per input pixel (mask, sum dZ, sum dZ*xhat) and the fp32 gamma*rstd*dZ output; odd H
+    leaves a dropped row / column that must come out zero."""
+    N, C = 4, 256
+    x = bf(torch.randn(N, H, H, C, device=DEV) * 2 + 0.3)
+    st = torch.cat([x.sum((0, 1, 2)), (x * x).sum((0, 1, 2))])
+    g, b = torch.rand(C, device=DEV) + 0.5, torch.randn(C, device=DEV) * 0.1
+    cnt = N * H * H
+    bn = fn.BN(stats=st, gamma=g, beta=b, count=cnt, eps=1e-3, act=1)
+    Ho = H // 2
+    dp = bf(torch.randn(N, Ho, Ho, C, device=DEV))
+    gsum = torch.zeros(C, device=DEV)
+    gsumx = torch.zeros(C, device=DEV)
+    out = fn.pool2d_bwd(dp.to(torch.bfloat16), (N, H, H, C), 2, 2, is_max=False, x=x.to(torch.bfloat16),
+                        bn=bn, gsum=gsum, gsumx=gsumx, out_f32=True)
+    mean = st[:C] / cnt
+    var = st[C:] / cnt - mean ** 2
+    rstd = torch.rsqrt(var + 1e-3)
+    xhat = (x - mean) * rstd
+    z = xhat * g + b
+    up = torch.zeros(N, H, H, C, device=DEV)
+    for dh in range(2):
+        for dw in range(2):
+            up[:, dh:2 * Ho:2, dw:2 * Ho:2, :] = dp / 4
+    dZ = up * (z > 0).float()
+    assert relerr(out, g * rstd * dZ) < 1e-2
+    if H % 2:
+        assert out[:, -1].abs().max().item() == 0 and out[:, :, -1].abs().max().item() == 0
+    assert relerr(gsum, dZ.sum((0, 1, 2))) < 1e-2
+    assert relerr(gsumx, (dZ * xhat).sum((0, 1, 2))) < 2e-2
