@@ -27,7 +27,12 @@ def main():
     marks = [i for i, r in enumerate(rows) if a.marker in r[0]]
     if len(marks) < 3:
         raise SystemExit("need >= 3 steps")
-    lo, hi = marks[-3], marks[-2]
+    # the step with the median wall time among the complete steps after warm-up (one step can
+    # carry a host hiccup, e.g. a Python GC pause before its optimizer launch)
+    cand = list(range(max(1, len(marks) - 8), len(marks) - 1))
+    walls = sorted((rows[marks[j + 1]][1] - rows[marks[j]][1], j) for j in cand)
+    j = walls[len(walls) // 2][1]
+    lo, hi = marks[j], marks[j + 1]
     step = rows[lo:hi]
     q0 = step[0][3]
     main_q = [r for r in step if r[3] == q0]
