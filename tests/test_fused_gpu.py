@@ -231,10 +231,13 @@ def test_tinycnn_fused_dropout_trains_and_eval_is_deterministic():
     assert torch.equal(g1, g2)  # no dropout at inference
 
 
-@pytest.mark.parametrize("arch", ["densenet121", "vgg16", "mobilenetv2"])
-def test_fused_matches_eager_at_bench_batch(arch):
-    """The benchmarked configuration, bs=256: 16 statistics slot copies on the large maps, the
-    autotuner's split-K choices and the full-size workspaces — not only the small test batches."""
+@pytest.mark.parametrize("arch,slots", [("densenet121", "0"), ("densenet121", "1"), ("vgg16", "0"),
+                                        ("mobilenetv2", "0"), ("mobilenetv2", "1")])
+def test_fused_matches_eager_at_bench_batch(monkeypatch, arch, slots):
+    """The benchmarked configuration, bs=256: the autotuner's tile and split-K choices, the
+    full-size workspaces and both statistics layouts (single copy, the default; IDC_STAT_SLOTS=1:
+    16 slot copies on the large maps) — not only the small test batches."""
+    monkeypatch.setenv("IDC_STAT_SLOTS", slots)
     m, ref, x, y = _setup(arch, 256)
     _check(m, ref, x, y)
 
