@@ -83,7 +83,8 @@ def fed_bench(args):
 
     proc = build_federated_averaging_process(
         model_fn, lambda: RMSprop(1e-4), average_bn_stats=True, backend=args.backend,
-        secure_aggregation="mask" if args.mode == "secure" else None)
+        secure_aggregation="mask" if args.mode == "secure" else None,
+        concurrent_clients=args.concurrent_clients)
     state = proc.initialize()
     state, _ = proc.next(state, clients)  # warm-up: builds and tunes the client program
     torch.cuda.synchronize(dev)
@@ -107,7 +108,8 @@ def fed_bench(args):
             "dtype": "bf16", "data": "synthetic uint8 50x50x3 patches, random-init weights",
             "client_images_per_sec": round(imgs / spr, 1),
             "train_loss": round(float(metrics["loss"]), 5),
-            "config": {"model": arch, "clients": args.clients, "client_size": args.client_size,
+            "config": {"model": arch, "clients": args.clients, "concurrent_clients": args.concurrent_clients,
+                       "client_size": args.client_size,
                        "client_batch": args.client_batch, "local_epochs": 1,
                        "client_optimizer": "RMSprop(lr=1e-4)", "server_optimizer": "SGD(lr=1.0)",
                        "aggregation": "DH-keyed additive masks, int32 all-reduce" if args.mode == "secure"
@@ -144,6 +146,8 @@ def main():
     ap.add_argument("--client-size", type=int, default=3000)
     ap.add_argument("--client-batch", type=int, default=32)
     ap.add_argument("--rounds", type=int, default=3)
+    ap.add_argument("--concurrent-clients", type=int, default=2,
+                    help="clients a rank trains at once, each on its own worker model and stream")
     args = ap.parse_args()
     if args.mode != "train":
         return fed_bench(args)

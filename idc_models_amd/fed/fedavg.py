@@ -114,8 +114,14 @@ class FedAvgProcess:
     def __init__(self, model_fn: Callable, client_optimizer_fn: Callable,
                  server_optimizer_fn: Optional[Callable] = None, average_bn_stats: bool = False,
                  local_epochs: int = 1, loss="binary_crossentropy", metrics=("binary_accuracy",),
-                 secure_aggregation: Optional[str] = None, backend: str = "auto"):
+                 secure_aggregation: Optional[str] = None, backend: str = "auto",
+                 concurrent_clients: int = 1):
         self.model_fn = model_fn
+        # ClientScheduler: a rank trains up to `concurrent_clients` of its clients at
+        # once, each on its own worker model and HIP stream (small-batch client steps leave most
+        # of an MI355X idle); aggregation still runs in client order
+        self.concurrent = max(1, int(concurrent_clients))
+        self._more_workers = []
         self.client_optimizer_fn = client_optimizer_fn
         self.server_lr = 1.0
         if server_optimizer_fn is not None:
@@ -139,6 +145,63 @@ class FedAvgProcess:
             m.compile(self.client_optimizer_fn(), self.loss, list(self.metric_names), backend=self.backend)
             self._worker = m
         return self._worker
+
+    def workers(self, n: int):
+        """``n`` worker models: the primary one plus independently built copies."""
+        while len(self._more_workers) < n - 1:
+            m = self.model_fn()
+            m.compile(self.client_optimizer_fn(), self.loss, list(self.metric_names), backend=self.backend)
+            self._more_workers.append(m)
+        return [self.worker()] + self._more_workers[:n - 1]
+
+    def _train_client(self, m, state: "ServerState", ds):
+        """Local training of one client from the server weights: returns its flat trainable
+        weights, flat non-trainable weights, example count and last-epoch logs."""
+        self._load(m, state.model)
+        m.reset_optimizer()
+        if hasattr(m.impl, "reset_stats_shift"):
+            m.impl.reset_stats_shift()
+        h = m.fit(ds, epochs=self.local_epochs, verbose=0)
+        n_k = float(len(ds.ds) if hasattr(ds, "ds") else len(ds))
+        m.impl.sync_to_module()
+        tr, ntr = self._tensors(m)
+        flat = torch.cat([t.detach().reshape(-1) for t in tr])
+        flat_ntr = torch.cat([t.detach().reshape(-1) for t in ntr]) if ntr else None
+        return flat, flat_ntr, n_k, {k2: v[-1] for k2, v in h.history.items()}
+
+    def _train_clients(self, mine, state, data):
+        """Train this rank's clients: sequentially, or `concurrent` at a time on worker threads,
+        each with its own model and current HIP stream (torch's current stream is per thread, so
+        the clients' staging, metrics and kernels never order each other)."""
+        W = min(self.concurrent, len(mine))
+        if W <= 1 or not torch.cuda.is_available() or self.worker().device.type != "cuda":
+            return {k: self._train_client(self.worker(), state, data[k]) for k in mine}
+        import threading
+        models = self.workers(W)
+        dev = models[0].device
+        out, errs = {}, []
+
+        def run(w):
+            try:
+                with torch.cuda.device(dev):
+                    s = torch.cuda.Stream(dev)
+                    s.wait_stream(torch.cuda.default_stream(dev))
+                    with torch.cuda.stream(s):
+                        for k in mine[w::W]:
+                            out[k] = self._train_client(models[w], state, data[k])
+                    s.synchronize()
+            except BaseException as e:  # surfaced on the calling thread
+                errs.append(e)
+
+        torch.cuda.current_stream(dev).synchronize()  # server weights final before the workers read
+        threads = [threading.Thread(target=run, args=(w,), daemon=True) for w in range(W)]
+        for t in threads:
+            t.start()
+        for t in threads:
+            t.join()
+        if errs:
+            raise errs[0]
+        return out
 
     def _tensors(self, m):
         tr = [p for p in m.net.trainable_weights]
@@ -174,29 +237,21 @@ class FedAvgProcess:
             ntr_sum = torch.zeros(sum(w.numel() for w in state.model.non_trainable), device=m.device)
         n_sum = torch.zeros(1, device=m.device, dtype=torch.float64)
         met = torch.zeros(1 + len(self.metric_names), device=m.device, dtype=torch.float64)
-        for k in mine:
-            ds = federated_train_data[k]
-            self._load(m, state.model)
-            m.reset_optimizer()
-            h = m.fit(ds, epochs=self.local_epochs, verbose=0)
-            n_k = float(len(ds.ds) if hasattr(ds, "ds") else len(ds))
-            m.impl.sync_to_module()
-            tr, ntr = self._tensors(m)
-            flat = torch.cat([t.detach().reshape(-1) for t in tr])
+        results = self._train_clients(mine, state, federated_train_data)
+        for k in mine:  # aggregation in client order, however the clients were scheduled
+            flat, flat_ntr, n_k, logs = results[k]
             delta = flat - flat_server
             finite = bool(torch.isfinite(delta).all())
             if self.secure:
-                v = [n_k * delta] + ([n_k * torch.cat([t.detach().reshape(-1) for t in ntr])]
-                                     if ntr_sum is not None else [])
+                v = [n_k * delta] + ([n_k * flat_ntr] if ntr_sum is not None else [])
                 masked[k] = torch.cat(v) if finite else torch.zeros(sum(x.numel() for x in v), device=m.device)
             if not finite:
                 continue  # TFF: non-finite client update gets weight 0
             if not self.secure:
                 delta_sum += n_k * delta
                 if ntr_sum is not None:
-                    ntr_sum += n_k * torch.cat([t.detach().reshape(-1) for t in ntr])
+                    ntr_sum += n_k * flat_ntr
             n_sum += n_k
-            logs = {k2: v[-1] for k2, v in h.history.items()}
             met[0] += n_k * logs.get("loss", 0.0)
             for i, name in enumerate(self.metric_names):
                 met[1 + i] += n_k * logs.get(name if name in logs else "accuracy", 0.0)

@@ -414,13 +414,24 @@ class FusedStep:
         torch.cuda.current_stream(self.m.device).wait_stream(p.stream)
         return p.io.loss.reshape(()).clone(), p.io.logits.clone()
 
+    def reset_stats_shift(self):
+        """Every program back to a first step's statistics shifts (a federated client starts
+        from the same state whichever worker model, and whatever client before it, it runs on)."""
+        for p in self.progs.values():
+            p.reset_stats_shift()
+
     def sync_from_module(self):
         # weights were overwritten on the module side (set_weights / load_weights): re-cast
         for p in self.progs.values():
             p.recast_all()
 
     def sync_to_module(self):
-        torch.cuda.synchronize(self.m.device)
+        # the programs' own streams, not the device: concurrent federated clients on other
+        # worker models keep running (the side lane joins the main stream inside every step)
+        for p in self.progs.values():
+            p.stream.synchronize()
+            p.comm_stream.synchronize()
+        torch.cuda.current_stream(self.m.device).synchronize()
 
     def close(self):
         for p in self.progs.values():

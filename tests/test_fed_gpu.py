@@ -112,3 +112,44 @@ def test_fedavg_secure_mask_equals_plain_on_gpu(monkeypatch):
     for a, b in zip(p_state.model.trainable, s_state.model.trainable):
         assert torch.allclose(a, b, atol=1e-6), float((a - b).abs().max())
     assert p_m["loss"] == pytest.approx(s_m["loss"], rel=1e-6)
+
+
+def test_fedavg_concurrent_clients_match_sequential(monkeypatch):
+    """ClientScheduler: four clients trained concurrently on their own worker models
+    and HIP streams give BITWISE the round of training them one after another on one model
+    (fixed-order reductions, IDC_DETERMINISTIC=1; every client starts from the same statistics
+    shifts), and a second concurrent round reproduces it."""
+    import copy
+    from idc_models_amd.data import contiguous_clients, synthetic_dataset
+    from idc_models_amd.engine import Model, RMSprop
+    from idc_models_amd.fed import build_federated_averaging_process
+    from idc_models_amd.models import build_model
+    from idc_models_amd.parallel import OneDeviceStrategy
+
+    monkeypatch.setenv("IDC_DETERMINISTIC", "1")
+    dev = torch.device("cuda", 0)
+    base = build_model("densenet121", None, 1, seed=3)
+    ds = synthetic_dataset(4 * 96, (50, 50, 3), 2, seed=7)
+
+    def run(conc):
+        # fresh batched views per run: a BatchedDataset reshuffles on every iteration
+        clients = [c.batch(32, True, 1000, True, seed=k) for k, c in enumerate(contiguous_clients(ds, 4, 96))]
+        proc = build_federated_averaging_process(
+            lambda: Model(copy.deepcopy(base), OneDeviceStrategy(dev)), lambda: RMSprop(1e-4),
+            average_bn_stats=True, backend="fused", concurrent_clients=conc)
+        state = proc.initialize()
+        state, met = proc.next(state, clients)
+        torch.cuda.synchronize()
+        w = torch.cat([w.reshape(-1) for w in state.model.trainable])
+        return w, torch.cat([w.reshape(-1) for w in state.model.non_trainable]), met
+
+    w1, n1, m1 = run(1)
+    w4, n4, m4 = run(4)
+    w4b, _, _ = run(4)
+    w0 = torch.cat([p.detach().reshape(-1).to(dev) for p in base.trainable_weights])
+    assert float((w1 - w0).norm()) > 0  # the round trained
+    assert torch.equal(w1, w4), float((w1 - w4).abs().max())
+    assert torch.equal(n1, n4)
+    assert torch.equal(w4, w4b)
+    # the weights are bitwise; the reported metrics come from the per-client fit logs
+    assert set(m1) == set(m4) and all(m1[k] == pytest.approx(m4[k], rel=1e-6) for k in m1), (m1, m4)
