@@ -57,6 +57,7 @@ class FedConfig:
     backend: str = "auto"
     secure_aggregation: Optional[str] = None  # "mask": config #5 secure FedAvg
     resume: bool = True                       # continue from {path}/fed_state/state.pt if present
+    concurrent_clients: int = 1               # clients a rank trains at once (own model + stream)
 
 
 def _fed_data(cfg: FedConfig):
@@ -119,7 +120,7 @@ def run_fedavg(cfg: FedConfig, printer=print):
     fed_avg = build_federated_averaging_process(
         model_fn, client_optimizer_fn=lambda: RMSprop(cfg.base_learning_rate / 10),
         average_bn_stats=cfg.average_bn_stats, metrics=("binary_accuracy",),
-        secure_aggregation=cfg.secure_aggregation)
+        secure_aggregation=cfg.secure_aggregation, concurrent_clients=cfg.concurrent_clients)
     evaluation = build_federated_evaluation(model_fn, metrics=("binary_accuracy",))
     results = []
     printer("Starting federated training")
