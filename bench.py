@@ -16,7 +16,14 @@ patches of that shape and random-init weights (no network on the box).
   that fit (``secure_fed_model.py:81-82`` reports AUC; here over the whole set, not per batch).
 
     python bench.py                     # 1 GPU, defaults
+    python bench.py --gpus 8            # starts 8 rank processes itself (torch.distributed.run)
     python -m torch.distributed.run --nproc-per-node 8 --master-addr 127.0.0.1 bench.py --gpus 8
+
+With ``--gpus N`` (N > 1) and no launcher environment (``WORLD_SIZE`` unset), bench.py starts the N
+rank processes itself through ``torch.distributed.run`` before anything touches the GPU and exits
+with their status; every rank refuses to run (exit 3) when the world it joined is not N.  On a GPU
+the ranks talk over RCCL: the fused step's gradient buckets are all-reduced by the native
+communicator from inside the C++ plan (``parallel/native_comm.py``).
 
 ``vs_baseline`` is relative to the in-situ stock PyTorch-ROCm measurement committed in
 ``benchmarks/stock_baseline.json`` (the reference publishes no number): the faster of
@@ -33,6 +40,41 @@ import time
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
+
+
+def _free_port() -> int:
+    import socket
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as sk:
+        sk.bind(("127.0.0.1", 0))
+        return sk.getsockname()[1]
+
+
+def launch_ranks(n: int) -> int:
+    """Start ``n`` rank processes of this script (one per GPU) and return their exit status.  The
+    parent never initialises the GPU; the children are started as new processes (no exec)."""
+    import subprocess
+    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()),
+           os.path.abspath(__file__)] + sys.argv[1:]
+    return subprocess.call(cmd, env=env)
+
+
+def check_world(expected: int, got: int):
+    if got != expected:
+        print(json.dumps({"error": f"--gpus {expected} but the job has {got} rank(s)"}), flush=True)
+        sys.exit(3)
+
+
+def rccl_version_of(strategy):
+    nc = getattr(strategy, "native_comm", None)
+    if nc is not None:
+        return nc.version()
+    try:
+        import torch
+        return ".".join(str(v) for v in torch.cuda.nccl.version())
+    except Exception:  # pragma: no cover - version query unsupported
+        return "unknown"
 
 
 def stock_img_s_per_gpu(model: str):
@@ -63,6 +105,7 @@ def fed_bench(args):
     from idc_models_amd.parallel import OneDeviceStrategy, comm
 
     rank, world, local = comm.init_process_group()
+    check_world(args.gpus, world)
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
     # config #4 backbone MobileNetV2, config #5 DenseNet-121 (--model overrides for fedavg only)
@@ -115,7 +158,8 @@ def fed_bench(args):
                        "aggregation": "DH-keyed additive masks, int32 all-reduce" if args.mode == "secure"
                        else "example-weighted mean, packed all-reduce",
                        "parallelism": f"clients over {world} rank(s)", "backend": args.backend,
-                       "comm_backend": dist.get_backend() if world > 1 else None},
+                       "comm_backend": dist.get_backend() if world > 1 else None,
+                       "world_size": world},
         }), flush=True)
     if world > 1:
         dist.destroy_process_group()
@@ -148,7 +192,13 @@ def main():
     ap.add_argument("--rounds", type=int, default=3)
     ap.add_argument("--concurrent-clients", type=int, default=2,
                     help="clients a rank trains at once, each on its own worker model and stream")
+    ap.add_argument("--force-collectives", action="store_true",
+                    help="run the RCCL data-parallel path (native bucket all-reduces) even on one GPU")
     args = ap.parse_args()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(launch_ranks(args.gpus))
+    if args.force_collectives:
+        os.environ["IDC_FORCE_COLLECTIVES"] = "1"
     if args.mode != "train":
         return fed_bench(args)
 
@@ -163,12 +213,17 @@ def main():
     from idc_models_amd.parallel.comm import all_reduce_max, barrier
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
+    check_world(args.gpus, world)
+    forced = os.environ.get("IDC_FORCE_COLLECTIVES", "0") == "1"
     if world > 1 and os.environ.get("IDC_BENCH_REHEARSE") == "1":
         # rehearsal of the N>1 path on a one-GPU box: every rank on cuda:0, gloo collectives
         # (RCCL refuses two ranks on one device); numbers from this mode are not throughput
         strategy = MirroredStrategy(backend="gloo", device="cuda:0")
-    elif world > 1:
-        strategy = MirroredStrategy()
+    elif args.device == "cpu" and world > 1:
+        strategy = MirroredStrategy(backend="gloo", device="cpu")
+        args.backend = "eager"
+    elif world > 1 or (forced and args.device == "cuda"):
+        strategy = MirroredStrategy(force_collectives=forced)
     elif args.device == "cpu":
         strategy = OneDeviceStrategy("cpu")
         args.backend = "eager"
@@ -176,12 +231,10 @@ def main():
         strategy = OneDeviceStrategy("cuda:0")
     rank = strategy.rank
     dev = strategy.device
-    comm_backend = dist.get_backend() if world > 1 else None
+    comm_backend = dist.get_backend() if strategy.active else None
     world = strategy.num_replicas_in_sync
-    try:
-        rccl = ".".join(str(v) for v in torch.cuda.nccl.version()) if comm_backend == "nccl" else None
-    except Exception:  # pragma: no cover - version query unsupported
-        rccl = "unknown"
+    check_world(args.gpus, world)
+    rccl = rccl_version_of(strategy) if comm_backend == "nccl" else None
     torch.manual_seed(1234)
 
     with strategy.scope():
@@ -212,7 +265,7 @@ def main():
     barrier()
     sync()
     dt = time.perf_counter() - t0
-    dt = all_reduce_max(dt, dev) if world > 1 else dt
+    dt = all_reduce_max(dt, dev) if strategy.active else dt
     ms = dt / args.steps * 1e3
     total_imgs = args.batch * world * args.steps
     value = total_imgs / dt
@@ -236,7 +289,7 @@ def main():
                   verbose=0)
         k = 1 if len(meter.epoch_seconds) > 1 else 0
         t_ep = max(sum(meter.epoch_seconds[k:]) / len(meter.epoch_seconds[k:]), 1e-9)
-        t_ep = all_reduce_max(t_ep, dev) if world > 1 else t_ep  # slowest rank sets the pace
+        t_ep = all_reduce_max(t_ep, dev) if strategy.active else t_ep  # slowest rank sets the pace
         fit_ips = gb * args.fit_steps / t_ep
         logs = model.evaluate(held.batch(gb, False, 1000, False), return_dict=True)
         val_auc, val_acc = float(logs["auc"]), float(logs["accuracy"])
@@ -267,12 +320,15 @@ def main():
                        "loss": "BCE(from_logits)", "final_loss": round(lossv, 5),
                        "backend": args.backend, "comm_backend": comm_backend, "rccl_version": rccl,
                        "world_size": world,
+                       "grad_allreduce": ("native RCCL communicator, bucket ops in the C++ plan"
+                                          if getattr(strategy, "native_comm", None) is not None
+                                          else "torch.distributed" if strategy.active else None),
                        "stock_baseline_img_s_per_gpu": base,
-                       "val": "exact AUC on a held-out learnable synthetic set after %d fit epochs of %d "
-                              "global batches" % (args.fit_epochs, args.fit_steps)},
+                       "val": ("exact AUC on a held-out learnable synthetic set after %d fit epochs of %d "
+                               "global batches" % (args.fit_epochs, args.fit_steps)) if val_auc is not None else None},
         }), flush=True)
-    if world > 1:
-        dist.destroy_process_group()
+    if strategy.active:
+        strategy.close()
 
 
 if __name__ == "__main__":

@@ -1,0 +1,147 @@
+// Native RCCL communicator (see communicator.h).
+#include "communicator.h"
+
+#include <cstring>
+#include <stdexcept>
+
+namespace idc {
+
+namespace {
+
+inline void nccl_check(ncclResult_t r, const char* what) {
+  if (r != ncclSuccess && r != ncclInProgress)
+    throw std::runtime_error(std::string(what) + ": " + ncclGetErrorString(r));
+}
+
+inline void hip_check(hipError_t e, const char* what) {
+  if (e != hipSuccess) throw std::runtime_error(std::string(what) + ": " + hipGetErrorString(e));
+}
+
+ncclDataType_t to_nccl(int dt) {
+  switch (dt) {
+    case CD_F32: return ncclFloat32;
+    case CD_BF16: return ncclBfloat16;
+    case CD_I32: return ncclInt32;
+    case CD_F64: return ncclFloat64;
+    case CD_U32: return ncclUint32;
+    case CD_I64: return ncclInt64;
+    case CD_U8: return ncclUint8;
+    default: throw std::runtime_error("Communicator: unknown dtype code");
+  }
+}
+
+ncclRedOp_t to_nccl_op(int op) {
+  switch (op) {
+    case CO_SUM: return ncclSum;
+    case CO_MAX: return ncclMax;
+    case CO_MIN: return ncclMin;
+    case CO_AVG: return ncclAvg;
+    default: throw std::runtime_error("Communicator: unknown reduction op");
+  }
+}
+
+}  // namespace
+
+std::string Communicator::make_unique_id() {
+  ncclUniqueId id;
+  nccl_check(ncclGetUniqueId(&id), "ncclGetUniqueId");
+  return std::string(id.internal, NCCL_UNIQUE_ID_BYTES);
+}
+
+Communicator::Communicator(int rank, int world, const std::string& unique_id, int device)
+    : rank_(rank), world_(world), device_(device) {
+  if (world < 1 || rank < 0 || rank >= world) throw std::runtime_error("Communicator: bad rank/world");
+  if (unique_id.size() != NCCL_UNIQUE_ID_BYTES) throw std::runtime_error("Communicator: unique id must be 128 bytes");
+  ncclUniqueId id;
+  std::memcpy(id.internal, unique_id.data(), NCCL_UNIQUE_ID_BYTES);
+  hip_check(hipSetDevice(device), "hipSetDevice");
+  // the collectives' own lane: non-blocking, so it never serialises against the legacy stream
+  hip_check(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking), "hipStreamCreate(comm)");
+  const ncclResult_t r = ncclCommInitRank(&comm_, world, id, rank);
+  if (r != ncclSuccess) {
+    hipStreamDestroy(stream_);
+    stream_ = nullptr;
+    comm_ = nullptr;
+    nccl_check(r, "ncclCommInitRank");
+  }
+}
+
+Communicator::~Communicator() {
+  try {
+    close();
+  } catch (...) {
+  }
+}
+
+void Communicator::close() {
+  if (comm_) {
+    if (stream_) hipStreamSynchronize(stream_);
+    ncclCommDestroy(comm_);
+    comm_ = nullptr;
+  }
+  if (stream_) {
+    hipStreamDestroy(stream_);
+    stream_ = nullptr;
+  }
+}
+
+void Communicator::abort() {
+  if (comm_) {
+    ncclCommAbort(comm_);
+    comm_ = nullptr;
+  }
+}
+
+void Communicator::require_open() const {
+  if (!comm_) throw std::runtime_error("Communicator: closed");
+}
+
+void Communicator::check_async() const {
+  require_open();
+  ncclResult_t ar = ncclSuccess;
+  nccl_check(ncclCommGetAsyncError(comm_, &ar), "ncclCommGetAsyncError");
+  nccl_check(ar, "RCCL asynchronous error");
+}
+
+void Communicator::all_reduce(void* buf, long long count, int dtype, int op, hipStream_t st) {
+  require_open();
+  if (count <= 0) return;
+  nccl_check(ncclAllReduce(buf, buf, (size_t)count, to_nccl(dtype), to_nccl_op(op), comm_, st ? st : stream_),
+             "ncclAllReduce");
+  ++ncoll_;
+}
+
+void Communicator::reduce(void* buf, long long count, int dtype, int op, int root, hipStream_t st) {
+  require_open();
+  if (count <= 0) return;
+  nccl_check(ncclReduce(buf, buf, (size_t)count, to_nccl(dtype), to_nccl_op(op), root, comm_, st ? st : stream_),
+             "ncclReduce");
+  ++ncoll_;
+}
+
+void Communicator::broadcast(void* buf, long long count, int dtype, int root, hipStream_t st) {
+  require_open();
+  if (count <= 0) return;
+  nccl_check(ncclBroadcast(buf, buf, (size_t)count, to_nccl(dtype), root, comm_, st ? st : stream_),
+             "ncclBroadcast");
+  ++ncoll_;
+}
+
+void Communicator::all_gather(const void* send, void* recv, long long count_per_rank, int dtype, hipStream_t st) {
+  require_open();
+  if (count_per_rank <= 0) return;
+  nccl_check(ncclAllGather(send, recv, (size_t)count_per_rank, to_nccl(dtype), comm_, st ? st : stream_),
+             "ncclAllGather");
+  ++ncoll_;
+}
+
+void Communicator::group_start() { nccl_check(ncclGroupStart(), "ncclGroupStart"); }
+void Communicator::group_end() { nccl_check(ncclGroupEnd(), "ncclGroupEnd"); }
+
+int rccl_version() {
+  int v = 0;
+  nccl_check(ncclGetVersion(&v), "ncclGetVersion");
+  return v;
+}
+
+}  // namespace idc

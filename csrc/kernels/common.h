@@ -139,6 +139,44 @@ __device__ __forceinline__ void prefetch_kernargs() {
   for (int i = 0; i < L; ++i) asm volatile("" ::"s"(v[i]));
 }
 
+// ---------------------------------------------------------------------------------------------
+// Grouped execution (client-batched federated training; runtime/grouped.py).
+// A grouped program keeps K copies of ALL its buffers at one fixed byte stride: copy g of any
+// buffer lives at (address of copy 0) + g * stride.  One grouped launch runs all K copies: the
+// launcher multiplies its grid's z extent by K (ggrid), and a workgroup's copy is
+// g = blockIdx.z / zn, zn being the kernel's own z extent (1 unless it splits over z itself).
+// Every pointer the workgroup dereferences -- its argument struct's and the ones it reads from
+// device descriptor tables -- is shifted by g * stride (gshift / gsh); null pointers stay null
+// (they select modes).  The host side checks that every pointer of a grouped plan lies inside
+// copy 0, so a shift never leaves the program's own memory.  Ungrouped launches: stride 0.
+struct GroupArg {
+  long long stride;  // bytes between copies (0: ungrouped)
+  int zn;            // the kernel's own z extent
+  int pad;
+};
+struct LaunchGroups {
+  int k = 1;
+  long long stride = 0;
+};
+LaunchGroups& launch_groups();  // per host thread; the plan executor sets it around grouped ops
+inline GroupArg garg(int zn = 1) {
+  const LaunchGroups& l = launch_groups();
+  return GroupArg{l.k > 1 ? l.stride : 0, zn, 0};
+}
+inline dim3 ggrid(dim3 g) {
+  g.z *= (unsigned)launch_groups().k;
+  return g;
+}
+inline dim3 ggrid(int gx) { return ggrid(dim3((unsigned)gx)); }
+__device__ __forceinline__ long long goff(const GroupArg& ga) {
+  return ga.stride ? (long long)(blockIdx.z / (unsigned)ga.zn) * ga.stride : 0;
+}
+__device__ __forceinline__ int gz(const GroupArg& ga) { return (int)(blockIdx.z % (unsigned)ga.zn); }
+template <typename T>
+__device__ __forceinline__ T* gsh(T* p, long long off) {
+  return p ? (T*)((uintptr_t)p + off) : p;
+}
+
 // BatchNorm descriptor shared by every kernel that applies a BN affine (+activation) to an
 // operand on the fly ("pending BN").  mode 1: batch statistics from `stats` ([sum|sumsq] over
 // `count` samples); mode 2: inference (moving statistics).  mode 0: identity (act only).
@@ -156,6 +194,11 @@ struct BnArgs {
   int slots;              // mode 1: `stats` holds this many [sum|sumsq] copies (0/1: one), see below
   const float* shift;     // mode 1 (nullable): per-channel shift K, stats hold sum(y-K), sum((y-K)^2)
 };
+
+__device__ __forceinline__ void gshift(BnArgs& b, long long o) {
+  b.stats = gsh(b.stats, o); b.gamma = gsh(b.gamma, o); b.beta = gsh(b.beta, o);
+  b.mmean = gsh(b.mmean, o); b.mvar = gsh(b.mvar, o); b.shift = gsh(b.shift, o);
+}
 
 // Shifted statistics.  Producers accumulate sum(y - K) and sum((y - K)^2) with a per-channel
 // shift K (the previous step's batch mean, updated after every backward by stats_shift_kernel),
@@ -392,6 +435,12 @@ struct BwdAff {
   float* fold_sum; float* fold_sumx;
 };
 
+__device__ __forceinline__ void gshift(BwdAff& b, long long o) {
+  b.x = gsh(b.x, o); gshift(b.bn, o); b.gsum = gsh(b.gsum, o); b.gsumx = gsh(b.gsumx, o);
+  b.fgsum = gsh(b.fgsum, o); b.fgsumx = gsh(b.fgsumx, o);
+  b.fold_sum = gsh(b.fold_sum, o); b.fold_sumx = gsh(b.fold_sumx, o);
+}
+
 // A/B/C table for channels c0 + [0, n) into sA/sB/sC[0, n) (LDS); channels at or past `lim` get
 // the identity; all loads of a channel are issued before its arithmetic.
 template <int NT>
@@ -490,8 +539,9 @@ __device__ __forceinline__ void bwd_aff_finish(const BwdAff& b, const BwdAffRaw&
 template <int NT>
 __device__ __forceinline__ void bwd_aff_fold(const BwdAff& b) {
   if (b.fold_sum == nullptr) return;
-  const int nb = gridDim.x * gridDim.y * gridDim.z;
-  const int bid = blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z);
+  // (x, y only: a grouped launch's z is the program copy, each copy folds its own sums)
+  const int nb = gridDim.x * gridDim.y;
+  const int bid = blockIdx.x + gridDim.x * blockIdx.y;
   int share = (b.fold_C + nb - 1) / nb;
   share = (share + 63) / 64 * 64;
   const int c0 = bid * share, c1 = min(b.fold_C, c0 + share);

@@ -49,7 +49,8 @@ __host__ __device__ inline HaloGeom halo_geom(int H, int W, int Cin, int Cout, i
 }  // namespace
 
 template <int COUT, int MT, typename TA, int PRO, int EPI>
-__global__ __launch_bounds__(NT) void conv3x3_halo_kernel(ConvArgs a) {
+__global__ __launch_bounds__(NT) void conv3x3_halo_kernel(ConvArgs a, GroupArg ga) {
+  gshift(a, goff(ga));
   constexpr int NTL = COUT / 16;  // n tiles (16 output channels each)
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const HaloGeom g = halo_geom(a.H, a.W, a.Cin, COUT, PRO, EPI);
@@ -314,10 +315,10 @@ template <int COUT, typename TA, int PRO, int EPI>
 static hipError_t halo_launch_mt(const ConvArgs& a, int mt, size_t shm, hipStream_t st) {
   dim3 grid(a.N), block(NT);
   switch (mt) {
-    case 1: hipLaunchKernelGGL((conv3x3_halo_kernel<COUT, 1, TA, PRO, EPI>), grid, block, shm, st, a); break;
-    case 2: hipLaunchKernelGGL((conv3x3_halo_kernel<COUT, 2, TA, PRO, EPI>), grid, block, shm, st, a); break;
-    case 3: hipLaunchKernelGGL((conv3x3_halo_kernel<COUT, 3, TA, PRO, EPI>), grid, block, shm, st, a); break;
-    default: hipLaunchKernelGGL((conv3x3_halo_kernel<COUT, 4, TA, PRO, EPI>), grid, block, shm, st, a); break;
+    case 1: hipLaunchKernelGGL((conv3x3_halo_kernel<COUT, 1, TA, PRO, EPI>), ggrid(grid), block, shm, st, a, garg()); break;
+    case 2: hipLaunchKernelGGL((conv3x3_halo_kernel<COUT, 2, TA, PRO, EPI>), ggrid(grid), block, shm, st, a, garg()); break;
+    case 3: hipLaunchKernelGGL((conv3x3_halo_kernel<COUT, 3, TA, PRO, EPI>), ggrid(grid), block, shm, st, a, garg()); break;
+    default: hipLaunchKernelGGL((conv3x3_halo_kernel<COUT, 4, TA, PRO, EPI>), ggrid(grid), block, shm, st, a, garg()); break;
   }
   return hipGetLastError();
 }

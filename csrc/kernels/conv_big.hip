@@ -61,8 +61,9 @@ __device__ __forceinline__ int bswz(int row, int chunk) { return chunk ^ (row & 
 }  // namespace
 
 template <int BN, int WM, int WN, int NBUF_, int EPI>
-__global__ __launch_bounds__(WM * WN * 64) void conv_big_kernel(ConvArgs a) {
-  prefetch_kernargs<sizeof(ConvArgs)>();
+__global__ __launch_bounds__(WM * WN * 64) void conv_big_kernel(ConvArgs a, GroupArg ga) {
+  prefetch_kernargs<sizeof(ConvArgs) + sizeof(GroupArg)>();
+  gshift(a, goff(ga));
   using C = BigCfg<BN, WM, WN, NBUF_>;
   constexpr int NW = C::NW;
   constexpr int BM = C::BM, BK = C::BK, TM = C::TM, TN = C::TN, WTN = C::WTN;
@@ -350,9 +351,9 @@ static hipError_t big_launch(const ConvArgs& a, hipStream_t st) {
   const int grid = tiles * ks;
   if (grid == 0) return hipSuccess;
   if (a.epi_mode == 0)
-    hipLaunchKernelGGL((conv_big_kernel<BN, WM, WN, NBUF, 0>), dim3(grid), dim3(C::NT), C::LDS_BYTES, st, a);
+    hipLaunchKernelGGL((conv_big_kernel<BN, WM, WN, NBUF, 0>), ggrid(grid), dim3(C::NT), C::LDS_BYTES, st, a, garg());
   else
-    hipLaunchKernelGGL((conv_big_kernel<BN, WM, WN, NBUF, 1>), dim3(grid), dim3(C::NT), C::LDS_BYTES, st, a);
+    hipLaunchKernelGGL((conv_big_kernel<BN, WM, WN, NBUF, 1>), ggrid(grid), dim3(C::NT), C::LDS_BYTES, st, a, garg());
   return hipGetLastError();
 }
 

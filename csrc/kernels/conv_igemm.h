@@ -68,6 +68,14 @@ struct ConvArgs {
 };
 
 // tile TILE_HALO selects the one-image-per-workgroup direct 3x3 kernel (conv3x3_halo.hip)
+__device__ __forceinline__ void gshift(ConvArgs& a, long long o) {
+  if (!o) return;
+  a.x = gsh(a.x, o); a.y = gsh(a.y, o); a.w = gsh(a.w, o); gshift(a.pro, o); a.bias = gsh(a.bias, o);
+  a.stats_out = gsh(a.stats_out, o); a.mx = gsh(a.mx, o); gshift(a.mbn, o); a.gsum = gsh(a.gsum, o);
+  a.gsumx = gsh(a.gsumx, o); a.slab = gsh(a.slab, o); a.tickets = gsh(a.tickets, o); gshift(a.bpro, o);
+  gshift(a.bepi, o); a.aout = gsh(a.aout, o); a.stats_shift = gsh(a.stats_shift, o);
+}
+
 constexpr int TILE_HALO = 100;
 // tiles TILE_BIG128 / TILE_BIG256 select the 256 x {128, 256} global_load_lds kernel for plain
 // wide layers (conv_big.hip)

@@ -74,9 +74,10 @@ struct IgemmCfg {
 };
 
 template <int BM, int BN, int BK, int WM, int WN, bool IS1X1, typename TA, int PRO, int EPI>
-__global__ __launch_bounds__(256) void conv_igemm_kernel(ConvArgs a) {
+__global__ __launch_bounds__(256) void conv_igemm_kernel(ConvArgs a, GroupArg ga) {
   IDC_PHASE_STAMP(0);
-  prefetch_kernargs<sizeof(ConvArgs)>();
+  prefetch_kernargs<sizeof(ConvArgs) + sizeof(GroupArg)>();
+  gshift(a, goff(ga));
   using C = IgemmCfg<BM, BN, BK, WM, WN>;
   constexpr int NT = C::NT, CPR = C::CPR, WTM = C::WTM, WTN = C::WTN;
   constexpr int NA = (BM * CPR + NT - 1) / NT;  // A chunks per thread
@@ -763,8 +764,8 @@ static inline hipError_t launch_cfg(const ConvArgs& a, bool is1x1, bool a_f32, i
   if (grid == 0) return hipSuccess;
   const size_t shm = IgemmCfg<BM, BN, BK, WM, WN>::smem_bytes(pro ? a.Cin : 0);
 #define IDC_L(IS1, TA, P, E)                                                                   \
-  hipLaunchKernelGGL((conv_igemm_kernel<BM, BN, BK, WM, WN, IS1, TA, P, E>), dim3(grid),     \
-                     dim3(256), shm, st, a)
+  hipLaunchKernelGGL((conv_igemm_kernel<BM, BN, BK, WM, WN, IS1, TA, P, E>), ggrid(grid),     \
+                     dim3(256), shm, st, a, garg())
 #define IDC_E(IS1, TA, P)      \
   if (epi == 0) IDC_L(IS1, TA, P, 0); \
   else IDC_L(IS1, TA, P, 1);

@@ -25,6 +25,12 @@ struct WgradArgs {
   long long part_floats;  // capacity, checked at launch
 };
 
+__device__ __forceinline__ void gshift(WgradArgs& a, long long o) {
+  if (!o) return;
+  a.x = gsh(a.x, o); a.g = gsh(a.g, o); gshift(a.pro, o); a.dw = gsh(a.dw, o); gshift(a.gpro, o);
+  a.part = gsh(a.part, o);
+}
+
 hipError_t conv_wgrad(WgradArgs a, int splits, bool g_f32, hipStream_t st);
 // dw[i] += sum_{z < splits} part[z * n + i], in slice order
 hipError_t wgrad_reduce(const float* part, float* dw, long long n, int splits, hipStream_t st);

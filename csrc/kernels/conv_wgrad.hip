@@ -63,8 +63,10 @@ __device__ __forceinline__ v8bf tr_frag(const bf16_t* tile, int col_base, int la
 }
 
 template <int BKR, int BC, int BP_, int WM, int WN, bool IS1X1, typename TG, int PRO, int GPRO>
-__global__ __launch_bounds__(256) void conv_wgrad_kernel(WgradArgs a) {
-  prefetch_kernargs<sizeof(WgradArgs)>();
+__global__ __launch_bounds__(256) void conv_wgrad_kernel(WgradArgs a, GroupArg ga) {
+  prefetch_kernargs<sizeof(WgradArgs) + sizeof(GroupArg)>();
+  gshift(a, goff(ga));
+  const int zslice = gz(ga);  // this workgroup's pixel slice (z = copy * splits + slice)
   using C = WgCfg<BKR, BC, BP_>;
   constexpr int NT = C::NT, BP = C::BP;
   constexpr int WTM = BKR / WM, WTN = BC / WN;
@@ -93,7 +95,7 @@ __global__ __launch_bounds__(256) void conv_wgrad_kernel(WgradArgs a) {
   const int k0 = blockIdx.x * BKR;
   const int c0 = blockIdx.y * BC;
   const int per = a.pix_per_split;
-  const int pbeg = blockIdx.z * per;
+  const int pbeg = zslice * per;
   const int pend = min(M, pbeg + per);
   if (pbeg >= pend) return;
 
@@ -270,7 +272,7 @@ __global__ __launch_bounds__(256) void conv_wgrad_kernel(WgradArgs a) {
       kdst = rs * a.cin_real + c;
     }
     const float v = Cs[row * CS_LD + col] * a.scale;
-    if (a.part) a.part[(size_t)blockIdx.z * ((size_t)a.KH * a.KW * (a.cin_real ? a.cin_real : a.Cin) * a.Cout) +
+    if (a.part) a.part[(size_t)zslice * ((size_t)a.KH * a.KW * (a.cin_real ? a.cin_real : a.Cin) * a.Cout) +
                        (size_t)kdst * a.Cout + co] = v;
     else atomicAdd(&a.dw[(size_t)kdst * a.Cout + co], v);
   }
@@ -329,7 +331,8 @@ __host__ __device__ inline WhGeom wh_geom(int H, int W, int ipw) {
 }
 }  // namespace
 
-__global__ __launch_bounds__(256) void wgrad3x3_img_kernel(WgradArgs a, int ipw) {
+__global__ __launch_bounds__(256) void wgrad3x3_img_kernel(WgradArgs a, int ipw, GroupArg ga) {
+  gshift(a, goff(ga));
   prefetch_kernargs<sizeof(WgradArgs)>();
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int H = a.H, W = a.W;
@@ -464,7 +467,10 @@ static int wgrad_halo_groups(const WgradArgs& a, int splits) {
 }
 
 __global__ __launch_bounds__(256) void wgrad_reduce_kernel(const float* __restrict__ part, float* __restrict__ dw,
-                                                           long long n, int splits) {
+                                                           long long n, int splits, GroupArg ga) {
+  const long long go = goff(ga);
+  part = gsh(part, go);
+  dw = gsh(dw, go);
   for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n; i += (long long)gridDim.x * blockDim.x) {
     float s = 0.f;
     for (int z = 0; z < splits; ++z) s += part[(size_t)z * n + i];
@@ -477,7 +483,7 @@ hipError_t wgrad_reduce(const float* part, float* dw, long long n, int splits, h
   if (part == nullptr || dw == nullptr || splits < 1) return hipErrorInvalidValue;
   long long b = (n + 255) / 256;
   if (b > 4096) b = 4096;
-  hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((int)b), dim3(256), 0, st, part, dw, n, splits);
+  hipLaunchKernelGGL(wgrad_reduce_kernel, ggrid((int)b), dim3(256), 0, st, part, dw, n, splits, garg());
   return hipGetLastError();
 }
 
@@ -489,7 +495,8 @@ static hipError_t launch_wg(const WgradArgs& a, bool is1x1, bool g_f32, int pro,
   const size_t shm = WgCfg<BKR, BC, BP>::smem_bytes(pro ? a.Cin : 0);
   const bool gpro = a.gpro.mode != 0;
 #define IDC_W(IS1, TG, P, GP) \
-  hipLaunchKernelGGL((conv_wgrad_kernel<BKR, BC, BP, WM, WN, IS1, TG, P, GP>), grid, dim3(256), shm, st, a)
+  hipLaunchKernelGGL((conv_wgrad_kernel<BKR, BC, BP, WM, WN, IS1, TG, P, GP>), ggrid(grid), dim3(256), shm, st, a, \
+                     garg(splits))
 #define IDC_WG(IS1, TG, P) if (gpro) IDC_W(IS1, TG, P, 1); else IDC_W(IS1, TG, P, 0);
 #define IDC_WP(IS1, TG) if (pro) { IDC_WG(IS1, TG, 1) } else { IDC_WG(IS1, TG, 0) }
   if (g_f32) {
@@ -531,7 +538,7 @@ hipError_t conv_wgrad(WgradArgs a, int splits, bool g_f32, hipStream_t st) {
     if (a.part && (long long)groups * 9 * a.Cin * 32 > a.part_floats) return hipErrorInvalidValue;
     const WhGeom geo = wh_geom(a.H, a.W, ipw);
     const size_t shm = geo.x_bytes + geo.g_bytes + 2 * (size_t)a.Cin * 4;
-    hipLaunchKernelGGL(wgrad3x3_img_kernel, dim3(groups, a.Cin / WH_CB), dim3(256), shm, st, a, ipw);
+    hipLaunchKernelGGL(wgrad3x3_img_kernel, ggrid(dim3(groups, a.Cin / WH_CB)), dim3(256), shm, st, a, ipw, garg());
     return hipGetLastError();
   }
   const bool is1x1 = a.KH == 1 && a.KW == 1 && a.SH == 1 && a.SW == 1 && a.PT == 0 && a.PL == 0;

@@ -29,6 +29,13 @@ struct DwArgs {
   const float* stats_shift;
 };
 
+__device__ __forceinline__ void gshift(DwArgs& a, long long o) {
+  if (!o) return;
+  a.x = gsh(a.x, o); gshift(a.pro, o); a.w = gsh(a.w, o); a.y = gsh(a.y, o); a.stats = gsh(a.stats, o);
+  a.dy = gsh(a.dy, o); a.dx = gsh(a.dx, o); a.gsum = gsh(a.gsum, o); a.gsumx = gsh(a.gsumx, o);
+  a.dw = gsh(a.dw, o); a.ws = gsh(a.ws, o); gshift(a.dyaff, o); a.stats_shift = gsh(a.stats_shift, o);
+}
+
 long long dwconv_wgrad_ws_floats(long long M, int C, int taps);
 
 hipError_t dwconv_fwd(const DwArgs& a, hipStream_t st);

@@ -30,7 +30,8 @@ inline int nblocks(long long rows, int C, int rows_per_thread) {
 }
 }  // namespace
 
-__global__ __launch_bounds__(256) void dw_fwd_kernel(DwArgs a) {
+__global__ __launch_bounds__(256) void dw_fwd_kernel(DwArgs a, GroupArg ga) {
+  gshift(a, goff(ga));
   extern __shared__ float sh[];
   float* s_sc = sh;
   float* s_sf = sh + a.C;
@@ -97,7 +98,8 @@ __global__ __launch_bounds__(256) void dw_fwd_kernel(DwArgs a) {
   }
 }
 
-__global__ __launch_bounds__(256) void dw_bwd_data_kernel(DwArgs a) {
+__global__ __launch_bounds__(256) void dw_bwd_data_kernel(DwArgs a, GroupArg ga) {
+  gshift(a, goff(ga));
   extern __shared__ float sh[];
   float* s_sc = sh;
   float* s_sf = sh + a.C;
@@ -170,7 +172,8 @@ __global__ __launch_bounds__(256) void dw_bwd_data_kernel(DwArgs a) {
   }
 }
 
-__global__ __launch_bounds__(256) void dw_wgrad_kernel(DwArgs a) {
+__global__ __launch_bounds__(256) void dw_wgrad_kernel(DwArgs a, GroupArg ga) {
+  gshift(a, goff(ga));
   extern __shared__ float sh[];
   float* s_sc = sh;
   float* s_sf = sh + a.C;
@@ -229,7 +232,8 @@ __global__ __launch_bounds__(256) void dw_wgrad_kernel(DwArgs a) {
 constexpr int kDwStrip = 4;
 
 template <int S>
-__global__ __launch_bounds__(256) void dw_fwd3_kernel(DwArgs a) {
+__global__ __launch_bounds__(256) void dw_fwd3_kernel(DwArgs a, GroupArg ga) {
+  gshift(a, goff(ga));
   constexpr int P = kDwStrip, NCOL = (P - 1) * S + 3;
   extern __shared__ float sh[];
   float* s_sc = sh;
@@ -337,7 +341,8 @@ __global__ __launch_bounds__(256) void dw_fwd3_kernel(DwArgs a) {
 // at an even w0, dy column (w0 >> 1) - 1 + q feeds pixel p through tap s = p + PL2 + 2 - 2q, so
 // which (pixel, column) pairs meet is known at compile time; PL2 < 0 gathers per pixel.
 template <int S, int PL2, bool AFF>
-__global__ __launch_bounds__(256) void dw_bwd3_kernel(DwArgs a) {
+__global__ __launch_bounds__(256) void dw_bwd3_kernel(DwArgs a, GroupArg ga) {
+  gshift(a, goff(ga));
   constexpr bool STRIP = S == 1 || PL2 >= 0;
   constexpr int P = STRIP ? kDwStrip : 1;
   constexpr int NCOL = S == 1 ? P + 2 : (PL2 >= 0 ? (P + PL2 + 2) / 2 + 1 : 3);
@@ -499,13 +504,13 @@ hipError_t dwconv_fwd(const DwArgs& a, hipStream_t st) {
   if (a.KH == 3 && a.KW == 3 && (a.S == 1 || a.S == 2) && a.C % 8 == 0 && a.C <= 2048) {
     const long long strips = (long long)a.N * a.Ho * ((a.Wo + kDwStrip - 1) / kDwStrip);
     if (a.S == 1)
-      hipLaunchKernelGGL(dw_fwd3_kernel<1>, dim3(strip_blocks(strips, a.C)), dim3(256), 4 * a.C * 4, st, a);
+      hipLaunchKernelGGL(dw_fwd3_kernel<1>, ggrid(dim3(strip_blocks(strips, a.C))), dim3(256), 4 * a.C * 4, st, a, garg());
     else
-      hipLaunchKernelGGL(dw_fwd3_kernel<2>, dim3(strip_blocks(strips, a.C)), dim3(256), 4 * a.C * 4, st, a);
+      hipLaunchKernelGGL(dw_fwd3_kernel<2>, ggrid(dim3(strip_blocks(strips, a.C))), dim3(256), 4 * a.C * 4, st, a, garg());
     return hipGetLastError();
   }
-  hipLaunchKernelGGL(dw_fwd_kernel, dim3(nblocks((long long)a.N * a.Ho * a.Wo, a.C, 4)), dim3(256), 4 * a.C * 4,
-                     st, a);
+  hipLaunchKernelGGL(dw_fwd_kernel, ggrid(dim3(nblocks((long long)a.N * a.Ho * a.Wo, a.C, 4))), dim3(256),
+                     4 * a.C * 4, st, a, garg());
   return hipGetLastError();
 }
 
@@ -516,8 +521,8 @@ hipError_t dwconv_bwd_data(const DwArgs& a, hipStream_t st) {
     const long long strips4 = (long long)a.N * a.H * ((a.W + kDwStrip - 1) / kDwStrip);
     const int g4 = strip_blocks(strips4, a.C), g1 = strip_blocks((long long)a.N * a.H * a.W, a.C);
 #define IDC_DWB(S_, PL_, G_)                                                                      \
-  if (aff) hipLaunchKernelGGL((dw_bwd3_kernel<S_, PL_, true>), dim3(G_), dim3(256), shm, st, a); \
-  else hipLaunchKernelGGL((dw_bwd3_kernel<S_, PL_, false>), dim3(G_), dim3(256), shm, st, a);
+  if (aff) hipLaunchKernelGGL((dw_bwd3_kernel<S_, PL_, true>), ggrid(dim3(G_)), dim3(256), shm, st, a, garg()); \
+  else hipLaunchKernelGGL((dw_bwd3_kernel<S_, PL_, false>), ggrid(dim3(G_)), dim3(256), shm, st, a, garg());
     if (a.S == 1) {
       IDC_DWB(1, -1, g4)
     } else if (a.PL == 0) {
@@ -531,8 +536,8 @@ hipError_t dwconv_bwd_data(const DwArgs& a, hipStream_t st) {
     return hipGetLastError();
   }
   if (aff) return hipErrorInvalidValue;  // the backward affine prologue is 3x3-only
-  hipLaunchKernelGGL(dw_bwd_data_kernel, dim3(nblocks((long long)a.N * a.H * a.W, a.C, 4)), dim3(256),
-                     6 * a.C * 4, st, a);
+  hipLaunchKernelGGL(dw_bwd_data_kernel, ggrid(dim3(nblocks((long long)a.N * a.H * a.W, a.C, 4))), dim3(256),
+                     6 * a.C * 4, st, a, garg());
   return hipGetLastError();
 }
 
@@ -558,7 +563,8 @@ long long dwconv_wgrad_ws_floats(long long M, int C, int taps) {
   return (long long)dw_wgrad_blocks(M, C) * taps * C;
 }
 
-__global__ __launch_bounds__(256) void dw_wgrad_part_kernel(DwArgs a, int rows_per_block) {
+__global__ __launch_bounds__(256) void dw_wgrad_part_kernel(DwArgs a, int rows_per_block, GroupArg ga) {
+  gshift(a, goff(ga));
   extern __shared__ float sh[];
   float* s_sc = sh;
   float* s_sf = sh + a.C;
@@ -626,7 +632,8 @@ __global__ __launch_bounds__(256) void dw_wgrad_part_kernel(DwArgs a, int rows_p
 // vectors are loaded once and multiplied into every tap they meet (stride 1: 18 loads and 4 dy
 // loads per 4 outputs instead of 40); block b owns strips [b*spb, (b+1)*spb).
 template <int S, bool AFF>
-__global__ __launch_bounds__(256) void dw_wgrad3_part_kernel(DwArgs a, int spb) {
+__global__ __launch_bounds__(256) void dw_wgrad3_part_kernel(DwArgs a, int spb, GroupArg ga) {
+  gshift(a, goff(ga));
   constexpr int P = kDwStrip, NCOL = (P - 1) * S + 3;
   extern __shared__ float sh[];
   float* s_sc = sh;
@@ -737,7 +744,10 @@ __global__ __launch_bounds__(256) void dw_wgrad3_part_kernel(DwArgs a, int spb) 
 // column sums of the per-block partials: blockIdx.y splits the blocks so the sum is spread over
 // many workgroups (a single pass per column was a few long latency chains on a handful of CUs)
 __global__ __launch_bounds__(256) void dw_wgrad_sum_kernel(const float* __restrict__ ws, int nblk, int n,
-                                                           float* __restrict__ dw) {
+                                                           float* __restrict__ dw, GroupArg ga) {
+  const long long go = goff(ga);
+  ws = gsh(ws, go);
+  dw = gsh(dw, go);
   const int k = blockIdx.x * blockDim.x + threadIdx.x;
   if (k >= n) return;
   const int per = (nblk + gridDim.y - 1) / gridDim.y;
@@ -768,27 +778,27 @@ hipError_t dwconv_wgrad(const DwArgs& a, hipStream_t st) {
       const int spb = (int)((strips + nblk - 1) / nblk);
       const size_t shm = (5 * a.C + 256 * 24) * 4;
       if (a.S == 1) {
-        if (aff) hipLaunchKernelGGL((dw_wgrad3_part_kernel<1, true>), dim3(nblk), dim3(256), shm, st, a, spb);
-        else hipLaunchKernelGGL((dw_wgrad3_part_kernel<1, false>), dim3(nblk), dim3(256), shm, st, a, spb);
+        if (aff) hipLaunchKernelGGL((dw_wgrad3_part_kernel<1, true>), ggrid(dim3(nblk)), dim3(256), shm, st, a, spb, garg());
+        else hipLaunchKernelGGL((dw_wgrad3_part_kernel<1, false>), ggrid(dim3(nblk)), dim3(256), shm, st, a, spb, garg());
       } else {
-        if (aff) hipLaunchKernelGGL((dw_wgrad3_part_kernel<2, true>), dim3(nblk), dim3(256), shm, st, a, spb);
-        else hipLaunchKernelGGL((dw_wgrad3_part_kernel<2, false>), dim3(nblk), dim3(256), shm, st, a, spb);
+        if (aff) hipLaunchKernelGGL((dw_wgrad3_part_kernel<2, true>), ggrid(dim3(nblk)), dim3(256), shm, st, a, spb, garg());
+        else hipLaunchKernelGGL((dw_wgrad3_part_kernel<2, false>), ggrid(dim3(nblk)), dim3(256), shm, st, a, spb, garg());
       }
     } else if (aff) {
       return hipErrorInvalidValue;
     } else {
       const int rpb = (int)((Mo + nblk - 1) / nblk);
-      hipLaunchKernelGGL(dw_wgrad_part_kernel, dim3(nblk), dim3(256), (2 + T) * a.C * 4, st, a, rpb);
+      hipLaunchKernelGGL(dw_wgrad_part_kernel, ggrid(dim3(nblk)), dim3(256), (2 + T) * a.C * 4, st, a, rpb, garg());
     }
     const int n = T * a.C;
     const int cols = (n + 255) / 256;
     int split = (nblk + 31) / 32;  // ~32 partials per thread, enough workgroups to fill the chip
     if (split > 64) split = 64;
     if (split < 1) split = 1;
-    hipLaunchKernelGGL(dw_wgrad_sum_kernel, dim3(cols, split), dim3(256), 0, st, a.ws, nblk, n, a.dw);
+    hipLaunchKernelGGL(dw_wgrad_sum_kernel, ggrid(dim3(cols, split)), dim3(256), 0, st, a.ws, nblk, n, a.dw, garg());
     return hipGetLastError();
   }
-  hipLaunchKernelGGL(dw_wgrad_kernel, dim3(nblocks(Mo, a.C, 32)), dim3(256), (2 + T) * a.C * 4, st, a);
+  hipLaunchKernelGGL(dw_wgrad_kernel, ggrid(dim3(nblocks(Mo, a.C, 32))), dim3(256), (2 + T) * a.C * 4, st, a, garg());
   return hipGetLastError();
 }
 

@@ -30,6 +30,14 @@ struct Mlp2Args {
   float* dx;              // [N][D0] fp32 gradient of the flattened input (may be null)
 };
 
+__device__ __forceinline__ void gshift(Mlp2Args& a, long long o) {
+  if (!o) return;
+  a.x = gsh(a.x, o); a.w1 = gsh(a.w1, o); a.b1 = gsh(a.b1, o); a.w2 = gsh(a.w2, o); a.b2 = gsh(a.b2, o);
+  a.step = gsh(a.step, o); a.labels = gsh(a.labels, o); a.logits = gsh(a.logits, o); a.h1 = gsh(a.h1, o);
+  a.loss = gsh(a.loss, o); a.dlogits = gsh(a.dlogits, o); a.dw1 = gsh(a.dw1, o); a.db1 = gsh(a.db1, o);
+  a.dw2 = gsh(a.dw2, o); a.db2 = gsh(a.db2, o); a.dx = gsh(a.dx, o);
+}
+
 hipError_t mlp2_fwd(const Mlp2Args& a, hipStream_t st);
 hipError_t mlp2_bwd(const Mlp2Args& a, hipStream_t st);
 hipError_t mlp2_step(unsigned int* step, hipStream_t st);

@@ -42,7 +42,8 @@ __device__ __forceinline__ float block_sum(float v, float* red) {
 }
 }  // namespace
 
-__global__ __launch_bounds__(256) void mlp2_fwd_kernel(Mlp2Args a) {
+__global__ __launch_bounds__(256) void mlp2_fwd_kernel(Mlp2Args a, GroupArg ga) {
+  gshift(a, goff(ga));
   extern __shared__ float sh[];
   float* s_x = sh;               // [D0] dropped input
   float* s_h = s_x + a.D0;       // [D1] dropped hidden
@@ -89,7 +90,8 @@ __global__ __launch_bounds__(256) void mlp2_fwd_kernel(Mlp2Args a) {
   atomicAdd(a.loss, lsum * a.loss_scale);
 }
 
-__global__ __launch_bounds__(256) void mlp2_bwd_kernel(Mlp2Args a) {
+__global__ __launch_bounds__(256) void mlp2_bwd_kernel(Mlp2Args a, GroupArg ga) {
+  gshift(a, goff(ga));
   extern __shared__ float sh[];
   float* s_x = sh;               // [D0] dropped input (recomputed)
   float* s_dh = s_x + a.D0;      // [D1] gradient at the hidden pre-activation
@@ -128,22 +130,22 @@ __global__ __launch_bounds__(256) void mlp2_bwd_kernel(Mlp2Args a) {
   }
 }
 
-__global__ void mlp2_step_kernel(unsigned int* step) { step[0] += 1u; }
+__global__ void mlp2_step_kernel(unsigned int* step, GroupArg ga) { gsh(step, goff(ga))[0] += 1u; }
 
 hipError_t mlp2_fwd(const Mlp2Args& a, hipStream_t st) {
   if (a.N == 0) return hipSuccess;
-  hipLaunchKernelGGL(mlp2_fwd_kernel, dim3(a.N), dim3(256), (a.D0 + a.D1 + 4) * 4, st, a);
+  hipLaunchKernelGGL(mlp2_fwd_kernel, ggrid(a.N), dim3(256), (a.D0 + a.D1 + 4) * 4, st, a, garg());
   return hipGetLastError();
 }
 
 hipError_t mlp2_bwd(const Mlp2Args& a, hipStream_t st) {
   if (a.N == 0) return hipSuccess;
-  hipLaunchKernelGGL(mlp2_bwd_kernel, dim3(a.N), dim3(256), (a.D0 + 2 * a.D1) * 4, st, a);
+  hipLaunchKernelGGL(mlp2_bwd_kernel, ggrid(a.N), dim3(256), (a.D0 + 2 * a.D1) * 4, st, a, garg());
   return hipGetLastError();
 }
 
 hipError_t mlp2_step(unsigned int* step, hipStream_t st) {
-  hipLaunchKernelGGL(mlp2_step_kernel, dim3(1), dim3(1), 0, st, step);
+  hipLaunchKernelGGL(mlp2_step_kernel, ggrid(1), dim3(1), 0, st, step, garg());
   return hipGetLastError();
 }
 

@@ -23,6 +23,12 @@
 
 namespace idc {
 
+LaunchGroups& launch_groups() {
+  static thread_local LaunchGroups lg;
+  return lg;
+}
+
+
 namespace {
 
 struct ChunkMap {
@@ -142,8 +148,9 @@ __device__ __forceinline__ void chunk_reduce(const ChunkMap& cm, int C, const fl
 // all of its loads before any arithmetic (RU independent 16-B loads in flight per operand), with
 // the destination type / accumulate mode as template parameters so the loop is branch-free.
 template <bool F32, bool ACC>
-__global__ __launch_bounds__(256) void bn_bwd_apply_kernel(BnBwdApplyArgs a) {
-  prefetch_kernargs<sizeof(BnBwdApplyArgs)>();
+__global__ __launch_bounds__(256) void bn_bwd_apply_kernel(BnBwdApplyArgs a, GroupArg ga) {
+  prefetch_kernargs<sizeof(BnBwdApplyArgs) + sizeof(GroupArg)>();
+  gshift(a, goff(ga));
   constexpr int RU = 4;
   extern __shared__ float sh[];
   float* sA = sh;
@@ -275,18 +282,19 @@ hipError_t bn_bwd_apply(const BnBwdApplyArgs& a, hipStream_t st) {
   dim3 grid(grid_rows(a.M, a.C, 4)), block(256);
   size_t shm = 3 * a.C * 4;
   if (a.dst_f32) {
-    if (a.accumulate) hipLaunchKernelGGL((bn_bwd_apply_kernel<true, true>), grid, block, shm, st, a);
-    else hipLaunchKernelGGL((bn_bwd_apply_kernel<true, false>), grid, block, shm, st, a);
+    if (a.accumulate) hipLaunchKernelGGL((bn_bwd_apply_kernel<true, true>), ggrid(grid), block, shm, st, a, garg());
+    else hipLaunchKernelGGL((bn_bwd_apply_kernel<true, false>), ggrid(grid), block, shm, st, a, garg());
   } else {
-    if (a.accumulate) hipLaunchKernelGGL((bn_bwd_apply_kernel<false, true>), grid, block, shm, st, a);
-    else hipLaunchKernelGGL((bn_bwd_apply_kernel<false, false>), grid, block, shm, st, a);
+    if (a.accumulate) hipLaunchKernelGGL((bn_bwd_apply_kernel<false, true>), ggrid(grid), block, shm, st, a, garg());
+    else hipLaunchKernelGGL((bn_bwd_apply_kernel<false, false>), ggrid(grid), block, shm, st, a, garg());
   }
   return hipGetLastError();
 }
 
 // ------------------------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(BnBwdReduceArgs a) {
-  prefetch_kernargs<sizeof(BnBwdReduceArgs)>();
+__global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(BnBwdReduceArgs a, GroupArg ga) {
+  prefetch_kernargs<sizeof(BnBwdReduceArgs) + sizeof(GroupArg)>();
+  gshift(a, goff(ga));
   extern __shared__ float sh[];
   float* s_sc = sh;
   float* s_sh = sh + a.C;
@@ -332,15 +340,16 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(BnBwdReduceArgs a) {
 
 hipError_t bn_bwd_reduce(const BnBwdReduceArgs& a, hipStream_t st) {
   if (a.M == 0) return hipSuccess;
-  hipLaunchKernelGGL(bn_bwd_reduce_kernel, dim3(grid_rows(a.M, a.C, 4)), dim3(256),
-                     (6 * a.C + 2 * 256 * 8) * 4, st, a);
+  hipLaunchKernelGGL(bn_bwd_reduce_kernel, ggrid(dim3(grid_rows(a.M, a.C, 4))), dim3(256),
+                     (6 * a.C + 2 * 256 * 8) * 4, st, a, garg());
   return hipGetLastError();
 }
 
 // ------------------------------------------------------------------------------------------
 template <bool IS_MAX, int K>
-__global__ __launch_bounds__(256) void pool_fwd_kernel(PoolArgs a) {
-  prefetch_kernargs<sizeof(PoolArgs)>();
+__global__ __launch_bounds__(256) void pool_fwd_kernel(PoolArgs a, GroupArg ga) {
+  prefetch_kernargs<sizeof(PoolArgs) + sizeof(GroupArg)>();
+  gshift(a, goff(ga));
   extern __shared__ float sh[];
   float* s_sc = sh;
   float* s_sh = sh + a.C;
@@ -441,9 +450,9 @@ static hipError_t pool_fwd(const PoolArgs& a, hipStream_t st) {
   // one output row per thread per pass: the k*k taps already give k*k loads in flight
   const dim3 grid(grid_rows(a.N * a.Ho * a.Wo, a.C, 1)), block(256);
   const size_t shm = (4 * a.C + 2 * 256 * 8) * 4;
-  if (a.k == 3) hipLaunchKernelGGL((pool_fwd_kernel<IS_MAX, 3>), grid, block, shm, st, a);
-  else if (a.k == 2) hipLaunchKernelGGL((pool_fwd_kernel<IS_MAX, 2>), grid, block, shm, st, a);
-  else hipLaunchKernelGGL((pool_fwd_kernel<IS_MAX, 0>), grid, block, shm, st, a);
+  if (a.k == 3) hipLaunchKernelGGL((pool_fwd_kernel<IS_MAX, 3>), ggrid(grid), block, shm, st, a, garg());
+  else if (a.k == 2) hipLaunchKernelGGL((pool_fwd_kernel<IS_MAX, 2>), ggrid(grid), block, shm, st, a, garg());
+  else hipLaunchKernelGGL((pool_fwd_kernel<IS_MAX, 0>), ggrid(grid), block, shm, st, a, garg());
   return hipGetLastError();
 }
 
@@ -457,8 +466,9 @@ hipError_t avgpool_fwd(const PoolArgs& a, hipStream_t st) { return pool_fwd<fals
 // k <= 2s): the window loop is unrolled and predicated, and each thread issues the loads of RU
 // rows (every window's dy / argmax, and x) before any arithmetic.
 template <int WIN, int RU>
-__global__ __launch_bounds__(256) void pool_bwd_kernel(PoolBwdArgs a) {
-  prefetch_kernargs<sizeof(PoolBwdArgs)>();
+__global__ __launch_bounds__(256) void pool_bwd_kernel(PoolBwdArgs a, GroupArg ga) {
+  prefetch_kernargs<sizeof(PoolBwdArgs) + sizeof(GroupArg)>();
+  gshift(a, goff(ga));
   extern __shared__ float sh[];
   float* s_sc = sh;
   float* s_sh = sh + a.C;
@@ -606,8 +616,9 @@ __global__ __launch_bounds__(256) void pool_bwd_kernel(PoolBwdArgs a) {
 // exactly as the gather form.  Used for the VGG16 max pools (no epilogue) and the DenseNet
 // transition average pools (BN epilogue, fp32 concat-gradient output).
 template <bool AVG, bool EPI>
-__global__ __launch_bounds__(256) void pool_bwd_scatter_kernel(PoolBwdArgs a) {
-  prefetch_kernargs<sizeof(PoolBwdArgs)>();
+__global__ __launch_bounds__(256) void pool_bwd_scatter_kernel(PoolBwdArgs a, GroupArg ga) {
+  prefetch_kernargs<sizeof(PoolBwdArgs) + sizeof(GroupArg)>();
+  gshift(a, goff(ga));
   extern __shared__ float sh[];
   float* s_sc = sh;
   float* s_sh = sh + a.C;
@@ -725,11 +736,11 @@ hipError_t pool_bwd(const PoolBwdArgs& a, hipStream_t st) {
     const bool epi = a.bn.mode != 0 || a.bn.act != ACT_NONE;
     const size_t shm_s = epi ? (9 * (size_t)a.C + 2 * 256 * 8) * 4 : 0;
     if (a.is_avg) {
-      if (epi) hipLaunchKernelGGL((pool_bwd_scatter_kernel<true, true>), dim3((int)blocks), dim3(256), shm_s, st, a);
-      else hipLaunchKernelGGL((pool_bwd_scatter_kernel<true, false>), dim3((int)blocks), dim3(256), shm_s, st, a);
+      if (epi) hipLaunchKernelGGL((pool_bwd_scatter_kernel<true, true>), ggrid((int)blocks), dim3(256), shm_s, st, a, garg());
+      else hipLaunchKernelGGL((pool_bwd_scatter_kernel<true, false>), ggrid((int)blocks), dim3(256), shm_s, st, a, garg());
     } else {
-      if (epi) hipLaunchKernelGGL((pool_bwd_scatter_kernel<false, true>), dim3((int)blocks), dim3(256), shm_s, st, a);
-      else hipLaunchKernelGGL((pool_bwd_scatter_kernel<false, false>), dim3((int)blocks), dim3(256), shm_s, st, a);
+      if (epi) hipLaunchKernelGGL((pool_bwd_scatter_kernel<false, true>), ggrid((int)blocks), dim3(256), shm_s, st, a, garg());
+      else hipLaunchKernelGGL((pool_bwd_scatter_kernel<false, false>), ggrid((int)blocks), dim3(256), shm_s, st, a, garg());
     }
     return hipGetLastError();
   }
@@ -737,9 +748,9 @@ hipError_t pool_bwd(const PoolBwdArgs& a, hipStream_t st) {
   const size_t shm = (9 * a.C + 2 * 256 * 8) * 4;
   const int M = a.N * a.H * a.W;
   if (a.k <= a.s) {
-    hipLaunchKernelGGL((pool_bwd_kernel<1, 4>), dim3(grid_rows(M, a.C, 4)), dim3(256), shm, st, a);
+    hipLaunchKernelGGL((pool_bwd_kernel<1, 4>), ggrid(dim3(grid_rows(M, a.C, 4))), dim3(256), shm, st, a, garg());
   } else if (a.k <= 2 * a.s) {
-    hipLaunchKernelGGL((pool_bwd_kernel<2, 2>), dim3(grid_rows(M, a.C, 2)), dim3(256), shm, st, a);
+    hipLaunchKernelGGL((pool_bwd_kernel<2, 2>), ggrid(dim3(grid_rows(M, a.C, 2))), dim3(256), shm, st, a, garg());
   } else {
     return hipErrorInvalidValue;  // windows overlapping more than 2 per dim: not used by any model
   }
@@ -747,8 +758,10 @@ hipError_t pool_bwd(const PoolBwdArgs& a, hipStream_t st) {
 }
 
 // ------------------------------------------------------------------------------------------
-__global__ void bn_update_moving_kernel(const BnMovingDesc* d, int n) {
-  const BnMovingDesc& b = d[blockIdx.y];
+__global__ void bn_update_moving_kernel(const BnMovingDesc* d, int n, GroupArg ga) {
+  const long long go = goff(ga);
+  BnMovingDesc b = gsh(d, go)[blockIdx.y];
+  gshift(b, go);
   for (int c = blockIdx.x * blockDim.x + threadIdx.x; c < b.C; c += gridDim.x * blockDim.x) {
     float s0 = 0.f, s1 = 0.f;
     for (int s = 0; s < stat_slots(b.slots); ++s) {
@@ -765,8 +778,10 @@ __global__ void bn_update_moving_kernel(const BnMovingDesc* d, int n) {
 
 // after the backward: every statistics array's shift becomes this step's batch mean (the next
 // step's producers accumulate around it, common.h "Shifted statistics")
-__global__ void stats_shift_kernel(const ShiftDesc* d, int n) {
-  const ShiftDesc& b = d[blockIdx.y];
+__global__ void stats_shift_kernel(const ShiftDesc* d, int n, GroupArg ga) {
+  const long long go = goff(ga);
+  ShiftDesc b = gsh(d, go)[blockIdx.y];
+  gshift(b, go);
   for (int c = blockIdx.x * blockDim.x + threadIdx.x; c < b.ld; c += gridDim.x * blockDim.x) {
     float s0 = 0.f;
     for (int s = 0; s < stat_slots(b.slots); ++s) s0 += b.stats[(size_t)s * 2 * b.ld + c];
@@ -778,21 +793,22 @@ __global__ void stats_shift_kernel(const ShiftDesc* d, int n) {
 
 hipError_t stats_shift(const ShiftDesc* d, int n, int maxC, hipStream_t st) {
   if (n == 0) return hipSuccess;
-  hipLaunchKernelGGL(stats_shift_kernel, dim3((maxC + 255) / 256, n), dim3(256), 0, st, d, n);
+  hipLaunchKernelGGL(stats_shift_kernel, ggrid(dim3((maxC + 255) / 256, n)), dim3(256), 0, st, d, n, garg());
   return hipGetLastError();
 }
 
 hipError_t bn_update_moving(const BnMovingDesc* d, int n, int maxC, hipStream_t st) {
   if (n == 0) return hipSuccess;
   dim3 grid((maxC + 255) / 256, n);
-  hipLaunchKernelGGL(bn_update_moving_kernel, grid, dim3(256), 0, st, d, n);
+  hipLaunchKernelGGL(bn_update_moving_kernel, ggrid(grid), dim3(256), 0, st, d, n, garg());
   return hipGetLastError();
 }
 
 // ------------------------------------------------------------------------------------------
 // head forward: one block per sample
-__global__ __launch_bounds__(256) void head_fwd_kernel(HeadArgs a) {
-  prefetch_kernargs<sizeof(HeadArgs)>();
+__global__ __launch_bounds__(256) void head_fwd_kernel(HeadArgs a, GroupArg ga) {
+  prefetch_kernargs<sizeof(HeadArgs) + sizeof(GroupArg)>();
+  gshift(a, goff(ga));
   extern __shared__ float sh[];
   float* s_feat = sh;            // [C]
   float* s_red = sh + a.C;       // [U][4 waves]
@@ -854,7 +870,7 @@ __global__ __launch_bounds__(256) void head_fwd_kernel(HeadArgs a) {
 }
 
 hipError_t head_fwd(const HeadArgs& a, hipStream_t st) {
-  hipLaunchKernelGGL(head_fwd_kernel, dim3(a.N), dim3(256), (a.C + 4 * a.U) * 4, st, a);
+  hipLaunchKernelGGL(head_fwd_kernel, ggrid(a.N), dim3(256), (a.C + 4 * a.U) * 4, st, a, garg());
   return hipGetLastError();
 }
 
@@ -864,8 +880,9 @@ hipError_t head_fwd(const HeadArgs& a, hipStream_t st) {
 // the pixels with 4 loads/stores in flight per lane.  (One block per channel slice — the old
 // form — left 16 blocks looping over all 256 samples: ~50 us for a 1 us job.)
 template <int HB>
-__global__ __launch_bounds__(256) void head_bwd_kernel(HeadBwdArgs a) {
-  prefetch_kernargs<sizeof(HeadBwdArgs)>();
+__global__ __launch_bounds__(256) void head_bwd_kernel(HeadBwdArgs a, GroupArg ga) {
+  prefetch_kernargs<sizeof(HeadBwdArgs) + sizeof(GroupArg)>();
+  gshift(a, goff(ga));
   __shared__ float s_dw[4][64][17];
   __shared__ float s_dl[HB][16];
   const int c0 = blockIdx.x * 64;
@@ -928,7 +945,7 @@ hipError_t head_bwd(const HeadBwdArgs& a, hipStream_t st) {
   if (a.U > 16) return hipErrorInvalidValue;
   constexpr int HB = 16;
   dim3 grid((a.C + 63) / 64, a.det ? 1 : (a.N + HB - 1) / HB);
-  hipLaunchKernelGGL(head_bwd_kernel<HB>, grid, dim3(256), 0, st, a);
+  hipLaunchKernelGGL(head_bwd_kernel<HB>, ggrid(grid), dim3(256), 0, st, a, garg());
   return hipGetLastError();
 }
 
@@ -936,7 +953,11 @@ hipError_t head_bwd(const HeadBwdArgs& a, hipStream_t st) {
 __global__ __launch_bounds__(256) void rmsprop_kernel(float* __restrict__ w, const float* __restrict__ g,
                                                       float* __restrict__ ms, long long n4, float lr,
                                                       float rho, float eps, float gs,
-                                                      const int* __restrict__ skip) {
+                                                      const int* __restrict__ skip, GroupArg ga) {
+  {
+    const long long go = goff(ga);
+    w = gsh(w, go); g = gsh(g, go); ms = gsh(ms, go); skip = gsh(skip, go);
+  }
   if (skip && *skip) return;  // non-finite gradients this step: keep weights and slots unchanged
   for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n4;
        i += (long long)gridDim.x * blockDim.x) {
@@ -958,7 +979,8 @@ __global__ __launch_bounds__(256) void rmsprop_kernel(float* __restrict__ w, con
 
 // zero fill as a plain kernel: keeps graph segments free of memset nodes and lets the fill
 // overlap with nothing but its own stream order (16-B stores for the aligned body)
-__global__ __launch_bounds__(256) void zero_fill_kernel(unsigned char* __restrict__ p, long long nbytes) {
+__global__ __launch_bounds__(256) void zero_fill_kernel(unsigned char* __restrict__ p, long long nbytes, GroupArg ga) {
+  p = gsh(p, goff(ga));
   const long long n16 = nbytes >> 4;
   uint4* q = reinterpret_cast<uint4*>(p);
   const long long stride = (long long)gridDim.x * blockDim.x;
@@ -974,14 +996,16 @@ hipError_t zero_fill(void* p, long long nbytes, hipStream_t st) {
   long long blocks = ((nbytes >> 4) + 255) / 256;
   if (blocks > 4096) blocks = 4096;
   if (blocks < 1) blocks = 1;
-  hipLaunchKernelGGL(zero_fill_kernel, dim3((int)blocks), dim3(256), 0, st,
-                     reinterpret_cast<unsigned char*>(p), nbytes);
+  hipLaunchKernelGGL(zero_fill_kernel, ggrid((int)blocks), dim3(256), 0, st,
+                     reinterpret_cast<unsigned char*>(p), nbytes, garg());
   return hipGetLastError();
 }
 
 // any non-finite value in g[0:n) -> *flag = 1 (the flag is cleared at the start of backward)
 __global__ __launch_bounds__(256) void finite_check_kernel(const float* __restrict__ g, long long n4,
-                                                           int* __restrict__ flag) {
+                                                           int* __restrict__ flag, GroupArg ga) {
+  g = gsh(g, goff(ga));
+  flag = gsh(flag, goff(ga));
   int bad = 0;
   for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n4;
        i += (long long)gridDim.x * blockDim.x) {
@@ -996,18 +1020,20 @@ hipError_t finite_check(const float* g, long long n, int* flag, hipStream_t st) 
   long long blocks = (n4 + 255) / 256;
   if (blocks > 2048) blocks = 2048;
   if (blocks < 1) blocks = 1;
-  hipLaunchKernelGGL(finite_check_kernel, dim3((int)blocks), dim3(256), 0, st, g, n4, flag);
+  hipLaunchKernelGGL(finite_check_kernel, ggrid((int)blocks), dim3(256), 0, st, g, n4, flag, garg());
   return hipGetLastError();
 }
 
-__global__ void finite_flag_reset_kernel(int* flag, int* status) {
+__global__ void finite_flag_reset_kernel(int* flag, int* status, GroupArg ga) {
+  flag = gsh(flag, goff(ga));
+  status = gsh(status, goff(ga));
   status[0] = flag[0];
   status[1] += flag[0];  // running count of skipped steps
   flag[0] = 0;
 }
 
 hipError_t finite_flag_reset(int* flag, int* status, hipStream_t st) {
-  hipLaunchKernelGGL(finite_flag_reset_kernel, dim3(1), dim3(1), 0, st, flag, status);
+  hipLaunchKernelGGL(finite_flag_reset_kernel, ggrid(1), dim3(1), 0, st, flag, status, garg());
   return hipGetLastError();
 }
 
@@ -1017,8 +1043,8 @@ hipError_t rmsprop(float* w, const float* g, float* ms, long long n, float lr, f
   long long blocks = (n4 + 255) / 256;
   if (blocks > 8192) blocks = 8192;
   if (blocks < 1) blocks = 1;
-  hipLaunchKernelGGL(rmsprop_kernel, dim3((int)blocks), dim3(256), 0, st, w, g, ms, n4, lr, rho, eps,
-                     grad_scale, skip);
+  hipLaunchKernelGGL(rmsprop_kernel, ggrid((int)blocks), dim3(256), 0, st, w, g, ms, n4, lr, rho, eps,
+                     grad_scale, skip, garg());
   return hipGetLastError();
 }
 
@@ -1032,10 +1058,14 @@ hipError_t rmsprop(float* w, const float* g, float* ms, long long n, float lr, f
 // first tile), so there is no per-element search and every global access is coalesced.
 __global__ __launch_bounds__(256) void cast_weights_kernel(const CastEntry* __restrict__ es,
                                                            const int* __restrict__ tile_entry,
-                                                           long long ntiles) {
+                                                           long long ntiles, GroupArg ga) {
   __shared__ float tile[64][65];
+  const long long go = goff(ga);
+  es = gsh(es, go);
+  tile_entry = gsh(tile_entry, go);
   for (long long b = blockIdx.x; b < ntiles; b += gridDim.x) {
-    const CastEntry& e = es[tile_entry[b]];
+    CastEntry e = es[tile_entry[b]];
+    gshift(e, go);
     const int R = e.KH * e.KW * e.Cin;
     const int tiles_c = (e.Cout + 63) / 64;
     const long long lt = b - e.begin;
@@ -1090,13 +1120,15 @@ __global__ __launch_bounds__(256) void cast_weights_kernel(const CastEntry* __re
 hipError_t cast_weights(const CastEntry* d_entries, const int* tile_entry, long long ntiles, hipStream_t st) {
   if (d_entries == nullptr || ntiles == 0) return hipSuccess;
   long long blocks = ntiles < 8192 ? ntiles : 8192;
-  hipLaunchKernelGGL(cast_weights_kernel, dim3((int)blocks), dim3(256), 0, st, d_entries, tile_entry, ntiles);
+  hipLaunchKernelGGL(cast_weights_kernel, ggrid((int)blocks), dim3(256), 0, st, d_entries, tile_entry, ntiles, garg());
   return hipGetLastError();
 }
 
 // ------------------------------------------------------------------------------------------
 __global__ __launch_bounds__(256) void input_stage_kernel(const void* x, int u8, long long npix, int C,
-                                                          bf16_t* y, int Cpad) {
+                                                          bf16_t* y, int Cpad, GroupArg ga) {
+  x = gsh(x, goff(ga));
+  y = gsh(y, goff(ga));
   for (long long p = blockIdx.x * (long long)blockDim.x + threadIdx.x; p < npix;
        p += (long long)gridDim.x * blockDim.x) {
     float v[8] = {0, 0, 0, 0, 0, 0, 0, 0};
@@ -1116,14 +1148,16 @@ hipError_t input_stage(const void* x, int x_u8, int N, int H, int W, int C, bf16
   long long npix = (long long)N * H * W;
   long long blocks = (npix + 255) / 256;
   if (blocks > 4096) blocks = 4096;
-  hipLaunchKernelGGL(input_stage_kernel, dim3((int)blocks), dim3(256), 0, st, x, x_u8, npix, C, y, Cpad);
+  hipLaunchKernelGGL(input_stage_kernel, ggrid((int)blocks), dim3(256), 0, st, x, x_u8, npix, C, y, Cpad, garg());
   return hipGetLastError();
 }
 
 // ------------------------------------------------------------------------------------------
 __global__ __launch_bounds__(256) void bn_stats_kernel(const bf16_t* x, int ldx, int M, int C,
                                                        float* stats, int stats_ld, int stats_off,
-                                                       int stats_slots) {
+                                                       int stats_slots, GroupArg ga) {
+  x = gsh(x, goff(ga));
+  stats = gsh(stats, goff(ga));
   extern __shared__ float sh[];
   float* s_a = sh;
   float* s_b = sh + C;
@@ -1148,15 +1182,19 @@ __global__ __launch_bounds__(256) void bn_stats_kernel(const bf16_t* x, int ldx,
 
 hipError_t bn_stats(const bf16_t* x, int ldx, int M, int C, float* stats, int stats_ld, int stats_off,
                     int stats_slots, hipStream_t st) {
-  hipLaunchKernelGGL(bn_stats_kernel, dim3(grid_rows(M, C, 16)), dim3(256), 2 * C * 4, st, x, ldx, M, C,
-                     stats, stats_ld, stats_off, stats_slots);
+  hipLaunchKernelGGL(bn_stats_kernel, ggrid(dim3(grid_rows(M, C, 16))), dim3(256), 2 * C * 4, st, x, ldx, M, C,
+                     stats, stats_ld, stats_off, stats_slots, garg());
   return hipGetLastError();
 }
 
 // y = act(bn(x)) [+ res]; optional stats of y  (MobileNetV2 block outputs, eval paths)
 __global__ __launch_bounds__(256) void bn_apply_kernel(const bf16_t* x, int ldx, BnArgs bn, const bf16_t* res,
                                                        int ldres, bf16_t* y, int ldy, int M, int C,
-                                                       float* stats, int stats_ld, int stats_slots) {
+                                                       float* stats, int stats_ld, int stats_slots, GroupArg ga) {
+  {
+    const long long go = goff(ga);
+    x = gsh(x, go); gshift(bn, go); res = gsh(res, go); y = gsh(y, go); stats = gsh(stats, go);
+  }
   extern __shared__ float sh[];
   float* s_sc = sh;
   float* s_sh = sh + C;
@@ -1203,8 +1241,8 @@ __global__ __launch_bounds__(256) void bn_apply_kernel(const bf16_t* x, int ldx,
 
 hipError_t bn_apply(const bf16_t* x, int ldx, BnArgs bn, const bf16_t* res, int ldres, bf16_t* y, int ldy,
                     int M, int C, float* stats, int stats_ld, int stats_slots, hipStream_t st) {
-  hipLaunchKernelGGL(bn_apply_kernel, dim3(grid_rows(M, C)), dim3(256), 4 * C * 4, st, x, ldx, bn, res, ldres,
-                     y, ldy, M, C, stats, stats_ld, stats_slots);
+  hipLaunchKernelGGL(bn_apply_kernel, ggrid(dim3(grid_rows(M, C))), dim3(256), 4 * C * 4, st, x, ldx, bn, res, ldres,
+                     y, ldy, M, C, stats, stats_ld, stats_slots, garg());
   return hipGetLastError();
 }
 
@@ -1213,7 +1251,11 @@ hipError_t bn_apply(const bf16_t* x, int ldx, BnArgs bn, const bf16_t* res, int 
 // of channel tx, then the 8 partials are added in ty order — the same bits every run (the
 // deterministic mode folds every producer's per-workgroup slots through here).
 __global__ __launch_bounds__(256) void slot_collapse_kernel(const float* src, float* dst, const float* src2,
-                                                            float* dst2, int slots, int ld, int C) {
+                                                            float* dst2, int slots, int ld, int C, GroupArg ga) {
+  {
+    const long long go = goff(ga);
+    src = gsh(src, go); dst = gsh(dst, go); src2 = gsh(src2, go); dst2 = gsh(dst2, go);
+  }
   __shared__ float sa[8][33], sb[8][33];
   const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;
   const int c = blockIdx.x * 32 + tx;
@@ -1244,8 +1286,8 @@ hipError_t slot_collapse(const float* src, float* dst, const float* src2, float*
   if (C <= 0) return hipSuccess;
   if (src == nullptr || dst == nullptr || (src2 == nullptr) != (dst2 == nullptr) || slots < 1 || ld < C)
     return hipErrorInvalidValue;
-  hipLaunchKernelGGL(slot_collapse_kernel, dim3((C + 31) / 32), dim3(256), 0, st, src, dst, src2, dst2, slots,
-                     ld, C);
+  hipLaunchKernelGGL(slot_collapse_kernel, ggrid(dim3((C + 31) / 32)), dim3(256), 0, st, src, dst, src2, dst2, slots,
+                     ld, C, garg());
   return hipGetLastError();
 }
 

@@ -30,9 +30,9 @@ __device__ __forceinline__ uint32_t philox(uint32_t c0, uint32_t c1, uint32_t c2
   return c0;
 }
 
-// segment of element i (seg_end ascending, seg_end[nseg-1] == n)
-__device__ __forceinline__ int segment_of(long long i, const long long* seg_end, int nseg) {
-  int lo = 0, hi = nseg - 1;
+// segment of element i at or after segment `from` (seg_end ascending, seg_end[nseg-1] == n)
+__device__ __forceinline__ int segment_from(long long i, const long long* seg_end, int from, int nseg) {
+  int lo = from, hi = nseg - 1;
   while (lo < hi) {
     const int mid = (lo + hi) >> 1;
     if (i < seg_end[mid]) hi = mid;
@@ -41,21 +41,26 @@ __device__ __forceinline__ int segment_of(long long i, const long long* seg_end,
   return lo;
 }
 
+// Grid-stride over elements: consecutive lanes own consecutive elements, so every load and store
+// is one coalesced 256-B wave access.  A thread's index only grows, so its segment index only moves
+// forward: it is re-searched (binary, from the current segment) only when the element leaves it.
 __global__ __launch_bounds__(256) void secagg_mask_kernel(const float* __restrict__ x, uint32_t* __restrict__ out,
                                                           long long n, const float* __restrict__ seg_scale,
                                                           const long long* __restrict__ seg_end, int nseg,
                                                           float clip, int K, int rank,
                                                           const uint32_t* __restrict__ keys, unsigned long long rnd,
                                                           unsigned long long alive) {
-  // a thread owns a contiguous run of elements: its segment search is done once per run
-  const long long per = (n + (long long)gridDim.x * blockDim.x - 1) / ((long long)gridDim.x * blockDim.x);
-  const long long i0 = (blockIdx.x * (long long)blockDim.x + threadIdx.x) * per;
-  if (i0 >= n) return;
-  const long long i1 = i0 + per < n ? i0 + per : n;
-  int s = segment_of(i0, seg_end, nseg);
-  for (long long i = i0; i < i1; ++i) {
-    while (i >= seg_end[s]) ++s;
-    float v = x[i] * seg_scale[s];
+  const long long stride = (long long)gridDim.x * blockDim.x;
+  long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  int s = segment_from(i, seg_end, 0, nseg);
+  float sc = seg_scale[s];
+  for (; i < n; i += stride) {
+    if (i >= seg_end[s]) {
+      s = segment_from(i, seg_end, s, nseg);
+      sc = seg_scale[s];
+    }
+    float v = x[i] * sc;
     v = fminf(fmaxf(v, -clip), clip);
     uint32_t acc = (uint32_t)(int32_t)rintf(v);
     for (int j = 0; j < K; ++j) {
@@ -72,15 +77,14 @@ __global__ __launch_bounds__(256) void secagg_unmask_kernel(const uint32_t* __re
                                                             long long n, const float* __restrict__ seg_scale,
                                                             const long long* __restrict__ seg_end, int nseg,
                                                             float divisor) {
-  const long long per = (n + (long long)gridDim.x * blockDim.x - 1) / ((long long)gridDim.x * blockDim.x);
-  const long long i0 = (blockIdx.x * (long long)blockDim.x + threadIdx.x) * per;
-  if (i0 >= n) return;
-  const long long i1 = i0 + per < n ? i0 + per : n;
-  int g = segment_of(i0, seg_end, nseg);
+  const long long stride = (long long)gridDim.x * blockDim.x;
+  long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  int g = segment_from(i, seg_end, 0, nseg);
   float inv = 1.f / (seg_scale[g] * divisor);
-  for (long long i = i0; i < i1; ++i) {
-    while (i >= seg_end[g]) {
-      ++g;
+  for (; i < n; i += stride) {
+    if (i >= seg_end[g]) {
+      g = segment_from(i, seg_end, g, nseg);
       inv = 1.f / (seg_scale[g] * divisor);
     }
     out[i] = (float)(int32_t)s[i] * inv;

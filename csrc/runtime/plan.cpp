@@ -37,6 +37,7 @@
 #include "../kernels/mlp_head.h"
 #include "../kernels/nn_kernels.h"
 #include "../kernels/secagg.h"
+#include "../comm/communicator.h"
 
 namespace py = pybind11;
 using namespace idc;
@@ -70,6 +71,9 @@ enum OpKind : int {
   OP_MLP_STEP = 23,
   OP_COLLAPSE = 24,
   OP_STATS_SHIFT = 25,
+  // gradient-bucket all-reduce on the communicator's stream (the "comm lane"): p[0] buffer,
+  // l[0] element count, i[0] dtype code, i[1] reduction op (csrc/comm/communicator.h)
+  OP_ALLREDUCE = 26,
 };
 
 struct Op {
@@ -99,7 +103,19 @@ class Plan {
     if (fork_) hipEventDestroy(fork_);
     if (join_) hipEventDestroy(join_);
     if (mark_) hipEventDestroy(mark_);
+    if (cfork_) hipEventDestroy(cfork_);
+    if (cjoin_) hipEventDestroy(cjoin_);
     if (side_) hipStreamDestroy(side_);
+  }
+
+  // attach the communicator whose stream runs this plan's OP_ALLREDUCE ops (kept alive by the
+  // Python binding for as long as the plan)
+  void set_comm(Communicator* c) { comm_ = c; }
+  bool has_comm_ops(int begin, int end) const {
+    if (end < 0 || end > (int)ops_.size()) end = (int)ops_.size();
+    for (int k = begin; k < end; ++k)
+      if (ops_[k].kind == OP_ALLREDUCE) return true;
+    return false;
   }
 
   int add(int kind, py::bytes payload, std::vector<int> ints, std::vector<float> floats,
@@ -141,6 +157,15 @@ class Plan {
     if (end < 0 || end > (int)ops_.size()) end = (int)ops_.size();
     issue(begin, end, st, join);
   }
+
+  // Grouped execution (csrc/kernels/common.h GroupArg): every launch of this plan runs `k` copies
+  // of the program whose buffers sit `stride` bytes apart (client-batched federated training).
+  void set_groups(int k, long long stride) {
+    if (k < 1 || (k > 1 && stride <= 0)) throw std::runtime_error("set_groups: bad group count / stride");
+    groups_ = k;
+    gstride_ = k > 1 ? stride : 0;
+  }
+  int groups() const { return groups_; }
 
   // make `stream` wait for every side-lane op issued so far (event record on the side lane)
   void wait_side(uintptr_t stream) {
@@ -191,6 +216,8 @@ class Plan {
     hipStream_t st = reinterpret_cast<hipStream_t>(stream);
     if (end < 0 || end > (int)ops_.size()) end = (int)ops_.size();
     ensure_side();
+    if (has_comm_ops(begin, end)) throw std::runtime_error("capture_dual: range holds collectives; use capture()");
+    GroupScope gscope(groups_, gstride_);
     Dual d;
     std::vector<std::vector<int>> batches;
     auto abort_capture = [](hipStream_t s) {
@@ -313,9 +340,9 @@ class Plan {
                                   "pool_bwd", "bn_moving", "head_fwd", "head_bwd", "rmsprop", "cast",
                                   "input", "memset", "bn_stats", "bn_apply", "dw_fwd", "dw_bwd_data",
                                   "dw_wgrad", "copy", "finite_check", "mlp_fwd", "mlp_bwd", "mlp_step",
-                                  "collapse", "stats_shift"};
+                                  "collapse", "stats_shift", "allreduce"};
     int k = ops_.at(idx).kind;
-    return (k >= 0 && k < 26) ? names[k] : "?";
+    return (k >= 0 && k < 27) ? names[k] : "?";
   }
 
  private:
@@ -340,7 +367,18 @@ class Plan {
   // precede the fork, and the lowering guarantees no later main op overwrites a side op's
   // inputs, so deferring is safe) — and one join at the end.  Batching keeps the host API calls
   // per step low: with direct (non-graph) issue the backward is otherwise host-bound.
+  // sets the launch-group context of the calling thread for the lifetime of one issue()
+  struct GroupScope {
+    LaunchGroups saved;
+    GroupScope(int k, long long stride) : saved(launch_groups()) {
+      launch_groups().k = k;
+      launch_groups().stride = stride;
+    }
+    ~GroupScope() { launch_groups() = saved; }
+  };
+
   void issue(int begin, int end, hipStream_t st, bool join = true) {
+    GroupScope gscope(groups_, gstride_);
     bool side_used = false;
     std::vector<int> pending;
     int main_since = 0;
@@ -353,8 +391,18 @@ class Plan {
       pending.clear();
       side_used = true;
     };
+    bool comm_used = false;
     for (int k = begin; k < end; ++k) {
       const Op& op = ops_[k];
+      if (op.kind == OP_ALLREDUCE) {
+        // a bucket's gradients are final once every main-lane op so far AND every side-lane op
+        // so far (weight gradients) has run: fork any pending side batch, then the comm stream
+        // waits on both lanes and enqueues the collective; the main lane runs on
+        flush();
+        issue_comm(op, st, side_used || side_open_);
+        comm_used = true;
+        continue;
+      }
       if (op.lane == 1) {
         if (pending.empty()) main_since = 0;
         pending.push_back(k);
@@ -372,6 +420,30 @@ class Plan {
     } else if (side_used) {
       side_open_ = true;
     }
+    if ((comm_used || comm_open_) && join) {
+      check(hipEventRecord(cjoin_, comm_->stream()), "hipEventRecord(comm join)");
+      check(hipStreamWaitEvent(st, cjoin_, 0), "hipStreamWaitEvent(comm join)");
+      comm_open_ = false;
+    } else if (comm_used) {
+      comm_open_ = true;
+    }
+  }
+
+  void issue_comm(const Op& op, hipStream_t st, bool side_active) {
+    if (!comm_) throw std::runtime_error("plan: OP_ALLREDUCE without a communicator (set_comm)");
+    if (groups_ > 1) throw std::runtime_error("plan: collectives inside a grouped plan");
+    if (!cfork_) {
+      check(hipEventCreateWithFlags(&cfork_, hipEventDisableTiming), "hipEventCreate(comm fork)");
+      check(hipEventCreateWithFlags(&cjoin_, hipEventDisableTiming), "hipEventCreate(comm join)");
+    }
+    hipStream_t cs = comm_->stream();
+    check(hipEventRecord(cfork_, st), "hipEventRecord(comm fork)");
+    check(hipStreamWaitEvent(cs, cfork_, 0), "hipStreamWaitEvent(comm fork)");
+    if (side_active) {
+      check(hipEventRecord(mark_, side_), "hipEventRecord(side mark)");
+      check(hipStreamWaitEvent(cs, mark_, 0), "hipStreamWaitEvent(side mark)");
+    }
+    comm_->all_reduce(reinterpret_cast<void*>(op.p[0]), op.l[0], op.i[0], op.i[1], cs);
   }
 
   void exec(const Op& op, hipStream_t st) {
@@ -458,10 +530,13 @@ class Plan {
         check(stats_shift(reinterpret_cast<const ShiftDesc*>(op.p[0]), op.i[0], op.i[1], st), "stats_shift");
         break;
       case OP_COPY:
-        check(hipMemcpyAsync(reinterpret_cast<void*>(op.p[0]), reinterpret_cast<const void*>(op.p[1]),
-                             (size_t)op.l[0], hipMemcpyDeviceToDevice, st),
-              "copy");
+        for (int g = 0; g < groups_; ++g)  // a copy engine transfer per program copy
+          check(hipMemcpyAsync(reinterpret_cast<void*>(op.p[0] + g * gstride_),
+                               reinterpret_cast<const void*>(op.p[1] + g * gstride_), (size_t)op.l[0],
+                               hipMemcpyDeviceToDevice, st),
+                "copy");
         break;
+      case OP_ALLREDUCE: throw std::runtime_error("OP_ALLREDUCE outside issue()");
       default: throw std::runtime_error("unknown op kind");
     }
   }
@@ -471,6 +546,11 @@ class Plan {
   int side_flush_ = 1;
   hipEvent_t fork_ = nullptr, join_ = nullptr, mark_ = nullptr;
   bool side_open_ = false;  // side-lane work issued by a join=false run, not yet joined
+  Communicator* comm_ = nullptr;
+  int groups_ = 1;
+  long long gstride_ = 0;
+  hipEvent_t cfork_ = nullptr, cjoin_ = nullptr;
+  bool comm_open_ = false;  // collectives issued by a join=false run, not yet joined
   std::vector<hipGraph_t> graphs_;
   std::vector<hipGraphExec_t> execs_;
   struct Dual {
@@ -597,8 +677,45 @@ void py_rmsprop(uintptr_t w, uintptr_t g, uintptr_t ms, long long n, float lr, f
 
 PYBIND11_MODULE(_idc_native, m) {
   m.doc() = "idc_models_amd native MI355X (gfx950) kernels and plan executor";
+  py::class_<Communicator>(m, "Communicator")
+      .def(py::init([](int rank, int world, py::bytes uid, int device) {
+             return new Communicator(rank, world, std::string(uid), device);
+           }),
+           py::arg("rank"), py::arg("world"), py::arg("unique_id"), py::arg("device"))
+      .def_static("make_unique_id", []() { return py::bytes(Communicator::make_unique_id()); })
+      .def("all_reduce", [](Communicator& c, uintptr_t buf, long long n, int dt, int op, uintptr_t st) {
+             c.all_reduce(reinterpret_cast<void*>(buf), n, dt, op, reinterpret_cast<hipStream_t>(st));
+           }, py::arg("buf"), py::arg("count"), py::arg("dtype"), py::arg("op"), py::arg("stream") = 0)
+      .def("reduce", [](Communicator& c, uintptr_t buf, long long n, int dt, int op, int root, uintptr_t st) {
+             c.reduce(reinterpret_cast<void*>(buf), n, dt, op, root, reinterpret_cast<hipStream_t>(st));
+           }, py::arg("buf"), py::arg("count"), py::arg("dtype"), py::arg("op"), py::arg("root"),
+           py::arg("stream") = 0)
+      .def("broadcast", [](Communicator& c, uintptr_t buf, long long n, int dt, int root, uintptr_t st) {
+             c.broadcast(reinterpret_cast<void*>(buf), n, dt, root, reinterpret_cast<hipStream_t>(st));
+           }, py::arg("buf"), py::arg("count"), py::arg("dtype"), py::arg("root"), py::arg("stream") = 0)
+      .def("all_gather", [](Communicator& c, uintptr_t send, uintptr_t recv, long long n, int dt, uintptr_t st) {
+             c.all_gather(reinterpret_cast<const void*>(send), reinterpret_cast<void*>(recv), n, dt,
+                          reinterpret_cast<hipStream_t>(st));
+           }, py::arg("send"), py::arg("recv"), py::arg("count_per_rank"), py::arg("dtype"), py::arg("stream") = 0)
+      .def("group_start", &Communicator::group_start)
+      .def("group_end", &Communicator::group_end)
+      .def("check_async", &Communicator::check_async)
+      .def("abort", &Communicator::abort)
+      .def("close", &Communicator::close)
+      .def_property_readonly("stream", [](const Communicator& c) { return reinterpret_cast<uintptr_t>(c.stream()); })
+      .def_property_readonly("rank", &Communicator::rank)
+      .def_property_readonly("world", &Communicator::world)
+      .def_property_readonly("device", &Communicator::device)
+      .def_property_readonly("is_open", &Communicator::open)
+      .def_property_readonly("collectives", &Communicator::collectives);
+  m.def("rccl_version", &rccl_version);
+  m.attr("OP_ALLREDUCE") = (int)OP_ALLREDUCE;
   py::class_<Plan>(m, "Plan")
       .def(py::init<>())
+      .def("set_comm", &Plan::set_comm, py::keep_alive<1, 2>())
+      .def("set_groups", &Plan::set_groups)
+      .def("groups", &Plan::groups)
+      .def("has_comm_ops", &Plan::has_comm_ops)
       .def("add", &Plan::add, py::arg("kind"), py::arg("payload"), py::arg("ints"), py::arg("floats"),
            py::arg("longs"), py::arg("ptrs"), py::arg("lane") = 0)
       .def("lane", &Plan::lane)

@@ -25,8 +25,8 @@ KERAS_VERSION = b"2.2.4-tf"
 
 def _h5():
     try:
-        from .. import _idc_h5
-        return _idc_h5
+        from ..utils.hostext import import_host_ext
+        return import_host_ext("_idc_h5")
     except ImportError:
         import sys
         root = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))

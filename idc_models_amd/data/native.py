@@ -36,7 +36,8 @@ def module():
             if pkg not in sys.path:
                 sys.path.insert(0, pkg)
             try:
-                _MOD = importlib.import_module("idc_models_amd._idc_data")
+                from ..utils.hostext import import_host_ext
+                _MOD = import_host_ext("_idc_data")
             except ImportError:
                 _MOD = None
     return _MOD

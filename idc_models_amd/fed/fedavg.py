@@ -94,6 +94,12 @@ def save_server_state(state: ServerState, path: str, extra: Optional[dict] = Non
     os.replace(tmp, path)
 
 
+def load_server_extra(path: str) -> dict:
+    """The ``extra`` dict saved with a server state (config fingerprint), without loading it."""
+    blob = torch.load(path, map_location="cpu", weights_only=True)
+    return dict(blob.get("extra", {}))
+
+
 def load_server_state(path: str, device=None) -> ServerState:
     blob = torch.load(path, map_location="cpu", weights_only=True)
     dev = torch.device(device) if device is not None else torch.device("cpu")
@@ -193,6 +199,28 @@ class FedAvgProcess:
             except BaseException as e:  # surfaced on the calling thread
                 errs.append(e)
 
+        # a worker whose program is not built yet builds (and autotunes) it on this thread, one
+        # worker at a time, with its first client: tile timings taken while another client's
+        # kernels share the GPU would be picked under contention
+        queues = [list(mine[w::W]) for w in range(W)]
+        for w in range(W):
+            if queues[w] and not getattr(models[w].impl, "progs", {1: 1}):
+                k = queues[w].pop(0)
+                out[k] = self._train_client(models[w], state, data[k])
+
+        def run_queue(w):
+            try:
+                with torch.cuda.device(dev):
+                    s = torch.cuda.Stream(dev)
+                    s.wait_stream(torch.cuda.default_stream(dev))
+                    with torch.cuda.stream(s):
+                        for k in queues[w]:
+                            out[k] = self._train_client(models[w], state, data[k])
+                    s.synchronize()
+            except BaseException as e:  # surfaced on the calling thread
+                errs.append(e)
+        run = run_queue
+
         torch.cuda.current_stream(dev).synchronize()  # server weights final before the workers read
         threads = [threading.Thread(target=run, args=(w,), daemon=True) for w in range(W)]
         for t in threads:
@@ -241,7 +269,11 @@ class FedAvgProcess:
         for k in mine:  # aggregation in client order, however the clients were scheduled
             flat, flat_ntr, n_k, logs = results[k]
             delta = flat - flat_server
-            finite = bool(torch.isfinite(delta).all())
+            # TFF gives a client weight 0 when its update is non-finite; the BatchNorm statistics
+            # that get averaged too (average_bn_stats) must be finite as well, or they would poison
+            # the mean (plain) or the masked segment ranges (secure)
+            finite = bool(torch.isfinite(delta).all()) and (
+                flat_ntr is None or ntr_sum is None or bool(torch.isfinite(flat_ntr).all()))
             if self.secure:
                 v = [n_k * delta] + ([n_k * flat_ntr] if ntr_sum is not None else [])
                 masked[k] = torch.cat(v) if finite else torch.zeros(sum(x.numel() for x in v), device=m.device)

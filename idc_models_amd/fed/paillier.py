@@ -28,7 +28,8 @@ def _native():
         _NATIVE = False
         if os.environ.get("IDC_NATIVE_PAILLIER", "1") != "0":
             try:
-                _NATIVE = importlib.import_module("idc_models_amd._idc_paillier")
+                from ..utils.hostext import import_host_ext
+                _NATIVE = import_host_ext("_idc_paillier")
             except ImportError:
                 _NATIVE = False
     return _NATIVE or None

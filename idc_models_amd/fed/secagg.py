@@ -105,7 +105,8 @@ def mask_quantize(x: torch.Tensor, scales, seg_end, nclients: int, rank: int, ke
         nat.require().secagg_mask(x.data_ptr(), out.data_ptr(), n, sc.data_ptr(), se.data_ptr(), len(seg_end),
                                   float(clip), int(nclients), int(rank), kt.data_ptr(), int(round_), alive,
                                   nat.stream_handle())
-        torch.cuda.current_stream().synchronize()  # the small tables above are freed on return
+        # no host sync: the small tables above were allocated on this stream, so the caching
+        # allocator hands their memory out again only to work ordered after this kernel
         return out
     sidx = _seg_index(n, seg_end)
     v = torch.clamp(x * torch.from_numpy(scales[sidx]), -clip, clip)
@@ -140,7 +141,6 @@ def unmask(total: torch.Tensor, scales, seg_end, divisor: float = 1.0) -> torch.
         se = torch.from_numpy(seg_end).to(dev)
         nat.require().secagg_unmask(total.data_ptr(), out.data_ptr(), n, sc.data_ptr(), se.data_ptr(),
                                     len(seg_end), float(divisor), nat.stream_handle())
-        torch.cuda.current_stream().synchronize()
         return out
     sidx = _seg_index(n, seg_end)
     return total.float() / (torch.from_numpy(scales[sidx]) * divisor)
@@ -158,7 +158,9 @@ def choose_scales(max_abs, nclients: int, headroom: float = 2.0) -> np.ndarray:
             out[i] = 2.0 ** 16
             continue
         s = (2 ** 31 - 1) / (nclients * v * headroom)
-        out[i] = 2.0 ** int(np.floor(np.log2(max(s, 1.0))))
+        # capped at 2^100: a tiny-but-nonzero segment (|x| < ~1e-29) would otherwise overflow the
+        # float32 scale to inf (0*inf = NaN in the kernel, and the decode divides by inf)
+        out[i] = 2.0 ** min(int(np.floor(np.log2(max(s, 1.0)))), 100)
     return out
 
 

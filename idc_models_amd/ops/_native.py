@@ -138,13 +138,15 @@ _STRUCTS = {"BnArgs": BnArgs, "BwdAff": BwdAff, "ConvArgs": ConvArgs, "WgradArgs
 OP_CONV, OP_WGRAD, OP_BN_BWD_APPLY, OP_BN_BWD_REDUCE, OP_MAXPOOL, OP_AVGPOOL, OP_POOL_BWD = range(7)
 OP_BN_MOVING, OP_HEAD_FWD, OP_HEAD_BWD, OP_RMSPROP, OP_CAST, OP_INPUT, OP_MEMSET = range(7, 14)
 OP_BN_STATS, OP_BN_APPLY, OP_DW_FWD, OP_DW_BWD_DATA, OP_DW_WGRAD, OP_COPY, OP_FINITE_CHECK = range(14, 21)
-OP_MLP_FWD, OP_MLP_BWD, OP_MLP_STEP, OP_COLLAPSE, OP_STATS_SHIFT = range(21, 26)
+OP_MLP_FWD, OP_MLP_BWD, OP_MLP_STEP, OP_COLLAPSE, OP_STATS_SHIFT, OP_ALLREDUCE = range(21, 27)
 
 ACT = {None: 0, "none": 0, "linear": 0, "relu": 1, "relu6": 2}
 OUT_BF16, OUT_F32, OUT_F32_ACC = 0, 1, 2
 
 
 def _verify(ext):
+    if ext.OP_ALLREDUCE != OP_ALLREDUCE:
+        raise RuntimeError("native op-kind table drifted (OP_ALLREDUCE)")
     sizes = ext.struct_sizes()
     for name, cls in _STRUCTS.items():
         if C.sizeof(cls) != sizes[name]:

@@ -20,13 +20,25 @@ def env_world() -> tuple:
             int(os.environ.get("LOCAL_RANK", os.environ.get("RANK", "0"))))
 
 
-def init_process_group(backend: Optional[str] = None, timeout_s: int = 600) -> tuple:
-    """Initialise the default group from the environment; returns (rank, world, local_rank)."""
+_FORCED = False  # collectives run even in a world of one (tests / benches of the comm path)
+
+
+def init_process_group(backend: Optional[str] = None, timeout_s: int = 600, force: bool = False) -> tuple:
+    """Initialise the default group from the environment; returns (rank, world, local_rank).
+
+    ``force``: create the group (and run every collective helper below for real) even when the
+    world has one rank, so the RCCL path can be exercised on a one-GPU machine."""
+    global _FORCED
     rank, world, local = env_world()
     os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
-    if world > 1 and not dist.is_initialized():
+    if force and world == 1:
+        _FORCED = True
+    if (world > 1 or force) and not dist.is_initialized():
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         os.environ.setdefault("MASTER_PORT", "29512")
+        os.environ.setdefault("RANK", str(rank))  # a forced world of one has no launcher env
+        os.environ.setdefault("WORLD_SIZE", str(world))
+        os.environ.setdefault("LOCAL_RANK", str(local))
         if backend is None:
             backend = "nccl" if torch.cuda.is_available() else "gloo"
         kw = {}
@@ -38,7 +50,19 @@ def init_process_group(backend: Optional[str] = None, timeout_s: int = 600) -> t
 
 
 def is_dist() -> bool:
-    return dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1
+    """True when collectives must run: a process group of more than one rank, or a forced one."""
+    return dist.is_available() and dist.is_initialized() and (dist.get_world_size() > 1 or _FORCED)
+
+
+def backend() -> Optional[str]:
+    return dist.get_backend() if dist.is_available() and dist.is_initialized() else None
+
+
+def destroy():
+    global _FORCED
+    if dist.is_available() and dist.is_initialized():
+        dist.destroy_process_group()
+    _FORCED = False
 
 
 def world_size() -> int:

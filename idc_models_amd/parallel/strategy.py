@@ -14,10 +14,17 @@ on MI355X the idiomatic form is one process per GPU over RCCL (SURVEY §2.3 D1/D
   convention; the dense script's ``256 * num_replicas`` global batch is the same thing.
 * ``CentralStorageStrategy`` — variables and optimizer state are owned by rank 0: gradients are
   ``reduce``-d to rank 0, rank 0 applies RMSprop, parameters are ``broadcast`` back (C5).
+
+On a GPU with the ``nccl`` (= RCCL) backend the strategy also owns a native RCCL communicator
+(``parallel/native_comm.py``): the fused runtime then issues its bucket all-reduces from the C++
+plan on the communicator's stream (no Python per bucket).  ``force_collectives=True`` (or
+``IDC_FORCE_COLLECTIVES=1``) runs every collective even in a world of one rank, so the whole RCCL
+path is exercised on a one-GPU machine.
 """
 from __future__ import annotations
 
 import contextlib
+import os
 from typing import List, Optional
 
 import torch
@@ -41,6 +48,13 @@ class Strategy:
     @property
     def num_replicas_in_sync(self) -> int:
         return self.world
+
+    @property
+    def active(self) -> bool:
+        """Collectives run (more than one replica, or forced in a world of one)."""
+        return False
+
+    native_comm = None
 
     @property
     def is_chief(self) -> bool:
@@ -87,10 +101,13 @@ def default_strategy() -> Strategy:
 
 class MirroredStrategy(Strategy):
     def __init__(self, devices=None, bucket_bytes: int = DEFAULT_BUCKET_BYTES, backend=None,
-                 device=None):
+                 device=None, force_collectives: Optional[bool] = None, native_comm: Optional[bool] = None):
         """``device`` overrides the per-rank device (e.g. several gloo ranks sharing one GPU to
-        rehearse the data-parallel path on a single-GPU machine)."""
-        rank, world, local = comm.init_process_group(backend)
+        rehearse the data-parallel path on a single-GPU machine).  ``native_comm``: own an RCCL
+        communicator for the fused runtime's gradient buckets (default: on for nccl on a GPU)."""
+        if force_collectives is None:
+            force_collectives = os.environ.get("IDC_FORCE_COLLECTIVES", "0") == "1"
+        rank, world, local = comm.init_process_group(backend, force=force_collectives)
         if device is not None:
             dev = torch.device(device)
             if dev.type == "cuda":
@@ -104,9 +121,27 @@ class MirroredStrategy(Strategy):
         self.rank, self.world, self.local_rank = rank, world, local
         self.bucket_bytes = bucket_bytes
         self.devices = devices
+        self.forced = bool(force_collectives) and world == 1
+        self.native_comm = None
+        if native_comm is None:
+            native_comm = os.environ.get("IDC_NATIVE_COMM", "1") != "0"
+        if native_comm and self.active and dev.type == "cuda" and comm.backend() == "nccl":
+            from .native_comm import NativeCommunicator
+            self.native_comm = NativeCommunicator(rank, world, dev)
+
+    @property
+    def active(self) -> bool:
+        return self.world > 1 or self.forced
+
+    def close(self):
+        """Release the native communicator and the process group (end of a run)."""
+        if self.native_comm is not None:
+            self.native_comm.close()
+            self.native_comm = None
+        comm.destroy()
 
     def broadcast_module(self, net):
-        if self.world == 1:
+        if not self.active:
             return
         with torch.no_grad():
             for t in net.weight_tensors():
@@ -122,14 +157,14 @@ class MirroredStrategy(Strategy):
         return b
 
     def apply_gradients(self, optimizer, arena):
-        if self.world == 1:
+        if not self.active:
             optimizer.step(arena)
             return
         self.bucketer(arena).finish()
         optimizer.step(arena, grad_scale=1.0 / self.world)
 
     def reduce_metrics(self, metrics):
-        if self.world == 1:
+        if not self.active:
             return
         states, owners = [], []
         for m in metrics:
@@ -164,7 +199,7 @@ class MirroredStrategy(Strategy):
                 m.scores, m.labels = [ss], [ll]
 
     def sync_bn_stats(self, model):
-        if self.world == 1:
+        if not self.active:
             return
         from ..models.layers import BatchNormalization
         if model.impl is not None:
@@ -199,13 +234,28 @@ class CentralStorageStrategy(MirroredStrategy):
         return None
 
     def apply_gradients(self, optimizer, arena):
-        if self.world == 1:
+        if not self.active:
             optimizer.step(arena)
             return
-        dist.reduce(arena.grad, 0, op=dist.ReduceOp.SUM)
+        self.reduce_to_root(arena.grad)
         if self.rank == 0:
             optimizer.step(arena, grad_scale=1.0 / self.world)
-        dist.broadcast(arena.data, 0)
+        self.broadcast_from_root(arena.data)
+
+    def reduce_to_root(self, t, stream=None):
+        """SUM-reduce ``t`` to rank 0 (native RCCL on the given / current stream when owned)."""
+        if self.native_comm is not None:
+            self.native_comm.reduce_(t, 0, "sum", stream)
+        else:
+            with torch.cuda.stream(stream) if stream is not None else contextlib.nullcontext():
+                dist.reduce(t, 0, op=dist.ReduceOp.SUM)
+
+    def broadcast_from_root(self, t, stream=None):
+        if self.native_comm is not None:
+            self.native_comm.broadcast_(t, 0, stream)
+        else:
+            with torch.cuda.stream(stream) if stream is not None else contextlib.nullcontext():
+                dist.broadcast(t, 0)
 
 
 class _ShardedBatches:

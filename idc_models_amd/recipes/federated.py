@@ -23,7 +23,7 @@ from ..data import (contiguous_clients, idc_dataset, prepare_for_training, shard
                     synthetic_dataset, train_test_clients)
 from ..engine import Model, ModelCheckpoint, RMSprop
 from ..fed import (broadcast_server_state, build_federated_averaging_process, build_federated_evaluation,
-                   load_server_state, save_server_state, state_with_new_model_weights)
+                   load_server_extra, load_server_state, save_server_state, state_with_new_model_weights)
 from ..fed.secure import SecureFederatedProcess
 from ..models import build_model
 from ..parallel import OneDeviceStrategy, comm
@@ -57,6 +57,7 @@ class FedConfig:
     backend: str = "auto"
     secure_aggregation: Optional[str] = None  # "mask": config #5 secure FedAvg
     resume: bool = True                       # continue from {path}/fed_state/state.pt if present
+                                              # (refused when it was written by another config)
     concurrent_clients: int = 1               # clients a rank trains at once (own model + stream)
 
 
@@ -67,6 +68,14 @@ def _fed_data(cfg: FedConfig):
             ds = ds.filter_label(1).concatenate(ds.filter_label(0))
         return ds
     return idc_dataset(cfg.path, "balanced", cfg.input_shape[0], cfg.seed, iid=cfg.iid)
+
+
+def _fed_fingerprint(cfg: FedConfig, state) -> dict:
+    """What a resumed run must share with the run that wrote the state."""
+    shapes = ";".join("x".join(str(d) for d in t.shape) for t in state.model.trainable)
+    return {"arch": cfg.arch, "num_clients": int(cfg.num_clients), "iid": bool(cfg.iid),
+            "secure_aggregation": str(cfg.secure_aggregation), "average_bn_stats": bool(cfg.average_bn_stats),
+            "trainable_shapes": shapes}
 
 
 def run_fedavg(cfg: FedConfig, printer=print):
@@ -127,10 +136,23 @@ def run_fedavg(cfg: FedConfig, printer=print):
     state_path = os.path.join(cfg.path, "fed_state", "state.pt")
     with Timer("Federated training", printer if comm.rank() == 0 else None):
         state = fed_avg.initialize()
+        fp = _fed_fingerprint(cfg, state)
         if cfg.resume and os.path.exists(state_path):
+            saved = load_server_extra(state_path)
+            diff = {k: (saved.get(k), v) for k, v in fp.items() if saved.get(k) != v}
+            if diff:
+                raise ValueError(f"{state_path} was written by a different federated configuration "
+                                 f"(saved, current): {diff}; use another path or resume=False")
             state = load_server_state(state_path, state.model.trainable[0].device)
             if comm.rank() == 0:
                 printer(f"Resuming federated training at round {state.round_num}")
+                if state.round_num >= cfg.rounds:
+                    printer(f"All {cfg.rounds} rounds are already done in {state_path}; nothing to train")
+            # every client's shuffle continues where the finished rounds left it (one local
+            # epoch per round), instead of replaying round 0's order
+            for d in fed_train:
+                if hasattr(d, "_epoch"):
+                    d._epoch = state.round_num
         else:
             state = state_with_new_model_weights(
                 state, [t.detach() for t in pre.net.trainable_weights],
@@ -144,7 +166,7 @@ def run_fedavg(cfg: FedConfig, printer=print):
             test_metrics = evaluation(state.model, fed_test)
             results.append((r, train_metrics, test_metrics))
             if comm.rank() == 0:
-                save_server_state(state, state_path)
+                save_server_state(state, state_path, extra=fp)
                 printer("{0:2d}, {1:f}, {2:f}, {3:f}, {4:f} \n".format(
                     r, train_metrics["binary_accuracy"], train_metrics["loss"],
                     test_metrics["binary_accuracy"], test_metrics["loss"]))

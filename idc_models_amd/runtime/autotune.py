@@ -14,6 +14,7 @@ from __future__ import annotations
 
 import json
 import os
+import threading
 from typing import Dict, Tuple
 
 import torch
@@ -22,6 +23,10 @@ from ..ops import _native as nat
 
 _CACHE: Dict[Tuple, int] = {}
 _LOADED = False
+# one tuning at a time per process (concurrent federated clients build their programs on worker
+# threads): trial timings taken beside another plan's trials would be picked under contention, and
+# the cache dict must not change size while it is being serialised
+_LOCK = threading.RLock()
 
 
 def _load_cache():
@@ -47,8 +52,10 @@ def _save_cache():
     if not p or int(os.environ.get("RANK", "0")) != 0:
         return
     tmp = f"{p}.tmp{os.getpid()}"
+    with _LOCK:
+        snap = dict(_CACHE)
     with open(tmp, "w") as f:
-        json.dump({json.dumps(list(k)): v for k, v in _CACHE.items()}, f)
+        json.dump({json.dumps(list(k)): v for k, v in snap.items()}, f)
     os.replace(tmp, p)
 
 
@@ -118,7 +125,7 @@ def _splits_for(ext, a, t: int, M: int, slab_floats: int):
     return [s for s in (2, 4, 8) if tiles * s * bm * bn <= slab_floats and nk >= 2 * s]
 
 
-def autotune_plan(plan, stream, verbose: bool = False, reset_tickets=None, slab_floats: int = 0,
+def _autotune_plan_unlocked(plan, stream, verbose: bool = False, reset_tickets=None, slab_floats: int = 0,
                   halo_ops=()) -> int:
     """Tune every conv / wgrad op of ``plan`` in place: tile shape, then the split-K factor of the
     best few tiles (ops whose payload carries a split-K workspace).  Returns the number tuned.
@@ -197,3 +204,9 @@ def autotune_plan(plan, stream, verbose: bool = False, reset_tickets=None, slab_
     _save_cache()
     torch.cuda.synchronize()
     return n
+
+
+def autotune_plan(plan, stream, *args, **kwargs):
+    """Tune every conv / wgrad op of ``plan`` (serialised per process, see ``_LOCK``)."""
+    with _LOCK:
+        return _autotune_plan_unlocked(plan, stream, *args, **kwargs)

@@ -129,13 +129,41 @@ class FusedProgram:
         mark_at = {}
         for pos, lo in b.bwd_marks:
             mark_at.setdefault(pos, []).append(lo)
+        # Data parallelism over the strategy's native RCCL communicator: every gradient bucket's
+        # all-reduce becomes a plan op (OP_ALLREDUCE, comm lane) placed at the first backward mark
+        # after which all of its parameters' gradients are final, so the C++ executor issues the
+        # whole backward + collectives in one call.
+        strategy = model.strategy
+        self.native_comm = None
+        pending_buckets: List[Tuple[int, int, int]] = []  # (lowest param index, start, end)
+        if training and model.arena.params and getattr(strategy, "native_comm", None) is not None \
+                and strategy.active and not getattr(strategy, "central_storage", False):
+            from ..parallel.buckets import GradBucketer
+            self.native_comm = strategy.native_comm
+            gb = GradBucketer(model.arena, strategy.bucket_bytes)
+            pending_buckets = sorted(((min(bk.param_ids), bk.start, bk.end) for bk in gb.buckets), reverse=True)
+        self.n_comm_ops = 0
+
+        def add_ready_buckets(lo_ready: int):
+            nonlocal op_index
+            while pending_buckets and pending_buckets[0][0] >= lo_ready:
+                _, s0, s1 = pending_buckets.pop(0)
+                self.plan.add(nat.OP_ALLREDUCE, b"", [0, 0], [], [s1 - s0],
+                              [model.arena.grad.data_ptr() + 4 * s0], 0)
+                op_index += 1
+                self.n_comm_ops += 1
+
         for i, (seg, kind, raw, ints, floats, longs, ptrs, lane) in enumerate(b.ops):
             if seg != cur:
+                if cur == "bwd" and pending_buckets:
+                    add_ready_buckets(-1)  # buckets no mark released (params without gradient)
                 if cur is not None:
                     self.seg[cur] = (start, op_index)
                 cur, start = seg, op_index
             if i in mark_at:
                 self.bwd_marks.append((op_index, min(mark_at[i])))
+                if pending_buckets:
+                    add_ready_buckets(min(mark_at[i]))
             if kind == "MOVING":
                 if b.moving_dev is None:
                     continue
@@ -146,8 +174,12 @@ class FusedProgram:
                 self.rms_index = op_index
             self.plan.add(kind, raw, ints, floats, longs, ptrs, lane)
             op_index += 1
+        if cur == "bwd" and pending_buckets:
+            add_ready_buckets(-1)
         if cur is not None:
             self.seg[cur] = (start, op_index)
+        if self.native_comm is not None:
+            self.plan.set_comm(self.native_comm.c)
         self.use_graphs = use_graphs and os.environ.get("IDC_NO_GRAPHS", "0") != "1"
         # Which segments replay as HIP graphs.  The backward is issued directly by default: one
         # captured fork/join graph loses the side lane's concurrency under ROCm's graph executor
@@ -211,7 +243,7 @@ class FusedProgram:
             return
         if graph is None:
             graph = self.use_graphs and self._graph_for(lo)
-        if graph and self.dual_graphs and self.plan.has_side(lo, hi):
+        if graph and self.dual_graphs and self.plan.has_side(lo, hi) and not self.plan.has_comm_ops(lo, hi):
             # main-lane and side-lane graphs joined by external events (plan.cpp capture_dual)
             g = self.graphs.get(("dual", lo, hi))
             if g is None:
@@ -327,14 +359,18 @@ class FusedStep:
         if validate:
             self._validate(p, "after fwd")
         strategy = m.strategy
-        world = strategy.num_replicas_in_sync
-        if world > 1 and getattr(strategy, "central_storage", False):
+        active = strategy.active
+        if active and getattr(strategy, "central_storage", False):
             return self._central_storage_step(p, validate)
         if "bwd" in p.seg:
             trace.push("seg:bwd")
             lo, hi = p.seg["bwd"]
-            bucketer = strategy.bucketer(m.arena) if world > 1 else None
-            if bucketer is not None and p.bwd_marks:
+            bucketer = strategy.bucketer(m.arena) if active and p.native_comm is None else None
+            if p.native_comm is not None:
+                # the plan itself issues every bucket all-reduce on the communicator's stream and
+                # joins it back into the main lane at the end of the range
+                p.run_range(lo, hi)
+            elif bucketer is not None and p.bwd_marks:
                 # backward in bucket-aligned segments: each bucket's all-reduce is issued from
                 # the comm stream as soon as its gradients are final — the comm stream waits for
                 # the main lane AND the side-lane weight gradients issued so far, while the main
@@ -375,12 +411,10 @@ class FusedStep:
         """CentralStorageStrategy (``dist_model_tf_dense.py:24``): gradients are reduced to rank 0,
         only rank 0 owns optimizer state and applies RMSprop, the updated fp32 parameters are
         broadcast and every rank re-casts its bf16 kernel copies."""
-        import torch.distributed as dist
         m = self.m
         st = m.strategy
         p.run_segment("bwd")
-        with torch.cuda.stream(p.stream):
-            dist.reduce(m.arena.grad, 0, op=dist.ReduceOp.SUM)
+        st.reduce_to_root(m.arena.grad, p.stream)
         if "opt" in p.seg:
             lo, hi = p.seg["opt"]  # [finite check] rmsprop | cast [flag reset]
             if p.host_optimizer:
@@ -392,8 +426,7 @@ class FusedStep:
                 if st.rank == 0:
                     p.run_range(lo, p.rms_index + 1, graph=False)
                 cast_lo = p.rms_index + 1
-            with torch.cuda.stream(p.stream):
-                dist.broadcast(m.arena.data, 0)
+            st.broadcast_from_root(m.arena.data, p.stream)
             p.run_range(cast_lo, hi, graph=False)
         torch.cuda.current_stream(m.device).wait_stream(p.stream)
         return p.io.loss.reshape(()).clone(), p.io.logits.clone()

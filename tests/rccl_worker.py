@@ -1,0 +1,172 @@
+"""Worker for tests/test_rccl_gpu.py: one rank on cuda:0 over the ``nccl`` (= RCCL) backend with
+collectives forced on in a world of one (``IDC_FORCE_COLLECTIVES=1``), launched by
+``torch.distributed.run``.  Every data-parallel / federated collective the framework issues then
+really runs through RCCL on the MI355X:
+
+* ``native``   — the C++ communicator: f32 / int32 / bf16 all-reduce, reduce, broadcast,
+                 all-gather, exact (a world of one is the identity, extreme int32 values included);
+* ``dp_det``   — DenseNet-121 fused training steps through MirroredStrategy with the native
+                 bucketed all-reduce ops inside the plan (comm stream, per-bucket ncclAllReduce,
+                 join) under IDC_DETERMINISTIC=1: bit-identical to the single-device program;
+* ``dp_tuned`` — the same with autotuned split-K tiles and float-atomic statistics (what ships):
+                 gradients within the bf16 floor of the single-device program;
+* ``masked``   — MaskedAggregator's int32 masked SUM all-reduce and decode;
+* ``fedavg``   — the FedAvg packed all-reduce and the server-state broadcast helpers.
+Prints ``RCCLCASE {json}`` per case.
+"""
+import json
+import os
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+
+def emit(d):
+    print("RCCLCASE " + json.dumps(d), flush=True)
+
+
+def case_native(st):
+    nc = st.native_comm
+    dev = st.device
+    before = nc.collectives
+    x = torch.randn(1 << 16, device=dev)
+    y = x.clone()
+    nc.all_reduce_(y)
+    i = torch.tensor([-(2 ** 31), 2 ** 31 - 1, -1, 0, 12345], dtype=torch.int32, device=dev)
+    j = i.clone()
+    nc.all_reduce_(j)
+    b = torch.randn(999, device=dev).bfloat16()
+    bb = b.clone()
+    nc.all_reduce_(bb, "max")
+    r = x.clone()
+    nc.reduce_(r, 0)
+    c = x.clone()
+    nc.broadcast_(c, 0)
+    g = nc.all_gather(i)
+    torch.cuda.synchronize()
+    ok = (torch.equal(x, y) and torch.equal(i, j) and torch.equal(b, bb) and torch.equal(r, x)
+          and torch.equal(c, x) and tuple(g.shape) == (1, 5) and torch.equal(g[0], i)
+          and nc.collectives - before == 6)
+    nc.check()
+    emit({"case": "native", "ok": bool(ok), "rccl": nc.version(), "collectives": nc.collectives - before})
+
+
+def _step_models(arch, per, det, bucket_bytes):
+    from idc_models_amd.engine import Model, RMSprop
+    from idc_models_amd.models import build_model
+    from idc_models_amd.parallel import MirroredStrategy, OneDeviceStrategy
+    os.environ["IDC_DETERMINISTIC"] = "1" if det else "0"
+    st = MirroredStrategy(bucket_bytes=bucket_bytes, force_collectives=True)
+    m = Model(build_model(arch, None, 1, seed=7), st)
+    m.compile(RMSprop(1e-4), "binary_crossentropy", [], backend="fused")
+    ref = Model(build_model(arch, None, 1, seed=7), OneDeviceStrategy("cuda:0"))
+    ref.compile(RMSprop(1e-4), "binary_crossentropy", [], backend="fused")
+    ref2 = None
+    if not det:  # a second single-device run gives the run-to-run noise floor of the float atomics
+        ref2 = Model(build_model(arch, None, 1, seed=7), OneDeviceStrategy("cuda:0"))
+        ref2.compile(RMSprop(1e-4), "binary_crossentropy", [], backend="fused")
+    g = torch.Generator().manual_seed(3)
+    H, W, C = m.net.input_shape
+    x = torch.randint(0, 256, (per, H, W, C), generator=g, dtype=torch.uint8)
+    y = torch.randint(0, 2, (per,), generator=g)
+    return st, m, ref, ref2, x, y
+
+
+def case_dp(det):
+    from idc_models_amd.parallel import comm
+    st, m, ref, ref2, x, y = _step_models("densenet121", 64, det, 2 << 20)
+    nc = st.native_comm
+    c0 = nc.collectives
+    m.impl.train_step(x, y)
+    ref.impl.train_step(x, y)
+    torch.cuda.synchronize()
+    p = m.impl._prog(x.shape[0], True, torch.uint8)
+    g_dp, g_ref = m.arena.grad.detach().clone(), ref.arena.grad.detach().clone()
+    rel = float((g_dp - g_ref).norm() / g_ref.norm().clamp_min(1e-30))
+    floor = 0.0
+    if ref2 is not None:
+        ref2.impl.train_step(x, y)
+        torch.cuda.synchronize()
+        floor = float((ref2.arena.grad - g_ref).norm() / g_ref.norm().clamp_min(1e-30))
+        ref2.impl.close()
+    m.impl.train_step(x, y)
+    ref.impl.train_step(x, y)
+    torch.cuda.synchronize()
+    wdp, wref = m.arena.data.detach(), ref.arena.data.detach()
+    wdiff = float((wdp - wref).abs().max())
+    n_ops = p.n_comm_ops
+    ran = nc.collectives - c0
+    out = {"case": "dp_det" if det else "dp_tuned", "backend": comm.backend(), "comm_ops_per_step": n_ops,
+           "collectives": ran, "grad_rel": rel, "noise_floor_rel": floor, "weight_max_diff": wdiff,
+           "native": p.native_comm is not None}
+    if det:
+        ok = n_ops >= 2 and ran == 2 * n_ops and rel == 0.0 and wdiff == 0.0
+    else:
+        # what ships (autotuned split-K, float-atomic statistics): the data-parallel gradient is
+        # as close to the single-device one as two single-device runs are to each other
+        ok = n_ops >= 2 and ran == 2 * n_ops and rel <= 3.0 * floor + 1e-3
+    out["ok"] = bool(ok and comm.backend() == "nccl" and p.native_comm is not None)
+    emit(out)
+    m.impl.close()
+    ref.impl.close()
+    st.native_comm.close()
+
+
+def case_masked(dev):
+    from idc_models_amd.fed.secagg import MaskedAggregator
+    from idc_models_amd.parallel import comm
+    agg = MaskedAggregator(2, [0, 1], dev)
+    gen = torch.Generator(device="cpu").manual_seed(5)
+    sizes = [1000, 37, 4096]
+    v0 = torch.randn(sum(sizes), generator=gen).to(dev)
+    v1 = torch.randn(sum(sizes), generator=gen).to(dev) * 3
+    tot = agg.masked_sum({0: v0, 1: v1}, sizes, round_=1)
+    ref = v0 + v1
+    # per element: one quantum of rounding per client, plus the float32 rounding of the decoded
+    # sum (the int32 fixed-point total converts to float32 with a 24-bit mantissa)
+    q = float(1.0 / min(agg.last_scales))
+    err = float(((tot - ref).abs() - ref.abs() * 2.0 ** -22).max())
+    tol = 2 * q
+    emit({"case": "masked", "ok": bool(err <= tol and comm.backend() == "nccl"), "err": err, "tol": tol})
+
+
+def case_fedavg(dev):
+    import torch.distributed as dist
+    from idc_models_amd.parallel import comm
+    a = torch.randn(333, device=dev)
+    b = torch.arange(7, dtype=torch.float64, device=dev)
+    ra, rb = comm.pack_all_reduce([a, b])
+    c = torch.randn(55, device=dev)
+    d = c.clone()
+    comm.broadcast_(d, 0)
+    mx = comm.all_reduce_max(3.5, dev)
+    torch.cuda.synchronize()
+    ok = (torch.allclose(ra, a) and torch.equal(rb, b) and torch.equal(c, d) and mx == 3.5
+          and comm.is_dist() and dist.get_backend() == "nccl")
+    emit({"case": "fedavg", "ok": bool(ok)})
+
+
+def main():
+    os.environ["IDC_FORCE_COLLECTIVES"] = "1"
+    from idc_models_amd.parallel import MirroredStrategy
+    cases = sys.argv[1].split(",") if len(sys.argv) > 1 else ["native", "dp_det", "dp_tuned", "masked", "fedavg"]
+    st = MirroredStrategy(force_collectives=True)
+    assert st.native_comm is not None, "no native communicator on a nccl GPU rank"
+    for c in cases:
+        if c == "native":
+            case_native(st)
+        elif c == "dp_det":
+            case_dp(True)
+        elif c == "dp_tuned":
+            case_dp(False)
+        elif c == "masked":
+            case_masked(st.device)
+        elif c == "fedavg":
+            case_fedavg(st.device)
+    st.close()
+
+
+if __name__ == "__main__":
+    main()

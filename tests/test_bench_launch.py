@@ -1,0 +1,35 @@
+"""bench.py's launcher contract: ``--gpus N`` with no launcher environment
+starts N rank processes itself and the job reports ``world_size == N``; a rank whose world is not N
+refuses to run.  CPU ranks over gloo here; on GPUs the same ranks use RCCL."""
+import json
+import os
+import subprocess
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _run(args, env_extra=None):
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    env.update(env_extra or {})
+    return subprocess.run([sys.executable, os.path.join(ROOT, "bench.py")] + args, cwd=ROOT, env=env,
+                          capture_output=True, text=True, timeout=300)
+
+
+def test_bench_spawns_requested_world_on_cpu():
+    r = _run(["--gpus", "2", "--device", "cpu", "--model", "mobilenetv2", "--batch", "4", "--steps", "1",
+              "--warmup", "0", "--fit-steps", "0"])
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [json.loads(l) for l in r.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, r.stdout  # rank 0 prints exactly one line
+    out = lines[0]
+    assert out["config"]["world_size"] == 2 and out["config"]["parallelism"] == "dp2"
+    assert out["config"]["comm_backend"] == "gloo"
+    assert out["config"]["global_batch"] == 8 and out["steps"] == 1
+
+
+def test_bench_refuses_mismatched_world():
+    r = _run(["--gpus", "4", "--device", "cpu", "--model", "mobilenetv2", "--batch", "4", "--steps", "1",
+              "--warmup", "0", "--fit-steps", "0"], {"WORLD_SIZE": "1", "RANK": "0", "LOCAL_RANK": "0"})
+    assert r.returncode == 3
+    assert "error" in json.loads(r.stdout.strip().splitlines()[-1])

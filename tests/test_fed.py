@@ -318,3 +318,64 @@ def test_secure_aggregation_survives_client_dropout(mode):
     full = [secagg.mask_quantize(x, [1.0], seg, 4, k, ks[k].round_keys(pubs, 0, range(4)), 0) for k in (0, 1, 3)]
     s = sum(t.to(torch.int64) for t in full) % (1 << 32)
     assert not torch.equal(s, torch.full((16,), 3, dtype=torch.int64))
+
+
+def test_choose_scales_stays_finite_for_tiny_segments():
+    """A tiny-but-nonzero protected tensor must not overflow its float32 fixed-point scale."""
+    sc = secagg.choose_scales([1e-35, 1.0, 0.0], 8)
+    assert np.all(np.isfinite(sc)) and sc[0] == np.float32(2.0 ** 100)
+    x = torch.tensor([1e-35, -3e-36, 0.5, -0.25, 0.0])
+    q = secagg.mask_quantize(x, sc[:2], np.array([2, 5]), 1, 0, {}, 0)
+    back = secagg.unmask(q, sc[:2], np.array([2, 5]))
+    assert torch.isfinite(back).all()
+    assert torch.allclose(back[2:4], x[2:4], atol=1e-8)
+
+
+def test_fedavg_skips_client_with_non_finite_bn_statistics():
+    """average_bn_stats: a client whose BatchNorm statistics are non-finite gets weight 0 too."""
+    from idc_models_amd.data import synthetic_dataset, contiguous_clients
+    from idc_models_amd.engine import Model, RMSprop
+    from idc_models_amd.fed import build_federated_averaging_process
+    from idc_models_amd.models import build_model
+    from idc_models_amd.parallel import OneDeviceStrategy
+    ds = synthetic_dataset(16, (32, 32, 3), 2, seed=1)
+    clients = [c.batch(8, True, 100, True, seed=i) for i, c in enumerate(contiguous_clients(ds, 2, 8))]
+    base = build_model("mobilenetv2", (32, 32, 3), 1, seed=0)
+
+    def model_fn():
+        import copy
+        return Model(copy.deepcopy(base), OneDeviceStrategy("cpu"))
+
+    proc = build_federated_averaging_process(model_fn, lambda: RMSprop(1e-3), average_bn_stats=True,
+                                             backend="eager")
+    state = proc.initialize()
+    m = proc.worker()
+    orig_fit = m.fit
+    calls = {"n": 0}
+
+    def fit(d, **kw):
+        calls["n"] += 1
+        h = orig_fit(d, **kw)
+        if calls["n"] == 2:
+            with torch.no_grad():
+                m.net.non_trainable_weights[0].fill_(float("inf"))
+        return h
+
+    m.fit = fit
+    new, _ = proc.next(state, clients)
+    assert all(torch.isfinite(w).all() for w in new.model.non_trainable)
+    assert all(torch.isfinite(w).all() for w in new.model.trainable)
+
+
+def test_fed_resume_refuses_a_foreign_state(tmp_path):
+    from idc_models_amd.fed import ModelWeights, ServerState, save_server_state
+    from idc_models_amd.recipes.federated import FedConfig, _fed_fingerprint
+    cfg = FedConfig(path=str(tmp_path), arch="tinycnn")
+    st = ServerState(ModelWeights([torch.zeros(3, 3)], []), 2)
+    fp = _fed_fingerprint(cfg, st)
+    p = tmp_path / "fed_state" / "state.pt"
+    save_server_state(st, str(p), extra=fp)
+    from idc_models_amd.fed import load_server_extra
+    assert load_server_extra(str(p)) == fp
+    other = _fed_fingerprint(FedConfig(path=str(tmp_path), arch="vgg16", num_clients=4), st)
+    assert other != fp

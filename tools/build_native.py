@@ -38,8 +38,15 @@ SOURCES = [
     "kernels/dwconv.hip",
     "kernels/mlp_head.hip",
     "kernels/secagg.hip",
+    "comm/communicator.cpp",
     "runtime/plan.cpp",
 ]
+
+# RCCL (= NCCL API on ROCm) for the native communicator.  Its soname is librccl.so.1, the same as
+# the copy torch ships: in a process that imported torch first (the package always does) the loader
+# reuses torch's already-mapped library, so one RCCL serves both communicators.
+ROCM = os.environ.get("ROCM_PATH", "/opt/rocm")
+LINK_LIBS = [f"-L{ROCM}/lib", "-lrccl", f"-Wl,-rpath,{ROCM}/lib"]
 
 
 def ext_path() -> str:
@@ -147,6 +154,58 @@ def build_host_module(name: str, src_rel: str, inc_sub: str, libs, verbose: bool
     return out
 
 
+SANITIZERS = {
+    # host code only (no GPU sanitizer on this pool): the threaded PNG loader / pinned ring, the
+    # GMP Paillier vector ops and the libhdf5 weight I/O
+    "address": ["-fsanitize=address,undefined", "-fno-sanitize-recover=undefined"],
+    "thread": ["-fsanitize=thread"],
+}
+
+
+SONAMES = {"gmp": "libgmp.so.10", "hdf5": "libhdf5.so.103", "png16": "libpng16.so.16", "z": "libz.so.1"}
+
+
+def sanitize_dir(kind: str) -> str:
+    return os.path.join(ROOT, "build", "sanitize", kind)
+
+
+def build_sanitized(kind: str, verbose: bool = True) -> str:
+    """Instrumented builds of every host-only module into build/sanitize/<kind>/ (loaded through
+    IDC_HOST_EXT_DIR, utils/hostext.py).  libstdc++ is linked dynamically here: the sanitizer
+    runtimes must intercept its allocator."""
+    import pybind11
+
+    out_dir = sanitize_dir(kind)
+    os.makedirs(out_dir, exist_ok=True)
+    # the image's /opt/conda/lib also carries an OLDER sanitizer runtime (libasan.so.5): an rpath
+    # to that prefix would map it beside the system runtime the test process preloads (two ASan
+    # shadows -> abort), so the instrumented modules rpath a directory holding only the libraries
+    # they need from the prefix
+    libdir = os.path.join(out_dir, "lib")
+    os.makedirs(libdir, exist_ok=True)
+    for so in SONAMES.values():
+        src_so, dst = os.path.join(CONDA_PREFIX, "lib", so), os.path.join(libdir, so)
+        if os.path.exists(src_so) and not os.path.lexists(dst):
+            os.symlink(os.path.realpath(src_so), dst)
+    mods = list(HOST_MODULES) + [("_idc_h5", "ckpt/h5io.cpp", "", ["hdf5"])]
+    for name, src_rel, inc_sub, libs in mods:
+        src = os.path.join(CSRC, src_rel)
+        out = os.path.join(out_dir, name + sysconfig.get_config_var("EXT_SUFFIX"))
+        if os.path.exists(out) and os.path.getmtime(out) >= os.path.getmtime(src):
+            continue
+        inc = os.path.join(CONDA_PREFIX, "include", inc_sub) if inc_sub else os.path.join(CONDA_PREFIX, "include")
+        cmd = (["g++", "-O1", "-g", "-fno-omit-frame-pointer", "-std=c++17", "-shared", "-fPIC", "-pthread"]
+               + SANITIZERS[kind] + [src, "-o", out, f"-I{pybind11.get_include()}",
+                                     f"-I{sysconfig.get_paths()['include']}", f"-I{inc}", f"-L{libdir}"]
+               + [f"-l:{SONAMES[l]}" for l in libs] + [f"-Wl,-rpath,{libdir}"])
+        r = subprocess.run(cmd, capture_output=True, text=True)
+        if r.returncode != 0:
+            raise RuntimeError(f"{name} ({kind} sanitizer) build failed:\n{r.stderr[-4000:]}")
+        if verbose:
+            print(f"[build_native] {out}")
+    return out_dir
+
+
 def build(clean: bool = False, jobs: int = 8, verbose: bool = True) -> str:
     build_h5(verbose)
     for name, src, inc, libs in HOST_MODULES:
@@ -160,7 +219,7 @@ def build(clean: bool = False, jobs: int = 8, verbose: bool = True) -> str:
     out = ext_path()
     if not os.path.exists(out) or os.path.getmtime(out) < max(os.path.getmtime(o) for o in objs):
         tmp = out + ".tmp"
-        cmd = [HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", tmp] + objs
+        cmd = [HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", tmp] + objs + LINK_LIBS
         r = subprocess.run(cmd, capture_output=True, text=True)
         if r.returncode != 0:
             raise RuntimeError(f"link failed:\n{r.stderr[-4000:]}")
@@ -174,5 +233,10 @@ if __name__ == "__main__":
     ap = argparse.ArgumentParser()
     ap.add_argument("--clean", action="store_true")
     ap.add_argument("-j", type=int, default=min(8, os.cpu_count() or 4))
+    ap.add_argument("--sanitize", choices=sorted(SANITIZERS), default=None,
+                    help="build the host-only modules with a sanitizer into build/sanitize/<kind>/")
     a = ap.parse_args()
-    build(a.clean, a.j)
+    if a.sanitize:
+        build_sanitized(a.sanitize)
+    else:
+        build(a.clean, a.j)
