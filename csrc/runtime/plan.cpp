@@ -27,6 +27,8 @@
 
 #include <cstdlib>
 #include <cstring>
+#include <mutex>
+#include <unordered_map>
 #include <stdexcept>
 #include <string>
 #include <vector>
@@ -137,6 +139,8 @@ class Plan {
     return (int)ops_.size() - 1;
   }
 
+  uintptr_t get_ptr(int idx, int slot) const { return ops_.at(idx).p[slot & 7]; }
+  long long get_long(int idx, int slot) const { return ops_.at(idx).l[slot & 3]; }
   void set_float(int idx, int slot, float v) { ops_.at(idx).f[slot] = v; }
   void set_int(int idx, int slot, int v) { ops_.at(idx).i[slot] = v; }
   int get_int(int idx, int slot) const { return ops_.at(idx).i[slot]; }
@@ -202,6 +206,92 @@ class Plan {
 
   void launch(int gid, uintptr_t stream) {
     check(hipGraphLaunch(execs_.at(gid), reinterpret_cast<hipStream_t>(stream)), "hipGraphLaunch");
+  }
+
+  // ---- lane-split chunk graphs (the backward) --------------------------------------------
+  // A backward chunk [begin, end) becomes TWO plain graphs: its main-lane ops and its side-lane
+  // ops (weight gradients), each a straight chain with no event nodes (ROCm replays those fast).
+  // The caller launches the main graph on the plan stream, forks the side stream after it
+  // (fork_side), launches the side graph there and keeps going with the next chunk's main graph,
+  // so chunk i's weight gradients overlap chunk i+1's data gradients.  A side op's producers all
+  // precede it in op order, hence sit in main chunks <= its own: ordering after the main graph of
+  // its chunk is sufficient, and the lowering guarantees no later main op overwrites its inputs.
+  // Returns -1 when the lane has no op in the range.
+  int capture_lane(int begin, int end, int lane, uintptr_t stream) {
+    hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+    if (end < 0 || end > (int)ops_.size()) end = (int)ops_.size();
+    bool any = false;
+    for (int k = begin; k < end; ++k)
+      if (ops_[k].lane == lane && ops_[k].kind != OP_ALLREDUCE) any = true;
+    if (!any) return -1;
+    GroupScope gscope(groups_, gstride_);
+    check(hipStreamBeginCapture(st, hipStreamCaptureModeThreadLocal), "hipStreamBeginCapture(lane)");
+    try {
+      for (int k = begin; k < end; ++k)
+        if (ops_[k].lane == lane && ops_[k].kind != OP_ALLREDUCE) exec(ops_[k], st);
+    } catch (...) {
+      hipGraph_t g = nullptr;
+      hipStreamEndCapture(st, &g);
+      if (g) hipGraphDestroy(g);
+      throw;
+    }
+    hipGraph_t g = nullptr;
+    check(hipStreamEndCapture(st, &g), "hipStreamEndCapture(lane)");
+    hipGraphExec_t ex = nullptr;
+    check(hipGraphInstantiate(&ex, g, nullptr, nullptr, 0), "hipGraphInstantiate(lane)");
+    graphs_.push_back(g);
+    execs_.push_back(ex);
+    return (int)execs_.size() - 1;
+  }
+
+  // the side stream waits for everything issued on `stream` so far
+  void fork_side(uintptr_t stream) {
+    ensure_side();
+    check(hipEventRecord(fork_, reinterpret_cast<hipStream_t>(stream)), "hipEventRecord(fork)");
+    check(hipStreamWaitEvent(side_, fork_, 0), "hipStreamWaitEvent(fork)");
+    side_open_ = true;
+  }
+  void launch_side(int gid) {
+    ensure_side();
+    check(hipGraphLaunch(execs_.at(gid), side_), "hipGraphLaunch(side)");
+    side_open_ = true;
+  }
+  // `stream` waits for every side-lane op issued so far
+  void join_side(uintptr_t stream) {
+    if (!side_ || !side_open_) return;
+    check(hipEventRecord(join_, side_), "hipEventRecord(join)");
+    check(hipStreamWaitEvent(reinterpret_cast<hipStream_t>(stream), join_, 0), "hipStreamWaitEvent(join)");
+    side_open_ = false;
+  }
+  // the collectives of [begin, end) on the comm stream, after everything issued so far on the
+  // side stream (whose last graph followed the main graph of the same chunk) and on `stream`
+  void comm_range(int begin, int end, uintptr_t stream) {
+    hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+    if (end < 0 || end > (int)ops_.size()) end = (int)ops_.size();
+    bool first = true;
+    for (int k = begin; k < end; ++k) {
+      if (ops_[k].kind != OP_ALLREDUCE) continue;
+      if (first) {
+        issue_comm(ops_[k], st, side_ != nullptr && side_open_);
+        first = false;
+      } else {
+        comm_->all_reduce(reinterpret_cast<void*>(ops_[k].p[0]), ops_[k].l[0], ops_[k].i[0], ops_[k].i[1],
+                          comm_->stream());
+      }
+      comm_open_ = true;
+    }
+  }
+  void join_comm(uintptr_t stream) {
+    if (!comm_ || !comm_open_) return;
+    check(hipEventRecord(cjoin_, comm_->stream()), "hipEventRecord(comm join)");
+    check(hipStreamWaitEvent(reinterpret_cast<hipStream_t>(stream), cjoin_, 0), "hipStreamWaitEvent(comm join)");
+    comm_open_ = false;
+  }
+  int count_lane(int begin, int end, int lane) const {
+    if (end < 0 || end > (int)ops_.size()) end = (int)ops_.size();
+    int n = 0;
+    for (int k = begin; k < end; ++k) n += (ops_[k].lane == lane && ops_[k].kind != OP_ALLREDUCE);
+    return n;
   }
 
   // Two-lane graphs.  A single captured graph with fork/join edges is executed by ROCm without
@@ -561,6 +651,38 @@ class Plan {
   std::vector<Dual> duals_;
 };
 
+// ---- grouped-program region allocator -------------------------------------------------------
+// A grouped program (csrc/kernels/common.h GroupArg) must have ALL its buffers inside copy 0 of
+// its region so that copy g is copy 0 + g * stride.  The runtime (runtime/grouped.py) routes every
+// torch allocation made while it builds the model and its program into a torch.cuda.MemPool
+// whose pluggable allocator is this bump allocator over the active region.  Frees are no-ops: a
+// region is released as a whole with its slab.
+struct RegionState {
+  uintptr_t base = 0;
+  size_t cap = 0, used = 0;
+};
+std::mutex g_region_mu;
+std::unordered_map<uintptr_t, RegionState> g_regions;
+uintptr_t g_region_active = 0;
+
+void region_activate(uintptr_t base, long long cap) {
+  std::lock_guard<std::mutex> l(g_region_mu);
+  RegionState& r = g_regions[base];
+  r.base = base;
+  r.cap = (size_t)cap;
+  g_region_active = base;
+}
+long long region_used(uintptr_t base) {
+  std::lock_guard<std::mutex> l(g_region_mu);
+  auto it = g_regions.find(base);
+  return it == g_regions.end() ? 0 : (long long)it->second.used;
+}
+void region_forget(uintptr_t base) {
+  std::lock_guard<std::mutex> l(g_region_mu);
+  g_regions.erase(base);
+  if (g_region_active == base) g_region_active = 0;
+}
+
 // direct (non-plan) entry points, used by the op-level python API and tests
 void py_conv(py::bytes payload, int tile, int a_f32, uintptr_t stream) {
   std::string s = payload;
@@ -675,6 +797,29 @@ void py_rmsprop(uintptr_t w, uintptr_t g, uintptr_t ms, long long n, float lr, f
 
 }  // namespace
 
+// torch.cuda.memory.CUDAPluggableAllocator entry points (looked up by name with dlsym)
+extern "C" __attribute__((visibility("default"))) void* idc_region_malloc(size_t size, int device,
+                                                                         hipStream_t stream) {
+  (void)device;
+  (void)stream;
+  std::lock_guard<std::mutex> l(g_region_mu);
+  auto it = g_regions.find(g_region_active);
+  if (it == g_regions.end()) return nullptr;
+  RegionState& r = it->second;
+  const size_t sz = (size + 511) & ~(size_t)511;
+  if (r.used + sz > r.cap) return nullptr;  // torch reports an out-of-memory error
+  void* p = reinterpret_cast<void*>(r.base + r.used);
+  r.used += sz;
+  return p;
+}
+extern "C" __attribute__((visibility("default"))) void idc_region_free(void* ptr, size_t size, int device,
+                                                                      hipStream_t stream) {
+  (void)ptr;
+  (void)size;
+  (void)device;
+  (void)stream;
+}
+
 PYBIND11_MODULE(_idc_native, m) {
   m.doc() = "idc_models_amd native MI355X (gfx950) kernels and plan executor";
   py::class_<Communicator>(m, "Communicator")
@@ -709,11 +854,16 @@ PYBIND11_MODULE(_idc_native, m) {
       .def_property_readonly("is_open", &Communicator::open)
       .def_property_readonly("collectives", &Communicator::collectives);
   m.def("rccl_version", &rccl_version);
+  m.def("region_activate", &region_activate);
+  m.def("region_used", &region_used);
+  m.def("region_forget", &region_forget);
   m.attr("OP_ALLREDUCE") = (int)OP_ALLREDUCE;
   py::class_<Plan>(m, "Plan")
       .def(py::init<>())
       .def("set_comm", &Plan::set_comm, py::keep_alive<1, 2>())
       .def("set_groups", &Plan::set_groups)
+      .def("get_ptr", &Plan::get_ptr)
+      .def("get_long", &Plan::get_long)
       .def("groups", &Plan::groups)
       .def("has_comm_ops", &Plan::has_comm_ops)
       .def("add", &Plan::add, py::arg("kind"), py::arg("payload"), py::arg("ints"), py::arg("floats"),
@@ -731,6 +881,13 @@ PYBIND11_MODULE(_idc_native, m) {
       .def("capture", &Plan::capture)
       .def("launch", &Plan::launch)
       .def("capture_dual", &Plan::capture_dual)
+      .def("capture_lane", &Plan::capture_lane)
+      .def("fork_side", &Plan::fork_side)
+      .def("launch_side", &Plan::launch_side)
+      .def("join_side", &Plan::join_side)
+      .def("comm_range", &Plan::comm_range)
+      .def("join_comm", &Plan::join_comm)
+      .def("count_lane", &Plan::count_lane)
       .def("launch_dual", &Plan::launch_dual)
       .def("has_side", &Plan::has_side)
       .def("clear_graphs", &Plan::clear_graphs)

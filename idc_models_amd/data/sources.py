@@ -102,8 +102,13 @@ def cifar10_dataset(root: str, train: bool = True) -> ArrayDataset:
 
 
 def synthetic_dataset(n: int, shape: Tuple[int, int, int] = (50, 50, 3), num_classes: int = 2,
-                      seed: int = 0, signal: float = 24.0) -> ArrayDataset:
-    """Deterministic synthetic patches: noise + a label-dependent colour/texture offset."""
+                      seed: int = 0, signal: float = 24.0, label_noise: float = 0.0) -> ArrayDataset:
+    """Deterministic synthetic patches: noise + a label-dependent colour/texture offset.
+
+    ``signal``: strength of the class offset (24 is trivially separable; the benchmark's
+    validation set uses a weak one).  ``label_noise``: each label is re-drawn uniformly with this
+    probability AFTER the images are made, so no model can exceed the noise ceiling (binary,
+    re-draw probability p: a fraction p/2 ends up flipped, held-out AUC <= 1 - p/2)."""
     rng = np.random.default_rng(seed)
     h, w, c = shape
     y = rng.integers(0, num_classes, size=n).astype(np.int64)
@@ -115,6 +120,9 @@ def synthetic_dataset(n: int, shape: Tuple[int, int, int] = (50, 50, 3), num_cla
     base += signal * shift[:, None, None, None] * chan[None, None, None, :]
     base += (signal * 0.5) * shift[:, None, None, None] * stripes
     x = np.clip(base, 0, 255).astype(np.uint8)
+    if label_noise > 0:
+        flip = rng.random(n) < label_noise
+        y = np.where(flip, rng.integers(0, num_classes, size=n), y).astype(np.int64)
     return ArrayDataset(x, y)
 
 

@@ -27,6 +27,7 @@ masking with a zero vector and weight 0, so its peers' masks cancel.
 from __future__ import annotations
 
 import collections
+import os
 from dataclasses import dataclass, field
 from typing import Callable, List, Optional, Sequence
 
@@ -121,8 +122,15 @@ class FedAvgProcess:
                  server_optimizer_fn: Optional[Callable] = None, average_bn_stats: bool = False,
                  local_epochs: int = 1, loss="binary_crossentropy", metrics=("binary_accuracy",),
                  secure_aggregation: Optional[str] = None, backend: str = "auto",
-                 concurrent_clients: int = 1):
+                 concurrent_clients: int = 1, client_batching: Optional[bool] = None):
         self.model_fn = model_fn
+        # client batching (fed/grouped.py): a rank's clients advance in lockstep through ONE
+        # grouped program, every launch covering all of them (default on, IDC_CLIENT_BATCHING=0
+        # or client_batching=False: one client at a time / `concurrent_clients` worker threads)
+        if client_batching is None:
+            client_batching = os.environ.get("IDC_CLIENT_BATCHING", "1") != "0"
+        self.client_batching = bool(client_batching)
+        self._grouped = None
         # ClientScheduler: a rank trains up to `concurrent_clients` of its clients at
         # once, each on its own worker model and HIP stream (small-batch client steps leave most
         # of an MI355X idle); aggregation still runs in client order
@@ -175,10 +183,28 @@ class FedAvgProcess:
         flat_ntr = torch.cat([t.detach().reshape(-1) for t in ntr]) if ntr else None
         return flat, flat_ntr, n_k, {k2: v[-1] for k2, v in h.history.items()}
 
+    def _grouped_trainer(self, n_clients: int, batch: int):
+        from .grouped import GroupedClientTrainer
+        g = self._grouped
+        if g is None or g.k < n_clients or g.B != batch:
+            m = self.worker()
+            g = GroupedClientTrainer(self.model_fn, self.client_optimizer_fn, self.loss, self.metric_names,
+                                     n_clients, batch, m.device)
+            self._grouped = g
+        return g
+
     def _train_clients(self, mine, state, data):
-        """Train this rank's clients: sequentially, or `concurrent` at a time on worker threads,
-        each with its own model and current HIP stream (torch's current stream is per thread, so
-        the clients' staging, metrics and kernels never order each other)."""
+        """Train this rank's clients: all at once through one grouped program (client batching),
+        sequentially, or `concurrent` at a time on worker threads, each with its own model and
+        current HIP stream (torch's current stream is per thread, so the clients' staging, metrics
+        and kernels never order each other)."""
+        if self.client_batching and len(mine) > 0 and self.local_epochs == 1:
+            from .grouped import eligible
+            sets = [data[k] for k in mine]
+            if eligible(sets, self.worker()):
+                g = self._grouped_trainer(len(mine), sets[0].batch_size)
+                res = g.train(lambda m: self._load(m, state.model), sets)
+                return dict(zip(mine, res))
         W = min(self.concurrent, len(mine))
         if W <= 1 or not torch.cuda.is_available() or self.worker().device.type != "cuda":
             return {k: self._train_client(self.worker(), state, data[k]) for k in mine}

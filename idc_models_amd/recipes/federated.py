@@ -73,7 +73,7 @@ def _fed_data(cfg: FedConfig):
 def _fed_fingerprint(cfg: FedConfig, state) -> dict:
     """What a resumed run must share with the run that wrote the state."""
     shapes = ";".join("x".join(str(d) for d in t.shape) for t in state.model.trainable)
-    return {"arch": cfg.arch, "num_clients": int(cfg.num_clients), "iid": bool(cfg.iid),
+    return {"arch": cfg.arch, "num_clients": int(cfg.num_clients),
             "secure_aggregation": str(cfg.secure_aggregation), "average_bn_stats": bool(cfg.average_bn_stats),
             "trainable_shapes": shapes}
 

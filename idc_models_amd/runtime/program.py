@@ -61,8 +61,11 @@ def fused_supported(net, loss) -> bool:
 
 class FusedProgram:
     def __init__(self, model, batch: int, training: bool, input_dtype, grad_scale: float = 1.0,
-                 use_graphs: bool = True, skip_nonfinite: bool = False):
+                 use_graphs: bool = True, skip_nonfinite: bool = False, group=None):
+        """``group``: a ``runtime.grouped.GroupRegion`` — the program is built inside copy 0 of the
+        region and every launch runs its K copies (client-batched federated training)."""
         nat.require()
+        self.group = group
         self.model = model
         self.training = training
         self.batch = batch
@@ -189,6 +192,10 @@ class FusedProgram:
         self.dual_graphs = os.environ.get("IDC_DUAL_GRAPH", "0") == "1"
         default_graphs = "fwd,bwd,opt" if self.dual_graphs else "fwd,opt"
         self.graph_segments = set(os.environ.get("IDC_GRAPH_SEGMENTS", default_graphs).split(","))
+        self.bwd_chunks = int(os.environ.get("IDC_BWD_CHUNKS", "8")) if self.use_graphs else 0
+        if self.dual_graphs or "bwd" in self.graph_segments:
+            self.bwd_chunks = 0  # the older whole-segment graph forms were asked for
+        self._bwd_graphs = None
         self.graphs: Dict[Tuple[int, int], int] = {}
         self.grad_scale = grad_scale
         # stream priorities are opt-in (IDC_MAIN_PRIO=high, IDC_SIDE_PRIO=low in plan.cpp): measured
@@ -206,6 +213,15 @@ class FusedProgram:
         else:
             self._cast_all_plan = None
         self.recast_all()
+        if group is not None:
+            # every pointer of the plan must lie in copy 0 of the region (the kernels reach copy g
+            # by adding g * stride); the other copies start as replicas of copy 0, so that even
+            # the autotuner's grouped trial launches only ever read well-formed data
+            group.validate_program(self)
+            group.replicate(self.stream)
+            self.plan.set_groups(group.k, group.stride)
+            if self._cast_all_plan is not None:
+                self._cast_all_plan.set_groups(group.k, group.stride)
         # autotuning picks tiles by timing, which may differ from run to run: a deterministic
         # program keeps the fixed default tiles (and no split-K)
         if os.environ.get("IDC_AUTOTUNE", "1") != "0" and not b.det:
@@ -270,6 +286,47 @@ class FusedProgram:
                 return name in self.graph_segments
         return True
 
+    # ---- backward as lane-split chunk graphs (plan.cpp capture_lane) ----------------------
+    def _bwd_chunks(self, nchunks: int):
+        lo, hi = self.seg["bwd"]
+        n_main = self.plan.count_lane(lo, hi, 0)
+        per = max(1, -(-n_main // max(1, nchunks)))
+        bounds, start, count = [], lo, 0
+        for i in range(lo, hi):
+            if self.plan.lane(i) == 0 and self.plan.kind(i) != nat.OP_ALLREDUCE:
+                count += 1
+                if count == per:
+                    bounds.append((start, i + 1))
+                    start, count = i + 1, 0
+        if start < hi:
+            bounds.append((start, hi))
+        return bounds
+
+    def run_bwd(self):
+        """The backward segment.  Default (IDC_BWD_CHUNKS=N, N>0): N chunks, each replayed as a
+        main-lane graph on the plan stream plus a side-lane (weight-gradient) graph forked after
+        it, so a chunk's weight gradients overlap the next chunk's data gradients; collectives of
+        a chunk (native data parallelism) follow its side graph on the comm stream.  N=0: direct
+        issue of every op with per-batch side forks (plan.cpp issue)."""
+        lo, hi = self.seg["bwd"]
+        if self.bwd_chunks <= 0:
+            self.run_range(lo, hi, graph=False)
+            return
+        plan, sh = self.plan, self._sh()
+        if self._bwd_graphs is None:
+            self._bwd_graphs = [(a, b2, plan.capture_lane(a, b2, 0, sh), plan.capture_lane(a, b2, 1, sh))
+                                for a, b2 in self._bwd_chunks(self.bwd_chunks)]
+        for a, b2, gm, gs in self._bwd_graphs:
+            if gm >= 0:
+                plan.launch(gm, sh)
+            if gs >= 0:
+                plan.fork_side(sh)
+                plan.launch_side(gs)
+            if self.native_comm is not None:
+                plan.comm_range(a, b2, sh)
+        plan.join_side(sh)
+        plan.join_comm(sh)
+
     def run_segment(self, name: str):
         if name in self.seg:
             with trace.range("seg:" + name):
@@ -280,6 +337,7 @@ class FusedProgram:
             self.plan.set_float(self.rms_index, 0, float(lr))
             self.plan.clear_graphs()
             self.graphs = {}
+            self._bwd_graphs = None
 
     def close(self):
         self.plan.clear_graphs()
@@ -309,6 +367,7 @@ class FusedStep:
         self.skip_nonfinite = skip_nonfinite
         self.progs: Dict[tuple, FusedProgram] = {}
         self._lr = model.optimizer.learning_rate if model.optimizer else None
+        self.group = None  # runtime.grouped.GroupRegion: programs run K copies (grouped.py)
 
     def _prog(self, batch: int, training: bool, dtype) -> FusedProgram:
         key = (batch, training, dtype)
@@ -316,7 +375,7 @@ class FusedStep:
         if p is None:
             gs = 1.0 / self.m.strategy.num_replicas_in_sync
             p = FusedProgram(self.m, batch, training, dtype, grad_scale=gs, use_graphs=self.use_graphs,
-                             skip_nonfinite=self.skip_nonfinite)
+                             skip_nonfinite=self.skip_nonfinite, group=self.group)
             self.progs[key] = p
         return p
 
@@ -366,10 +425,10 @@ class FusedStep:
             trace.push("seg:bwd")
             lo, hi = p.seg["bwd"]
             bucketer = strategy.bucketer(m.arena) if active and p.native_comm is None else None
-            if p.native_comm is not None:
+            if p.native_comm is not None or bucketer is None:
                 # the plan itself issues every bucket all-reduce on the communicator's stream and
                 # joins it back into the main lane at the end of the range
-                p.run_range(lo, hi)
+                p.run_bwd()
             elif bucketer is not None and p.bwd_marks:
                 # backward in bucket-aligned segments: each bucket's all-reduce is issued from
                 # the comm stream as soon as its gradients are final — the comm stream waits for
@@ -392,9 +451,8 @@ class FusedStep:
                 p.stream.wait_stream(cs)
             else:
                 p.run_range(lo, hi)
-                if bucketer is not None:
-                    with torch.cuda.stream(p.stream):
-                        bucketer.finish()
+                with torch.cuda.stream(p.stream):
+                    bucketer.finish()
             trace.pop()
         if p.host_optimizer:
             with torch.cuda.stream(p.stream):

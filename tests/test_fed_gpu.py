@@ -114,9 +114,10 @@ def test_fedavg_secure_mask_equals_plain_on_gpu(monkeypatch):
     assert p_m["loss"] == pytest.approx(s_m["loss"], rel=1e-6)
 
 
-def test_fedavg_concurrent_clients_match_sequential(monkeypatch):
+def test_fedavg_concurrent_and_batched_clients_match_sequential(monkeypatch):
     """ClientScheduler: four clients trained concurrently on their own worker models
-    and HIP streams give BITWISE the round of training them one after another on one model
+    and HIP streams, or batched through one grouped program, give BITWISE the round of training
+    them one after another on one model
     (fixed-order reductions, IDC_DETERMINISTIC=1; every client starts from the same statistics
     shifts), and a second concurrent round reproduces it."""
     import copy
@@ -131,21 +132,33 @@ def test_fedavg_concurrent_clients_match_sequential(monkeypatch):
     base = build_model("densenet121", None, 1, seed=3)
     ds = synthetic_dataset(4 * 96, (50, 50, 3), 2, seed=7)
 
-    def run(conc):
+    def run(conc, batching=False, rounds=1):
         # fresh batched views per run: a BatchedDataset reshuffles on every iteration
         clients = [c.batch(32, True, 1000, True, seed=k) for k, c in enumerate(contiguous_clients(ds, 4, 96))]
         proc = build_federated_averaging_process(
             lambda: Model(copy.deepcopy(base), OneDeviceStrategy(dev)), lambda: RMSprop(1e-4),
-            average_bn_stats=True, backend="fused", concurrent_clients=conc)
+            average_bn_stats=True, backend="fused", concurrent_clients=conc, client_batching=batching)
         state = proc.initialize()
-        state, met = proc.next(state, clients)
+        for _ in range(rounds):
+            state, met = proc.next(state, clients)
         torch.cuda.synchronize()
+        if batching:
+            assert proc._grouped is not None and proc._grouped.k == 4  # the grouped path ran
         w = torch.cat([w.reshape(-1) for w in state.model.trainable])
         return w, torch.cat([w.reshape(-1) for w in state.model.non_trainable]), met
 
     w1, n1, m1 = run(1)
     w4, n4, m4 = run(4)
     w4b, _, _ = run(4)
+    # client batching: the four clients as ONE grouped program, every launch
+    # covering all of them, give bitwise the sequential round -- and the second round too
+    wg, ng, mg = run(1, batching=True)
+    assert torch.equal(w1, wg), float((w1 - wg).abs().max())
+    assert torch.equal(n1, ng)
+    assert all(m1[k] == pytest.approx(mg[k], rel=1e-6) for k in m1), (m1, mg)
+    w1r, n1r, _ = run(1, rounds=2)
+    wgr, ngr, _ = run(1, batching=True, rounds=2)
+    assert torch.equal(w1r, wgr) and torch.equal(n1r, ngr)
     w0 = torch.cat([p.detach().reshape(-1).to(dev) for p in base.trainable_weights])
     assert float((w1 - w0).norm()) > 0  # the round trained
     assert torch.equal(w1, w4), float((w1 - w4).abs().max())
@@ -153,3 +166,36 @@ def test_fedavg_concurrent_clients_match_sequential(monkeypatch):
     assert torch.equal(w4, w4b)
     # the weights are bitwise; the reported metrics come from the per-client fit logs
     assert set(m1) == set(m4) and all(m1[k] == pytest.approx(m4[k], rel=1e-6) for k in m1), (m1, m4)
+
+
+def test_fedavg_batched_clients_mobilenetv2_matches_sequential():
+    """Client batching with what ships (autotuned tiles, float-atomic statistics; MobileNetV2 has
+    no fixed-order mode): the grouped round's update is as close to the sequential round's as two
+    sequential rounds are to each other."""
+    from idc_models_amd.data import contiguous_clients, synthetic_dataset
+    from idc_models_amd.engine import Model, RMSprop
+    from idc_models_amd.fed import build_federated_averaging_process
+    from idc_models_amd.models import build_model
+    from idc_models_amd.parallel import OneDeviceStrategy
+    base = build_model("mobilenetv2", None, 1, seed=11)
+    ds = synthetic_dataset(8 * 64, (50, 50, 3), 2, seed=12)
+
+    def run(batching):
+        clients = [c.batch(32, True, 1000, True, seed=k) for k, c in enumerate(contiguous_clients(ds, 8, 64))]
+        proc = build_federated_averaging_process(
+            lambda: Model(copy.deepcopy(base), OneDeviceStrategy(DEV)), lambda: RMSprop(1e-4),
+            average_bn_stats=True, backend="fused", client_batching=batching)
+        s0 = proc.initialize()
+        s1, met = proc.next(s0, clients)
+        d = torch.cat([(a - b).reshape(-1) for a, b in zip(s1.model.trainable, s0.model.trainable)]).double()
+        nt = torch.cat([w.reshape(-1) for w in s1.model.non_trainable]).double()
+        return d, nt, met
+
+    ds_a, nt_a, m_a = run(False)
+    ds_b, nt_b, _ = run(False)
+    dg, ntg, mg = run(True)
+    floor = float((ds_a - ds_b).norm() / ds_a.norm())
+    rel = float((dg - ds_a).norm() / ds_a.norm())
+    assert rel <= 3 * floor + 2e-2, (rel, floor)
+    assert float((ntg - nt_a).norm() / nt_a.norm()) <= 3 * float((nt_b - nt_a).norm() / nt_a.norm()) + 1e-3
+    assert mg["loss"] == pytest.approx(m_a["loss"], rel=0.05)
