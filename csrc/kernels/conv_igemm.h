@@ -83,6 +83,12 @@ constexpr int TILE_BIG128 = 101;
 constexpr int TILE_BIG256 = 102;
 constexpr int TILE_BIG64 = 103;
 constexpr int TILE_BIG128D = 104;  // 256 x 128 with three LDS buffers
+// deep-ring LDS-DMA small tiles (conv_ring.hip): TILE_RING + variant, variants
+// 0: 64x32  1: 64x64  2: 32x32  3: 32x64  4: 64x128
+constexpr int TILE_RING = 110;
+constexpr int TILE_RING_N = 5;
+bool conv_ring_ok(const ConvArgs& a, bool a_f32);
+hipError_t conv_ring(const ConvArgs& a, int variant, bool a_f32, hipStream_t st);
 bool conv_big_ok(const ConvArgs& a, bool a_f32);
 hipError_t conv_big(const ConvArgs& a, int bn, bool a_f32, hipStream_t st);
 hipError_t conv_igemm(const ConvArgs& a, int tile, bool a_f32, hipStream_t st);
@@ -92,5 +98,6 @@ int conv_pick_tile(int M, int Cout);
 int conv_num_tiles();
 int conv_tile_bm(int t);
 int conv_tile_bn(int t);
+int conv_tile_bk(int t);
 
 }  // namespace idc

@@ -13,22 +13,29 @@ hipError_t conv_igemm_group3(const ConvArgs& a, int tile, bool is1x1, bool a_f32
                               hipStream_t st);
 hipError_t conv_igemm_group4(const ConvArgs& a, int tile, bool is1x1, bool a_f32, int pro, int epi,
                               hipStream_t st);
+hipError_t conv_igemm_group5(const ConvArgs& a, int tile, bool is1x1, bool a_f32, int pro, int epi,
+                              hipStream_t st);
 
-struct TileInfo { int bm, bn; };
+struct TileInfo { int bm, bn, bk; };
 static const TileInfo kTiles[] = {
-    {128, 128}, {128, 64}, {256, 32}, {64, 64}, {64, 32},   // BK 32
-    {128, 128}, {128, 64}, {128, 32}, {64, 64}, {64, 32},   // BK 64
-    {256, 32}, {64, 128},                                  // BK 64
-    {64, 32}, {128, 32}, {64, 64}, {64, 128}, {128, 64},   // BK 128: half the K steps of BK 64
-    {64, 32}, {64, 64}};  // BK 256: deep-K, small-M layers (stages 3-4) are K-loop latency bound
+    {128, 128, 32}, {128, 64, 32}, {256, 32, 32}, {64, 64, 32}, {64, 32, 32},  // BK 32
+    {128, 128, 64}, {128, 64, 64}, {128, 32, 64}, {64, 64, 64}, {64, 32, 64},  // BK 64
+    {256, 32, 64}, {64, 128, 64},                                              // BK 64
+    // BK 128: half the K steps of BK 64
+    {64, 32, 128}, {128, 32, 128}, {64, 64, 128}, {64, 128, 128}, {128, 64, 128},
+    {64, 32, 256}, {64, 64, 256},  // BK 256: deep-K, small-M layers (stages 3-4)
+    // 32-row tiles (conv_igemm_g5.hip): twice the workgroups on small-M layers
+    {32, 32, 64}, {32, 32, 128}, {32, 64, 64}, {32, 64, 128}};
 
 int conv_num_tiles() { return (int)(sizeof(kTiles) / sizeof(kTiles[0])); }
 int conv_tile_bm(int t) { return kTiles[t].bm; }
 int conv_tile_bn(int t) { return kTiles[t].bn; }
+int conv_tile_bk(int t) { return kTiles[t].bk; }
 
 hipError_t conv_igemm(const ConvArgs& a, int tile, bool a_f32, hipStream_t st) {
+  const bool ring = tile >= TILE_RING && tile < TILE_RING + TILE_RING_N;
   if (tile < 0 || (tile >= conv_num_tiles() && tile != TILE_HALO && tile != TILE_BIG128 && tile != TILE_BIG256 &&
-                   tile != TILE_BIG64 && tile != TILE_BIG128D))
+                   tile != TILE_BIG64 && tile != TILE_BIG128D && !ring))
     return hipErrorInvalidValue;
   const bool is1x1 = a.KH == 1 && a.KW == 1 && a.SH == 1 && a.SW == 1 && a.PT == 0 && a.PL == 0;
   const int pro = a.bpro.mode != 0 ? 2 : (a.pro.mode != 0 || a.pro.act != ACT_NONE) ? 1 : 0;
@@ -40,17 +47,22 @@ hipError_t conv_igemm(const ConvArgs& a, int tile, bool a_f32, hipStream_t st) {
   if (tile == TILE_BIG128 || tile == TILE_BIG256 || tile == TILE_BIG64 || tile == TILE_BIG128D)
     return conv_big(a, tile == TILE_BIG256 ? 256 : tile == TILE_BIG128 ? 128 : tile == TILE_BIG128D ? -128 : 64,
                     a_f32, st);
+  if (ring) {
+    if (a.ksplit > 1) return hipErrorInvalidValue;
+    return conv_ring(a, tile - TILE_RING, a_f32, st);
+  }
   if (tile == TILE_HALO) {
     if (a.ksplit > 1 || pro == 2 || epi == 2) return hipErrorInvalidValue;
     return conv3x3_halo(a, a_f32, st);
   }
-  const int group = tile < 4 ? 0 : tile < 8 ? 1 : tile < 12 ? 2 : tile < 16 ? 3 : 4;
+  const int group = tile < 4 ? 0 : tile < 8 ? 1 : tile < 12 ? 2 : tile < 16 ? 3 : tile < 19 ? 4 : 5;
   switch (group) {
     case 0: return conv_igemm_group0(a, tile, is1x1, a_f32, pro, epi, st);
     case 1: return conv_igemm_group1(a, tile, is1x1, a_f32, pro, epi, st);
     case 2: return conv_igemm_group2(a, tile, is1x1, a_f32, pro, epi, st);
     case 3: return conv_igemm_group3(a, tile, is1x1, a_f32, pro, epi, st);
-    default: return conv_igemm_group4(a, tile, is1x1, a_f32, pro, epi, st);
+    case 4: return conv_igemm_group4(a, tile, is1x1, a_f32, pro, epi, st);
+    default: return conv_igemm_group5(a, tile, is1x1, a_f32, pro, epi, st);
   }
 }
 

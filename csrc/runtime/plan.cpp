@@ -761,6 +761,13 @@ bool py_big_ok(py::bytes payload, int a_f32) {
   return conv_big_ok(a, a_f32 != 0);
 }
 int py_pick_splits(int M, int K, int Cout) { return wgrad_pick_splits(M, K, Cout); }
+bool py_ring_ok(py::bytes payload, int a_f32) {
+  std::string s = payload;
+  if (s.size() != sizeof(ConvArgs)) throw std::runtime_error("ConvArgs size mismatch");
+  ConvArgs a;
+  std::memcpy(&a, s.data(), sizeof(a));
+  return conv_ring_ok(a, a_f32 != 0);
+}
 
 int py_effective_splits(py::bytes payload, int splits) {
   std::string s = payload;
@@ -905,11 +912,15 @@ PYBIND11_MODULE(_idc_native, m) {
   m.attr("TILE_BIG64") = TILE_BIG64;
   m.attr("TILE_BIG128D") = TILE_BIG128D;
   m.def("pick_splits", &py_pick_splits);
+  m.def("ring_ok", &py_ring_ok);
+  m.attr("TILE_RING") = TILE_RING;
+  m.attr("TILE_RING_N") = TILE_RING_N;
   m.def("effective_splits", &py_effective_splits);
   m.def("rows_grid", &rows_grid);
   m.def("num_tiles", &conv_num_tiles);
   m.def("tile_bm", &conv_tile_bm);
   m.def("tile_bn", &conv_tile_bn);
+  m.def("tile_bk", &conv_tile_bk);
   m.def("rmsprop", &py_rmsprop);
   m.def("secagg_mask", &py_secagg_mask);
   m.def("secagg_unmask", &py_secagg_unmask);

@@ -77,8 +77,11 @@ def _conv_candidates(ext, M: int, cout: int, payload: bytes = None, halo: bool =
     ntile = ext.num_tiles()
     cap = 32 if cout <= 32 else (64 if cout <= 64 else 128)
     out = []
+    no32 = os.environ.get("IDC_NO_TILE32", "0") == "1"
     for t in range(ntile):
         bm, bn = ext.tile_bm(t), ext.tile_bn(t)
+        if bm < 64 and no32:
+            continue
         if bn > cap:
             continue
         if bm > 64 and M <= 2 * 64:
@@ -86,6 +89,11 @@ def _conv_candidates(ext, M: int, cout: int, payload: bytes = None, halo: bool =
         out.append(t)
     if payload is not None and (halo or os.environ.get("IDC_HALO", "0") == "1") and ext.halo_ok(payload):
         out.append(ext.TILE_HALO)
+    # deep-ring LDS-DMA small tiles (conv_ring.hip): forward convs with a bf16 operand
+    if payload is not None and os.environ.get("IDC_CONV_RING", "1") != "0" and ext.ring_ok(payload, a_f32):
+        for v, bn in ((0, 32), (1, 64), (2, 32), (3, 64), (4, 128)):
+            if bn <= cap:
+                out.append(ext.TILE_RING + v)
     # 256 x {128, 256} global_load_lds tiles for plain wide layers (conv_big.hip), when they
     # still make >= 128 workgroups
     if payload is not None and os.environ.get("IDC_CONV_BIG", "1") != "0" and ext.big_ok(payload, a_f32):
@@ -103,8 +111,7 @@ def _tile_shape(ext, t: int):
         return 256, 256, 64
     if t >= ext.num_tiles():
         return None
-    bk = 256 if t >= 17 else (128 if t >= 12 else (64 if t >= 5 else 32))
-    return ext.tile_bm(t), ext.tile_bn(t), bk
+    return ext.tile_bm(t), ext.tile_bn(t), ext.tile_bk(t)
 
 
 def _splits_for(ext, a, t: int, M: int, slab_floats: int):

@@ -313,7 +313,7 @@ class Builder:
 
     @staticmethod
     def _conv_row_tiles(M: int) -> int:
-        return -(-M // 64)  # the most row tiles any conv tile shape (BM >= 64) produces
+        return -(-M // 32)  # the most row tiles any conv tile shape (BM >= 32) produces
 
     def _rows_grid(self, M: int, C: int, per: int) -> int:
         return int(nat.load().rows_grid(int(M), int(C), int(per)))
@@ -507,7 +507,7 @@ class Builder:
     def _splitk(self, a, M: int, cout: int):
         if self.splitk_slab is None:
             self.splitk_slab = self.alloc((self.SLAB_FLOATS,), F32)
-        tiles = -(-M // 64) * -(-cout // 32)  # the smallest tile shape has the most tiles
+        tiles = -(-M // 32) * -(-cout // 32)  # the smallest tile shape (32 x 32) has the most tiles
         t = self.alloc((tiles,), torch.int32)
         self.tickets.append(t)
         a.slab, a.tickets, a.ksplit = self.splitk_slab.data_ptr(), t.data_ptr(), 1

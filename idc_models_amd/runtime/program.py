@@ -192,7 +192,9 @@ class FusedProgram:
         self.dual_graphs = os.environ.get("IDC_DUAL_GRAPH", "0") == "1"
         default_graphs = "fwd,bwd,opt" if self.dual_graphs else "fwd,opt"
         self.graph_segments = set(os.environ.get("IDC_GRAPH_SEGMENTS", default_graphs).split(","))
-        self.bwd_chunks = int(os.environ.get("IDC_BWD_CHUNKS", "8")) if self.use_graphs else 0
+        # opt-in: measured slower than direct issue on DenseNet-121 bs256 (4.62-5.0 vs 4.45-4.53
+        # ms/step at 4-16 chunks): the side lane then waits for whole main chunks
+        self.bwd_chunks = int(os.environ.get("IDC_BWD_CHUNKS", "0")) if self.use_graphs else 0
         if self.dual_graphs or "bwd" in self.graph_segments:
             self.bwd_chunks = 0  # the older whole-segment graph forms were asked for
         self._bwd_graphs = None

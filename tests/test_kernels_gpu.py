@@ -73,7 +73,7 @@ def test_conv_fwd(fn, N, H, Cin, Cout, k, s, pads, outhw):
     assert relerr(y, ref) < 1e-2
 
 
-@pytest.mark.parametrize("tile", list(range(19)))
+@pytest.mark.parametrize("tile", list(range(23)))
 def test_conv_every_tile_large_m_odd_ktiles(fn, tile):
     """Every tile config at scale: M = 40000 with an odd K-tile count (K = 392 -> 7 / 13 tiles)
     exercises the pipeline tail + epilogue LDS aliasing (a missing barrier once raced here)."""
@@ -87,7 +87,7 @@ def test_conv_every_tile_large_m_odd_ktiles(fn, tile):
     assert relerr(st[:Cout], ref.sum((0, 1, 2))) < 1e-2
 
 
-@pytest.mark.parametrize("tile,ks", [(4, 2), (9, 4), (12, 2), (17, 2), (18, 4), (8, 8), (7, 3)])
+@pytest.mark.parametrize("tile,ks", [(4, 2), (9, 4), (12, 2), (17, 2), (18, 4), (8, 8), (7, 3), (19, 4), (22, 2)])
 def test_conv_split_k_matches_reference(fn, tile, ks):
     """Split-K (in-launch last-arriver reduction) on a small-M deep-K layer with the BN prologue
     and output statistics; launched three times to check the modulo tickets realign."""
@@ -737,3 +737,44 @@ def test_avgpool_bwd_scatter_bn_epilogue_f32(fn, H):
         assert out[:, -1].abs().max().item() == 0 and out[:, :, -1].abs().max().item() == 0
     assert relerr(gsum, dZ.sum((0, 1, 2))) < 1e-2
     assert relerr(gsumx, (dZ * xhat).sum((0, 1, 2))) < 2e-2
+
+
+@pytest.mark.parametrize("variant", range(5))
+@pytest.mark.parametrize("case", ["1x1_ktail_bn", "3x3_bn", "1x1_plain_bias"])
+def test_conv_ring_tiles_match_reference(fn, variant, case):
+    """Deep-ring LDS-DMA tiles (conv_ring.hip): 1x1 with a K tail (Cin = 544, DenseNet's 64+32k)
+    and 3x3 'same' (padding zero AFTER the activation), both through the pending-BN prologue with
+    shifted output statistics; and a plain 1x1 with bias + ReLU epilogue."""
+    from idc_models_amd.ops import _native as nat
+    tile = nat.load().TILE_RING + variant
+    g0 = torch.Generator(device="cpu").manual_seed(variant)
+    if case == "1x1_ktail_bn":
+        N, H, Cin, Cout, k, pads = 16, 6, 544, 128, 1, (0, 0)
+    elif case == "3x3_bn":
+        N, H, Cin, Cout, k, pads = 8, 13, 128, 32, 3, (1, 1)
+    else:
+        N, H, Cin, Cout, k, pads = 16, 9, 96, 64, 1, (0, 0)
+    x = bf(torch.randn(N, H, H, Cin, generator=g0).to(DEV) * 2 + 0.5)
+    w = bf(torch.randn(k, k, Cin, Cout, generator=g0).to(DEV) * (0.5 / (k * Cin ** 0.5)))
+    if case == "1x1_plain_bias":
+        bias = torch.randn(Cout, generator=g0).to(DEV) * 0.1
+        y = fn.conv2d(x.to(torch.bfloat16), w, pads=pads, bias=bias, act=1, tile=tile)
+        ref = torch.relu(ref_conv(x, w, 1, (0, 0, 0, 0)) + bias)
+        assert relerr(y.float(), ref) < 1e-2
+        return
+    st_in = torch.cat([x.sum((0, 1, 2)), (x * x).sum((0, 1, 2))])
+    g = torch.rand(Cin, generator=g0).to(DEV) + 0.5
+    be = torch.randn(Cin, generator=g0).to(DEV) * 0.1
+    bn = fn.BN(stats=st_in, gamma=g, beta=be, count=N * H * H, eps=1e-3, act=1)
+    mean = x.mean((0, 1, 2))
+    var = (x * x).mean((0, 1, 2)) - mean * mean
+    xa = torch.relu((x - mean) / torch.sqrt(var + 1e-3) * g + be)
+    ref = ref_conv(xa, w, 1, (pads[0], pads[0], pads[1], pads[1]))
+    shift = torch.randn(Cout, generator=g0).to(DEV) * 0.1
+    for _ in range(2):
+        st = torch.zeros(2 * Cout, device=DEV)
+        y = fn.conv2d(x.to(torch.bfloat16), w, pads=pads, pro=bn, tile=tile, stats=st, stats_shift=shift)
+        assert relerr(y.float(), ref) < 1e-2, case
+        yb = y.float()
+        assert relerr(st[:Cout], (yb - shift).sum((0, 1, 2))) < 1e-3
+        assert relerr(st[Cout:], ((yb - shift) ** 2).sum((0, 1, 2))) < 1e-3

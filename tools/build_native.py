@@ -31,8 +31,10 @@ SOURCES = [
     "kernels/conv_igemm_g2.hip",
     "kernels/conv_igemm_g3.hip",
     "kernels/conv_igemm_g4.hip",
+    "kernels/conv_igemm_g5.hip",
     "kernels/conv3x3_halo.hip",
     "kernels/conv_big.hip",
+    "kernels/conv_ring.hip",
     "kernels/conv_wgrad.hip",
     "kernels/nn_kernels.hip",
     "kernels/dwconv.hip",

@@ -15,6 +15,12 @@ __device__ unsigned long long g_stamps[4096][16];
 #include "conv_igemm_impl.h"
 
 using namespace idc;
+namespace idc {
+LaunchGroups& launch_groups() {  // (defined in nn_kernels.hip in the extension)
+  static LaunchGroups l;
+  return l;
+}
+}  // namespace idc
 
 static void* dalloc(size_t bytes) {
   void* p = nullptr;
@@ -102,6 +108,11 @@ static void run_case(const Case& c) {
 }
 
 int main() {
+  // DenseNet-121 bs256 stage-1/2 1x1 shapes (M = 43264 / 9216)
+  run_case<256, 32, 32, 4, 1>({"fwd s1 1x1 pro1 epi0 K64 t2", 43264, 64, 128, 1, 0, 0, 0});
+  run_case<64, 32, 64, 2, 2>({"fwd s1 1x1 pro1 epi0 K64 t9", 43264, 64, 128, 1, 0, 0, 0});
+  run_case<64, 32, 64, 2, 2>({"fwd s1 1x1 pro0 epi0 K64 t9", 43264, 64, 128, 0, 0, 0, 0});
+  run_case<64, 32, 64, 2, 2>({"fwd s2 1x1 pro1 epi0 K480 t9", 9216, 480, 128, 1, 0, 0, 0});
   // DenseNet-121 bs256 tail shapes (stage 4: M=256, stage 3: M=2304)
   run_case<64, 32, 64, 2, 2>({"fwd s4 1x1 pro1 epi0 K544", 256, 544, 128, 1, 0, 0, 0});
   run_case<64, 32, 64, 2, 2>({"fwd s3 1x1 pro1 epi0 K544", 2304, 544, 128, 1, 0, 0, 0});
