@@ -90,7 +90,9 @@ def _conv_candidates(ext, M: int, cout: int, payload: bytes = None, halo: bool =
     if payload is not None and (halo or os.environ.get("IDC_HALO", "0") == "1") and ext.halo_ok(payload):
         out.append(ext.TILE_HALO)
     # deep-ring LDS-DMA small tiles (conv_ring.hip): forward convs with a bf16 operand
-    if payload is not None and os.environ.get("IDC_CONV_RING", "1") != "0" and ext.ring_ok(payload, a_f32):
+    # (opt-in: measured 20-100 % slower than the best general tile on every DenseNet-121 forward
+    # shape, tools/bench_ring.py)
+    if payload is not None and os.environ.get("IDC_CONV_RING", "0") == "1" and ext.ring_ok(payload, a_f32):
         for v, bn in ((0, 32), (1, 64), (2, 32), (3, 64), (4, 128)):
             if bn <= cap:
                 out.append(ext.TILE_RING + v)
