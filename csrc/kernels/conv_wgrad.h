@@ -31,10 +31,17 @@ __device__ __forceinline__ void gshift(WgradArgs& a, long long o) {
   a.part = gsh(a.part, o);
 }
 
-hipError_t conv_wgrad(WgradArgs a, int splits, bool g_f32, hipStream_t st);
+// variant 0: the general kernel; 1..wgrad_num_variants()-1: the large-tile DMA kernel
+// (wgrad_big.hip) where wgrad_big_ok holds, else the general kernel
+hipError_t conv_wgrad(WgradArgs a, int splits, bool g_f32, hipStream_t st, int variant = 0);
+hipError_t wgrad_big(WgradArgs a, int splits, bool g_f32, int variant, hipStream_t st);
+bool wgrad_big_ok(const WgradArgs& a, bool g_f32, int variant);
+int wgrad_big_pick_splits(int M, int K, int Cout, int variant);
+int wgrad_num_variants();
+int wgrad_variant_bp(int variant);
 // dw[i] += sum_{z < splits} part[z * n + i], in slice order
 hipError_t wgrad_reduce(const float* part, float* dw, long long n, int splits, hipStream_t st);
-int wgrad_effective_splits(const WgradArgs& a, int splits);
+int wgrad_effective_splits(const WgradArgs& a, int splits, int variant = 0);
 int wgrad_pick_splits(int M, int K, int Cout);
 
 }  // namespace idc

@@ -531,7 +531,8 @@ static bool wgrad_big_tile(const WgradArgs& a) {
   return wgrad_big_on() && a.Cout >= 128 && a.KH * a.KW * a.Cin >= 512 && a.N * a.Ho * a.Wo <= 16384;
 }
 
-hipError_t conv_wgrad(WgradArgs a, int splits, bool g_f32, hipStream_t st) {
+hipError_t conv_wgrad(WgradArgs a, int splits, bool g_f32, hipStream_t st, int variant) {
+  if (variant > 0 && wgrad_big_ok(a, g_f32, variant)) return wgrad_big(a, splits, g_f32, variant, st);
   if (wgrad_halo_ok(a, g_f32)) {
     const int groups = wgrad_halo_groups(a, splits);
     const int ipw = (a.N + groups - 1) / groups;
@@ -560,11 +561,12 @@ hipError_t conv_wgrad(WgradArgs a, int splits, bool g_f32, hipStream_t st) {
   return launch_wg<64, 128, 32, 2, 2>(a, is1x1, g_f32, pro, splits, st);
 }
 
-int wgrad_effective_splits(const WgradArgs& a, int splits) {
-  if (wgrad_halo_ok(a, false)) return wgrad_halo_groups(a, splits);
+int wgrad_effective_splits(const WgradArgs& a, int splits, int variant) {
+  const bool big = variant > 0 && wgrad_big_ok(a, false, variant);
+  if (!big && wgrad_halo_ok(a, false)) return wgrad_halo_groups(a, splits);
   const int M = a.N * a.Ho * a.Wo;
   if (splits < 1) splits = 1;
-  const int bp = wgrad_bp(a.Cout);
+  const int bp = big ? wgrad_variant_bp(variant) : wgrad_bp(a.Cout);
   int per = (M + splits - 1) / splits;
   per = (per + bp - 1) / bp * bp;
   return (M + per - 1) / per;

@@ -546,10 +546,10 @@ class Plan {
       }
       case OP_WGRAD: {
         const WgradArgs& a = as<WgradArgs>(op);
-        check(conv_wgrad(a, op.i[0], op.i[1] != 0, st), "conv_wgrad");
+        check(conv_wgrad(a, op.i[0], op.i[1] != 0, st, op.i[2]), "conv_wgrad");
         if (a.part) {  // deterministic mode: fixed-order sum of the per-slice partials
           const long long n = (long long)a.KH * a.KW * (a.cin_real ? a.cin_real : a.Cin) * a.Cout;
-          check(wgrad_reduce(a.part, a.dw, n, wgrad_effective_splits(a, op.i[0]), st), "wgrad_reduce");
+          check(wgrad_reduce(a.part, a.dw, n, wgrad_effective_splits(a, op.i[0], op.i[2]), st), "wgrad_reduce");
         }
         break;
       }
@@ -693,13 +693,22 @@ void py_conv(py::bytes payload, int tile, int a_f32, uintptr_t stream) {
   check(conv_igemm(a, tile, a_f32 != 0, reinterpret_cast<hipStream_t>(stream)), "conv_igemm");
 }
 
-void py_wgrad(py::bytes payload, int splits, int g_f32, uintptr_t stream) {
+void py_wgrad(py::bytes payload, int splits, int g_f32, uintptr_t stream, int variant) {
   std::string s = payload;
   if (s.size() != sizeof(WgradArgs)) throw std::runtime_error("WgradArgs size mismatch");
   WgradArgs a;
   std::memcpy(&a, s.data(), sizeof(a));
   if (splits <= 0) splits = wgrad_pick_splits(a.N * a.Ho * a.Wo, a.KH * a.KW * a.Cin, a.Cout);
-  check(conv_wgrad(a, splits, g_f32 != 0, reinterpret_cast<hipStream_t>(stream)), "conv_wgrad");
+  if (splits <= 0 && variant > 0) splits = wgrad_big_pick_splits(a.N * a.Ho * a.Wo, a.KH * a.KW * a.Cin, a.Cout, variant);
+  check(conv_wgrad(a, splits, g_f32 != 0, reinterpret_cast<hipStream_t>(stream), variant), "conv_wgrad");
+}
+
+bool py_wgrad_big_ok(py::bytes payload, int g_f32, int variant) {
+  std::string s = payload;
+  if (s.size() != sizeof(WgradArgs)) throw std::runtime_error("WgradArgs size mismatch");
+  WgradArgs a;
+  std::memcpy(&a, s.data(), sizeof(a));
+  return wgrad_big_ok(a, g_f32 != 0, variant);
 }
 
 py::dict struct_sizes() {
@@ -900,7 +909,11 @@ PYBIND11_MODULE(_idc_native, m) {
       .def("clear_graphs", &Plan::clear_graphs)
       .def("describe", &Plan::describe);
   m.def("conv", &py_conv);
-  m.def("wgrad", &py_wgrad);
+  m.def("wgrad", &py_wgrad, py::arg("payload"), py::arg("splits"), py::arg("g_f32"), py::arg("stream"),
+        py::arg("variant") = 0);
+  m.def("wgrad_big_ok", &py_wgrad_big_ok);
+  m.def("wgrad_big_pick_splits", &wgrad_big_pick_splits);
+  m.def("wgrad_num_variants", &wgrad_num_variants);
   m.def("struct_sizes", &struct_sizes);
   m.def("pick_tile", &py_pick_tile);
   m.def("halo_ok", &py_halo_ok);

@@ -193,30 +193,49 @@ def conv2d_dgrad(dy: torch.Tensor, kernel_hwio: torch.Tensor, in_hw: Tuple[int, 
     return dx
 
 
-def conv2d_wgrad(x: torch.Tensor, dy: torch.Tensor, kernel_shape, stride=(1, 1), pads=(0, 0),
-                 pro: Optional[BN] = None, cin_real: int = 0, splits: int = -1,
-                 out: Optional[torch.Tensor] = None, gpro: Optional[nat.BwdAff] = None) -> torch.Tensor:
-    """dW (Keras HWIO fp32) accumulated into ``out`` (zeros if not given)."""
+def _wgrad_args(x, dy, kernel_shape, stride, pads, pro, cin_real, out, gpro):
     N, H, W, Cin = x.shape
     _, Ho, Wo, Cout = dy.shape
-    kh, kw = kernel_shape[0], kernel_shape[1]
-    creal = cin_real or Cin
-    if out is None:
-        out = torch.zeros((kh, kw, creal, Cout), dtype=torch.float32, device=x.device)
     a = nat.WgradArgs()
     a.x = x.data_ptr()
     a.N, a.H, a.W, a.Cin, a.ldx = N, H, W, Cin, Cin
     a.g, a.ldg = dy.data_ptr(), Cout
     a.Ho, a.Wo, a.Cout = Ho, Wo, Cout
-    a.KH, a.KW, a.SH, a.SW = kh, kw, stride[0], stride[1]
+    a.KH, a.KW, a.SH, a.SW = kernel_shape[0], kernel_shape[1], stride[0], stride[1]
     a.PT, a.PL = pads
     a.pro = pro.args() if pro is not None else _ident()
-    a.dw = out.data_ptr()
+    a.dw = out.data_ptr() if out is not None else 0
     a.scale = 1.0
     a.cin_real = cin_real
     if gpro is not None:
         a.gpro = gpro
-    nat.require().wgrad(nat.raw(a), splits, 1 if dy.dtype == torch.float32 else 0, nat.stream_handle())
+    return a
+
+
+def wgrad_big_applies(x, dy, kernel_shape, stride=(1, 1), pads=(0, 0), variant: int = 1) -> bool:
+    """Whether ``conv2d_wgrad(..., variant=variant)`` runs the large-tile kernel (wgrad_big.hip)."""
+    a = _wgrad_args(x, dy, kernel_shape, stride, pads, None, 0, None, None)
+    return bool(nat.require().wgrad_big_ok(nat.raw(a), 1 if dy.dtype == torch.float32 else 0, variant))
+
+
+def conv2d_wgrad(x: torch.Tensor, dy: torch.Tensor, kernel_shape, stride=(1, 1), pads=(0, 0),
+                 pro: Optional[BN] = None, cin_real: int = 0, splits: int = -1,
+                 out: Optional[torch.Tensor] = None, gpro: Optional[nat.BwdAff] = None,
+                 variant: int = 0, part: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """dW (Keras HWIO fp32) accumulated into ``out`` (zeros if not given).  ``variant`` > 0 picks a
+    large-tile kernel (``wgrad_big.hip``) where it applies; ``part`` (zeros, with ``splits``)
+    selects the deterministic per-slice partial slab, summed here in slice order."""
+    Cin, Cout = x.shape[3], dy.shape[3]
+    kh, kw = kernel_shape[0], kernel_shape[1]
+    creal = cin_real or Cin
+    if out is None:
+        out = torch.zeros((kh, kw, creal, Cout), dtype=torch.float32, device=x.device)
+    a = _wgrad_args(x, dy, kernel_shape, stride, pads, pro, cin_real, out, gpro)
+    if part is not None:
+        a.part, a.part_floats = part.data_ptr(), part.numel()
+    nat.require().wgrad(nat.raw(a), splits, 1 if dy.dtype == torch.float32 else 0, nat.stream_handle(), variant)
+    if part is not None:
+        out += part.view(-1, out.numel()).sum(0).view_as(out)
     return out
 
 

@@ -192,23 +192,42 @@ def _autotune_plan_unlocked(plan, stream, verbose: bool = False, reset_tickets=N
             f32 = plan.get_int(i, 1)
             s0 = max(plan.get_int(i, 0), 1)
             M = a.N * a.Ho * a.Wo
-            key = ("wgrad", M, a.Cout, a.Cin, a.KH, a.KW, a.SH, f32, int(a.pro.mode != 0 or a.pro.act != 0),
+            key = ("wgrad2", M, a.Cout, a.Cin, a.KH, a.KW, a.SH, f32, int(a.pro.mode != 0 or a.pro.act != 0),
                    int(a.gpro.mode != 0))
             best = _CACHE.get(key)
             if best is None:
                 cands = sorted({max(1, s0 // 4), max(1, s0 // 2), s0, s0 * 2, s0 * 4})
                 cands = [s for s in cands if (M + s - 1) // s >= 32] or [1]
                 times = {}
+                plan.set_int(i, 2, 0)
                 for s in cands:
                     plan.set_int(i, 0, s)
-                    times[s] = _time_op(plan, i, stream)
+                    times[(0, s)] = _time_op(plan, i, stream)
+                # the large-tile LDS-DMA kernels (wgrad_big.hip) where they apply
+                if hasattr(ext, "wgrad_big_ok") and os.environ.get("IDC_WG_TILES", "1") != "0":
+                    K = a.KH * a.KW * a.Cin
+                    for v in range(1, ext.wgrad_num_variants()):
+                        if not ext.wgrad_big_ok(plan.payload(i), f32, v):
+                            continue
+                        sp = ext.wgrad_big_pick_splits(M, K, a.Cout, v)
+                        for s in sorted({max(1, sp // 2), sp, sp * 2}):
+                            plan.set_int(i, 0, s)
+                            plan.set_int(i, 2, v)
+                            times[(v, s)] = _time_op(plan, i, stream)
+                    plan.set_int(i, 2, 0)
                 # the isolated optimum: biasing wgrad splits either way (fewest / most slices
                 # within 10-50% of it) measured 1-23% slower steps on DenseNet-121 and VGG16
                 best = min(times, key=times.get)
                 _CACHE[key] = best
                 if verbose:
-                    print("tune wgrad", key, {k: round(v * 1e3, 1) for k, v in times.items()}, "->", best)
-            plan.set_int(i, 0, best)
+                    print("tune wgrad", key, {f"{k[0]}/{k[1]}": round(v * 1e3, 1) for k, v in times.items()},
+                          "->", best)
+            if isinstance(best, list):  # JSON round trip
+                best = tuple(best)
+            if not isinstance(best, tuple):  # caches written before the large-tile variants
+                best = (0, best)
+            plan.set_int(i, 0, best[1])
+            plan.set_int(i, 2, best[0])
             n += 1
     _save_cache()
     torch.cuda.synchronize()

@@ -362,7 +362,8 @@ def test_bn_stats(fn):
 
 
 @pytest.mark.parametrize("s,H,pads,ho,C", [(1, 13, (1, 1), 13, 96), (2, 26, (0, 0), 13, 96), (2, 13, (1, 1), 7, 96),
-                                            (1, 4, (1, 1), 4, 384), (2, 4, (0, 0), 2, 960)])
+                                            (1, 4, (1, 1), 4, 384), (2, 4, (0, 0), 2, 960),
+                                            (1, 25, (1, 1), 25, 32), (1, 13, (1, 1), 13, 144)])
 def test_dwconv(fn, s, H, pads, ho, C):
     N = 2
     x = bf(torch.randn(N, H, H, C, device=DEV))
@@ -778,3 +779,51 @@ def test_conv_ring_tiles_match_reference(fn, variant, case):
         yb = y.float()
         assert relerr(st[:Cout], (yb - shift).sum((0, 1, 2))) < 1e-3
         assert relerr(st[Cout:], ((yb - shift) ** 2).sum((0, 1, 2))) < 1e-3
+
+
+@pytest.mark.parametrize("N,H,Cin,Cout,k,s,pads", [
+    (2, 25, 64, 128, 3, 1, (1, 1)),     # VGG block 2 conv 1: K = 576 (a partial 256-row k tile)
+    (4, 12, 128, 256, 3, 1, (1, 1)),    # block 3
+    (8, 3, 512, 512, 3, 1, (1, 1)),     # block 5: 72 pixels, most of each step past the slice
+    (2, 13, 64, 128, 3, 2, (1, 1)),     # strided
+    (3, 10, 128, 128, 1, 1, (0, 0)),    # 1x1
+])
+def test_wgrad_big_tiles(fn, N, H, Cin, Cout, k, s, pads):
+    """Every large-tile weight-gradient variant (wgrad_big.hip: LDS-DMA operands, transposed LDS
+    reads, 32x32x16 MFMA, atomics straight from the accumulators) against fp32 PyTorch, at the
+    default and at explicit pixel splits."""
+    ext = fn.nat.require()
+    x = bf(torch.randn(N, H, H, Cin, device=DEV))
+    Ho = (H + 2 * pads[0] - k) // s + 1
+    dy = bf(torch.randn(N, Ho, Ho, Cout, device=DEV))
+    ref = torch.nn.grad.conv2d_weight(x.permute(0, 3, 1, 2), (Cout, Cin, k, k), dy.permute(0, 3, 1, 2),
+                                      stride=s, padding=pads[0]).permute(2, 3, 1, 0)
+    xb, dyb = x.to(torch.bfloat16), dy.to(torch.bfloat16)
+    ran = 0
+    for v in range(1, ext.wgrad_num_variants()):
+        if not fn.wgrad_big_applies(xb, dyb, (k, k), (s, s), pads, v):
+            assert Cout % 256, (v, Cout)  # only the 256-column variants may decline (Cout 128)
+            continue
+        for splits in (-1, 1, 3):
+            dw = fn.conv2d_wgrad(xb, dyb, (k, k), stride=(s, s), pads=pads, splits=splits, variant=v)
+            torch.cuda.synchronize()
+            assert relerr(dw, ref) < 1e-2, (v, splits, relerr(dw, ref))
+        ran += 1
+    assert ran >= 4
+
+
+def test_wgrad_big_deterministic_partials(fn):
+    """Deterministic mode of the large-tile kernel: per-slice partials stored (no atomics), summed
+    in slice order — bitwise reproducible, and equal to the fp32 reference."""
+    N, H, Cin, Cout = 4, 12, 128, 256
+    x = bf(torch.randn(N, H, H, Cin, device=DEV)).to(torch.bfloat16)
+    dy = bf(torch.randn(N, H, H, Cout, device=DEV)).to(torch.bfloat16)
+    ref = torch.nn.grad.conv2d_weight(x.float().permute(0, 3, 1, 2), (Cout, Cin, 3, 3),
+                                      dy.float().permute(0, 3, 1, 2), padding=1).permute(2, 3, 1, 0)
+    outs = []
+    for _ in range(2):
+        part = torch.zeros(3 * 9 * Cin * Cout, device=DEV)
+        outs.append(fn.conv2d_wgrad(x, dy, (3, 3), pads=(1, 1), splits=3, variant=2, part=part))
+    torch.cuda.synchronize()
+    assert torch.equal(outs[0], outs[1])
+    assert relerr(outs[0], ref) < 1e-2

@@ -35,7 +35,7 @@ SOURCES = [
     "kernels/conv3x3_halo.hip",
     "kernels/conv_big.hip",
     "kernels/conv_ring.hip",
-    "kernels/conv_wgrad.hip",
+    "kernels/conv_wgrad.hip", "kernels/wgrad_big.hip",
     "kernels/nn_kernels.hip",
     "kernels/dwconv.hip",
     "kernels/mlp_head.hip",
