@@ -231,26 +231,57 @@ __global__ __launch_bounds__(256) void dw_wgrad_kernel(DwArgs a, GroupArg ga) {
 // clamp, and padding taps are masked after the activation (Keras pads the activated tensor).
 constexpr int kDwStrip = 4;
 
+// Strip-kernel geometry: a block owns c8b 8-channel chunks (c8b = the largest divisor of C/8 that
+// is <= 8: 64, 48 or fewer channels) x R = 256 / c8b strips in flight, blockIdx.y = channel
+// chunk.  A block holding ALL C channels (C/8 chunks x 256/(C/8) rows) left MobileNetV2's deep
+// layers (C 384-960: 2-5 strip rows per block) with a few dozen long-running blocks on 256 CUs.
+struct DwChunks {
+  int c8b, nchunk, R;
+};
+__host__ __device__ inline DwChunks dw_chunks(int C) {
+  const int C8 = C / 8;
+  int b = C8 < 8 ? C8 : 8;
+  while (b > 1 && C8 % b) --b;
+  if (b < 1) b = 1;
+  DwChunks d;
+  d.c8b = b;
+  d.nchunk = C8 / b;
+  d.R = 256 / b;
+  return d;
+}
+constexpr int kDwTargetBlocks = 2048;  // ~8 blocks per CU across the chunks
+// pixel blocks (gridDim.x) of a strip kernel: >= 1 strip per thread row, ~kDwTargetBlocks total
+inline int dw_pblocks(long long strips, const DwChunks& d) {
+  long long b = (strips + d.R - 1) / d.R;
+  long long cap = kDwTargetBlocks / d.nchunk;
+  if (cap < 1) cap = 1;
+  if (b > cap) b = cap;
+  return b < 1 ? 1 : (int)b;
+}
+
 template <int S>
 __global__ __launch_bounds__(256) void dw_fwd3_kernel(DwArgs a, GroupArg ga) {
   gshift(a, goff(ga));
   constexpr int P = kDwStrip, NCOL = (P - 1) * S + 3;
   extern __shared__ float sh[];
+  const int CBX = dw_chunks(a.C).c8b * 8;  // table stride: the block's channels
   float* s_sc = sh;
-  float* s_sf = sh + a.C;
-  float* s_a = sh + 2 * a.C;
-  float* s_b = sh + 3 * a.C;
-  for (int c = threadIdx.x; c < a.C; c += blockDim.x) {
-    bn_coeffs(a.pro, c, s_sc[c], s_sf[c]);
-    s_a[c] = 0.f;
-    s_b[c] = 0.f;
+  float* s_sf = sh + CBX;
+  float* s_a = sh + 2 * CBX;
+  float* s_b = sh + 3 * CBX;
+  const DwChunks dc = dw_chunks(a.C);
+  const int CB = dc.c8b * 8, cb = blockIdx.y * CB;  // this block's channels [cb, cb + CB)
+  for (int i = threadIdx.x; i < CB; i += blockDim.x) {
+    bn_coeffs(a.pro, cb + i, s_sc[i], s_sf[i]);
+    s_a[i] = 0.f;
+    s_b[i] = 0.f;
   }
   __syncthreads();
-  Map8 mp(a.C);
+  const int tx = threadIdx.x % dc.c8b, ty = threadIdx.x / dc.c8b;
   const int WS = (a.Wo + P - 1) / P;
   const int strips = a.N * a.Ho * WS;
-  if (mp.ty < mp.R) {
-    const int c = mp.tx * 8;
+  if (ty < dc.R) {
+    const int cl = tx * 8, c = cb + cl;
     float wk[9][8], sc[8], sf[8];
 #pragma unroll
     for (int t = 0; t < 9; ++t) {
@@ -260,12 +291,12 @@ __global__ __launch_bounds__(256) void dw_fwd3_kernel(DwArgs a, GroupArg ga) {
       wk[t][4] = w1.x; wk[t][5] = w1.y; wk[t][6] = w1.z; wk[t][7] = w1.w;
     }
 #pragma unroll
-    for (int j = 0; j < 8; ++j) { sc[j] = s_sc[c + j]; sf[j] = s_sf[c + j]; }
+    for (int j = 0; j < 8; ++j) { sc[j] = s_sc[cl + j]; sf[j] = s_sf[cl + j]; }
     const float lo = act_lo(a.pro.act), hi = act_hi(a.pro.act);
     float ps[8] = {0}, pq[8] = {0}, kk[8];
 #pragma unroll
     for (int j = 0; j < 8; ++j) kk[j] = a.stats_shift ? a.stats_shift[c + j] : 0.f;
-    for (int st = blockIdx.x * mp.R + mp.ty; st < strips; st += gridDim.x * mp.R) {
+    for (int st = blockIdx.x * dc.R + ty; st < strips; st += gridDim.x * dc.R) {
       const int ws = st % WS, t = st / WS, ho = t % a.Ho, n = t / a.Ho;
       const int wo0 = ws * P;
       float acc[P][8];
@@ -321,15 +352,15 @@ __global__ __launch_bounds__(256) void dw_fwd3_kernel(DwArgs a, GroupArg ga) {
     }
     if (a.stats) {
 #pragma unroll
-      for (int j = 0; j < 8; ++j) { atomicAdd(&s_a[c + j], ps[j]); atomicAdd(&s_b[c + j], pq[j]); }
+      for (int j = 0; j < 8; ++j) { atomicAdd(&s_a[cl + j], ps[j]); atomicAdd(&s_b[cl + j], pq[j]); }
     }
   }
   if (a.stats) {
     __syncthreads();
     float* so = a.stats + (size_t)(blockIdx.x % stat_slots(a.stats_slots)) * 2 * a.stats_ld;
-    for (int c = threadIdx.x; c < a.C; c += blockDim.x) {
-      atomicAdd(&so[c], s_a[c]);
-      atomicAdd(&so[a.stats_ld + c], s_b[c]);
+    for (int i = threadIdx.x; i < CB; i += blockDim.x) {
+      atomicAdd(&so[cb + i], s_a[i]);
+      atomicAdd(&so[a.stats_ld + cb + i], s_b[i]);
     }
   }
 }
@@ -347,32 +378,36 @@ __global__ __launch_bounds__(256) void dw_bwd3_kernel(DwArgs a, GroupArg ga) {
   constexpr int P = STRIP ? kDwStrip : 1;
   constexpr int NCOL = S == 1 ? P + 2 : (PL2 >= 0 ? (P + PL2 + 2) / 2 + 1 : 3);
   extern __shared__ float sh[];
+  const int CBX = dw_chunks(a.C).c8b * 8;  // table stride: the block's channels
   float* s_sc = sh;
-  float* s_sf = sh + a.C;
-  float* s_mu = sh + 2 * a.C;
-  float* s_rs = sh + 3 * a.C;
-  float* s_a = sh + 4 * a.C;
-  float* s_b = sh + 5 * a.C;
-  float* s_fA = sh + 6 * a.C;  // AFF: dy' = A*dy + B*x + C
-  float* s_fB = sh + 7 * a.C;
-  float* s_fC = sh + 8 * a.C;
+  float* s_sf = sh + CBX;
+  float* s_mu = sh + 2 * CBX;
+  float* s_rs = sh + 3 * CBX;
+  float* s_a = sh + 4 * CBX;
+  float* s_b = sh + 5 * CBX;
+  float* s_fA = sh + 6 * CBX;  // AFF: dy' = A*dy + B*x + C
+  float* s_fB = sh + 7 * CBX;
+  float* s_fC = sh + 8 * CBX;
   const bool epi = !(a.pro.mode == 0 && a.pro.act == ACT_NONE);
-  for (int c = threadIdx.x; c < a.C; c += blockDim.x) {
-    bn_coeffs(a.pro, c, s_sc[c], s_sf[c]);
+  const DwChunks dc = dw_chunks(a.C);
+  const int CB = dc.c8b * 8, cb = blockIdx.y * CB;  // this block's channels [cb, cb + CB)
+  for (int i = threadIdx.x; i < CB; i += blockDim.x) {
+    const int c = cb + i;
+    bn_coeffs(a.pro, c, s_sc[i], s_sf[i]);
     float mean = 0.f, rstd = 1.f;
     if (a.pro.mode) bn_mean_rstd(a.pro, c, mean, rstd);
-    s_mu[c] = mean; s_rs[c] = rstd; s_a[c] = 0.f; s_b[c] = 0.f;
+    s_mu[i] = mean; s_rs[i] = rstd; s_a[i] = 0.f; s_b[i] = 0.f;
   }
   if constexpr (AFF) {
-    bwd_aff_table<256>(a.dyaff, 0, a.C, a.C, s_fA, s_fB, s_fC);
+    bwd_aff_table<256>(a.dyaff, cb, CB, a.C, s_fA, s_fB, s_fC);
     bwd_aff_fold<256>(a.dyaff);
   }
   __syncthreads();
-  Map8 mp(a.C);
+  const int tx = threadIdx.x % dc.c8b, ty = threadIdx.x / dc.c8b;
   const int WS = (a.W + P - 1) / P;
   const int strips = a.N * a.H * WS;
-  if (mp.ty < mp.R) {
-    const int c = mp.tx * 8;
+  if (ty < dc.R) {
+    const int cl = tx * 8, c = cb + cl;
     float wk[9][8], sc[8], sf[8], mu[8], rs[8], fA[8], fB[8], fC[8];
 #pragma unroll
     for (int t = 0; t < 9; ++t) {
@@ -383,12 +418,12 @@ __global__ __launch_bounds__(256) void dw_bwd3_kernel(DwArgs a, GroupArg ga) {
     }
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
-      sc[j] = s_sc[c + j]; sf[j] = s_sf[c + j]; mu[j] = s_mu[c + j]; rs[j] = s_rs[c + j];
-      if constexpr (AFF) { fA[j] = s_fA[c + j]; fB[j] = s_fB[c + j]; fC[j] = s_fC[c + j]; }
+      sc[j] = s_sc[cl + j]; sf[j] = s_sf[cl + j]; mu[j] = s_mu[cl + j]; rs[j] = s_rs[cl + j];
+      if constexpr (AFF) { fA[j] = s_fA[cl + j]; fB[j] = s_fB[cl + j]; fC[j] = s_fC[cl + j]; }
     }
     const float lo = act_lo(a.pro.act), hi = act_hi(a.pro.act);
     float ps[8] = {0}, px[8] = {0};
-    for (int st = blockIdx.x * mp.R + mp.ty; st < strips; st += gridDim.x * mp.R) {
+    for (int st = blockIdx.x * dc.R + ty; st < strips; st += gridDim.x * dc.R) {
       const int ws = st % WS, t = st / WS, h = t % a.H, n = t / a.H;
       const int w0 = ws * P;
       float g[P][8];
@@ -476,37 +511,30 @@ __global__ __launch_bounds__(256) void dw_bwd3_kernel(DwArgs a, GroupArg ga) {
     }
     if (epi) {
 #pragma unroll
-      for (int j = 0; j < 8; ++j) { atomicAdd(&s_a[c + j], ps[j]); atomicAdd(&s_b[c + j], px[j]); }
+      for (int j = 0; j < 8; ++j) { atomicAdd(&s_a[cl + j], ps[j]); atomicAdd(&s_b[cl + j], px[j]); }
     }
   }
   if (epi) {
     __syncthreads();
     const size_t so = (size_t)(blockIdx.x % stat_slots(a.gsum_slots)) * a.gsum_ld;
-    for (int c = threadIdx.x; c < a.C; c += blockDim.x) {
-      if (a.gsum) atomicAdd(&a.gsum[so + c], s_a[c]);
-      if (a.gsumx) atomicAdd(&a.gsumx[so + c], s_b[c]);
+    for (int i = threadIdx.x; i < CB; i += blockDim.x) {
+      if (a.gsum) atomicAdd(&a.gsum[so + cb + i], s_a[i]);
+      if (a.gsumx) atomicAdd(&a.gsumx[so + cb + i], s_b[i]);
     }
   }
 }
 
-namespace {
-// grid of a strip kernel: ~2 strips per thread row (amortises the per-thread tap registers)
-inline int strip_blocks(long long strips, int C) {
-  int C8 = C / 8, R = 256 / C8;
-  if (R < 1) R = 1;
-  long long b = (strips + 2LL * R - 1) / (2LL * R);
-  if (b > 4096) b = 4096;
-  return b < 1 ? 1 : (int)b;
-}
-}  // namespace
 
 hipError_t dwconv_fwd(const DwArgs& a, hipStream_t st) {
   if (a.KH == 3 && a.KW == 3 && (a.S == 1 || a.S == 2) && a.C % 8 == 0 && a.C <= 2048) {
     const long long strips = (long long)a.N * a.Ho * ((a.Wo + kDwStrip - 1) / kDwStrip);
+    const DwChunks dc = dw_chunks(a.C);
+    const dim3 g(dw_pblocks(strips, dc), dc.nchunk);
+    const size_t shm = 4 * dc.c8b * 8 * 4;
     if (a.S == 1)
-      hipLaunchKernelGGL(dw_fwd3_kernel<1>, ggrid(dim3(strip_blocks(strips, a.C))), dim3(256), 4 * a.C * 4, st, a, garg());
+      hipLaunchKernelGGL(dw_fwd3_kernel<1>, ggrid(g), dim3(256), shm, st, a, garg());
     else
-      hipLaunchKernelGGL(dw_fwd3_kernel<2>, ggrid(dim3(strip_blocks(strips, a.C))), dim3(256), 4 * a.C * 4, st, a, garg());
+      hipLaunchKernelGGL(dw_fwd3_kernel<2>, ggrid(g), dim3(256), shm, st, a, garg());
     return hipGetLastError();
   }
   hipLaunchKernelGGL(dw_fwd_kernel, ggrid(dim3(nblocks((long long)a.N * a.Ho * a.Wo, a.C, 4))), dim3(256),
@@ -517,12 +545,13 @@ hipError_t dwconv_fwd(const DwArgs& a, hipStream_t st) {
 hipError_t dwconv_bwd_data(const DwArgs& a, hipStream_t st) {
   const bool aff = a.dyaff.mode != 0;
   if (a.KH == 3 && a.KW == 3 && (a.S == 1 || a.S == 2) && a.C % 8 == 0 && a.C <= 2048) {
-    const size_t shm = 9 * a.C * 4;
+    const DwChunks dc = dw_chunks(a.C);
+    const size_t shm = 9 * dc.c8b * 8 * 4;
     const long long strips4 = (long long)a.N * a.H * ((a.W + kDwStrip - 1) / kDwStrip);
-    const int g4 = strip_blocks(strips4, a.C), g1 = strip_blocks((long long)a.N * a.H * a.W, a.C);
+    const dim3 g4(dw_pblocks(strips4, dc), dc.nchunk), g1(dw_pblocks((long long)a.N * a.H * a.W, dc), dc.nchunk);
 #define IDC_DWB(S_, PL_, G_)                                                                      \
-  if (aff) hipLaunchKernelGGL((dw_bwd3_kernel<S_, PL_, true>), ggrid(dim3(G_)), dim3(256), shm, st, a, garg()); \
-  else hipLaunchKernelGGL((dw_bwd3_kernel<S_, PL_, false>), ggrid(dim3(G_)), dim3(256), shm, st, a, garg());
+  if (aff) hipLaunchKernelGGL((dw_bwd3_kernel<S_, PL_, true>), ggrid(G_), dim3(256), shm, st, a, garg()); \
+  else hipLaunchKernelGGL((dw_bwd3_kernel<S_, PL_, false>), ggrid(G_), dim3(256), shm, st, a, garg());
     if (a.S == 1) {
       IDC_DWB(1, -1, g4)
     } else if (a.PL == 0) {
@@ -560,7 +589,9 @@ inline int dw_wgrad_blocks(long long M, int C) {
 }  // namespace
 
 long long dwconv_wgrad_ws_floats(long long M, int C, int taps) {
-  return (long long)dw_wgrad_blocks(M, C) * taps * C;
+  // the larger of the general two-stage grid and the strip kernel's pixel blocks (strips <= M)
+  const long long a = dw_wgrad_blocks(M, C), b = dw_pblocks(M, dw_chunks(C));
+  return (a > b ? a : b) * taps * C;
 }
 
 __global__ __launch_bounds__(256) void dw_wgrad_part_kernel(DwArgs a, int rows_per_block, GroupArg ga) {
@@ -636,16 +667,18 @@ __global__ __launch_bounds__(256) void dw_wgrad3_part_kernel(DwArgs a, int spb, 
   gshift(a, goff(ga));
   constexpr int P = kDwStrip, NCOL = (P - 1) * S + 3;
   extern __shared__ float sh[];
+  const DwChunks dc = dw_chunks(a.C);
+  const int CB = dc.c8b * 8, cb = blockIdx.y * CB;  // this block's channels [cb, cb + CB)
   float* s_sc = sh;
-  float* s_sf = sh + a.C;
-  float* s_fA = sh + 2 * a.C;   // AFF: dy' = A*dy + B*x + C
-  float* s_fB = sh + 3 * a.C;
-  float* s_fC = sh + 4 * a.C;
-  float* s_red = sh + 5 * a.C;  // [256 threads][3 taps][8]: one tap row per reduction round
-  for (int c = threadIdx.x; c < a.C; c += blockDim.x) bn_coeffs(a.pro, c, s_sc[c], s_sf[c]);
-  if constexpr (AFF) bwd_aff_table<256>(a.dyaff, 0, a.C, a.C, s_fA, s_fB, s_fC);
+  float* s_sf = sh + CB;
+  float* s_fA = sh + 2 * CB;   // AFF: dy' = A*dy + B*x + C
+  float* s_fB = sh + 3 * CB;
+  float* s_fC = sh + 4 * CB;
+  float* s_red = sh + 5 * CB;  // [256 threads][3 taps][8]: one tap row per reduction round
+  for (int i = threadIdx.x; i < CB; i += blockDim.x) bn_coeffs(a.pro, cb + i, s_sc[i], s_sf[i]);
+  if constexpr (AFF) bwd_aff_table<256>(a.dyaff, cb, CB, a.C, s_fA, s_fB, s_fC);
   __syncthreads();
-  Map8 mp(a.C);
+  const int tx = threadIdx.x % dc.c8b, ty = threadIdx.x / dc.c8b;
   const int WS = (a.Wo + P - 1) / P;
   const int strips = a.N * a.Ho * WS;
   const int s0 = blockIdx.x * spb, s1 = min(strips, s0 + spb);
@@ -655,15 +688,15 @@ __global__ __launch_bounds__(256) void dw_wgrad3_part_kernel(DwArgs a, int spb, 
   for (int t = 0; t < 9; ++t)
 #pragma unroll
     for (int j = 0; j < 8; ++j) acc[t][j] = 0.f;
-  if (mp.ty < mp.R) {
-    const int c = mp.tx * 8;
+  if (ty < dc.R) {
+    const int cl = tx * 8, c = cb + cl;
     float sc[8], sf[8], fA[8], fB[8], fC[8];
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
-      sc[j] = s_sc[c + j]; sf[j] = s_sf[c + j];
-      if constexpr (AFF) { fA[j] = s_fA[c + j]; fB[j] = s_fB[c + j]; fC[j] = s_fC[c + j]; }
+      sc[j] = s_sc[cl + j]; sf[j] = s_sf[cl + j];
+      if constexpr (AFF) { fA[j] = s_fA[cl + j]; fB[j] = s_fB[cl + j]; fC[j] = s_fC[cl + j]; }
     }
-    for (int st = s0 + mp.ty; st < s1; st += mp.R) {
+    for (int st = s0 + ty; st < s1; st += dc.R) {
       const int ws = st % WS, t = st / WS, ho = t % a.Ho, n = t / a.Ho;
       const int wo0 = ws * P;
       float d[P][8];
@@ -718,9 +751,9 @@ __global__ __launch_bounds__(256) void dw_wgrad3_part_kernel(DwArgs a, int spb, 
   // block reduction over the R thread rows of each chunk, one tap row (3 taps) per round:
   // every thread's 24 partials to LDS, then each (tap, channel) output sums its R entries in
   // order (the per-address LDS atomics this replaces serialised R-way on small C)
-  float* out = a.ws + (size_t)blockIdx.x * 9 * a.C;
-  const int C8 = a.C / 8;
-  const bool act = mp.ty < mp.R;
+  float* out = a.ws + (size_t)blockIdx.x * 9 * a.C + cb;
+  const int C8 = dc.c8b;
+  const bool act = ty < dc.R;
 #pragma unroll
   for (int r = 0; r < 3; ++r) {
     if (r) __syncthreads();
@@ -732,10 +765,10 @@ __global__ __launch_bounds__(256) void dw_wgrad3_part_kernel(DwArgs a, int spb, 
       d[2 * s + 1] = act ? make_float4(v[4], v[5], v[6], v[7]) : make_float4(0.f, 0.f, 0.f, 0.f);
     }
     __syncthreads();
-    for (int o = threadIdx.x; o < 3 * a.C; o += blockDim.x) {
-      const int s = o / a.C, c = o - s * a.C, tx = c >> 3, j = c & 7;
+    for (int o = threadIdx.x; o < 3 * CB; o += blockDim.x) {
+      const int s = o / CB, c = o - s * CB, cx = c >> 3, j = c & 7;
       float sum = 0.f;
-      for (int ty = 0; ty < mp.R; ++ty) sum += s_red[(ty * C8 + tx) * 24 + s * 8 + j];
+      for (int y = 0; y < dc.R; ++y) sum += s_red[(y * C8 + cx) * 24 + s * 8 + j];
       out[(r * 3 + s) * a.C + c] = sum;
     }
   }
@@ -771,18 +804,22 @@ hipError_t dwconv_wgrad(const DwArgs& a, hipStream_t st) {
   const long long Mo = (long long)a.N * a.Ho * a.Wo;
   const int T = a.KH * a.KW;
   if (a.ws) {
-    const int nblk = dw_wgrad_blocks(Mo, a.C);
+    int nblk = dw_wgrad_blocks(Mo, a.C);
     const bool aff = a.dyaff.mode != 0;
     if (a.KH == 3 && a.KW == 3 && (a.S == 1 || a.S == 2) && a.C % 8 == 0) {
       const long long strips = (long long)a.N * a.Ho * ((a.Wo + kDwStrip - 1) / kDwStrip);
+      const DwChunks dc = dw_chunks(a.C);
+      nblk = dw_pblocks(strips, dc);
       const int spb = (int)((strips + nblk - 1) / nblk);
-      const size_t shm = (5 * a.C + 256 * 24) * 4;
+      nblk = (int)((strips + spb - 1) / spb);
+      const size_t shm = (5 * dc.c8b * 8 + 256 * 24) * 4;
+      const dim3 g(nblk, dc.nchunk);
       if (a.S == 1) {
-        if (aff) hipLaunchKernelGGL((dw_wgrad3_part_kernel<1, true>), ggrid(dim3(nblk)), dim3(256), shm, st, a, spb, garg());
-        else hipLaunchKernelGGL((dw_wgrad3_part_kernel<1, false>), ggrid(dim3(nblk)), dim3(256), shm, st, a, spb, garg());
+        if (aff) hipLaunchKernelGGL((dw_wgrad3_part_kernel<1, true>), ggrid(g), dim3(256), shm, st, a, spb, garg());
+        else hipLaunchKernelGGL((dw_wgrad3_part_kernel<1, false>), ggrid(g), dim3(256), shm, st, a, spb, garg());
       } else {
-        if (aff) hipLaunchKernelGGL((dw_wgrad3_part_kernel<2, true>), ggrid(dim3(nblk)), dim3(256), shm, st, a, spb, garg());
-        else hipLaunchKernelGGL((dw_wgrad3_part_kernel<2, false>), ggrid(dim3(nblk)), dim3(256), shm, st, a, spb, garg());
+        if (aff) hipLaunchKernelGGL((dw_wgrad3_part_kernel<2, true>), ggrid(g), dim3(256), shm, st, a, spb, garg());
+        else hipLaunchKernelGGL((dw_wgrad3_part_kernel<2, false>), ggrid(g), dim3(256), shm, st, a, spb, garg());
       }
     } else if (aff) {
       return hipErrorInvalidValue;
