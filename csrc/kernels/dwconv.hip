@@ -280,6 +280,7 @@ __global__ __launch_bounds__(256) void dw_fwd3_kernel(DwArgs a, GroupArg ga) {
   const int tx = threadIdx.x % dc.c8b, ty = threadIdx.x / dc.c8b;
   const int WS = (a.Wo + P - 1) / P;
   const int strips = a.N * a.Ho * WS;
+  float ps[8] = {0}, pq[8] = {0};
   if (ty < dc.R) {
     const int cl = tx * 8, c = cb + cl;
     float wk[9][8], sc[8], sf[8];
@@ -293,7 +294,7 @@ __global__ __launch_bounds__(256) void dw_fwd3_kernel(DwArgs a, GroupArg ga) {
 #pragma unroll
     for (int j = 0; j < 8; ++j) { sc[j] = s_sc[cl + j]; sf[j] = s_sf[cl + j]; }
     const float lo = act_lo(a.pro.act), hi = act_hi(a.pro.act);
-    float ps[8] = {0}, pq[8] = {0}, kk[8];
+    float kk[8];
 #pragma unroll
     for (int j = 0; j < 8; ++j) kk[j] = a.stats_shift ? a.stats_shift[c + j] : 0.f;
     for (int st = blockIdx.x * dc.R + ty; st < strips; st += gridDim.x * dc.R) {
@@ -350,12 +351,9 @@ __global__ __launch_bounds__(256) void dw_fwd3_kernel(DwArgs a, GroupArg ga) {
         }
       }
     }
-    if (a.stats) {
-#pragma unroll
-      for (int j = 0; j < 8; ++j) { atomicAdd(&s_a[cl + j], ps[j]); atomicAdd(&s_b[cl + j], pq[j]); }
-    }
   }
   if (a.stats) {
+    chunk_sums(CB, dc.R, tx, ty, ps, pq, sh + 4 * CBX, s_a, s_b);
     __syncthreads();
     float* so = a.stats + (size_t)(blockIdx.x % stat_slots(a.stats_slots)) * 2 * a.stats_ld;
     for (int i = threadIdx.x; i < CB; i += blockDim.x) {
@@ -406,6 +404,7 @@ __global__ __launch_bounds__(256) void dw_bwd3_kernel(DwArgs a, GroupArg ga) {
   const int tx = threadIdx.x % dc.c8b, ty = threadIdx.x / dc.c8b;
   const int WS = (a.W + P - 1) / P;
   const int strips = a.N * a.H * WS;
+  float ps[8] = {0}, px[8] = {0};
   if (ty < dc.R) {
     const int cl = tx * 8, c = cb + cl;
     float wk[9][8], sc[8], sf[8], mu[8], rs[8], fA[8], fB[8], fC[8];
@@ -422,7 +421,6 @@ __global__ __launch_bounds__(256) void dw_bwd3_kernel(DwArgs a, GroupArg ga) {
       if constexpr (AFF) { fA[j] = s_fA[cl + j]; fB[j] = s_fB[cl + j]; fC[j] = s_fC[cl + j]; }
     }
     const float lo = act_lo(a.pro.act), hi = act_hi(a.pro.act);
-    float ps[8] = {0}, px[8] = {0};
     for (int st = blockIdx.x * dc.R + ty; st < strips; st += gridDim.x * dc.R) {
       const int ws = st % WS, t = st / WS, h = t % a.H, n = t / a.H;
       const int w0 = ws * P;
@@ -509,12 +507,9 @@ __global__ __launch_bounds__(256) void dw_bwd3_kernel(DwArgs a, GroupArg ga) {
         }
       }
     }
-    if (epi) {
-#pragma unroll
-      for (int j = 0; j < 8; ++j) { atomicAdd(&s_a[cl + j], ps[j]); atomicAdd(&s_b[cl + j], px[j]); }
-    }
   }
   if (epi) {
+    chunk_sums(CB, dc.R, tx, ty, ps, px, sh + 9 * CBX, s_a, s_b);
     __syncthreads();
     const size_t so = (size_t)(blockIdx.x % stat_slots(a.gsum_slots)) * a.gsum_ld;
     for (int i = threadIdx.x; i < CB; i += blockDim.x) {
@@ -530,7 +525,7 @@ hipError_t dwconv_fwd(const DwArgs& a, hipStream_t st) {
     const long long strips = (long long)a.N * a.Ho * ((a.Wo + kDwStrip - 1) / kDwStrip);
     const DwChunks dc = dw_chunks(a.C);
     const dim3 g(dw_pblocks(strips, dc), dc.nchunk);
-    const size_t shm = 4 * dc.c8b * 8 * 4;
+    const size_t shm = (4 * dc.c8b * 8 + 2 * 256 * 8) * 4;  // tables + chunk_sums scratch
     if (a.S == 1)
       hipLaunchKernelGGL(dw_fwd3_kernel<1>, ggrid(g), dim3(256), shm, st, a, garg());
     else
@@ -546,7 +541,7 @@ hipError_t dwconv_bwd_data(const DwArgs& a, hipStream_t st) {
   const bool aff = a.dyaff.mode != 0;
   if (a.KH == 3 && a.KW == 3 && (a.S == 1 || a.S == 2) && a.C % 8 == 0 && a.C <= 2048) {
     const DwChunks dc = dw_chunks(a.C);
-    const size_t shm = 9 * dc.c8b * 8 * 4;
+    const size_t shm = (9 * dc.c8b * 8 + 2 * 256 * 8) * 4;  // tables + chunk_sums scratch
     const long long strips4 = (long long)a.N * a.H * ((a.W + kDwStrip - 1) / kDwStrip);
     const dim3 g4(dw_pblocks(strips4, dc), dc.nchunk), g1(dw_pblocks((long long)a.N * a.H * a.W, dc), dc.nchunk);
 #define IDC_DWB(S_, PL_, G_)                                                                      \

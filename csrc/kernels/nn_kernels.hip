@@ -114,31 +114,10 @@ __device__ __forceinline__ void flush_sums(float* s_a, float* s_b, int C, float*
   }
 }
 
-// Per-channel block totals of per-thread 8-channel partials laid out by ChunkMap (thread (tx, ty)
-// owns channels [8tx, 8tx+8) of row group ty): partials are transposed through LDS and summed
-// down the row groups, so no LDS address sees more than one writer (per-thread LDS float atomics
-// here serialise R = 256/(C/8) ways).  `tmp` holds 2*256*8 floats; results land in s_a / s_b.
+// per-channel block totals of ChunkMap-laid partials (common.h chunk_sums)
 __device__ __forceinline__ void chunk_reduce(const ChunkMap& cm, int C, const float* pa, const float* pb,
                                              float* tmp, float* s_a, float* s_b) {
-  float* ta = tmp;
-  float* tb = tmp + 256 * 8;
-  if (cm.active()) {
-    const int o = cm.ty * C + cm.tx * 8;
-    *reinterpret_cast<float4*>(ta + o) = make_float4(pa[0], pa[1], pa[2], pa[3]);
-    *reinterpret_cast<float4*>(ta + o + 4) = make_float4(pa[4], pa[5], pa[6], pa[7]);
-    *reinterpret_cast<float4*>(tb + o) = make_float4(pb[0], pb[1], pb[2], pb[3]);
-    *reinterpret_cast<float4*>(tb + o + 4) = make_float4(pb[4], pb[5], pb[6], pb[7]);
-  }
-  __syncthreads();
-  for (int c = threadIdx.x; c < C; c += blockDim.x) {
-    float sa = 0.f, sb = 0.f;
-    for (int r = 0; r < cm.R; ++r) {
-      sa += ta[r * C + c];
-      sb += tb[r * C + c];
-    }
-    s_a[c] = sa;
-    s_b[c] = sb;
-  }
+  chunk_sums(C, cm.R, cm.tx, cm.ty, pa, pb, tmp, s_a, s_b);
 }
 
 }  // namespace
@@ -1161,28 +1140,26 @@ __global__ __launch_bounds__(256) void bn_stats_kernel(const bf16_t* x, int ldx,
   extern __shared__ float sh[];
   float* s_a = sh;
   float* s_b = sh + C;
-  for (int c = threadIdx.x; c < C; c += blockDim.x) { s_a[c] = 0.f; s_b[c] = 0.f; }
-  __syncthreads();
+  float* s_tmp = sh + 2 * C;
   ChunkMap cm(C);
+  float ps[8] = {0}, pq[8] = {0};
   if (cm.active()) {
     const int c = cm.tx * 8;
-    float ps[8] = {0}, pq[8] = {0};
     for (int row = blockIdx.x * cm.R + cm.ty; row < M; row += gridDim.x * cm.R) {
       float v[8];
       unpack8(*reinterpret_cast<const uint4*>(x + (size_t)row * ldx + c), v);
 #pragma unroll
       for (int j = 0; j < 8; ++j) { ps[j] += v[j]; pq[j] += v[j] * v[j]; }
     }
-#pragma unroll
-    for (int j = 0; j < 8; ++j) { atomicAdd(&s_a[c + j], ps[j]); atomicAdd(&s_b[c + j], pq[j]); }
   }
+  chunk_reduce(cm, C, ps, pq, s_tmp, s_a, s_b);
   float* so = slot_ptr(stats, stats_slots, 2 * (size_t)stats_ld);
   flush_sums(s_a, s_b, C, so + stats_off, so + stats_ld + stats_off);
 }
 
 hipError_t bn_stats(const bf16_t* x, int ldx, int M, int C, float* stats, int stats_ld, int stats_off,
                     int stats_slots, hipStream_t st) {
-  hipLaunchKernelGGL(bn_stats_kernel, ggrid(dim3(grid_rows(M, C, 16))), dim3(256), 2 * C * 4, st, x, ldx, M, C,
+  hipLaunchKernelGGL(bn_stats_kernel, ggrid(dim3(grid_rows(M, C, 16))), dim3(256), (2 * C + 2 * 256 * 8) * 4, st, x, ldx, M, C,
                      stats, stats_ld, stats_off, stats_slots, garg());
   return hipGetLastError();
 }
@@ -1200,15 +1177,13 @@ __global__ __launch_bounds__(256) void bn_apply_kernel(const bf16_t* x, int ldx,
   float* s_sh = sh + C;
   float* s_a = sh + 2 * C;
   float* s_b = sh + 3 * C;
-  for (int c = threadIdx.x; c < C; c += blockDim.x) {
-    bn_coeffs(bn, c, s_sc[c], s_sh[c]);
-    s_a[c] = 0.f; s_b[c] = 0.f;
-  }
+  float* s_tmp = sh + 4 * C;
+  for (int c = threadIdx.x; c < C; c += blockDim.x) bn_coeffs(bn, c, s_sc[c], s_sh[c]);
   __syncthreads();
   ChunkMap cm(C);
+  float ps[8] = {0}, pq[8] = {0};
   if (cm.active()) {
     const int c = cm.tx * 8;
-    float ps[8] = {0}, pq[8] = {0};
     for (int row = blockIdx.x * cm.R + cm.ty; row < M; row += gridDim.x * cm.R) {
       float v[8];
       unpack8(*reinterpret_cast<const uint4*>(x + (size_t)row * ldx + c), v);
@@ -1228,12 +1203,9 @@ __global__ __launch_bounds__(256) void bn_apply_kernel(const bf16_t* x, int ldx,
         for (int j = 0; j < 8; ++j) { ps[j] += v[j]; pq[j] += v[j] * v[j]; }
       }
     }
-    if (stats) {
-#pragma unroll
-      for (int j = 0; j < 8; ++j) { atomicAdd(&s_a[c + j], ps[j]); atomicAdd(&s_b[c + j], pq[j]); }
-    }
   }
   if (stats) {
+    chunk_reduce(cm, C, ps, pq, s_tmp, s_a, s_b);
     float* so = slot_ptr(stats, stats_slots, 2 * (size_t)stats_ld);
     flush_sums(s_a, s_b, C, so, so + stats_ld);
   }
@@ -1241,7 +1213,7 @@ __global__ __launch_bounds__(256) void bn_apply_kernel(const bf16_t* x, int ldx,
 
 hipError_t bn_apply(const bf16_t* x, int ldx, BnArgs bn, const bf16_t* res, int ldres, bf16_t* y, int ldy,
                     int M, int C, float* stats, int stats_ld, int stats_slots, hipStream_t st) {
-  hipLaunchKernelGGL(bn_apply_kernel, ggrid(dim3(grid_rows(M, C))), dim3(256), 4 * C * 4, st, x, ldx, bn, res, ldres,
+  hipLaunchKernelGGL(bn_apply_kernel, ggrid(dim3(grid_rows(M, C))), dim3(256), (4 * C + 2 * 256 * 8) * 4, st, x, ldx, bn, res, ldres,
                      y, ldy, M, C, stats, stats_ld, stats_slots, garg());
   return hipGetLastError();
 }

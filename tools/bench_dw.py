@@ -75,10 +75,21 @@ def main():
         pw.add(nat.OP_DW_WGRAD, nat.raw(b), [], [], [], [])
         sh = lambda: torch.cuda.current_stream().cuda_stream  # noqa: E731
         tf = graph_us(lambda: pf.run(0, -1, sh()))
+        # the same forward without the statistics epilogue, and with 16 statistics slots
+        a.stats = 0
+        pn = ext.Plan()
+        pn.add(nat.OP_DW_FWD, nat.raw(a), [], [], [], [])
+        tn = graph_us(lambda: pn.run(0, -1, sh()))
+        st16 = torch.zeros(16 * 2 * C, device=dev)
+        a.stats, a.stats_slots = st16.data_ptr(), 16
+        p16 = ext.Plan()
+        p16.add(nat.OP_DW_FWD, nat.raw(a), [], [], [], [])
+        t16 = graph_us(lambda: p16.run(0, -1, sh()))
         tb = graph_us(lambda: pb.run(0, -1, sh()))
         tw = graph_us(lambda: pw.run(0, -1, sh()))
         mb_in, mb_out = N * H * H * C * 2 / 1e6, N * Ho * Ho * C * 2 / 1e6
-        print(f"H={H:2d} C={C:3d} s{S}: fwd {tf:6.1f} us ({(mb_in + mb_out) / tf:.2f} TB/s) | "
+        print(f"H={H:2d} C={C:3d} s{S}: fwd {tf:6.1f} us ({(mb_in + mb_out) / tf:.2f} TB/s) "
+              f"[no stats {tn:5.1f}, 16 slots {t16:5.1f}] | "
               f"bwd-data {tb:6.1f} us ({(2 * mb_in + mb_out) / tb:.2f} TB/s) | wgrad {tw:6.1f} us", flush=True)
 
 
