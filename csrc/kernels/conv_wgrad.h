@@ -44,4 +44,25 @@ hipError_t wgrad_reduce(const float* part, float* dw, long long n, int splits, h
 int wgrad_effective_splits(const WgradArgs& a, int splits, int variant = 0);
 int wgrad_pick_splits(int M, int K, int Cout);
 
+// ---- batched weight gradients -----------------------------------------------------------------
+// Many independent weight gradients with the same kernel shape in ONE launch (DenseNet's
+// late-stage dense layers: dozens of small wgrads whose operands are final once the stage's
+// data-gradient chain has run).  Workgroup b of the 1-D grid runs tile (b - begin[m]) of member
+// m = #{begin <= b} - 1, found with one ballot over the <= 64 member begins.
+constexpr int WG_BATCH_MAX = 64;
+struct WgBatchEntry {
+  WgradArgs a;       // pix_per_split resolved
+  int gx, gy, gz;    // the member's own grid (general: k tiles, cout tiles, pixel slices;
+                     // halo: image groups, 64-channel blocks, 1)
+  int ipw;           // halo kernel: images per workgroup
+};
+// batch signature of one member (members of one launch must share it), -1: not batchable
+int wgrad_batch_sig(const WgradArgs& a, bool g_f32, int variant);
+// fill entry `e` for a member launched with `splits`; returns its workgroup count, `smem` = its
+// LDS bytes
+int wgrad_batch_entry(const WgradArgs& a, int splits, WgBatchEntry& e, long long& smem);
+// dev_entries / dev_begins: device copies (begins padded with INT_MAX to WG_BATCH_MAX)
+hipError_t wgrad_batch(const WgBatchEntry* dev_entries, const int* dev_begins, int n, int total, int sig,
+                       long long smem, hipStream_t st);
+
 }  // namespace idc

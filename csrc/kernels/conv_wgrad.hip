@@ -62,11 +62,10 @@ __device__ __forceinline__ v8bf tr_frag(const bf16_t* tile, int col_base, int la
   return out;
 }
 
+// One (k tile bkx, cout tile bky, pixel slice zslice) workgroup of the pixel-split GEMM; shared by
+// the per-layer kernel below and the batched launch (conv_wgrad_batch_kernel).
 template <int BKR, int BC, int BP_, int WM, int WN, bool IS1X1, typename TG, int PRO, int GPRO>
-__global__ __launch_bounds__(256) void conv_wgrad_kernel(WgradArgs a, GroupArg ga) {
-  prefetch_kernargs<sizeof(WgradArgs) + sizeof(GroupArg)>();
-  gshift(a, goff(ga));
-  const int zslice = gz(ga);  // this workgroup's pixel slice (z = copy * splits + slice)
+__device__ __forceinline__ void wgrad_tile(const WgradArgs& a, const int bkx, const int bky, const int zslice) {
   using C = WgCfg<BKR, BC, BP_>;
   constexpr int NT = C::NT, BP = C::BP;
   constexpr int WTM = BKR / WM, WTN = BC / WN;
@@ -92,8 +91,8 @@ __global__ __launch_bounds__(256) void conv_wgrad_kernel(WgradArgs a, GroupArg g
   const int wr = wid / WN, wc = wid % WN;
   const int M = a.N * a.Ho * a.Wo;
   const int K = a.KH * a.KW * a.Cin;
-  const int k0 = blockIdx.x * BKR;
-  const int c0 = blockIdx.y * BC;
+  const int k0 = bkx * BKR;
+  const int c0 = bky * BC;
   const int per = a.pix_per_split;
   const int pbeg = zslice * per;
   const int pend = min(M, pbeg + per);
@@ -278,6 +277,14 @@ __global__ __launch_bounds__(256) void conv_wgrad_kernel(WgradArgs a, GroupArg g
   }
 }
 
+template <int BKR, int BC, int BP_, int WM, int WN, bool IS1X1, typename TG, int PRO, int GPRO>
+__global__ __launch_bounds__(256) void conv_wgrad_kernel(WgradArgs a, GroupArg ga) {
+  prefetch_kernargs<sizeof(WgradArgs) + sizeof(GroupArg)>();
+  gshift(a, goff(ga));
+  // this workgroup's pixel slice (z = copy * splits + slice)
+  wgrad_tile<BKR, BC, BP_, WM, WN, IS1X1, TG, PRO, GPRO>(a, blockIdx.x, blockIdx.y, gz(ga));
+}
+
 // ----------------------------------------------------------------------------------------------
 // Direct 3x3 weight gradient for SMALL images (DenseNet growth convs: 3x3 / s1 / 'same',
 // Cout = 32, on 13x13, 6x6 and 3x3 maps).  As a pixel-split GEMM (conv_wgrad_kernel) these take
@@ -331,9 +338,7 @@ __host__ __device__ inline WhGeom wh_geom(int H, int W, int ipw) {
 }
 }  // namespace
 
-__global__ __launch_bounds__(256) void wgrad3x3_img_kernel(WgradArgs a, int ipw, GroupArg ga) {
-  gshift(a, goff(ga));
-  prefetch_kernargs<sizeof(WgradArgs)>();
+__device__ __forceinline__ void wgrad3x3_img_tile(const WgradArgs& a, const int ipw, const int bx, const int by) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int H = a.H, W = a.W;
   const WhGeom geo = wh_geom(H, W, ipw);
@@ -343,8 +348,8 @@ __global__ __launch_bounds__(256) void wgrad3x3_img_kernel(WgradArgs a, int ipw,
   float* s_shift = s_scale + a.Cin;
 
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-  const int c0 = blockIdx.y * WH_CB;
-  const int img_beg = blockIdx.x * ipw;
+  const int c0 = by * WH_CB;
+  const int img_beg = bx * ipw;
   const int img_end = min(a.N, img_beg + ipw);
   const int HW = H * W, Wp = geo.Wp, RI = geo.RI, P = geo.P;
 
@@ -442,9 +447,15 @@ __global__ __launch_bounds__(256) void wgrad3x3_img_kernel(WgradArgs a, int ipw,
         const int co = j * 16 + (lane & 15);
         const size_t k = (size_t)t * a.Cin + c;
         const float v = acc[t][j][r] * a.scale;
-        if (a.part) a.part[(size_t)blockIdx.x * n_dw + k * 32 + co] = v;
+        if (a.part) a.part[(size_t)bx * n_dw + k * 32 + co] = v;
         else atomicAdd(&a.dw[k * 32 + co], v);
       }
+}
+
+__global__ __launch_bounds__(256) void wgrad3x3_img_kernel(WgradArgs a, int ipw, GroupArg ga) {
+  gshift(a, goff(ga));
+  prefetch_kernargs<sizeof(WgradArgs)>();
+  wgrad3x3_img_tile(a, ipw, blockIdx.x, blockIdx.y);
 }
 
 // the direct small-image path applies (and then `splits` counts image groups): 3x3 / s1 / pad 1,
@@ -570,6 +581,126 @@ int wgrad_effective_splits(const WgradArgs& a, int splits, int variant) {
   int per = (M + splits - 1) / splits;
   per = (per + bp - 1) / bp * bp;
   return (M + per - 1) / per;
+}
+
+// ---- batched weight gradients (conv_wgrad.h) -------------------------------------------------
+__device__ __forceinline__ int wg_batch_member(const int* __restrict__ begins, int lin) {
+  const int lane = threadIdx.x & 63;
+  const int v = begins[lane];  // padded with INT_MAX to WG_BATCH_MAX entries
+  return __popcll(__ballot(v <= lin)) - 1;
+}
+
+template <int BKR, int BC, int BP, int WM, int WN, bool IS1X1, int PRO>
+__global__ __launch_bounds__(256) void conv_wgrad_batch_kernel(const WgBatchEntry* __restrict__ list,
+                                                               const int* __restrict__ begins, GroupArg ga) {
+  const int lin = blockIdx.x;
+  const int m = wg_batch_member(begins, lin);
+  WgradArgs a = list[m].a;
+  gshift(a, goff(ga));
+  const int gx = list[m].gx, gxy = gx * list[m].gy;
+  const int r = lin - begins[m];
+  const int z = r / gxy, rem = r - z * gxy;
+  wgrad_tile<BKR, BC, BP, WM, WN, IS1X1, bf16_t, PRO, 0>(a, rem % gx, rem / gx, z);
+}
+
+__global__ __launch_bounds__(256) void wgrad3x3_img_batch_kernel(const WgBatchEntry* __restrict__ list,
+                                                                 const int* __restrict__ begins, GroupArg ga) {
+  const int lin = blockIdx.x;
+  const int m = wg_batch_member(begins, lin);
+  WgradArgs a = list[m].a;
+  gshift(a, goff(ga));
+  const int gx = list[m].gx;
+  const int r = lin - begins[m];
+  wgrad3x3_img_tile(a, list[m].ipw, r % gx, r / gx);
+}
+
+// general-kernel tile of a member: 0 <128,32>, 1 <128,64>, 2 <128,128>, 3 <64,128>
+static int wg_tile_sel(const WgradArgs& a) {
+  if (a.Cout <= 32) return 0;
+  if (a.Cout <= 64) return 1;
+  if (wgrad_big_tile(a)) return 2;
+  return 3;
+}
+
+int wgrad_batch_sig(const WgradArgs& a, bool g_f32, int variant) {
+  if (a.part || g_f32 || a.gpro.mode != 0) return -1;
+  if (variant > 0 && wgrad_big_ok(a, g_f32, variant)) return -1;
+  if (wgrad_halo_ok(a, g_f32)) return 1;
+  const bool is1x1 = a.KH == 1 && a.KW == 1 && a.SH == 1 && a.SW == 1 && a.PT == 0 && a.PL == 0;
+  const int pro = (a.pro.mode != 0 || a.pro.act != ACT_NONE) ? 1 : 0;
+  return 16 + wg_tile_sel(a) * 4 + (is1x1 ? 2 : 0) + pro;
+}
+
+int wgrad_batch_entry(const WgradArgs& a0, int splits, WgBatchEntry& e, long long& smem) {
+  WgradArgs a = a0;
+  e.ipw = 0;
+  if (wgrad_halo_ok(a, false)) {
+    const int groups = wgrad_halo_groups(a, splits);
+    e.ipw = (a.N + groups - 1) / groups;
+    const WhGeom geo = wh_geom(a.H, a.W, e.ipw);
+    smem = (long long)(geo.x_bytes + geo.g_bytes + 2 * (size_t)a.Cin * 4);
+    e.a = a;
+    e.gx = groups;
+    e.gy = a.Cin / WH_CB;
+    e.gz = 1;
+    return e.gx * e.gy;
+  }
+  const int M = a.N * a.Ho * a.Wo;
+  if (splits < 1) splits = 1;
+  const int bp = wgrad_bp(a.Cout);
+  int per = (M + splits - 1) / splits;
+  per = (per + bp - 1) / bp * bp;
+  splits = (M + per - 1) / per;
+  a.pix_per_split = per;
+  const int K = a.KH * a.KW * a.Cin;
+  const int pro = (a.pro.mode != 0 || a.pro.act != ACT_NONE) ? 1 : 0;
+  int bkr = 64, bc = 128;
+  switch (wg_tile_sel(a)) {
+    case 0: bkr = 128; bc = 32; smem = WgCfg<128, 32, 32>::smem_bytes(pro ? a.Cin : 0); break;
+    case 1: bkr = 128; bc = 64; smem = WgCfg<128, 64, 32>::smem_bytes(pro ? a.Cin : 0); break;
+    case 2: bkr = 128; bc = 128; smem = WgCfg<128, 128, 32>::smem_bytes(pro ? a.Cin : 0); break;
+    default: smem = WgCfg<64, 128, 32>::smem_bytes(pro ? a.Cin : 0); break;
+  }
+  e.a = a;
+  e.gx = (K + bkr - 1) / bkr;
+  e.gy = (a.Cout + bc - 1) / bc;
+  e.gz = splits;
+  return e.gx * e.gy * e.gz;
+}
+
+hipError_t wgrad_batch(const WgBatchEntry* list, const int* begins, int n, int total, int sig, long long smem,
+                       hipStream_t st) {
+  if (n <= 0 || total <= 0) return hipSuccess;
+  if (n > WG_BATCH_MAX || list == nullptr || begins == nullptr || smem > 160 * 1024) return hipErrorInvalidValue;
+  const size_t shm = (size_t)smem;
+  if (sig == 1) {
+    hipLaunchKernelGGL(wgrad3x3_img_batch_kernel, ggrid(total), dim3(256), shm, st, list, begins, garg());
+    return hipGetLastError();
+  }
+  if (sig < 16 || sig >= 32) return hipErrorInvalidValue;
+  const int tile = (sig - 16) / 4, is1x1 = (sig >> 1) & 1, pro = sig & 1;
+#define IDC_WB(BKR, BC, WM, WN)                                                                              \
+  {                                                                                                          \
+    if (is1x1) {                                                                                             \
+      if (pro) hipLaunchKernelGGL((conv_wgrad_batch_kernel<BKR, BC, 32, WM, WN, true, 1>), ggrid(total),     \
+                                  dim3(256), shm, st, list, begins, garg());                                 \
+      else hipLaunchKernelGGL((conv_wgrad_batch_kernel<BKR, BC, 32, WM, WN, true, 0>), ggrid(total),         \
+                              dim3(256), shm, st, list, begins, garg());                                     \
+    } else {                                                                                                 \
+      if (pro) hipLaunchKernelGGL((conv_wgrad_batch_kernel<BKR, BC, 32, WM, WN, false, 1>), ggrid(total),    \
+                                  dim3(256), shm, st, list, begins, garg());                                 \
+      else hipLaunchKernelGGL((conv_wgrad_batch_kernel<BKR, BC, 32, WM, WN, false, 0>), ggrid(total),        \
+                              dim3(256), shm, st, list, begins, garg());                                     \
+    }                                                                                                        \
+  }
+  switch (tile) {
+    case 0: IDC_WB(128, 32, 4, 1) break;
+    case 1: IDC_WB(128, 64, 2, 2) break;
+    case 2: IDC_WB(128, 128, 2, 2) break;
+    default: IDC_WB(64, 128, 2, 2) break;
+  }
+#undef IDC_WB
+  return hipGetLastError();
 }
 
 int wgrad_pick_splits(int M, int K, int Cout) {

@@ -26,7 +26,9 @@
 #include <pybind11/stl.h>
 
 #include <cstdlib>
+#include <algorithm>
 #include <cstring>
+#include <limits>
 #include <mutex>
 #include <unordered_map>
 #include <stdexcept>
@@ -76,6 +78,9 @@ enum OpKind : int {
   // gradient-bucket all-reduce on the communicator's stream (the "comm lane"): p[0] buffer,
   // l[0] element count, i[0] dtype code, i[1] reduction op (csrc/comm/communicator.h)
   OP_ALLREDUCE = 26,
+  // batched weight gradients (conv_wgrad.h): p[0] device WgBatchEntry[n], p[1] device begins
+  // (WG_BATCH_MAX ints), i[0] n, i[1] total workgroups, i[2] batch signature, l[0] LDS bytes
+  OP_WGRAD_BATCH = 27,
 };
 
 struct Op {
@@ -616,6 +621,11 @@ class Plan {
                             op.i[1], op.i[2], st),
               "slot_collapse");
         break;
+      case OP_WGRAD_BATCH:
+        check(wgrad_batch(reinterpret_cast<const WgBatchEntry*>(op.p[0]), reinterpret_cast<const int*>(op.p[1]),
+                          op.i[0], op.i[1], op.i[2], op.l[0], st),
+              "wgrad_batch");
+        break;
       case OP_STATS_SHIFT:
         check(stats_shift(reinterpret_cast<const ShiftDesc*>(op.p[0]), op.i[0], op.i[1], st), "stats_shift");
         break;
@@ -716,6 +726,7 @@ py::dict struct_sizes() {
   d["BnArgs"] = sizeof(BnArgs);
   d["ConvArgs"] = sizeof(ConvArgs);
   d["WgradArgs"] = sizeof(WgradArgs);
+  d["WgBatchEntry"] = sizeof(WgBatchEntry);
   d["BnBwdApplyArgs"] = sizeof(BnBwdApplyArgs);
   d["BnBwdReduceArgs"] = sizeof(BnBwdReduceArgs);
   d["PoolArgs"] = sizeof(PoolArgs);
@@ -784,6 +795,43 @@ int py_effective_splits(py::bytes payload, int splits) {
   WgradArgs a;
   std::memcpy(&a, s.data(), sizeof(a));
   return wgrad_effective_splits(a, splits);
+}
+
+int py_wgrad_batch_sig(py::bytes payload, int g_f32, int variant) {
+  std::string s = payload;
+  if (s.size() != sizeof(WgradArgs)) throw std::runtime_error("WgradArgs size mismatch");
+  WgradArgs a;
+  std::memcpy(&a, s.data(), sizeof(a));
+  return wgrad_batch_sig(a, g_f32 != 0, variant);
+}
+
+// members' WgradArgs payloads + split factors -> (WgBatchEntry table bytes, begins padded to
+// WG_BATCH_MAX, total workgroups, LDS bytes)
+py::tuple py_wgrad_batch_pack(py::list payloads, py::list splits) {
+  const int n = (int)py::len(payloads);
+  if (n < 1 || n > WG_BATCH_MAX || (int)py::len(splits) != n) throw std::runtime_error("wgrad_batch_pack: bad member count");
+  std::vector<WgBatchEntry> ents(n);
+  std::vector<int> begins(WG_BATCH_MAX, std::numeric_limits<int>::max());
+  long long total = 0, smem = 0;
+  int sig = -2;
+  for (int i = 0; i < n; ++i) {
+    std::string s = payloads[i].cast<py::bytes>();
+    if (s.size() != sizeof(WgradArgs)) throw std::runtime_error("WgradArgs size mismatch");
+    WgradArgs a;
+    std::memcpy(&a, s.data(), sizeof(a));
+    const int si = wgrad_batch_sig(a, false, 0);
+    if (si < 0 || (sig != -2 && si != sig)) throw std::runtime_error("wgrad_batch_pack: members differ in kernel shape");
+    sig = si;
+    long long sm = 0;
+    begins[i] = (int)total;
+    total += wgrad_batch_entry(a, splits[i].cast<int>(), ents[i], sm);
+    smem = std::max(smem, sm);
+  }
+  if (total > (1LL << 30)) throw std::runtime_error("wgrad_batch_pack: grid too large");
+  py::bytes tab(reinterpret_cast<const char*>(ents.data()), ents.size() * sizeof(WgBatchEntry));
+  py::list bl;
+  for (int b : begins) bl.append(b);
+  return py::make_tuple(tab, bl, total, smem, sig);
 }
 
 void py_secagg_mask(uintptr_t x, uintptr_t out, long long n, uintptr_t seg_scale, uintptr_t seg_end, int nseg,
@@ -929,6 +977,9 @@ PYBIND11_MODULE(_idc_native, m) {
   m.attr("TILE_RING") = TILE_RING;
   m.attr("TILE_RING_N") = TILE_RING_N;
   m.def("effective_splits", &py_effective_splits);
+  m.def("wgrad_batch_sig", &py_wgrad_batch_sig);
+  m.def("wgrad_batch_pack", &py_wgrad_batch_pack);
+  m.attr("WG_BATCH_MAX") = WG_BATCH_MAX;
   m.def("rows_grid", &rows_grid);
   m.def("num_tiles", &conv_num_tiles);
   m.def("tile_bm", &conv_tile_bm);

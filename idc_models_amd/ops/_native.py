@@ -128,7 +128,13 @@ class Mlp2Args(C.Structure):
                 ("db2", vp), ("dx", vp)]
 
 
+class WgBatchEntry(C.Structure):
+    """One member of a batched weight-gradient launch (conv_wgrad.h)."""
+    _fields_ = [("a", WgradArgs), ("gx", ci), ("gy", ci), ("gz", ci), ("ipw", ci)]
+
+
 _STRUCTS = {"BnArgs": BnArgs, "BwdAff": BwdAff, "ConvArgs": ConvArgs, "WgradArgs": WgradArgs,
+            "WgBatchEntry": WgBatchEntry,
             "BnBwdApplyArgs": BnBwdApplyArgs, "BnBwdReduceArgs": BnBwdReduceArgs,
             "PoolArgs": PoolArgs, "PoolBwdArgs": PoolBwdArgs, "BnMovingDesc": BnMovingDesc,
             "HeadArgs": HeadArgs, "HeadBwdArgs": HeadBwdArgs, "CastEntry": CastEntry,
@@ -138,7 +144,7 @@ _STRUCTS = {"BnArgs": BnArgs, "BwdAff": BwdAff, "ConvArgs": ConvArgs, "WgradArgs
 OP_CONV, OP_WGRAD, OP_BN_BWD_APPLY, OP_BN_BWD_REDUCE, OP_MAXPOOL, OP_AVGPOOL, OP_POOL_BWD = range(7)
 OP_BN_MOVING, OP_HEAD_FWD, OP_HEAD_BWD, OP_RMSPROP, OP_CAST, OP_INPUT, OP_MEMSET = range(7, 14)
 OP_BN_STATS, OP_BN_APPLY, OP_DW_FWD, OP_DW_BWD_DATA, OP_DW_WGRAD, OP_COPY, OP_FINITE_CHECK = range(14, 21)
-OP_MLP_FWD, OP_MLP_BWD, OP_MLP_STEP, OP_COLLAPSE, OP_STATS_SHIFT, OP_ALLREDUCE = range(21, 27)
+OP_MLP_FWD, OP_MLP_BWD, OP_MLP_STEP, OP_COLLAPSE, OP_STATS_SHIFT, OP_ALLREDUCE, OP_WGRAD_BATCH = range(21, 28)
 
 ACT = {None: 0, "none": 0, "linear": 0, "relu": 1, "relu6": 2}
 OUT_BF16, OUT_F32, OUT_F32_ACC = 0, 1, 2

@@ -239,6 +239,35 @@ def conv2d_wgrad(x: torch.Tensor, dy: torch.Tensor, kernel_shape, stride=(1, 1),
     return out
 
 
+def conv2d_wgrad_batch(members) -> list:
+    """Several weight gradients in ONE batched launch (OP_WGRAD_BATCH, conv_wgrad.h): ``members``
+    is a list of dicts with the ``conv2d_wgrad`` arguments x, dy, kernel_shape and optionally
+    stride, pads, pro, splits, out.  All members must share one batch signature (kernel shape
+    class).  Returns the dW tensors."""
+    ext = nat.require()
+    outs, raws, splits = [], [], []
+    for mb in members:
+        x, dy, ks = mb["x"], mb["dy"], mb["kernel_shape"]
+        out = mb.get("out")
+        if out is None:
+            out = torch.zeros((ks[0], ks[1], x.shape[3], dy.shape[3]), dtype=torch.float32, device=x.device)
+        a = _wgrad_args(x, dy, ks, mb.get("stride", (1, 1)), mb.get("pads", (0, 0)), mb.get("pro"), 0, out, None)
+        sp = mb.get("splits", -1)
+        if sp < 0:
+            sp = ext.pick_splits(dy.shape[0] * dy.shape[1] * dy.shape[2], ks[0] * ks[1] * x.shape[3], dy.shape[3])
+        outs.append(out)
+        raws.append(nat.raw(a))
+        splits.append(int(sp))
+    tab, begins, total, smem, sig = ext.wgrad_batch_pack(raws, splits)
+    dev = members[0]["x"].device
+    tdev = torch.frombuffer(bytearray(tab), dtype=torch.uint8).to(dev)
+    bdev = torch.tensor(begins, dtype=torch.int32).to(dev)
+    _plan1(nat.OP_WGRAD_BATCH, ints=(len(members), int(total), int(sig)), longs=(int(smem),),
+           ptrs=(tdev.data_ptr(), bdev.data_ptr()))
+    torch.cuda.current_stream(dev).synchronize()  # the tables die with this frame
+    return outs
+
+
 def _plan1(kind, payload=None, ints=(), floats=(), longs=(), ptrs=()):
     p = nat.require().Plan()
     p.add(kind, nat.raw(payload) if payload is not None else b"", list(ints), list(floats),

@@ -169,6 +169,11 @@ class Builder:
         self.all_stats: List[Stats] = []
         # shifted statistics (IDC_STATS_SHIFT=0: plain E[y^2] - E[y]^2, for comparisons)
         self.shift_stats = os.environ.get("IDC_STATS_SHIFT", "1") != "0"
+        # batched weight gradients (conv_wgrad.h WgBatchEntry): side-lane wgrads a lowering marks
+        # ``batch=True`` are collected and launched as ONE kernel per kernel shape at the next
+        # flush_wgrad_batch (DenseNet: the end of a late stage's dense layers)
+        self._wg_batch: List[tuple] = []
+        self._wg_batch_marks: list = []
 
     # ------------------------------------------------------------------ allocation
     def alloc(self, shape, dtype=BF16) -> torch.Tensor:
@@ -319,7 +324,11 @@ class Builder:
         return int(nat.load().rows_grid(int(M), int(C), int(per)))
 
     def mark_grads_ready(self, params):
-        """Backward has finished producing the grads of ``params`` (for DP bucket overlap)."""
+        """Backward has finished producing the grads of ``params`` (for DP bucket overlap).
+        While batched weight gradients are pending, the mark waits for their launch."""
+        if self._wg_batch:
+            self._wg_batch_marks.extend(params)
+            return
         self.flush_grad_sums(params)
         idx = [i for i, p in enumerate(self.arena.params) if any(p is q for q in params)]
         if idx:
@@ -585,7 +594,7 @@ class Builder:
         self.finish_grad_sums(gbn)
 
     def wgrad(self, x: Tensor4, layer, g: Tensor4, dw: torch.Tensor, *, stride=(1, 1), pads=(0, 0),
-              pro=None, cin_real=0, splits=-1, lane=0, gpro: Optional[nat.BwdAff] = None):
+              pro=None, cin_real=0, splits=-1, lane=0, gpro: Optional[nat.BwdAff] = None, batch=False):
         kh, kw = layer.kernel_size
         if self.is_center_only(layer, x.H, x.W, stride, pads):
             # only the centre tap sees data: its gradient is the 1x1 wgrad; the other taps keep
@@ -616,6 +625,10 @@ class Builder:
         a.cin_real = cin_real
         if splits < 0:
             splits = nat.load().pick_splits(g.M, kh * kw * x.C, g.C)
+        if batch and not self.det and lane == 1 and self.side_lane:
+            if nat.load().wgrad_batch_sig(nat.raw(a), 1 if g.is_f32 else 0, 0) >= 0:
+                self._wg_batch.append((a, splits))
+                return
         if self.det:
             # per-slice partials + a fixed-order reduce instead of float atomics (plan.cpp OP_WGRAD);
             # one slab per lane, reused by that lane's wgrads (a lane runs them one after another)
@@ -627,6 +640,34 @@ class Builder:
                 self._wslab[ln] = slab
             a.part, a.part_floats = slab.data_ptr(), slab.numel()
         self.emit(nat.OP_WGRAD, a, ints=(splits, 1 if g.is_f32 else 0), lane=lane)
+
+    def has_wgrad_batch(self) -> bool:
+        return bool(self._wg_batch)
+
+    def flush_wgrad_batch(self):
+        """Launch the collected weight gradients: one OP_WGRAD_BATCH per kernel shape (members in
+        collection order, at most WG_BATCH_MAX each) on the side lane, then the gradient-ready
+        marks that waited for them."""
+        if not self._wg_batch:
+            return
+        ext = nat.load()
+        members, self._wg_batch = self._wg_batch, []
+        groups: Dict[int, list] = {}
+        for a, splits in members:
+            groups.setdefault(int(ext.wgrad_batch_sig(nat.raw(a), 0, 0)), []).append((a, splits))
+        for sig, mem in groups.items():
+            for i in range(0, len(mem), int(ext.WG_BATCH_MAX)):
+                chunk = mem[i:i + int(ext.WG_BATCH_MAX)]
+                tab, begins, total, smem, sig2 = ext.wgrad_batch_pack([nat.raw(a) for a, _ in chunk],
+                                                                       [int(s) for _, s in chunk])
+                tdev = torch.frombuffer(bytearray(tab), dtype=torch.uint8).to(self.device)
+                bdev = torch.tensor(begins, dtype=torch.int32).to(self.device)
+                self.keep += [tdev, bdev]
+                self.emit(nat.OP_WGRAD_BATCH, ints=(len(chunk), int(total), int(sig2)), longs=(int(smem),),
+                          ptrs=(tdev.data_ptr(), bdev.data_ptr()), lane=1)
+        marks, self._wg_batch_marks = self._wg_batch_marks, []
+        if marks:
+            self.mark_grads_ready(marks)
 
     def bn_bwd_apply(self, dz: Tensor4, x: Tensor4, bn: BNRef, dst: Tensor4, accumulate: bool):
         a = nat.BnBwdApplyArgs()

@@ -41,7 +41,7 @@ _PAYLOAD = {
 }
 # descriptor-table ops: (ptr slot of the table, int slot of its length, entry type)
 _TABLES = {nat.OP_BN_MOVING: (0, 0, nat.BnMovingDesc), nat.OP_STATS_SHIFT: (0, 0, nat.ShiftDesc),
-           nat.OP_CAST: (0, 0, nat.CastEntry)}
+           nat.OP_CAST: (0, 0, nat.CastEntry), nat.OP_WGRAD_BATCH: (0, 0, nat.WgBatchEntry)}
 
 
 def _struct_ptrs(obj, path=""):

@@ -138,10 +138,18 @@ def lower_densenet(b: Builder, net, U: int, input_dtype):
     def pend_params():
         return [pend.gamma, pend.beta]
 
+    # Late stages (M <= IDC_WG_BATCH_MAXM pixels; default 9216: stages 2-4 at bs 256) batch their weight
+    # gradients: each dense layer's wgrads are launch-latency bound (10-20 us for < 1 us of MFMA
+    # work, 2 side-lane launches + a fork per layer), and their operands (the per-layer staged
+    # gradients dO16 / dt, the forward buffers) are final once the stage's dgrad chain has run, so
+    # the stage issues them as one OP_WGRAD_BATCH per kernel shape that fills the GPU beside the
+    # previous stage's data gradients (builder.flush_wgrad_batch).
+    batch_maxm = int(os.environ.get("IDC_WG_BATCH_MAXM", "9216"))
     for si in range(len(stages) - 1, -1, -1):
         st = stages[si]
         buf = st["buf"]
         N, Hs, Ws = buf.N, st["H"], st["W"]
+        wb = N * Hs * Ws <= batch_maxm
         z2 = b.nhwc(N, Hs, Ws, 128)  # dZ of bn2, consumed by the next dgrad only
         for lay in reversed(st["layers"]):
             cin, bn1, cv1, bn2, cv2, t = lay["cin"], lay["bn1"], lay["cv1"], lay["bn2"], lay["cv2"], lay["t"]
@@ -160,7 +168,8 @@ def lower_densenet(b: Builder, net, U: int, input_dtype):
             b.dgrad(dO, cv2, z2, pads=(1, 1), mx=t, mbn=bn2.args(), gbn=bn2,
                     bpro=b.bwd_aff(pend, xO, c0=cin, unit_alpha=True, fold=True), aout=dO16)
             if fz.trainable(cv2):
-                b.wgrad(t, cv2, dO16, b.arena.grad_of(cv2.kernel), pads=(1, 1), pro=bn2.args(), lane=1)
+                b.wgrad(t, cv2, dO16, b.arena.grad_of(cv2.kernel), pads=(1, 1), pro=bn2.args(), lane=1,
+                        batch=wb)
             if not fz.before(bn2.layer):
                 b.mark_grads_ready([cv2.kernel, bn2.gamma, bn2.beta] + pend_params())
                 return
@@ -177,12 +186,14 @@ def lower_densenet(b: Builder, net, U: int, input_dtype):
                     bpro=b.bwd_aff(bn2, t, fold=True),
                     bepi=b.bwd_aff(pend, buf.slice(0, cin), unit_alpha=True), aout=dt)
             if fz.trainable(cv1):
-                b.wgrad(buf.slice(0, cin), cv1, dt, b.arena.grad_of(cv1.kernel), pro=bn1.args(), lane=1)
+                b.wgrad(buf.slice(0, cin), cv1, dt, b.arena.grad_of(cv1.kernel), pro=bn1.args(), lane=1,
+                        batch=wb)
             b.mark_grads_ready(ready)
             pend = bn1
             if not fz.before(bn1.layer):
                 b.mark_grads_ready(pend_params())
                 return
+        b.flush_wgrad_batch()
         if si == 0:
             break
         # transition of the previous stage (wrote this stage's channels [0:c0)), through pend

@@ -73,6 +73,9 @@ class FusedProgram:
         self.U = net.num_outputs
         b = Builder(net, model.arena, model.device, batch, training)
         _lowering_for(net)(b, net, self.U, input_dtype)
+        if b.has_wgrad_batch():  # a lowering that returned early (frozen layers) mid-batch
+            b.segment = "bwd"
+            b.flush_wgrad_batch()
         if b.pending_sums:  # BatchNorm gradient slot copies no apply kernel folded
             b.segment = "bwd"
             b.flush_grad_sums()
@@ -312,7 +315,9 @@ class FusedProgram:
         issue of every op with per-batch side forks (plan.cpp issue)."""
         lo, hi = self.seg["bwd"]
         if self.bwd_chunks <= 0:
-            self.run_range(lo, hi, graph=False)
+            # whole-segment forms (IDC_DUAL_GRAPH=1 / "bwd" in IDC_GRAPH_SEGMENTS) replay graphs,
+            # everything else issues directly
+            self.run_range(lo, hi, graph=None if self.use_graphs else False)
             return
         plan, sh = self.plan, self._sh()
         if self._bwd_graphs is None:

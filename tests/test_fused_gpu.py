@@ -276,3 +276,38 @@ def test_moving_statistics_match_eager_every_bn(arch):
         if em > 2 * em16 + 0.05 or ev > 2 * ev16 + 0.05:
             bad.append((l.name, round(em, 3), round(em16, 3), round(ev, 3), round(ev16, 3)))
     assert not bad, bad[:12]
+
+
+@pytest.mark.parametrize("maxm", ["2304", "9216"])
+def test_batched_weight_gradients_match_per_layer(monkeypatch, maxm):
+    """DenseNet-121 at the bench batch: the late stages' weight gradients launched as one batched
+    kernel per shape (OP_WGRAD_BATCH, the default for M <= 2304 pixels; here also stage 2) against
+    the per-layer launches.  Without IDC_DETERMINISTIC the statistics' float-atomic order already
+    makes two identical per-layer programs differ (bf16 roundings flip and propagate through 120
+    layers), so the batched program must sit within the per-layer run-to-run spread; the kernel
+    itself is checked exactly in test_kernels_gpu.py::test_wgrad_batch_matches_single_launches."""
+    from idc_models_amd.engine import Model, RMSprop
+    from idc_models_amd.models import build_model
+    from idc_models_amd.ops import _native as nat
+    g = torch.Generator().manual_seed(17)
+    x = torch.randint(0, 256, (256, 50, 50, 3), generator=g, dtype=torch.uint8)
+    y = torch.randint(0, 2, (256,), generator=g)
+    grads = []
+    for mm in ("0", "0", maxm):
+        monkeypatch.setenv("IDC_WG_BATCH_MAXM", mm)
+        net = build_model("densenet121", None, num_outputs=1, seed=3)
+        m = Model(net, device=DEV)
+        m.compile(RMSprop(1e-4), "binary_crossentropy", [], backend="fused")
+        m.impl.train_step(x, y)
+        torch.cuda.synchronize()
+        p = m.impl._prog(256, True, torch.uint8)
+        nb = sum(1 for i in range(p.plan.size()) if p.plan.kind(i) == nat.OP_WGRAD_BATCH)
+        assert (nb > 0) == (mm != "0"), (mm, nb)
+        grads.append(m.arena.grad.clone())
+    g0, g1, gb = grads
+
+    def rel(a, b):
+        return float((a - b).norm() / (b.norm() + 1e-12))
+
+    noise, dev = rel(g1, g0), rel(gb, g0)
+    assert dev <= 3 * noise + 1e-3, (dev, noise)

@@ -827,3 +827,42 @@ def test_wgrad_big_deterministic_partials(fn):
     torch.cuda.synchronize()
     assert torch.equal(outs[0], outs[1])
     assert relerr(outs[0], ref) < 1e-2
+
+
+def _bn_pro(fn, t, seed):
+    g_ = torch.Generator(device=DEV).manual_seed(seed)
+    C = t.shape[-1]
+    st = torch.cat([t.sum((0, 1, 2)), (t * t).sum((0, 1, 2))])
+    gam = torch.rand(C, device=DEV, generator=g_) + 0.5
+    bet = torch.randn(C, device=DEV, generator=g_) * 0.1
+    cnt = t.shape[0] * t.shape[1] * t.shape[2]
+    return fn.BN(stats=st, gamma=gam, beta=bet, count=cnt, eps=1e-3, act=1), (st, gam, bet, cnt)
+
+
+@pytest.mark.parametrize("kind,N,H", [("1x1", 32, 3), ("1x1", 16, 6), ("3x3", 64, 3), ("3x3", 16, 6),
+                                      ("c32", 64, 1)])
+def test_wgrad_batch_matches_single_launches(fn, kind, N, H):
+    """OP_WGRAD_BATCH (conv_wgrad.h WgBatchEntry): members of mixed Cin in one launch give the
+    per-layer launches' dW (fp32 atomic order only) and the fp32 reference (bf16 operands).
+    Shapes: DenseNet late-stage 1x1 bottleneck wgrads (Cout 128, BN prologue), the direct 3x3
+    growth-conv wgrads on 3x3 / 6x6 maps, and the centre-tap 128 -> 32 wgrads of 1x1 maps."""
+    torch.manual_seed(11)
+    members, refs, singles = [], [], []
+    cins = (256, 288, 544, 992) if kind == "1x1" else (128, 128, 128)
+    for j, cin in enumerate(cins):
+        cout = 128 if kind == "1x1" else 32
+        k = 3 if kind == "3x3" else 1
+        x = bf(torch.randn(N, H, H, cin, device=DEV) * (1 + 0.1 * j) + 0.2 * j)
+        dy = bf(torch.randn(N, H, H, cout, device=DEV))
+        pro, (st, gam, bet, cnt) = _bn_pro(fn, x, 100 + j)
+        pads = (1, 1) if k == 3 else (0, 0)
+        mb = dict(x=x.to(torch.bfloat16), dy=dy.to(torch.bfloat16), kernel_shape=(k, k), pads=pads, pro=pro)
+        members.append(mb)
+        singles.append(fn.conv2d_wgrad(mb["x"], mb["dy"], (k, k), pads=pads, pro=pro))
+        a = bf(bn_ref(x, st, gam, bet, cnt, 1e-3, 1))
+        refs.append(torch.nn.grad.conv2d_weight(a.permute(0, 3, 1, 2), (cout, cin, k, k), dy.permute(0, 3, 1, 2),
+                                                padding=pads[0]).permute(2, 3, 1, 0))
+    outs = fn.conv2d_wgrad_batch(members)
+    for o, s1, r in zip(outs, singles, refs):
+        assert relerr(o, s1) < 1e-5
+        assert relerr(o, r) < 1.5e-2

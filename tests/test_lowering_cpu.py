@@ -66,6 +66,14 @@ def test_plan_pointers_are_live(arch, ft):
         if kind in STRUCTS:
             assert len(raw) == C.sizeof(STRUCTS[kind]), (i, kind)
             _pointers(STRUCTS[kind].from_buffer_copy(raw), vals)
+        if kind == nat.OP_WGRAD_BATCH:  # the member table's argument structs
+            tab = next(t for t in b.keep if t.data_ptr() == ptrs[0])
+            n = ints[0]
+            raw_tab = bytes(tab.cpu().numpy().tobytes())
+            assert len(raw_tab) == n * C.sizeof(nat.WgBatchEntry), (i, n)
+            for j in range(n):
+                e = nat.WgBatchEntry.from_buffer_copy(raw_tab, j * C.sizeof(nat.WgBatchEntry))
+                _pointers(e.a, vals)
         for name, v in vals:
             if not any(lo <= v < hi for lo, hi in ranges):
                 bad.append((i, kind, name))
@@ -93,14 +101,27 @@ def test_fine_tune_backward_stops_at_first_trainable_layer():
     assert n_wgrad == len(trainable_convs)
 
 
-def test_weight_gradients_are_on_the_side_lane():
-    _, _, b = _lower("densenet121", None, True)
+@pytest.mark.parametrize("maxm", ["0", "2304", "9216", "100000000"])
+def test_weight_gradients_are_on_the_side_lane(monkeypatch, maxm):
+    monkeypatch.setenv("IDC_WG_BATCH_MAXM", maxm)
+    _, net, b = _lower("densenet121", None, True, B=256)
     wg = [op for op in b.ops if op[1] == nat.OP_WGRAD]
+    batches = [op for op in b.ops if op[1] == nat.OP_WGRAD_BATCH]
     # every weight gradient but the stem's (it consumes the last main-lane op's output, so it
-    # runs on the main lane next to the side lane's backlog) is on the side lane
-    assert {op[7] for op in wg[:-1]} == ({1} if b.side_lane else {0})
+    # runs on the main lane next to the side lane's backlog) is on the side lane, single or batched
+    assert {op[7] for op in wg[:-1] + batches} == ({1} if b.side_lane else {0})
     assert wg[-1][7] == 0
-    assert all(op[7] == 0 for op in b.ops if op[1] != nat.OP_WGRAD)
+    assert all(op[7] == 0 for op in b.ops if op[1] not in (nat.OP_WGRAD, nat.OP_WGRAD_BATCH))
+    # every conv's weight gradient is computed exactly once
+    convs = [l for l in net.base.layers if l.keras_class == "Conv2D"]
+    assert len(wg) + sum(op[3][0] for op in batches) == len(convs)
+    # stages 3-4 at bs 256 (M = 2304 / 256 pixels) batch by default: one launch per kernel shape
+    if maxm == "2304":
+        assert len(batches) == 4 and len(wg) == len(convs) - 80
+    if maxm == "9216":  # the default: stages 2-4
+        assert len(batches) == 6 and len(wg) == len(convs) - 104
+    if maxm == "0":
+        assert not batches
 
 
 def test_struct_layouts_match_native():
