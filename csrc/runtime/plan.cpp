@@ -37,6 +37,7 @@
 
 #include "../kernels/conv_igemm.h"
 #include "../kernels/conv_wgrad.h"
+#include "../kernels/dense_stage.h"
 #include "../kernels/dwconv.h"
 #include "../kernels/mlp_head.h"
 #include "../kernels/nn_kernels.h"
@@ -81,6 +82,8 @@ enum OpKind : int {
   // batched weight gradients (conv_wgrad.h): p[0] device WgBatchEntry[n], p[1] device begins
   // (WG_BATCH_MAX ints), i[0] n, i[1] total workgroups, i[2] batch signature, l[0] LDS bytes
   OP_WGRAD_BATCH = 27,
+  // persistent dense-stage forward (dense_stage.hip): payload DenseStageArgs, i[0] = grid
+  OP_DENSE_STAGE = 28,
 };
 
 struct Op {
@@ -435,9 +438,9 @@ class Plan {
                                   "pool_bwd", "bn_moving", "head_fwd", "head_bwd", "rmsprop", "cast",
                                   "input", "memset", "bn_stats", "bn_apply", "dw_fwd", "dw_bwd_data",
                                   "dw_wgrad", "copy", "finite_check", "mlp_fwd", "mlp_bwd", "mlp_step",
-                                  "collapse", "stats_shift", "allreduce"};
+                                  "collapse", "stats_shift", "allreduce", "wgrad_batch", "dense_stage"};
     int k = ops_.at(idx).kind;
-    return (k >= 0 && k < 27) ? names[k] : "?";
+    return (k >= 0 && k < 29) ? names[k] : "?";
   }
 
  private:
@@ -626,6 +629,7 @@ class Plan {
                           op.i[0], op.i[1], op.i[2], op.l[0], st),
               "wgrad_batch");
         break;
+      case OP_DENSE_STAGE: check(dense_stage_fwd(as<DenseStageArgs>(op), op.i[0], st), "dense_stage_fwd"); break;
       case OP_STATS_SHIFT:
         check(stats_shift(reinterpret_cast<const ShiftDesc*>(op.p[0]), op.i[0], op.i[1], st), "stats_shift");
         break;
@@ -733,6 +737,8 @@ py::dict struct_sizes() {
   d["PoolBwdArgs"] = sizeof(PoolBwdArgs);
   d["BnMovingDesc"] = sizeof(BnMovingDesc);
   d["ShiftDesc"] = sizeof(ShiftDesc);
+  d["DenseStageArgs"] = sizeof(DenseStageArgs);
+  d["DenseLayerDesc"] = sizeof(DenseLayerDesc);
   d["BnArgs.shift"] = offsetof(BnArgs, shift);
   d["ConvArgs.stats_shift"] = offsetof(ConvArgs, stats_shift);
   d["PoolArgs.stats_shift"] = offsetof(PoolArgs, stats_shift);
@@ -989,4 +995,10 @@ PYBIND11_MODULE(_idc_native, m) {
   m.def("secagg_mask", &py_secagg_mask);
   m.def("secagg_unmask", &py_secagg_unmask);
   m.attr("OP_CONV") = (int)OP_CONV;
+  m.attr("OP_DENSE_STAGE") = (int)OP_DENSE_STAGE;
+  m.def("dense_stage_tasks", [](py::bytes payload) {
+    std::string s = payload;
+    if (s.size() != sizeof(DenseStageArgs)) throw std::runtime_error("dense_stage_tasks: bad payload");
+    return dense_stage_tasks(*reinterpret_cast<const DenseStageArgs*>(s.data()));
+  });
 }

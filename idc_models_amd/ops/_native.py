@@ -133,18 +133,32 @@ class WgBatchEntry(C.Structure):
     _fields_ = [("a", WgradArgs), ("gx", ci), ("gy", ci), ("gz", ci), ("ipw", ci)]
 
 
+class DenseLayerDesc(C.Structure):
+    """One dense layer of a persistent dense-stage launch (dense_stage.h)."""
+    _fields_ = [("w1", vp), ("w2", vp), ("g1", vp), ("b1", vp), ("g2", vp), ("b2", vp), ("t", vp),
+                ("tstats", vp), ("tshift", vp), ("eps1", cf), ("eps2", cf), ("cin", ci), ("pad_", ci)]
+
+
+class DenseStageArgs(C.Structure):
+    _fields_ = [("buf", vp), ("sstats", vp), ("sshift", vp), ("layers", vp), ("sync", vp), ("err", vp),
+                ("N", ci), ("H", ci), ("W", ci), ("ld", ci), ("nlayers", ci), ("k2", ci),
+                ("act1", ci), ("act2", ci), ("inv_count", cf), ("pad_", ci)]
+
+
 _STRUCTS = {"BnArgs": BnArgs, "BwdAff": BwdAff, "ConvArgs": ConvArgs, "WgradArgs": WgradArgs,
             "WgBatchEntry": WgBatchEntry,
             "BnBwdApplyArgs": BnBwdApplyArgs, "BnBwdReduceArgs": BnBwdReduceArgs,
             "PoolArgs": PoolArgs, "PoolBwdArgs": PoolBwdArgs, "BnMovingDesc": BnMovingDesc,
             "HeadArgs": HeadArgs, "HeadBwdArgs": HeadBwdArgs, "CastEntry": CastEntry,
-            "DwArgs": DwArgs, "Mlp2Args": Mlp2Args, "ShiftDesc": ShiftDesc}
+            "DwArgs": DwArgs, "Mlp2Args": Mlp2Args, "ShiftDesc": ShiftDesc,
+            "DenseStageArgs": DenseStageArgs, "DenseLayerDesc": DenseLayerDesc}
 
 # op kinds (csrc/runtime/plan.cpp)
 OP_CONV, OP_WGRAD, OP_BN_BWD_APPLY, OP_BN_BWD_REDUCE, OP_MAXPOOL, OP_AVGPOOL, OP_POOL_BWD = range(7)
 OP_BN_MOVING, OP_HEAD_FWD, OP_HEAD_BWD, OP_RMSPROP, OP_CAST, OP_INPUT, OP_MEMSET = range(7, 14)
 OP_BN_STATS, OP_BN_APPLY, OP_DW_FWD, OP_DW_BWD_DATA, OP_DW_WGRAD, OP_COPY, OP_FINITE_CHECK = range(14, 21)
 OP_MLP_FWD, OP_MLP_BWD, OP_MLP_STEP, OP_COLLAPSE, OP_STATS_SHIFT, OP_ALLREDUCE, OP_WGRAD_BATCH = range(21, 28)
+OP_DENSE_STAGE = 28
 
 ACT = {None: 0, "none": 0, "linear": 0, "relu": 1, "relu6": 2}
 OUT_BF16, OUT_F32, OUT_F32_ACC = 0, 1, 2
@@ -153,6 +167,8 @@ OUT_BF16, OUT_F32, OUT_F32_ACC = 0, 1, 2
 def _verify(ext):
     if ext.OP_ALLREDUCE != OP_ALLREDUCE:
         raise RuntimeError("native op-kind table drifted (OP_ALLREDUCE)")
+    if ext.OP_DENSE_STAGE != OP_DENSE_STAGE:
+        raise RuntimeError("native op-kind table drifted (OP_DENSE_STAGE)")
     sizes = ext.struct_sizes()
     for name, cls in _STRUCTS.items():
         if C.sizeof(cls) != sizes[name]:

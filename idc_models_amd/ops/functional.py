@@ -425,3 +425,35 @@ def bn_moments(stats: torch.Tensor, count: int, shift: Optional[torch.Tensor] = 
     _plan1(nat.OP_BN_MOVING, ints=(1, C), ptrs=(dev.data_ptr(),))
     torch.cuda.synchronize()
     return mean, var
+
+
+def dense_stage(buf: torch.Tensor, sstats: torch.Tensor, layers, sshift: Optional[torch.Tensor] = None,
+                act: int = RELU, grid: int = 256, k2: int = 3):
+    """All dense layers of a DenseNet stage in one persistent launch (csrc/kernels/dense_stage.hip).
+
+    ``buf``: NHWC bf16 stage buffer [N, H, W, ld] whose channels [0, c0) are filled and whose
+    ``sstats`` ([2*ld] fp32, shifted by ``sshift``) hold their statistics; ``layers``: dicts with
+    w1 ([128][cin] bf16 kernel layout), w2 ([32][k2][k2][128] bf16), g1, b1 ([cin]), g2, b2 ([128]),
+    t ([N,H,W,128] bf16 output), tstats ([256] zeroed fp32), tshift ([128] or None), eps1, eps2, cin.
+    Returns (sync counters, err flag) for inspection."""
+    N, H, W, ld = buf.shape
+    arr = (nat.DenseLayerDesc * len(layers))()
+    for d, L in zip(arr, layers):
+        d.w1, d.w2 = L["w1"].data_ptr(), L["w2"].data_ptr()
+        d.g1, d.b1, d.g2, d.b2 = (L[k].data_ptr() for k in ("g1", "b1", "g2", "b2"))
+        d.t, d.tstats, d.tshift = L["t"].data_ptr(), L["tstats"].data_ptr(), nat.ptr(L.get("tshift"))
+        d.eps1, d.eps2, d.cin = L["eps1"], L["eps2"], L["cin"]
+    import ctypes
+    tab = torch.frombuffer(bytearray(ctypes.string_at(ctypes.addressof(arr), ctypes.sizeof(arr))),
+                           dtype=torch.uint8).to(buf.device)
+    sync = torch.zeros(2 + 2 * len(layers), dtype=torch.int32, device=buf.device)
+    err = torch.zeros(1, dtype=torch.int32, device=buf.device)
+    a = nat.DenseStageArgs()
+    a.buf, a.sstats, a.sshift = buf.data_ptr(), sstats.data_ptr(), nat.ptr(sshift)
+    a.layers, a.sync, a.err = tab.data_ptr(), sync.data_ptr(), err.data_ptr()
+    a.N, a.H, a.W, a.ld, a.nlayers, a.k2 = N, H, W, ld, len(layers), k2
+    a.act1 = a.act2 = act
+    a.inv_count = 1.0 / float(N * H * W)
+    _plan1(nat.OP_DENSE_STAGE, a, ints=(grid, len(layers)), ptrs=(tab.data_ptr(),))
+    torch.cuda.current_stream().synchronize()
+    return sync, err

@@ -669,6 +669,57 @@ class Builder:
         if marks:
             self.mark_grads_ready(marks)
 
+    # ------------------------------------------------------------------ persistent dense stage
+    def dense_stage_ok(self, sbuf: Optional[Stats], layers, H: int, W: int) -> bool:
+        """Whether the dense layers of one stage can run as ONE persistent launch
+        (csrc/kernels/dense_stage.hip): training-mode BatchNorms on single-copy statistics,
+        1x1 inputs of <= 1024 channels in multiples of 32, 128-channel bottlenecks, 32 new channels
+        per layer, and no fixed-order (deterministic) reductions."""
+        if os.environ.get("IDC_DENSE_STAGE", "1") == "0" or not self.training or self.det:
+            return False
+        if sbuf is None or sbuf.slots != 1:
+            return False
+        for lay in layers:
+            if lay["bn1"].mode != 1 or lay["bn2"].mode != 1 or lay["stt"].slots != 1:
+                return False
+            if lay["cin"] % 32 or lay["cin"] > 1024 or lay["cv1"].filters != 128 or lay["cv2"].filters != 32:
+                return False
+            if tuple(lay["cv2"].kernel_size) != (3, 3) or tuple(lay["cv1"].kernel_size) != (1, 1):
+                return False
+        return True
+
+    def dense_stage(self, buf: Tensor4, sbuf: Stats, layers, act: int):
+        """Emit ONE persistent launch for the dense layers ``layers`` of a stage (dicts with cin,
+        bn1, cv1, bn2, cv2, t, stt as in lower_densenet): same buffers, statistics and weights as
+        the per-layer convs, so everything downstream (backward included) is unchanged."""
+        H, W = buf.H, buf.W
+        center = self.is_center_only(layers[0]["cv2"], H, W, (1, 1), (1, 1))
+        arr = (nat.DenseLayerDesc * len(layers))()
+        for d, lay in zip(arr, layers):
+            cin, bn1, bn2 = lay["cin"], lay["bn1"], lay["bn2"]
+            d.w1 = self.conv_weight(lay["cv1"], cin_pad=cin)["fwd"].data_ptr()
+            d.w2 = self.conv_weight(lay["cv2"], cin_pad=128, center=center)["fwd"].data_ptr()
+            d.g1, d.b1 = bn1.gamma.data_ptr(), bn1.beta.data_ptr()
+            d.g2, d.b2 = bn2.gamma.data_ptr(), bn2.beta.data_ptr()
+            d.t, d.tstats, d.tshift = lay["t"].ptr, lay["stt"].ptr, lay["stt"].shift_ptr()
+            d.eps1, d.eps2 = bn1.layer.epsilon, bn2.layer.epsilon
+            d.cin = cin
+        host = torch.frombuffer(bytearray(C.string_at(C.addressof(arr), C.sizeof(arr))), dtype=torch.uint8)
+        tab = host.to(self.device)
+        self.keep.append(tab)
+        if getattr(self, "dense_err", None) is None:
+            # sticky timeout flag of every dense-stage launch of this program (tests read it)
+            self.dense_err = self.alloc((4,), torch.int32)
+        sync = self._stats_floats(2 + 2 * len(layers))  # zeroed with the stats arena every step
+        a = nat.DenseStageArgs()
+        a.buf, a.sstats, a.sshift = buf.ptr, sbuf.ptr, sbuf.shift_ptr()
+        a.layers, a.sync, a.err = tab.data_ptr(), sync.data_ptr(), self.dense_err.data_ptr()
+        a.N, a.H, a.W, a.ld, a.nlayers, a.k2 = buf.N, H, W, buf.ld, len(layers), 1 if center else 3
+        a.act1 = a.act2 = act
+        a.inv_count = 1.0 / float(buf.N * H * W)
+        grid = int(os.environ.get("IDC_DS_GRID", "256"))
+        self.emit(nat.OP_DENSE_STAGE, a, ints=(grid, len(layers)), ptrs=(tab.data_ptr(),))
+
     def bn_bwd_apply(self, dz: Tensor4, x: Tensor4, bn: BNRef, dst: Tensor4, accumulate: bool):
         a = nat.BnBwdApplyArgs()
         a.dz, a.lddz = dz.ptr, dz.ld

@@ -61,6 +61,10 @@ def lower_densenet(b: Builder, net, U: int, input_dtype):
     b.pool(ys, buf.slice(0, 64), k=3, s=2, pt=1, pl=1, pro=bn_stem.args(), is_max=True,
            argmax=argmax, stats=sbuf, stats_off=0)
 
+    # Late stages (M <= IDC_DENSE_STAGE_MAXM pixels; default 2304: stages 3-4 at bs 256) run all
+    # their dense layers as ONE persistent work-queue launch (builder.dense_stage, dense_stage.hip)
+    # instead of 2 launch-latency-bound convs per layer
+    stage_maxm = int(os.environ.get("IDC_DENSE_STAGE_MAXM", "2304"))
     for si, nb in enumerate(nblocks):
         st = {"buf": buf, "stats": sbuf, "c0": c0, "ctot": ctot, "H": Hs, "W": Ws, "layers": []}
         M = B * Hs * Ws
@@ -71,12 +75,19 @@ def lower_densenet(b: Builder, net, U: int, input_dtype):
             cv1, bn2l, cv2 = L[name + "_1_conv"], L[name + "_1_bn"], L[name + "_2_conv"]
             t = b.nhwc(B, Hs, Ws, 128)
             stt = b.stats(128, M) if training else None
-            b.conv(buf.slice(0, cin), cv1, t, pro=bn1.args(), stats=stt)
             bn2 = BNRef(bn2l, b, stt, RELU)
-            b.conv(t, cv2, buf.slice(cin, 32), pads=(1, 1), pro=bn2.args(), stats=sbuf, stats_off=cin)
-            b.add_moving(bn1)
-            b.add_moving(bn2)
-            st["layers"].append({"cin": cin, "bn1": bn1, "cv1": cv1, "bn2": bn2, "cv2": cv2, "t": t})
+            st["layers"].append({"cin": cin, "bn1": bn1, "cv1": cv1, "bn2": bn2, "cv2": cv2, "t": t, "stt": stt})
+        if M <= stage_maxm and b.dense_stage_ok(sbuf, st["layers"], Hs, Ws):
+            b.dense_stage(buf, sbuf, st["layers"], RELU)
+        else:
+            for lay in st["layers"]:
+                cin, t = lay["cin"], lay["t"]
+                b.conv(buf.slice(0, cin), lay["cv1"], t, pro=lay["bn1"].args(), stats=lay["stt"])
+                b.conv(t, lay["cv2"], buf.slice(cin, 32), pads=(1, 1), pro=lay["bn2"].args(), stats=sbuf,
+                       stats_off=cin)
+        for lay in st["layers"]:
+            b.add_moving(lay["bn1"])
+            b.add_moving(lay["bn2"])
         if si < len(nblocks) - 1:
             bnt = BNRef(L[f"pool{si + 2}_bn"], b, sbuf, RELU)
             cvt = L[f"pool{si + 2}_conv"]

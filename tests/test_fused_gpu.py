@@ -311,3 +311,54 @@ def test_batched_weight_gradients_match_per_layer(monkeypatch, maxm):
 
     noise, dev = rel(g1, g0), rel(gb, g0)
     assert dev <= 3 * noise + 1e-3, (dev, noise)
+
+
+@pytest.mark.parametrize("B,maxm", [(8, "2304"), (256, "2304"), (256, "9216")])
+def test_dense_stage_matches_per_layer(monkeypatch, B, maxm):
+    """DenseNet-121 at the bench batch: the late stages' dense layers as ONE persistent work-queue
+    launch each (OP_DENSE_STAGE, csrc/kernels/dense_stage.hip; default for M <= 2304 pixels, here
+    also stage 2) against the per-layer convs on the same weights and input.  Forward stage buffers
+    and every statistics array must agree to the per-layer program's own run-to-run spread (float
+    atomics order), the timeout flag must stay clear, and the training step's gradients too."""
+    from idc_models_amd.engine import Model, RMSprop
+    from idc_models_amd.models import build_model
+    from idc_models_amd.ops import _native as nat
+    g = torch.Generator().manual_seed(5)
+    x = torch.randint(0, 256, (B, 50, 50, 3), generator=g, dtype=torch.uint8)
+    y = torch.randint(0, 2, (B,), generator=g)
+    outs = []
+    want = {8: 4, 256: 3 if maxm == "9216" else 2}[B]
+    for on in ("0", "0", "1"):
+        monkeypatch.setenv("IDC_DENSE_STAGE", on)
+        monkeypatch.setenv("IDC_DENSE_STAGE_MAXM", maxm)
+        net = build_model("densenet121", None, num_outputs=1, seed=4)
+        m = Model(net, device=DEV)
+        m.compile(RMSprop(1e-4), "binary_crossentropy", [], backend="fused")
+        p = m.impl._prog(B, True, torch.uint8)
+        nds = sum(1 for i in range(p.plan.size()) if p.plan.kind(i) == nat.OP_DENSE_STAGE)
+        assert nds == (0 if on == "0" else want), (on, maxm, nds)
+        m.impl._stage_inputs(p, x, y)
+        p.run_segment("fwd")
+        torch.cuda.synchronize()
+        st = p.b.debug["stages"]
+        bufs = [s["buf"].t.float().clone() for s in st]
+        stats = torch.cat([s.t.clone() for s in p.b.all_stats])
+        if on == "1":
+            print("dense_err", p.b.dense_err.tolist())
+            assert int(p.b.dense_err[0]) == 0
+        p.run_segment("bwd")
+        torch.cuda.synchronize()
+        outs.append((bufs, stats, m.arena.grad.clone(), float(p.io.loss.item())))
+
+    def rel(a, b):
+        return float((a - b).norm() / (b.norm() + 1e-12))
+
+    (b0, s0, g0, l0), (b1, s1, g1, l1), (bd, sd, gd, ld) = outs
+    print("stage buf noise/dev", [(round(rel(b1[i], b0[i]), 5), round(rel(bd[i], b0[i]), 5)) for i in range(len(b0))])
+    print("stats", rel(s1, s0), rel(sd, s0), "grads", rel(g1, g0), rel(gd, g0), "loss", l0, l1, ld)
+    for i in range(len(b0)):
+        noise, dev = rel(b1[i], b0[i]), rel(bd[i], b0[i])
+        assert dev <= 3 * noise + 2e-3, ("stage", i, dev, noise)
+    assert rel(sd, s0) <= 3 * rel(s1, s0) + 2e-3, (rel(sd, s0), rel(s1, s0))
+    assert rel(gd, g0) <= 3 * rel(g1, g0) + 2e-3, (rel(gd, g0), rel(g1, g0))
+    assert abs(ld - l0) <= 3 * abs(l1 - l0) + 1e-3, (ld, l0, l1)

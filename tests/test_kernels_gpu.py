@@ -866,3 +866,74 @@ def test_wgrad_batch_matches_single_launches(fn, kind, N, H):
     for o, s1, r in zip(outs, singles, refs):
         assert relerr(o, s1) < 1e-5
         assert relerr(o, r) < 1.5e-2
+
+
+@pytest.mark.parametrize("N,H,c0,L,grid", [(4, 3, 64, 3, 256), (6, 1, 96, 4, 7), (3, 5, 32, 2, 1)])
+def test_dense_stage_persistent_matches_reference(fn, N, H, c0, L, grid):
+    """The persistent dense-stage launch (work queue + per-phase completion counters) vs a PyTorch
+    fp32 reference of the same dense layers: BN1(shifted batch stats)->ReLU->1x1(128) stored bf16
+    with its shifted statistics, BN2->ReLU->3x3(32) (centre tap on 1x1 maps) into the stage buffer
+    slice with its statistics.  grid 7 / 1: far fewer workgroups than tiles (the queue must still
+    drain: every wait depends only on earlier tickets)."""
+    W = H
+    ld = c0 + 32 * L
+    g = torch.Generator(device="cpu").manual_seed(N * 100 + H)
+    buf = torch.zeros(N, H, W, ld)
+    buf[..., :c0] = torch.randn(N, H, W, c0, generator=g) * 1.5 + 0.3
+    buf = buf.to(torch.bfloat16).to(DEV)  # the stage buffer is bf16 (kernel operand)
+    K = torch.randn(ld, generator=g).to(DEV) * 0.2  # statistics shifts
+    x0 = buf[..., :c0].float().reshape(-1, c0)
+    sst = torch.zeros(2 * ld, device=DEV)
+    sst[:c0] = (x0 - K[:c0]).sum(0)
+    sst[ld:ld + c0] = ((x0 - K[:c0]) ** 2).sum(0)
+    k2 = 1 if H == 1 else 3
+    lays, refs = [], []
+    for i in range(L):
+        cin = c0 + 32 * i
+        w1 = bf(torch.randn(1, 1, cin, 128, generator=g) * (2.0 / cin) ** 0.5).to(DEV)
+        w2 = bf(torch.randn(3, 3, 128, 32, generator=g) * (2.0 / 1152) ** 0.5).to(DEV)
+        w2l = fn.weight_fwd_layout(w2[1:2, 1:2] if k2 == 1 else w2, 128)
+        d = dict(w1=fn.weight_fwd_layout(w1, cin), w2=w2l,
+                 g1=(torch.rand(cin, generator=g) + 0.5).to(DEV), b1=(torch.randn(cin, generator=g) * 0.1).to(DEV),
+                 g2=(torch.rand(128, generator=g) + 0.5).to(DEV), b2=(torch.randn(128, generator=g) * 0.1).to(DEV),
+                 t=torch.zeros(N, H, W, 128, dtype=torch.bfloat16, device=DEV),
+                 tstats=torch.zeros(256, device=DEV), tshift=(torch.randn(128, generator=g) * 0.1).to(DEV),
+                 eps1=1.001e-5, eps2=1.001e-5, cin=cin)
+        lays.append(d)
+        refs.append((w1, w2))
+    # reference, layer by layer (operands rounded to bf16 where the kernel rounds them)
+    rbuf = buf.float().clone()
+    rst = sst.clone()
+    rts, rtst = [], []
+    cnt = N * H * W
+    for i, d in enumerate(lays):
+        cin = d["cin"]
+        w1, w2 = refs[i]
+        mean = K[:cin] + rst[:cin] / cnt
+        var = (rst[ld:ld + cin] / cnt - (rst[:cin] / cnt) ** 2).clamp_min(0)
+        a1 = bf(torch.relu((rbuf[..., :cin] - mean) * torch.rsqrt(var + 1.001e-5) * d["g1"] + d["b1"]))
+        t = bf(ref_conv(a1, w1, 1, (0, 0, 0, 0)))
+        tk = (t - d["tshift"]).reshape(-1, 128)
+        tst = torch.cat([tk.sum(0), (tk * tk).sum(0)])
+        m2 = d["tshift"] + tst[:128] / cnt
+        v2 = (tst[128:] / cnt - (tst[:128] / cnt) ** 2).clamp_min(0)
+        a2 = bf(torch.relu((t - m2) * torch.rsqrt(v2 + 1.001e-5) * d["g2"] + d["b2"]))
+        y = bf(ref_conv(a2, w2, 1, (1, 1, 1, 1)))
+        rbuf[..., cin:cin + 32] = y
+        yk = (y - K[cin:cin + 32]).reshape(-1, 32)
+        rst[cin:cin + 32] = yk.sum(0)
+        rst[ld + cin:ld + cin + 32] = (yk * yk).sum(0)
+        rts.append(t)
+        rtst.append(tst)
+    sync, err = fn.dense_stage(buf, sst, lays, sshift=K, grid=grid, k2=k2)
+    M = N * H * W
+    nA, nB = -(-M // 32) * 4, -(-M // 16)
+    assert int(err[0].item()) == 0 and int(sync[-1].item()) == 0
+    assert sync[1:-1:2].tolist() == [nA] * L and sync[2:-1:2].tolist() == [nB] * L, sync.tolist()
+    errs = {}
+    for i, d in enumerate(lays):
+        errs[f"t{i}"] = relerr(d["t"].float(), rts[i])
+        errs[f"tstats{i}"] = relerr(d["tstats"], rtst[i])
+    errs["buf"] = relerr(buf.float(), rbuf)
+    errs["sst"] = relerr(sst, rst)
+    assert all(v < 2e-2 for v in errs.values()), errs

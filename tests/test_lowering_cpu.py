@@ -42,7 +42,7 @@ STRUCTS = {nat.OP_CONV: nat.ConvArgs, nat.OP_WGRAD: nat.WgradArgs, nat.OP_BN_BWD
            nat.OP_AVGPOOL: nat.PoolArgs, nat.OP_POOL_BWD: nat.PoolBwdArgs, nat.OP_HEAD_FWD: nat.HeadArgs,
            nat.OP_HEAD_BWD: nat.HeadBwdArgs, nat.OP_DW_FWD: nat.DwArgs, nat.OP_DW_BWD_DATA: nat.DwArgs,
            nat.OP_DW_WGRAD: nat.DwArgs, nat.OP_BN_APPLY: nat.BnArgs, nat.OP_MLP_FWD: nat.Mlp2Args,
-           nat.OP_MLP_BWD: nat.Mlp2Args}
+           nat.OP_MLP_BWD: nat.Mlp2Args, nat.OP_DENSE_STAGE: nat.DenseStageArgs}
 
 
 def _pointers(obj, out):
@@ -74,6 +74,15 @@ def test_plan_pointers_are_live(arch, ft):
             for j in range(n):
                 e = nat.WgBatchEntry.from_buffer_copy(raw_tab, j * C.sizeof(nat.WgBatchEntry))
                 _pointers(e.a, vals)
+        if kind == nat.OP_DENSE_STAGE:  # the per-layer descriptor table of a persistent stage
+            tab = next(t for t in b.keep if t.data_ptr() == ptrs[0])
+            n = ints[1]
+            raw_tab = bytes(tab.cpu().numpy().tobytes())
+            assert len(raw_tab) == n * C.sizeof(nat.DenseLayerDesc), (i, n)
+            for j in range(n):
+                e = nat.DenseLayerDesc.from_buffer_copy(raw_tab, j * C.sizeof(nat.DenseLayerDesc))
+                assert e.cin % 32 == 0 and e.cin <= 1024, (i, j, e.cin)
+                _pointers(e, vals)
         for name, v in vals:
             if not any(lo <= v < hi for lo, hi in ranges):
                 bad.append((i, kind, name))
@@ -128,3 +137,21 @@ def test_struct_layouts_match_native():
     sizes = nat.load().struct_sizes()
     for name, st in nat._STRUCTS.items():
         assert C.sizeof(st) == sizes[name], name
+
+
+def test_dense_stage_lowering(monkeypatch):
+    """Late DenseNet stages lower to one OP_DENSE_STAGE each (per-layer convs otherwise); the
+    deterministic mode and slotted statistics keep the per-layer convs."""
+    def count(env):
+        for k, v in env.items():
+            monkeypatch.setenv(k, v)
+        _, _, b = _lower("densenet121", None, True, B=256)
+        kinds = [k for (_, k, *_r) in b.ops]
+        return kinds.count(nat.OP_DENSE_STAGE), kinds.count(nat.OP_CONV)
+    n_on, conv_on = count({"IDC_DENSE_STAGE": "1"})
+    n_off, conv_off = count({"IDC_DENSE_STAGE": "0"})
+    assert (n_on, n_off) == (2, 0)
+    assert conv_off - conv_on == 2 * (24 + 16)  # stages 3 and 4: two convs per dense layer
+    assert count({"IDC_DENSE_STAGE": "1", "IDC_DETERMINISTIC": "1"})[0] == 0
+    monkeypatch.delenv("IDC_DETERMINISTIC")
+    assert count({"IDC_STAT_SLOTS": "1"})[0] == 2  # stage 3/4 rows (<= 4096) keep one copy

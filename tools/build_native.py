@@ -38,6 +38,7 @@ SOURCES = [
     "kernels/conv_wgrad.hip", "kernels/wgrad_big.hip",
     "kernels/nn_kernels.hip",
     "kernels/dwconv.hip",
+    "kernels/dense_stage.hip",
     "kernels/mlp_head.hip",
     "kernels/secagg.hip",
     "comm/communicator.cpp",
