@@ -313,7 +313,7 @@ def test_batched_weight_gradients_match_per_layer(monkeypatch, maxm):
     assert dev <= 3 * noise + 1e-3, (dev, noise)
 
 
-@pytest.mark.parametrize("B,maxm", [(8, "2304"), (256, "2304"), (256, "9216")])
+@pytest.mark.parametrize("B,maxm", [(8, "2304"), (256, "512"), (256, "2304"), (256, "9216")])
 def test_dense_stage_matches_per_layer(monkeypatch, B, maxm):
     """DenseNet-121 at the bench batch: the late stages' dense layers as ONE persistent work-queue
     launch each (OP_DENSE_STAGE, csrc/kernels/dense_stage.hip; default for M <= 2304 pixels, here
@@ -327,7 +327,7 @@ def test_dense_stage_matches_per_layer(monkeypatch, B, maxm):
     x = torch.randint(0, 256, (B, 50, 50, 3), generator=g, dtype=torch.uint8)
     y = torch.randint(0, 2, (B,), generator=g)
     outs = []
-    want = {8: 4, 256: 3 if maxm == "9216" else 2}[B]
+    want = {8: 4, 256: {"512": 1, "2304": 2, "9216": 3}[maxm]}[B]
     for on in ("0", "0", "1"):
         monkeypatch.setenv("IDC_DENSE_STAGE", on)
         monkeypatch.setenv("IDC_DENSE_STAGE_MAXM", maxm)

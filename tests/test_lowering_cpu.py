@@ -148,10 +148,12 @@ def test_dense_stage_lowering(monkeypatch):
         _, _, b = _lower("densenet121", None, True, B=256)
         kinds = [k for (_, k, *_r) in b.ops]
         return kinds.count(nat.OP_DENSE_STAGE), kinds.count(nat.OP_CONV)
-    n_on, conv_on = count({"IDC_DENSE_STAGE": "1"})
+    n_on, conv_on = count({"IDC_DENSE_STAGE": "1", "IDC_DENSE_STAGE_MAXM": "2304"})
     n_off, conv_off = count({"IDC_DENSE_STAGE": "0"})
     assert (n_on, n_off) == (2, 0)
     assert conv_off - conv_on == 2 * (24 + 16)  # stages 3 and 4: two convs per dense layer
+    monkeypatch.delenv("IDC_DENSE_STAGE_MAXM")
+    assert count({"IDC_DENSE_STAGE": "1"})[0] == 1  # default: stage 4 (M = 256) only
     assert count({"IDC_DENSE_STAGE": "1", "IDC_DETERMINISTIC": "1"})[0] == 0
     monkeypatch.delenv("IDC_DETERMINISTIC")
-    assert count({"IDC_STAT_SLOTS": "1"})[0] == 2  # stage 3/4 rows (<= 4096) keep one copy
+    assert count({"IDC_STAT_SLOTS": "1"})[0] == 1  # stage-4 rows (<= 4096) keep one copy
