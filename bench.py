@@ -151,6 +151,7 @@ def fed_bench(args):
             "dtype": "bf16", "data": "synthetic uint8 50x50x3 patches, random-init weights",
             "client_images_per_sec": round(imgs / spr, 1),
             "train_loss": round(float(metrics["loss"]), 5),
+            "train_metrics": {k: float(v) for k, v in metrics.items()},
             "config": {"model": arch, "clients": args.clients, "concurrent_clients": args.concurrent_clients,
                        "client_batching": bool(args.client_batching and proc._grouped is not None),
                        "client_size": args.client_size,

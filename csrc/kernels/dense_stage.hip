@@ -368,7 +368,11 @@ hipError_t dense_stage_fwd(const DenseStageArgs& a, int grid, hipStream_t st) {
       a.buf == nullptr || a.sstats == nullptr || a.layers == nullptr || a.sync == nullptr)
     return hipErrorInvalidValue;
   const int tasks = dense_stage_tasks(a);
-  if (grid <= 0) grid = 512;
+  if (grid <= 0) grid = 256;
+  // a grouped launch (K copies, each with its own queue) shares the CUs: one resident workgroup
+  // per CU (256 VGPRs), so K copies of a full-chip grid would run one copy after another
+  const int k = launch_groups().k;
+  if (k > 1) grid = grid / k > 8 ? grid / k : 8;
   if (grid > tasks) grid = tasks;
   hipLaunchKernelGGL(dense_stage_kernel, ggrid(grid), dim3(NT), 0, st, a, garg());
   return hipGetLastError();

@@ -361,4 +361,6 @@ def test_dense_stage_matches_per_layer(monkeypatch, B, maxm):
         assert dev <= 3 * noise + 2e-3, ("stage", i, dev, noise)
     assert rel(sd, s0) <= 3 * rel(s1, s0) + 2e-3, (rel(sd, s0), rel(s1, s0))
     assert rel(gd, g0) <= 3 * rel(g1, g0) + 2e-3, (rel(gd, g0), rel(g1, g0))
-    assert abs(ld - l0) <= 3 * abs(l1 - l0) + 1e-3, (ld, l0, l1)
+    # the loss: within the run-to-run spread or 1% (two identical per-layer runs can agree to 3e-4
+    # by chance while bf16 rounding flips move it by ~0.3%)
+    assert abs(ld - l0) <= max(3 * abs(l1 - l0), 0.01 * abs(l0)) + 1e-3, (ld, l0, l1)
