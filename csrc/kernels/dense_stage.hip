@@ -120,6 +120,9 @@ __device__ __forceinline__ v8bf bn_act8(const uint4& x, const float* sc, const f
   return __builtin_bit_cast(v8bf, pack8(f));
 }
 
+}  // namespace
+
+// (outside the anonymous namespace so profiles name it: idc::dense_stage_kernel)
 __global__ __launch_bounds__(NT) void dense_stage_kernel(DenseStageArgs a, GroupArg ga) {
   prefetch_kernargs<sizeof(DenseStageArgs) + sizeof(GroupArg)>();
   const long long go = goff(ga);
@@ -355,8 +358,6 @@ __global__ __launch_bounds__(NT) void dense_stage_kernel(DenseStageArgs a, Group
     }
   }
 }
-
-}  // namespace
 
 int dense_stage_tasks(const DenseStageArgs& a) {
   const long long M = (long long)a.N * a.H * a.W;
