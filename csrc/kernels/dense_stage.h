@@ -32,7 +32,12 @@ struct DenseStageArgs {
   int N, H, W, ld, nlayers, k2;
   int act1, act2;
   float inv_count;              // 1 / (N*H*W)
-  int pad_;
+  // cross-workgroup hand-off: 0 = agent-scope release/acquire fences around the completion
+  // counters (default); bit 0 = outputs stored with agent-coherent (sc1) stores and no release
+  // fence; bit 1 = operands/statistics produced in this launch read with agent-coherent loads and
+  // no acquire fence (3: both; measured within noise of 0 on DenseNet-121 stage 4, and 2,304-row
+  // stage 3 4.34-4.40 vs 4.48-4.53 ms/step fenced)
+  int coh;
 };
 
 // number of work items of one launch (the grid never needs more workgroups than this)

@@ -48,9 +48,21 @@ struct Smem {
   int bad;
 };
 
+// Agent-coherent loads of data other workgroups of this launch produced (sc1: never served from a
+// stale line of this XCD's L2), so a consumer needs no L2-invalidating acquire fence
+__device__ __forceinline__ uint4 ld_coh16(const void* p) {
+  unsigned long long* q = (unsigned long long*)p;
+  const unsigned long long lo = __hip_atomic_load(q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  const unsigned long long hi = __hip_atomic_load(q + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  return make_uint4((uint32_t)lo, (uint32_t)(lo >> 32), (uint32_t)hi, (uint32_t)(hi >> 32));
+}
+__device__ __forceinline__ float ld_coh(const float* p) {
+  return __hip_atomic_load((float*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
 // thread 0: wait until *cnt >= need (then acquire), or give up after MAX_POLLS / when another
 // workgroup already gave up.  Returns false on a timeout.
-__device__ bool wait_count(unsigned* cnt, unsigned need, unsigned* fail) {
+__device__ bool wait_count(unsigned* cnt, unsigned need, unsigned* fail, bool coherent_loads) {
   // the counter is read with an atomic RMW (add 0): performed at the same coherence point as the
   // producers' increments whatever XCD / L2 this workgroup runs on.  The bound is a poll count
   // (each poll is a memory round trip plus an s_sleep), not a clock reading.
@@ -63,16 +75,16 @@ __device__ bool wait_count(unsigned* cnt, unsigned need, unsigned* fail) {
       return false;
     }
   }
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+  if (!coherent_loads) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
   return true;
 }
 
 // every thread's stores / atomics of this tile performed, then one agent-scope release + count
-__device__ __forceinline__ void publish(unsigned* cnt) {
+__device__ __forceinline__ void publish(unsigned* cnt, bool coherent_stores) {
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   if (threadIdx.x == 0) {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    if (!coherent_stores) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __hip_atomic_fetch_add(cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
@@ -81,15 +93,16 @@ __device__ __forceinline__ void publish(unsigned* cnt) {
 // BN scale/shift for channels [0, C) (C <= 1024) from shifted [sum|sumsq] statistics (row length
 // ld), all loads of a thread issued before any arithmetic
 __device__ __forceinline__ void bn_table(const float* st, int ld, const float* shift, const float* g,
-                                         const float* b, float inv_n, float eps, int C, float* sc, float* sh) {
+                                         const float* b, float inv_n, float eps, int C, float* sc, float* sh,
+                                         bool coh) {
   const int tid = threadIdx.x;
   float s0[4], s1[4], k[4], gg[4], bb[4];
 #pragma unroll
   for (int u = 0; u < 4; ++u) {
     const int c = tid + u * NT;
     const int cc = c < C ? c : 0;
-    s0[u] = st[cc];
-    s1[u] = st[ld + cc];
+    s0[u] = coh ? ld_coh(st + cc) : st[cc];
+    s1[u] = coh ? ld_coh(st + ld + cc) : st[ld + cc];
     k[u] = shift ? shift[cc] : 0.f;
     gg[u] = g[cc];
     bb[u] = b[cc];
@@ -144,6 +157,7 @@ __global__ __launch_bounds__(NT) void dense_stage_kernel(DenseStageArgs a, Group
   const int taps = a.k2 * a.k2, pad = a.k2 >> 1;
   const float lo1 = act_lo(a.act1), hi1 = act_hi(a.act1);
   const float lo2 = act_lo(a.act2), hi2 = act_hi(a.act2);
+  const bool coh = (a.coh & 2) != 0;  // coherent loads, no acquire fence (dense_stage.h)
 
   for (;;) {
     // The ticket fetch is a thread-0 region enclosed by barriers on both sides.  Without the
@@ -190,7 +204,7 @@ __global__ __launch_bounds__(NT) void dense_stage_kernel(DenseStageArgs a, Group
 #pragma unroll
       for (int q = 0; q < 4; ++q) kq[q] = tsh ? tsh[n0 + ecol + q] : 0.f;
       if (l > 0) {
-        if (tid == 0) s.bad = !wait_count(&sync[2 * l], (unsigned)nB, fail);  // 3x3 phase of layer l-1
+        if (tid == 0) s.bad = !wait_count(&sync[2 * l], (unsigned)nB, fail, coh);  // 3x3 phase of layer l-1
         __syncthreads();
         if (__builtin_amdgcn_readfirstlane(s.bad)) return;
       }
@@ -201,11 +215,12 @@ __global__ __launch_bounds__(NT) void dense_stage_kernel(DenseStageArgs a, Group
 #pragma unroll
         for (int h = 0; h < 2; ++h) {
           const int m = m0 + h * 16 + fr;
-          ar[i][h] = (ks < nks && m < M) ? *reinterpret_cast<const uint4*>(buf + (size_t)m * a.ld + ks * 32 + fk)
+          const bf16_t* src = buf + (size_t)m * a.ld + ks * 32 + fk;
+          ar[i][h] = (ks < nks && m < M) ? (coh ? ld_coh16(src) : *reinterpret_cast<const uint4*>(src))
                                          : make_uint4(0, 0, 0, 0);
         }
       }
-      bn_table(sstats, a.ld, sshift, gsh(d.g1, go), gsh(d.b1, go), a.inv_count, d.eps1, cin, s.sc, s.sh);
+      bn_table(sstats, a.ld, sshift, gsh(d.g1, go), gsh(d.b1, go), a.inv_count, d.eps1, cin, s.sc, s.sh, coh);
       __syncthreads();
       v4f acc[2][2];
 #pragma unroll
@@ -243,7 +258,15 @@ __global__ __launch_bounds__(NT) void dense_stage_kernel(DenseStageArgs a, Group
         }
         const int m = m0 + erow;
         const uint32_t p0 = pack2bf(v[0], v[1]), p1 = pack2bf(v[2], v[3]);
-        if (m < M) *reinterpret_cast<uint2*>(tb + (size_t)m * 128 + n0 + ecol) = make_uint2(p0, p1);
+        if (m < M) {
+          uint32_t* o = reinterpret_cast<uint32_t*>(tb + (size_t)m * 128 + n0 + ecol);
+          if ((a.coh & 1)) {  // agent-coherent (sc1) stores: no release fence needed
+            __hip_atomic_store(reinterpret_cast<unsigned long long*>(o),
+                               ((unsigned long long)p1 << 32) | p0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          } else {
+            *reinterpret_cast<uint2*>(o) = make_uint2(p0, p1);
+          }
+        }
         const float rv[4] = {__uint_as_float(p0 << 16), __uint_as_float(p0 & 0xffff0000u),
                              __uint_as_float(p1 << 16), __uint_as_float(p1 & 0xffff0000u)};
 #pragma unroll
@@ -260,7 +283,7 @@ __global__ __launch_bounds__(NT) void dense_stage_kernel(DenseStageArgs a, Group
         }
         atomicAdd(&tst[which * 128 + n0 + c], sum);
       }
-      publish(&sync[1 + 2 * l]);
+      publish(&sync[1 + 2 * l], (a.coh & 1));
     } else {
       // ------------------------------------------------ 3x3 phase: buf[:, cin:cin+32] = conv3x3(relu(bn2(t)))
       const int m0 = (r - nA) * 16;
@@ -283,7 +306,7 @@ __global__ __launch_bounds__(NT) void dense_stage_kernel(DenseStageArgs a, Group
       const int mm = m < M ? m : M - 1;
       const int img = mm / HW, rem = mm - img * HW;
       const int ph = rem / a.W, pw = rem - ph * a.W;
-      if (tid == 0) s.bad = !wait_count(&sync[1 + 2 * l], (unsigned)nA, fail);  // 1x1 phase of layer l
+      if (tid == 0) s.bad = !wait_count(&sync[1 + 2 * l], (unsigned)nA, fail, coh);  // 1x1 phase of layer l
       __syncthreads();
       if (__builtin_amdgcn_readfirstlane(s.bad)) return;
       uint4 ar[KB];
@@ -295,15 +318,15 @@ __global__ __launch_bounds__(NT) void dense_stage_kernel(DenseStageArgs a, Group
         const int kr = tap / a.k2, kc = tap - kr * a.k2;
         const int hh = ph + kr - pad, ww = pw + kc - pad;
         okr[i] = ks < nks && m < M && hh >= 0 && hh < a.H && ww >= 0 && ww < a.W;
-        ar[i] = okr[i] ? *reinterpret_cast<const uint4*>(tb + ((size_t)(img * a.H + hh) * a.W + ww) * 128 +
-                                                          (ks & 3) * 32 + fk)
-                       : make_uint4(0, 0, 0, 0);
+        const bf16_t* src = tb + ((size_t)(img * a.H + hh) * a.W + ww) * 128 + (ks & 3) * 32 + fk;
+        ar[i] = okr[i] ? (coh ? ld_coh16(src) : *reinterpret_cast<const uint4*>(src)) : make_uint4(0, 0, 0, 0);
       }
       if (tid < 128) {
         // 128 channels: one per thread (the 4-way table builder's other slots stay idle)
         const int c = tid;
         float mean, var;
-        shifted_mean_var(tsh ? tsh[c] : 0.f, tst[c], tst[128 + c], a.inv_count, mean, var);
+        shifted_mean_var(tsh ? tsh[c] : 0.f, coh ? ld_coh(tst + c) : tst[c], coh ? ld_coh(tst + 128 + c) : tst[128 + c],
+                         a.inv_count, mean, var);
         const float rr = gsh(d.g2, go)[c] * rsqrtf(var + d.eps2);
         s.sc[c] = rr;
         s.sh[c] = gsh(d.b2, go)[c] - mean * rr;
@@ -338,7 +361,11 @@ __global__ __launch_bounds__(NT) void dense_stage_kernel(DenseStageArgs a, Group
         }
         const int mo = m0 + erow;
         const uint32_t p = pack2bf(v[0], v[1]);
-        if (mo < M) *reinterpret_cast<uint32_t*>(buf + (size_t)mo * a.ld + cin + ecol) = p;
+        if (mo < M) {
+          uint32_t* o = reinterpret_cast<uint32_t*>(buf + (size_t)mo * a.ld + cin + ecol);
+          if ((a.coh & 1)) __hip_atomic_store(o, p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          else *o = p;
+        }
         const float rv[2] = {__uint_as_float(p << 16), __uint_as_float(p & 0xffff0000u)};
 #pragma unroll
         for (int q = 0; q < 2; ++q) s.red[0][erow * RLD + ecol + q] = mo < M ? rv[q] - kq[q] : 0.f;
@@ -354,7 +381,7 @@ __global__ __launch_bounds__(NT) void dense_stage_kernel(DenseStageArgs a, Group
         }
         atomicAdd(&sstats[which * a.ld + cin + c], sum);
       }
-      publish(&sync[2 + 2 * l]);
+      publish(&sync[2 + 2 * l], (a.coh & 1));
     }
   }
 }

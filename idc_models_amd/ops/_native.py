@@ -142,7 +142,7 @@ class DenseLayerDesc(C.Structure):
 class DenseStageArgs(C.Structure):
     _fields_ = [("buf", vp), ("sstats", vp), ("sshift", vp), ("layers", vp), ("sync", vp), ("err", vp),
                 ("N", ci), ("H", ci), ("W", ci), ("ld", ci), ("nlayers", ci), ("k2", ci),
-                ("act1", ci), ("act2", ci), ("inv_count", cf), ("pad_", ci)]
+                ("act1", ci), ("act2", ci), ("inv_count", cf), ("coh", ci)]
 
 
 _STRUCTS = {"BnArgs": BnArgs, "BwdAff": BwdAff, "ConvArgs": ConvArgs, "WgradArgs": WgradArgs,

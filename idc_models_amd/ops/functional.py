@@ -428,7 +428,7 @@ def bn_moments(stats: torch.Tensor, count: int, shift: Optional[torch.Tensor] = 
 
 
 def dense_stage(buf: torch.Tensor, sstats: torch.Tensor, layers, sshift: Optional[torch.Tensor] = None,
-                act: int = RELU, grid: int = 256, k2: int = 3):
+                act: int = RELU, grid: int = 256, k2: int = 3, coherent: int = 0):
     """All dense layers of a DenseNet stage in one persistent launch (csrc/kernels/dense_stage.hip).
 
     ``buf``: NHWC bf16 stage buffer [N, H, W, ld] whose channels [0, c0) are filled and whose
@@ -454,6 +454,7 @@ def dense_stage(buf: torch.Tensor, sstats: torch.Tensor, layers, sshift: Optiona
     a.N, a.H, a.W, a.ld, a.nlayers, a.k2 = N, H, W, ld, len(layers), k2
     a.act1 = a.act2 = act
     a.inv_count = 1.0 / float(N * H * W)
+    a.coh = coherent
     _plan1(nat.OP_DENSE_STAGE, a, ints=(grid, len(layers)), ptrs=(tab.data_ptr(),))
     torch.cuda.current_stream().synchronize()
     return sync, err

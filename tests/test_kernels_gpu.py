@@ -868,13 +868,15 @@ def test_wgrad_batch_matches_single_launches(fn, kind, N, H):
         assert relerr(o, r) < 1.5e-2
 
 
-@pytest.mark.parametrize("N,H,c0,L,grid", [(4, 3, 64, 3, 256), (6, 1, 96, 4, 7), (3, 5, 32, 2, 1)])
-def test_dense_stage_persistent_matches_reference(fn, N, H, c0, L, grid):
+@pytest.mark.parametrize("N,H,c0,L,grid,coh", [(4, 3, 64, 3, 256, 0), (6, 1, 96, 4, 7, 0), (3, 5, 32, 2, 1, 0),
+                                              (4, 3, 64, 3, 256, 3), (8, 6, 64, 3, 64, 3)])
+def test_dense_stage_persistent_matches_reference(fn, N, H, c0, L, grid, coh):
     """The persistent dense-stage launch (work queue + per-phase completion counters) vs a PyTorch
     fp32 reference of the same dense layers: BN1(shifted batch stats)->ReLU->1x1(128) stored bf16
     with its shifted statistics, BN2->ReLU->3x3(32) (centre tap on 1x1 maps) into the stage buffer
     slice with its statistics.  grid 7 / 1: far fewer workgroups than tiles (the queue must still
-    drain: every wait depends only on earlier tickets)."""
+    drain: every wait depends only on earlier tickets).  coh 3: the fence-free hand-off (agent-
+    coherent stores and loads)."""
     W = H
     ld = c0 + 32 * L
     g = torch.Generator(device="cpu").manual_seed(N * 100 + H)
@@ -925,7 +927,7 @@ def test_dense_stage_persistent_matches_reference(fn, N, H, c0, L, grid):
         rst[ld + cin:ld + cin + 32] = (yk * yk).sum(0)
         rts.append(t)
         rtst.append(tst)
-    sync, err = fn.dense_stage(buf, sst, lays, sshift=K, grid=grid, k2=k2)
+    sync, err = fn.dense_stage(buf, sst, lays, sshift=K, grid=grid, k2=k2, coherent=coh)
     M = N * H * W
     nA, nB = -(-M // 32) * 4, -(-M // 16)
     assert int(err[0].item()) == 0 and int(sync[-1].item()) == 0
