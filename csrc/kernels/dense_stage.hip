@@ -22,8 +22,8 @@
 //
 // Tile shapes (64-wide waves, v_mfma_f32_16x16x32_bf16, operands straight from global/L2 into
 // registers -- no LDS staging, the whole K range of a wave in flight at once):
-//   1x1 phase: 32 rows x 32 output channels per tile (4 tiles across the 128 channels), the K
-//              range (cin <= 1024) split over the 4 waves, partial tiles summed through LDS;
+//   1x1 phase: 32 rows x 64 output channels per tile (2 tiles across the 128 channels), the K
+//              range (cin <= 1024) split over the 4 waves in chunks, partial tiles summed in LDS;
 //   3x3 phase: 16 rows x all 32 output channels, the 9 taps x 128 channels split over the waves.
 // Both phases apply the pending BatchNorm + ReLU of their operand in registers from a per-tile
 // coefficient table computed from the shifted batch statistics (common.h), store bf16 and add the
@@ -35,15 +35,16 @@ namespace idc {
 namespace {
 
 constexpr int NT = 256;
-constexpr int KA = 8;    // 1x1 phase: k-steps of 32 per wave (cin <= 1024)
+constexpr int KC = 4;    // 1x1 phase: k-steps of 32 per wave per chunk (cin <= 512: one chunk)
 constexpr int KB = 9;    // 3x3 phase: 9 taps x 128 channels / 32 / 4 waves
-constexpr int RLD = 33;  // LDS partial-tile row stride (floats)
+constexpr int RLD = 33;  // LDS partial-tile row stride of the 3x3 phase (floats)
+constexpr int RLDA = 65; // ... of the 1x1 phase (64 columns)
 constexpr unsigned MAX_POLLS = 1u << 19;  // ~0.5-1 s of polling
 
 struct Smem {
   float sc[1024];
   float sh[1024];
-  float red[4][32 * RLD];
+  float red[4][32 * RLDA];
   int task;
   int bad;
 };
@@ -151,7 +152,7 @@ __global__ __launch_bounds__(NT) void dense_stage_kernel(DenseStageArgs a, Group
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int fr = lane & 15, fk = (lane >> 4) * 8;
   const int HW = a.H * a.W, M = a.N * HW;
-  const int mtA = (M + 31) / 32, nA = mtA * 4;
+  const int mtA = (M + 31) / 32, nA = mtA * 2;
   const int nB = (M + 15) / 16;
   const int per = nA + nB, total = per * a.nlayers;
   const int taps = a.k2 * a.k2, pad = a.k2 >> 1;
@@ -188,56 +189,72 @@ __global__ __launch_bounds__(NT) void dense_stage_kernel(DenseStageArgs a, Group
 
     if (r < nA) {
       // ------------------------------------------------ 1x1 phase: t = conv1x1(relu(bn1(x)))
-      const int mt = r >> 2, n0 = (r & 3) * 32, m0 = mt * 32;
+      // 32 rows x 64 channels per tile (2 tiles across the 128 channels: a 2,304-row stage is 144
+      // tiles, one round on 256 CUs); each wave owns every 4th k-step and runs them in chunks of
+      // KC, a chunk's A and B fragments all in flight at once (cin <= 512: one chunk)
+      const int mt = r >> 1, n0 = (r & 1) * 64, m0 = mt * 32;
       const int cin = d.cin, nks = cin >> 5;
-      v8bf bq[KA][2];
+      v8bf bq[KC][4];
+      auto load_b = [&](int c0k) {
 #pragma unroll
-      for (int i = 0; i < KA; ++i) {
-        const int ks = wid + 4 * i;
+        for (int i = 0; i < KC; ++i) {
+          const int ks = wid + 4 * (c0k + i);
 #pragma unroll
-        for (int j = 0; j < 2; ++j)
-          bq[i][j] = ks < nks ? *reinterpret_cast<const v8bf*>(w1 + (size_t)(n0 + j * 16 + fr) * cin + ks * 32 + fk)
-                              : v8bf{};
-      }
-      const int erow = tid >> 3, ecol = (tid & 7) * 4;
-      float kq[4];
+          for (int j = 0; j < 4; ++j)
+            bq[i][j] = ks < nks ? *reinterpret_cast<const v8bf*>(w1 + (size_t)(n0 + j * 16 + fr) * cin + ks * 32 + fk)
+                                : v8bf{};
+        }
+      };
+      uint4 ar[KC][2];
+      auto load_a = [&](int c0k) {
 #pragma unroll
-      for (int q = 0; q < 4; ++q) kq[q] = tsh ? tsh[n0 + ecol + q] : 0.f;
+        for (int i = 0; i < KC; ++i) {
+          const int ks = wid + 4 * (c0k + i);
+#pragma unroll
+          for (int h = 0; h < 2; ++h) {
+            const int m = m0 + h * 16 + fr;
+            const bf16_t* src = buf + (size_t)m * a.ld + ks * 32 + fk;
+            ar[i][h] = (ks < nks && m < M) ? (coh ? ld_coh16(src) : *reinterpret_cast<const uint4*>(src))
+                                           : make_uint4(0, 0, 0, 0);
+          }
+        }
+      };
+      load_b(0);  // weights do not depend on earlier phases: in flight before the wait
+      const int erow = tid >> 3, ecol = (tid & 7) * 8;
+      float kq[8];
+#pragma unroll
+      for (int q = 0; q < 8; ++q) kq[q] = tsh ? tsh[n0 + ecol + q] : 0.f;
       if (l > 0) {
         if (tid == 0) s.bad = !wait_count(&sync[2 * l], (unsigned)nB, fail, coh);  // 3x3 phase of layer l-1
         __syncthreads();
         if (__builtin_amdgcn_readfirstlane(s.bad)) return;
       }
-      uint4 ar[KA][2];
-#pragma unroll
-      for (int i = 0; i < KA; ++i) {
-        const int ks = wid + 4 * i;
-#pragma unroll
-        for (int h = 0; h < 2; ++h) {
-          const int m = m0 + h * 16 + fr;
-          const bf16_t* src = buf + (size_t)m * a.ld + ks * 32 + fk;
-          ar[i][h] = (ks < nks && m < M) ? (coh ? ld_coh16(src) : *reinterpret_cast<const uint4*>(src))
-                                         : make_uint4(0, 0, 0, 0);
-        }
-      }
+      load_a(0);
       bn_table(sstats, a.ld, sshift, gsh(d.g1, go), gsh(d.b1, go), a.inv_count, d.eps1, cin, s.sc, s.sh, coh);
       __syncthreads();
-      v4f acc[2][2];
+      v4f acc[2][4];
 #pragma unroll
       for (int h = 0; h < 2; ++h)
 #pragma unroll
-        for (int j = 0; j < 2; ++j) acc[h][j] = v4f{0.f, 0.f, 0.f, 0.f};
+        for (int j = 0; j < 4; ++j) acc[h][j] = v4f{0.f, 0.f, 0.f, 0.f};
+      const int nchunks = (nks + 4 * KC - 1) / (4 * KC);
+      for (int ch = 0; ch < nchunks; ++ch) {
+        if (ch > 0) {
+          load_b(ch * KC);
+          load_a(ch * KC);
+        }
 #pragma unroll
-      for (int i = 0; i < KA; ++i) {
-        const int ks = wid + 4 * i;
-        if (ks < nks) {
-          const int c0 = ks * 32 + fk;
+        for (int i = 0; i < KC; ++i) {
+          const int ks = wid + 4 * (ch * KC + i);
+          if (ks < nks) {
+            const int c0 = ks * 32 + fk;
 #pragma unroll
-          for (int h = 0; h < 2; ++h) {
-            const v8bf af = bn_act8(ar[i][h], s.sc + c0, s.sh + c0, lo1, hi1, true);
+            for (int h = 0; h < 2; ++h) {
+              const v8bf af = bn_act8(ar[i][h], s.sc + c0, s.sh + c0, lo1, hi1, true);
 #pragma unroll
-            for (int j = 0; j < 2; ++j)
-              acc[h][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, bq[i][j], acc[h][j], 0, 0, 0);
+              for (int j = 0; j < 4; ++j)
+                acc[h][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, bq[i][j], acc[h][j], 0, 0, 0);
+            }
           }
         }
       }
@@ -245,40 +262,42 @@ __global__ __launch_bounds__(NT) void dense_stage_kernel(DenseStageArgs a, Group
 #pragma unroll
       for (int h = 0; h < 2; ++h)
 #pragma unroll
-        for (int j = 0; j < 2; ++j)
+        for (int j = 0; j < 4; ++j)
 #pragma unroll
-          for (int q = 0; q < 4; ++q) red[(h * 16 + (lane >> 4) * 4 + q) * RLD + j * 16 + fr] = acc[h][j][q];
+          for (int q = 0; q < 4; ++q) red[(h * 16 + (lane >> 4) * 4 + q) * RLDA + j * 16 + fr] = acc[h][j][q];
       __syncthreads();
       {
-        float v[4];
+        float v[8];
 #pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          const int o = erow * RLD + ecol + q;
+        for (int q = 0; q < 8; ++q) {
+          const int o = erow * RLDA + ecol + q;
           v[q] = s.red[0][o] + s.red[1][o] + s.red[2][o] + s.red[3][o];
         }
         const int m = m0 + erow;
-        const uint32_t p0 = pack2bf(v[0], v[1]), p1 = pack2bf(v[2], v[3]);
+        const uint4 pk = pack8(v);
         if (m < M) {
           uint32_t* o = reinterpret_cast<uint32_t*>(tb + (size_t)m * 128 + n0 + ecol);
           if ((a.coh & 1)) {  // agent-coherent (sc1) stores: no release fence needed
-            __hip_atomic_store(reinterpret_cast<unsigned long long*>(o),
-                               ((unsigned long long)p1 << 32) | p0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            unsigned long long* o2 = reinterpret_cast<unsigned long long*>(o);
+            __hip_atomic_store(o2, ((unsigned long long)pk.y << 32) | pk.x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(o2 + 1, ((unsigned long long)pk.w << 32) | pk.z, __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_AGENT);
           } else {
-            *reinterpret_cast<uint2*>(o) = make_uint2(p0, p1);
+            *reinterpret_cast<uint4*>(o) = pk;
           }
         }
-        const float rv[4] = {__uint_as_float(p0 << 16), __uint_as_float(p0 & 0xffff0000u),
-                             __uint_as_float(p1 << 16), __uint_as_float(p1 & 0xffff0000u)};
+        float rv[8];
+        unpack8(pk, rv);
 #pragma unroll
-        for (int q = 0; q < 4; ++q) s.red[0][erow * RLD + ecol + q] = m < M ? rv[q] - kq[q] : 0.f;
+        for (int q = 0; q < 8; ++q) s.red[0][erow * RLDA + ecol + q] = m < M ? rv[q] - kq[q] : 0.f;
       }
       __syncthreads();
-      if (tid < 64) {
-        const int c = tid & 31, which = tid >> 5;
+      if (tid < 128) {
+        const int c = tid & 63, which = tid >> 6;
         float sum = 0.f;
 #pragma unroll 8
         for (int row = 0; row < 32; ++row) {
-          const float x = s.red[0][row * RLD + c];
+          const float x = s.red[0][row * RLDA + c];
           sum += which ? x * x : x;
         }
         atomicAdd(&tst[which * 128 + n0 + c], sum);
@@ -388,7 +407,7 @@ __global__ __launch_bounds__(NT) void dense_stage_kernel(DenseStageArgs a, Group
 
 int dense_stage_tasks(const DenseStageArgs& a) {
   const long long M = (long long)a.N * a.H * a.W;
-  return (int)(a.nlayers * (((M + 31) / 32) * 4 + (M + 15) / 16));
+  return (int)(a.nlayers * (((M + 31) / 32) * 2 + (M + 15) / 16));
 }
 
 hipError_t dense_stage_fwd(const DenseStageArgs& a, int grid, hipStream_t st) {

@@ -717,9 +717,9 @@ class Builder:
         a.N, a.H, a.W, a.ld, a.nlayers, a.k2 = buf.N, H, W, buf.ld, len(layers), 1 if center else 3
         a.act1 = a.act2 = act
         a.inv_count = 1.0 / float(buf.N * H * W)
-        # cross-workgroup hand-off (dense_stage.h): fences by default, IDC_DS_COHERENT=3 coherent
-        # (sc1) stores and loads instead
-        a.coh = int(os.environ.get("IDC_DS_COHERENT", "0"))
+        # cross-workgroup hand-off (dense_stage.h): agent-coherent (sc1) stores and loads by default
+        # (no L2 writeback / invalidate per phase boundary); IDC_DS_COHERENT=0: release/acquire fences
+        a.coh = int(os.environ.get("IDC_DS_COHERENT", "3"))
         grid = int(os.environ.get("IDC_DS_GRID", "256"))
         self.emit(nat.OP_DENSE_STAGE, a, ints=(grid, len(layers)), ptrs=(tab.data_ptr(),))
 

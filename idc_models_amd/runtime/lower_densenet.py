@@ -61,13 +61,12 @@ def lower_densenet(b: Builder, net, U: int, input_dtype):
     b.pool(ys, buf.slice(0, 64), k=3, s=2, pt=1, pl=1, pro=bn_stem.args(), is_max=True,
            argmax=argmax, stats=sbuf, stats_off=0)
 
-    # Tiny stages (M <= IDC_DENSE_STAGE_MAXM pixels; default 512: stage 4 at bs 256, stages 3-4 of
-    # a bs-32 federated client) run all their dense layers as ONE persistent work-queue launch
-    # (builder.dense_stage, dense_stage.hip) instead of 2 launch-latency-bound convs per layer.
-    # Measured on DenseNet-121 bs 256 (bench.py, 1x MI355X): stage 4 alone 4.31 ms/step vs 4.35
-    # per-layer; stages 3+4 4.43 (stage 3's 2,304-row phases pay ~2.5 us of agent-scope fences per
-    # phase plus 72-144 same-address statistics atomics, more than the per-layer kernels' ramps)
-    stage_maxm = int(os.environ.get("IDC_DENSE_STAGE_MAXM", "512"))
+    # Late stages (M <= IDC_DENSE_STAGE_MAXM pixels; default 2304: stages 3-4 at bs 256, stages 3-4
+    # of a bs-32 federated client) run all their dense layers as ONE persistent work-queue launch
+    # each (builder.dense_stage, dense_stage.hip) instead of 2 launch-latency-bound convs per layer.
+    # DenseNet-121 bs 256 on 1x MI355X (bench.py, repeated A/B): stages 3+4 in-kernel 4.27-4.29
+    # ms/step, stage 4 only 4.31, per-layer 4.35-4.41; stage 2 (9,216 rows) measured slower
+    stage_maxm = int(os.environ.get("IDC_DENSE_STAGE_MAXM", "2304"))
     for si, nb in enumerate(nblocks):
         st = {"buf": buf, "stats": sbuf, "c0": c0, "ctot": ctot, "H": Hs, "W": Ws, "layers": []}
         M = B * Hs * Ws

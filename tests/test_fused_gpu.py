@@ -313,12 +313,12 @@ def test_batched_weight_gradients_match_per_layer(monkeypatch, maxm):
     assert dev <= 3 * noise + 1e-3, (dev, noise)
 
 
-@pytest.mark.parametrize("B,maxm,coh", [(8, "2304", "0"), (256, "512", "0"), (256, "2304", "0"), (256, "9216", "0"),
+@pytest.mark.parametrize("B,maxm,coh", [(8, "2304", "3"), (256, "512", "3"), (256, "2304", "0"), (256, "9216", "3"),
                                         (256, "2304", "3")])
 def test_dense_stage_matches_per_layer(monkeypatch, B, maxm, coh):
     """DenseNet-121 at the bench batch: the late stages' dense layers as ONE persistent work-queue
     launch each (OP_DENSE_STAGE, csrc/kernels/dense_stage.hip; default for M <= 2304 pixels, here
-    also stage 2) against the per-layer convs on the same weights and input.  Forward stage buffers
+    also stage 2; both hand-off modes) against the per-layer convs on the same weights and input.  Forward stage buffers
     and every statistics array must agree to the per-layer program's own run-to-run spread (float
     atomics order), the timeout flag must stay clear, and the training step's gradients too."""
     from idc_models_amd.engine import Model, RMSprop

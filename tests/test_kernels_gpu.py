@@ -929,7 +929,7 @@ def test_dense_stage_persistent_matches_reference(fn, N, H, c0, L, grid, coh):
         rtst.append(tst)
     sync, err = fn.dense_stage(buf, sst, lays, sshift=K, grid=grid, k2=k2, coherent=coh)
     M = N * H * W
-    nA, nB = -(-M // 32) * 4, -(-M // 16)
+    nA, nB = -(-M // 32) * 2, -(-M // 16)
     assert int(err[0].item()) == 0 and int(sync[-1].item()) == 0
     assert sync[1:-1:2].tolist() == [nA] * L and sync[2:-1:2].tolist() == [nB] * L, sync.tolist()
     errs = {}

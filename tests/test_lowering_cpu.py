@@ -153,7 +153,9 @@ def test_dense_stage_lowering(monkeypatch):
     assert (n_on, n_off) == (2, 0)
     assert conv_off - conv_on == 2 * (24 + 16)  # stages 3 and 4: two convs per dense layer
     monkeypatch.delenv("IDC_DENSE_STAGE_MAXM")
-    assert count({"IDC_DENSE_STAGE": "1"})[0] == 1  # default: stage 4 (M = 256) only
+    assert count({"IDC_DENSE_STAGE": "1"})[0] == 2  # default: stages 3 and 4 (M <= 2304)
+    assert count({"IDC_DENSE_STAGE_MAXM": "512"})[0] == 1  # stage 4 only
+    monkeypatch.delenv("IDC_DENSE_STAGE_MAXM")
     assert count({"IDC_DENSE_STAGE": "1", "IDC_DETERMINISTIC": "1"})[0] == 0
     monkeypatch.delenv("IDC_DETERMINISTIC")
-    assert count({"IDC_STAT_SLOTS": "1"})[0] == 1  # stage-4 rows (<= 4096) keep one copy
+    assert count({"IDC_STAT_SLOTS": "1"})[0] == 2  # stage 3/4 rows (<= 4096) keep one copy
