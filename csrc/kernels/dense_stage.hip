@@ -14,14 +14,18 @@
 // handed out in queue order, so every tile a waiting workgroup depends on was taken earlier by a
 // workgroup that is already running (or done): the queue cannot deadlock whatever number of
 // workgroups is resident (no co-residency assumption, no cooperative launch), and each wait has a
-// bounded poll count besides (a per-launch fail flag: every workgroup then leaves, and the launch is counted in a
-// persistent error counter) so a bug can never hang the
-// GPU.  Weight fragments do not depend on earlier phases and are loaded BEFORE the wait, so a
-// workgroup that took a ticket of the next phase early has its B operand in registers when the
-// dependency clears.
+// bounded poll count besides (a per-launch fail flag: every workgroup then leaves, and the launch
+// is counted in a persistent error counter), so a bug can never hang the GPU.  Weight fragments do
+// not depend on earlier phases and are loaded BEFORE the wait, so a workgroup that took a ticket of
+// the next phase early has its B operand in registers when the dependency clears.
+//
+// Hand-off between phases (DenseStageArgs::coh): by default the outputs are stored and the
+// operands / statistics produced in this launch are loaded with agent-coherent (sc1) accesses, so
+// no phase boundary pays an L2 writeback (release) or invalidate (acquire); with coh = 0 the
+// counters are guarded by agent-scope release/acquire fences instead (~2.5 us per boundary).
 //
 // Tile shapes (64-wide waves, v_mfma_f32_16x16x32_bf16, operands straight from global/L2 into
-// registers -- no LDS staging, the whole K range of a wave in flight at once):
+// registers -- no LDS staging, a wave's K range in flight at once, in chunks for cin > 512):
 //   1x1 phase: 32 rows x 64 output channels per tile (2 tiles across the 128 channels), the K
 //              range (cin <= 1024) split over the 4 waves in chunks, partial tiles summed in LDS;
 //   3x3 phase: 16 rows x all 32 output channels, the 9 taps x 128 channels split over the waves.
