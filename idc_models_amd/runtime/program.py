@@ -121,10 +121,10 @@ class FusedProgram:
         self.plan = nat.load().Plan()
         # side-lane ops are issued in batches every IDC_SIDE_FLUSH main ops (plan.cpp: issue).
         # Batching saves host calls where the backward is many short kernels (DenseNet: 128 main
-        # ops; 3-4 measured best, 4.27-4.34 ms/step vs 4.30-4.43 at 6-8 and 4.42 at 2; MobileNetV2
-        # neutral); a backward of few long kernels (VGG16: 19 main ops of
-        # 45-220 us) forks every side op at once (0), or its weight gradients would wait for the
-        # next dgrads to finish before starting
+        # ops; 3-4 measured best, 4.27-4.34 ms/step vs 4.30-4.43 at 6-8 and 4.42 at 2; MobileNetV2,
+        # 89 main ops: 2.47 ms/step at 4 vs 2.56 at 0, 3 A/B pairs in round 3); a backward of few
+        # long kernels (VGG16: 20 main ops of 45-220 us) forks every side op at once (0), or its
+        # weight gradients would wait for the next dgrads to finish before starting
         n_bwd_main = sum(1 for op in b.ops if op[0] == "bwd" and op[7] == 0)
         self.plan.set_side_flush(int(os.environ.get("IDC_SIDE_FLUSH", "4" if n_bwd_main >= 64 else "0")))
         self.seg: Dict[str, Tuple[int, int]] = {}
