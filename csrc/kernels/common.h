@@ -201,9 +201,25 @@ __device__ __forceinline__ long long goff(const GroupArg& ga) {
   return ga.stride ? (long long)(blockIdx.z / (unsigned)ga.zn) * ga.stride : 0;
 }
 __device__ __forceinline__ int gz(const GroupArg& ga) { return (int)(blockIdx.z % (unsigned)ga.zn); }
+// Every pointer a kernel dereferences is device global memory (hipMalloc / torch allocations),
+// but pointers read from argument structs and device tables are generic ("flat") to the
+// compiler, and an integer round trip hides their provenance for good: hipcc then emits FLAT
+// loads/stores, which count in both vmcnt and lgkmcnt, so every LDS wait (lgkmcnt) of a K loop
+// also waited for the global prefetch in flight, and flat accesses are invalid for the sc1
+// hand-off protocol (MI355X_MICROARCH.md "Valid forms").  gsh therefore routes every pointer
+// through the global address space (addrspace(1)); LLVM's address-space inference then turns
+// every access derived from it into global_* / buffer-free vector memory instructions.
+template <typename T>
+using gptr_t = __attribute__((address_space(1))) T*;
+template <typename T>
+__device__ __forceinline__ T* as_global(T* p) {
+  return (T*)(gptr_t<T>)p;
+}
 template <typename T>
 __device__ __forceinline__ T* gsh(T* p, long long off) {
-  return p ? (T*)((uintptr_t)p + off) : p;
+  typedef __attribute__((address_space(1))) char gchar;
+  gchar* q = (gchar*)(gptr_t<T>)p;
+  return (T*)(gptr_t<T>)(q ? q + off : q);  // null pointers stay null (they select modes)
 }
 
 // BatchNorm descriptor shared by every kernel that applies a BN affine (+activation) to an

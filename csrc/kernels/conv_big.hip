@@ -71,7 +71,8 @@ __global__ __launch_bounds__(WM * WN * 64) void conv_big_kernel(ConvArgs a, Grou
   extern __shared__ __attribute__((aligned(16))) char smem[];
   bf16_t* lds = reinterpret_cast<bf16_t*>(smem);
 
-  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform: scalar branches on it
   const int wr = wid / C::WN, wc = wid % C::WN;
   const int M = a.N * a.Ho * a.Wo;
   const int K = a.KH * a.KW * a.Cin;

@@ -67,33 +67,23 @@ struct ConvArgs {
   const float* stats_shift;
 };
 
-// tile TILE_HALO selects the one-image-per-workgroup direct 3x3 kernel (conv3x3_halo.hip)
 __device__ __forceinline__ void gshift(ConvArgs& a, long long o) {
-  if (!o) return;
+  // (no early return at o == 0: gsh also moves every pointer into the global address space)
   a.x = gsh(a.x, o); a.y = gsh(a.y, o); a.w = gsh(a.w, o); gshift(a.pro, o); a.bias = gsh(a.bias, o);
   a.stats_out = gsh(a.stats_out, o); a.mx = gsh(a.mx, o); gshift(a.mbn, o); a.gsum = gsh(a.gsum, o);
   a.gsumx = gsh(a.gsumx, o); a.slab = gsh(a.slab, o); a.tickets = gsh(a.tickets, o); gshift(a.bpro, o);
   gshift(a.bepi, o); a.aout = gsh(a.aout, o); a.stats_shift = gsh(a.stats_shift, o);
 }
 
-constexpr int TILE_HALO = 100;
 // tiles TILE_BIG128 / TILE_BIG256 select the 256 x {128, 256} global_load_lds kernel for plain
 // wide layers (conv_big.hip)
 constexpr int TILE_BIG128 = 101;
 constexpr int TILE_BIG256 = 102;
 constexpr int TILE_BIG64 = 103;
 constexpr int TILE_BIG128D = 104;  // 256 x 128 with three LDS buffers
-// deep-ring LDS-DMA small tiles (conv_ring.hip): TILE_RING + variant, variants
-// 0: 64x32  1: 64x64  2: 32x32  3: 32x64  4: 64x128
-constexpr int TILE_RING = 110;
-constexpr int TILE_RING_N = 5;
-bool conv_ring_ok(const ConvArgs& a, bool a_f32);
-hipError_t conv_ring(const ConvArgs& a, int variant, bool a_f32, hipStream_t st);
 bool conv_big_ok(const ConvArgs& a, bool a_f32);
 hipError_t conv_big(const ConvArgs& a, int bn, bool a_f32, hipStream_t st);
 hipError_t conv_igemm(const ConvArgs& a, int tile, bool a_f32, hipStream_t st);
-bool conv3x3_halo_ok(const ConvArgs& a);
-hipError_t conv3x3_halo(const ConvArgs& a, bool a_f32, hipStream_t st);
 int conv_pick_tile(int M, int Cout);
 int conv_num_tiles();
 int conv_tile_bm(int t);

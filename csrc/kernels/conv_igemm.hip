@@ -33,9 +33,8 @@ int conv_tile_bn(int t) { return kTiles[t].bn; }
 int conv_tile_bk(int t) { return kTiles[t].bk; }
 
 hipError_t conv_igemm(const ConvArgs& a, int tile, bool a_f32, hipStream_t st) {
-  const bool ring = tile >= TILE_RING && tile < TILE_RING + TILE_RING_N;
-  if (tile < 0 || (tile >= conv_num_tiles() && tile != TILE_HALO && tile != TILE_BIG128 && tile != TILE_BIG256 &&
-                   tile != TILE_BIG64 && tile != TILE_BIG128D && !ring))
+  if (tile < 0 || (tile >= conv_num_tiles() && tile != TILE_BIG128 && tile != TILE_BIG256 && tile != TILE_BIG64 &&
+                   tile != TILE_BIG128D))
     return hipErrorInvalidValue;
   const bool is1x1 = a.KH == 1 && a.KW == 1 && a.SH == 1 && a.SW == 1 && a.PT == 0 && a.PL == 0;
   const int pro = a.bpro.mode != 0 ? 2 : (a.pro.mode != 0 || a.pro.act != ACT_NONE) ? 1 : 0;
@@ -47,14 +46,6 @@ hipError_t conv_igemm(const ConvArgs& a, int tile, bool a_f32, hipStream_t st) {
   if (tile == TILE_BIG128 || tile == TILE_BIG256 || tile == TILE_BIG64 || tile == TILE_BIG128D)
     return conv_big(a, tile == TILE_BIG256 ? 256 : tile == TILE_BIG128 ? 128 : tile == TILE_BIG128D ? -128 : 64,
                     a_f32, st);
-  if (ring) {
-    if (a.ksplit > 1) return hipErrorInvalidValue;
-    return conv_ring(a, tile - TILE_RING, a_f32, st);
-  }
-  if (tile == TILE_HALO) {
-    if (a.ksplit > 1 || pro == 2 || epi == 2) return hipErrorInvalidValue;
-    return conv3x3_halo(a, a_f32, st);
-  }
   const int group = tile < 4 ? 0 : tile < 8 ? 1 : tile < 12 ? 2 : tile < 16 ? 3 : tile < 19 ? 4 : 5;
   switch (group) {
     case 0: return conv_igemm_group0(a, tile, is1x1, a_f32, pro, epi, st);

@@ -110,7 +110,7 @@ __global__ __launch_bounds__(256) void conv_igemm_kernel(ConvArgs a, GroupArg ga
 
   const int tid = threadIdx.x;
   const int lane = tid & 63;
-  const int wid = tid >> 6;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform: scalar branches on it
   const int wr = wid / WN, wc = wid % WN;
 
   const int M = a.N * a.Ho * a.Wo;

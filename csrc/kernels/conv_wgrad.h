@@ -26,7 +26,7 @@ struct WgradArgs {
 };
 
 __device__ __forceinline__ void gshift(WgradArgs& a, long long o) {
-  if (!o) return;
+  // (no early return at o == 0: gsh also moves every pointer into the global address space)
   a.x = gsh(a.x, o); a.g = gsh(a.g, o); gshift(a.pro, o); a.dw = gsh(a.dw, o); gshift(a.gpro, o);
   a.part = gsh(a.part, o);
 }

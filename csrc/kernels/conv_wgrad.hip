@@ -87,7 +87,8 @@ __device__ __forceinline__ void wgrad_tile(const WgradArgs& a, const int bkx, co
   float* s_gb = s_ga + BC;
   float* s_gc = s_gb + BC;
 
-  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform: scalar branches on it
   const int wr = wid / WN, wc = wid % WN;
   const int M = a.N * a.Ho * a.Wo;
   const int K = a.KH * a.KW * a.Cin;
@@ -347,7 +348,8 @@ __device__ __forceinline__ void wgrad3x3_img_tile(const WgradArgs& a, const int 
   float* s_scale = reinterpret_cast<float*>(smem + geo.x_bytes + geo.g_bytes);
   float* s_shift = s_scale + a.Cin;
 
-  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform: scalar branches on it
   const int c0 = by * WH_CB;
   const int img_beg = bx * ipw;
   const int img_end = min(a.N, img_beg + ipw);

@@ -14,35 +14,110 @@ struct DenseLayerDesc {
   const float* g2;      // _1_bn gamma / beta [128]
   const float* b2;
   bf16_t* t;            // raw 1x1 output [M][128] (saved for the backward)
-  float* tstats;        // [2][128] shifted statistics of t (zeroed per step)
+  float* tstats;        // [2][128] shifted statistics of t (zeroed per step; written once, whole)
   const float* tshift;  // [128] statistics shift of t (nullable)
   float eps1, eps2;
   int cin;              // input channels = this layer's slice offset in the stage buffer
   int pad_;
 };
 
+// Slot copies of the in-launch statistics (the per-channel float atomics of one phase are spread
+// over DS_SLOTS copies so no address takes more than ~tiles/DS_SLOTS adds)
+constexpr int DS_SLOTS = 8;
+// floats of in-launch statistics scratch per layer: [DS_SLOTS][2][32] slice + [DS_SLOTS][2][128] t
+constexpr int DS_SCRATCH_PER_LAYER = DS_SLOTS * 2 * (32 + 128);
+// the widest 1x1 input a launch accepts (BN coefficient tables in LDS): DenseNet-201 stage 4 = 1888
+constexpr int DS_MAX_CIN = 2048;
+// staged 3x3-operand rows per tile (32 output rows plus the images' halo rows): maps up to ~8x8
+constexpr int DS_MAX_STAGE_ROWS = 128;
+
 struct DenseStageArgs {
   bf16_t* buf;                  // stage buffer [M][ld] (channels [0, c0) written before the launch)
-  float* sstats;                // [2][ld] shifted statistics of the stage buffer
+  float* sstats;                // [2][ld] shifted statistics of the stage buffer (single copy)
   const float* sshift;          // [ld] (nullable)
   const DenseLayerDesc* layers; // device table [nlayers]
   unsigned* sync;               // [2 + 2 * nlayers] ticket, per-phase completion counters, fail flag
                                 // (zeroed before every launch: the program's stats-arena memset)
   int* err;                     // persistent count of launches that gave up on a wait (nullable)
+  float* scratch;               // [nlayers * DS_SCRATCH_PER_LAYER] zeroed per launch (stats arena)
+  unsigned long long* stamps;   // nullable: 4 s_memrealtime stamps per work item (diagnostics)
   int N, H, W, ld, nlayers, k2;
   int act1, act2;
   float inv_count;              // 1 / (N*H*W)
-  // cross-workgroup hand-off: 0 = agent-scope release/acquire fences around the completion
-  // counters (an L2 writeback + invalidate per phase boundary, ~2.5 us each); bit 0 = outputs
-  // stored with agent-coherent (sc1) stores, completed (vmcnt) before the counter increment, no
-  // release fence; bit 1 = operands / statistics produced in this launch read with agent-coherent
-  // loads (never a stale line of this XCD's L2), no acquire fence.  3 (the lowering's default):
-  // DenseNet-121 bs 256 stages 3+4 4.27-4.29 ms/step vs 4.36-4.41 with fences
-  int coh;
+  unsigned max_polls;           // bound on one wait's polls (0: default, ~0.5 s)
 };
 
 // number of work items of one launch (the grid never needs more workgroups than this)
 int dense_stage_tasks(const DenseStageArgs& a);
+// work items of each phase of one layer: 1x1 tiles (32 rows x 64 channels), 3x3 tiles (32 rows)
+void dense_stage_phase_tiles(int M, int& nA, int& nB);
+// whether a stage shape fits the launch (cin, staged rows)
+bool dense_stage_shape_ok(int N, int H, int W, int max_cin);
 hipError_t dense_stage_fwd(const DenseStageArgs& a, int grid, hipStream_t st);
+
+// ---------------------------------------------------------------------------------------------
+// Persistent dense-stage BACKWARD (dense_stage_bwd.hip): the data gradients of every dense layer
+// of a stage, its BatchNorm reductions and d gamma / d beta, in ONE launch.
+struct DenseBwdLayerDesc {
+  const bf16_t* w1d;    // cv1 dgrad layout [cin][128]
+  const bf16_t* w2d;    // cv2 dgrad layout [128][k2][k2][32] (flipped taps)
+  const float* g1;      // _0_bn gamma / beta [cin]
+  const float* b1;
+  const float* g2;      // _1_bn gamma / beta [128]
+  const float* b2;
+  const bf16_t* t;      // forward raw 1x1 output [M][128]
+  const float* tstats;  // forward [2][128] shifted statistics of t
+  const float* tshift;  // [128] (nullable)
+  bf16_t* dO16;         // [M][32] out: the layer's staged output gradient (cv2 weight gradient)
+  bf16_t* dt;           // [M][128] out: d t (cv1 weight gradient, older-channel dgrad operand)
+  float* dbeta1;        // gradient arena [cin] of _0_bn
+  float* dgamma1;
+  float* dbeta2;        // gradient arena [128] of _1_bn
+  float* dgamma2;
+  float* r1;            // scratch [DS_SLOTS][2][cin]: sum dZ1, sum dZ1*xhat1 (zeroed per step)
+  float* r2;            // scratch [DS_SLOTS][2][128]: sum dZ2, sum dZ2*xhat2
+  float eps1, eps2;
+  int cin;
+  int pad_;
+};
+
+// one entry of the launch's work queue, in ticket order
+struct DenseBwdPhase {
+  int first;   // first ticket
+  int kind;    // DSB_P / DSB_QN / DSB_G / DSB_GIN / DSB_FIN1 / DSB_FIN2
+  int layer;   // P, QN: the layer; G: the slice (= the layer that produced it)
+  int tiles;
+};
+enum { DSB_P = 1, DSB_QN = 2, DSB_G = 3, DSB_GIN = 4, DSB_FIN1 = 5, DSB_FIN2 = 6 };
+constexpr int DSB_KG = 6;          // later layers gathered per G / GIN tile
+constexpr int DSB_MAX_CG = 64;     // 32-channel groups of the stage input (c0 <= 2048)
+// sync words: [0] ticket; layer l at 1 + 32 l: P (8 shards), QN (8 shards), G arrivals, G done;
+// then GIN (8 shards), FIN1 arrivals per input channel group, FIN1 done, FIN2, fail
+constexpr int DSB_SYNC_PER_LAYER = 32;
+inline int dsb_sync_words(int L) { return 1 + DSB_SYNC_PER_LAYER * L + 8 + DSB_MAX_CG + 3; }
+
+struct DenseBwdArgs {
+  const bf16_t* buf;              // stage buffer [M][ld] (forward, raw)
+  const float* sstats;            // [2][ld] forward shifted statistics of the stage buffer
+  const float* sshift;            // [ld] (nullable)
+  float* dbuf;                    // fp32 [M][ld]: on entry A*dZ of the stage's consumer BatchNorm;
+                                  // the gathered older-layer terms are added in place
+  float* dnew;                    // fp32 [2][M][32] scratch: newest-slice 1x1 data gradients
+  bf16_t* dx16;                   // [M][c0] out: final gradient of the stage input channels (bf16)
+  bf16_t* z2;                     // [M][128] scratch: dZ of the current layer's _1_bn
+  BwdAff pend;                    // the consumer BatchNorm's pending B*x + C, channels [0, ld)
+                                  // (its reductions complete before the launch)
+  const DenseBwdLayerDesc* layers;
+  const DenseBwdPhase* phases;    // work queue, nphases entries
+  unsigned* sync;                 // [dsb_sync_words(nlayers)] counters (zeroed per step)
+  float* btot;                    // [2][ld] scratch: each channel's summed B / C (written once)
+  int* err;
+  unsigned long long* stamps;     // nullable: 4 stamps per ticket
+  int N, H, W, ld, c0, nlayers, k2, act, nphases, ntickets;
+  float inv_count;
+  unsigned max_polls;
+};
+
+hipError_t dense_stage_bwd(const DenseBwdArgs& a, int grid, hipStream_t st);
 
 }  // namespace idc

@@ -2,128 +2,76 @@
 //
 // A dense layer is  y = conv3x3(ReLU(BN2(conv1x1(ReLU(BN1(x[:, :cin]))))))  written into channels
 // [cin, cin+32) of the stage buffer (reference: /root/reference/dist_model_tf_dense.py:131-133
-// builds DenseNet-121 through Keras Applications).  In the late stages (bs 256:
-// 3x3 and 1x1 maps, M = 2,304 / 256 pixels) every such conv is a few hundred MFLOP that the
-// per-layer implicit GEMM runs in 7-15 us, almost all of it launch ramp, the serial K loop and the
-// BN tables' memory round trips, while 40 layers x 2 convs = 80 launches sit on the critical path.
+// builds DenseNet-121 / -201 through Keras Applications).  In the late stages (bs
+// 256: 3x3 and 1x1 maps, M = 2,304 / 256 pixels) every conv is a few hundred MFLOP, so the stage is
+// a chain of 2 x layers dependent phases whose cost is the hand-off between them, not arithmetic.
 //
-// Here one launch walks the whole stage as a WORK QUEUE of tiles:
-//     [layer 0: 1x1 tiles][layer 0: 3x3 tiles][layer 1: 1x1 tiles] ...
-// A workgroup takes the next ticket (one agent-scope atomic), and before it reads anything the
-// previous phase produced it waits until that phase's completion counter is full.  Tickets are
-// handed out in queue order, so every tile a waiting workgroup depends on was taken earlier by a
-// workgroup that is already running (or done): the queue cannot deadlock whatever number of
-// workgroups is resident (no co-residency assumption, no cooperative launch), and each wait has a
-// bounded poll count besides (a per-launch fail flag: every workgroup then leaves, and the launch
-// is counted in a persistent error counter), so a bug can never hang the GPU.  Weight fragments do
-// not depend on earlier phases and are loaded BEFORE the wait, so a workgroup that took a ticket of
-// the next phase early has its B operand in registers when the dependency clears.
+// One launch walks the stage as a WORK QUEUE of tiles:
+//     [layer 0: 1x1 tiles (A_0)][layer 0: 3x3 tiles (B_0)][layer 1: 1x1 tiles (A_1)] ...
+// A workgroup takes the next ticket (one agent-scope atomic) and waits, where it must, until an
+// earlier phase's completion counter is full.  Tickets are handed out in queue order, so every
+// tile a waiting workgroup depends on was taken earlier by a workgroup that is already running
+// (or done): the queue cannot deadlock whatever number of workgroups is resident.  Every wait is
+// poll-bounded; a workgroup that gives up sets the launch's fail flag (all others then leave) and
+// the first one to set it counts the launch in the persistent error counter.
 //
-// Hand-off between phases (DenseStageArgs::coh): by default the outputs are stored and the
-// operands / statistics produced in this launch are loaded with agent-coherent (sc1) accesses, so
-// no phase boundary pays an L2 writeback (release) or invalidate (acquire); with coh = 0 the
-// counters are guarded by agent-scope release/acquire fences instead (~2.5 us per boundary).
+// What is on the dependent chain, and what is not (the DenseNet structure):
+//   * A_l's 1x1 input is the concatenation of every earlier slice, and a slice's batch statistics
+//     are final once its producer phase is.  Only the NEWEST slice (32 channels, from B_{l-1}) is
+//     on the chain: an A_l tile first accumulates the channels [0, cin-32) -- final since A_{l-1}
+//     -- into registers, then waits for B_{l-1} and adds one 32-deep k-step.  Workgroups that run
+//     ahead of the chain do that accumulation while B_{l-1} is still computing.
+//   * BatchNorm statistics produced in the launch go into DS_SLOTS slot copies (float atomics
+//     serialise per address at ~24 ns, common.h "Statistics slots": 144 tiles adding into one
+//     row cost ~3.5 us per phase); a consumer sums the copies of the channels it needs (<= 8 KB).
+//     Tile 0 of the consuming phase writes the summed statistics into the program's single-copy
+//     rows (tstats, sstats) that the backward and the moving averages read after the launch.
+//   * Completion counters are polled with agent-coherent (sc1) loads from ONE lane (an atomic
+//     read-modify-write poll by ~200 workgroups contends with the producers' increments).
 //
-// Tile shapes (64-wide waves, v_mfma_f32_16x16x32_bf16, operands straight from global/L2 into
-// registers -- no LDS staging, a wave's K range in flight at once, in chunks for cin > 512):
-//   1x1 phase: 32 rows x 64 output channels per tile (2 tiles across the 128 channels), the K
-//              range (cin <= 1024) split over the 4 waves in chunks, partial tiles summed in LDS;
-//   3x3 phase: 16 rows x all 32 output channels, the 9 taps x 128 channels split over the waves.
-// Both phases apply the pending BatchNorm + ReLU of their operand in registers from a per-tile
-// coefficient table computed from the shifted batch statistics (common.h), store bf16 and add the
-// shifted statistics of the stored (rounded) values into the consumer's [sum|sumsq] arrays, exactly
-// the contract of the per-layer kernels (conv_igemm_impl.h EPI 0), so the backward is unchanged.
+// Hand-off memory model: every byte produced inside the launch (t, the stage-buffer slices, the
+// statistics) is stored and loaded with agent-scope atomic accesses (sc1), the producer drains
+// them (s_waitcnt vmcnt(0)) before its counter increment, the consumer loads after its poll
+// matched and a workgroup barrier (MI355X_MICROARCH.md, "Valid forms", first table row).
+//
+// Tile shapes (64-wide waves, v_mfma_f32_16x16x32_bf16):
+//   A (1x1): 32 rows x 64 output channels; each wave owns 16 channels over the whole K (no
+//            cross-wave reduction); the 32-row A operand is staged once per workgroup in LDS,
+//            BN1+ReLU applied while staging, in 256-channel chunks, one chunk's loads in flight
+//            under the previous chunk's MFMAs.
+//   B (3x3): 32 rows x all 32 output channels; the rows of t under the tile's 3x3 windows (whole
+//            images: 45 rows on 3x3 maps) are staged in LDS with BN2+ReLU applied, the 9 taps x 128
+//            channels are split over the 4 waves and reduced in LDS.
+// Diagnostics: with `stamps` set, thread 0 writes s_memrealtime (100 MHz) at ticket / dependency
+// cleared / operands staged / before publish for every work item (tools/dense_stamps.py).
 #include "dense_stage.h"
+#include "persist.h"
 
 namespace idc {
 namespace {
 
 constexpr int NT = 256;
-constexpr int KC = 4;    // 1x1 phase: k-steps of 32 per wave per chunk (cin <= 512: one chunk)
-constexpr int KB = 9;    // 3x3 phase: 9 taps x 128 channels / 32 / 4 waves
-constexpr int RLD = 33;  // LDS partial-tile row stride of the 3x3 phase (floats)
-constexpr int RLDA = 65; // ... of the 1x1 phase (64 columns)
-constexpr unsigned MAX_POLLS = 1u << 19;  // ~0.5-1 s of polling
+constexpr int S = DS_SLOTS;
+constexpr int ACH = 256;            // A-phase staging chunk (channels)
+constexpr int APITCH = ACH + 8;     // LDS row pitch (bf16): 528 B rows, conflict-free b128 reads
+constexpr int TPITCH = 128 + 8;     // B-phase staged t row pitch (bf16)
+constexpr int RLD = 33;             // B-phase partial-tile row stride (floats)
+constexpr int RLDA = 65;            // A-phase epilogue tile row stride (floats)
 
 struct Smem {
-  float sc[1024];
-  float sh[1024];
-  float red[4][32 * RLDA];
+  float sc[DS_MAX_CIN];
+  float sh[DS_MAX_CIN];
+  union {
+    bf16_t a[2][32 * APITCH];
+    bf16_t t[(DS_MAX_STAGE_ROWS + 1) * TPITCH];  // + one all-zero row (3x3 padding taps)
+  } u;
+  float red[4][32 * RLD];
   int task;
   int bad;
 };
+static_assert(sizeof(float) * 32 * RLDA <= sizeof(float) * 4 * 32 * RLD, "A epilogue tile fits red");
 
-// Agent-coherent loads of data other workgroups of this launch produced (sc1: never served from a
-// stale line of this XCD's L2), so a consumer needs no L2-invalidating acquire fence
-__device__ __forceinline__ uint4 ld_coh16(const void* p) {
-  unsigned long long* q = (unsigned long long*)p;
-  const unsigned long long lo = __hip_atomic_load(q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  const unsigned long long hi = __hip_atomic_load(q + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  return make_uint4((uint32_t)lo, (uint32_t)(lo >> 32), (uint32_t)hi, (uint32_t)(hi >> 32));
-}
-__device__ __forceinline__ float ld_coh(const float* p) {
-  return __hip_atomic_load((float*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-
-// thread 0: wait until *cnt >= need (then acquire), or give up after MAX_POLLS / when another
-// workgroup already gave up.  Returns false on a timeout.
-__device__ bool wait_count(unsigned* cnt, unsigned need, unsigned* fail, bool coherent_loads) {
-  // the counter is read with an atomic RMW (add 0): performed at the same coherence point as the
-  // producers' increments whatever XCD / L2 this workgroup runs on.  The bound is a poll count
-  // (each poll is a memory round trip plus an s_sleep), not a clock reading.
-  unsigned polls = 0;
-  while (__hip_atomic_fetch_add(cnt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < need) {
-    __builtin_amdgcn_s_sleep(2);
-    if ((++polls & 255u) == 0 &&
-        (polls > MAX_POLLS || __hip_atomic_fetch_add(fail, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0)) {
-      __hip_atomic_fetch_or(fail, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      return false;
-    }
-  }
-  if (!coherent_loads) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-  return true;
-}
-
-// every thread's stores / atomics of this tile performed, then one agent-scope release + count
-__device__ __forceinline__ void publish(unsigned* cnt, bool coherent_stores) {
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    if (!coherent_stores) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __hip_atomic_fetch_add(cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  }
-}
-
-// BN scale/shift for channels [0, C) (C <= 1024) from shifted [sum|sumsq] statistics (row length
-// ld), all loads of a thread issued before any arithmetic
-__device__ __forceinline__ void bn_table(const float* st, int ld, const float* shift, const float* g,
-                                         const float* b, float inv_n, float eps, int C, float* sc, float* sh,
-                                         bool coh) {
-  const int tid = threadIdx.x;
-  float s0[4], s1[4], k[4], gg[4], bb[4];
-#pragma unroll
-  for (int u = 0; u < 4; ++u) {
-    const int c = tid + u * NT;
-    const int cc = c < C ? c : 0;
-    s0[u] = coh ? ld_coh(st + cc) : st[cc];
-    s1[u] = coh ? ld_coh(st + ld + cc) : st[ld + cc];
-    k[u] = shift ? shift[cc] : 0.f;
-    gg[u] = g[cc];
-    bb[u] = b[cc];
-  }
-#pragma unroll
-  for (int u = 0; u < 4; ++u) {
-    const int c = tid + u * NT;
-    if (c < C) {
-      float mean, var;
-      shifted_mean_var(k[u], s0[u], s1[u], inv_n, mean, var);
-      const float r = gg[u] * rsqrtf(var + eps);
-      sc[c] = r;
-      sh[c] = bb[u] - mean * r;
-    }
-  }
-}
+using namespace persist;
 
 __device__ __forceinline__ v8bf bn_act8(const uint4& x, const float* sc, const float* sh, float lo, float hi,
                                         bool keep) {
@@ -138,6 +86,38 @@ __device__ __forceinline__ v8bf bn_act8(const uint4& x, const float* sc, const f
   return __builtin_bit_cast(v8bf, pack8(f));
 }
 
+// BN scale/shift for channels [0, C) (C <= DS_MAX_CIN) from the single-copy shifted statistics
+// (row length ld), read agent-coherently (some of them were written in this launch); each thread's
+// loads of a batch of 4 channels are all issued before the arithmetic
+__device__ __forceinline__ void bn_table(const float* st, int ld, const float* shift, const float* g,
+                                         const float* b, float inv_n, float eps, int C, float* sc, float* sh) {
+  const int tid = threadIdx.x;
+  for (int base = 0; base < C; base += 4 * NT) {
+    float s0[4], s1[4], k[4], gg[4], bb[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int c = base + tid + u * NT;
+      const int cc = c < C ? c : 0;
+      s0[u] = ld_coh(st + cc);
+      s1[u] = ld_coh(st + ld + cc);
+      k[u] = shift ? shift[cc] : 0.f;
+      gg[u] = g[cc];
+      bb[u] = b[cc];
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int c = base + tid + u * NT;
+      if (c < C) {
+        float mean, var;
+        shifted_mean_var(k[u], s0[u], s1[u], inv_n, mean, var);
+        const float r = gg[u] * rsqrtf(var + eps);
+        sc[c] = r;
+        sh[c] = bb[u] - mean * r;
+      }
+    }
+  }
+}
+
 }  // namespace
 
 // (outside the anonymous namespace so profiles name it: idc::dense_stage_kernel)
@@ -149,151 +129,215 @@ __global__ __launch_bounds__(NT) void dense_stage_kernel(DenseStageArgs a, Group
   const float* __restrict__ sshift = gsh(a.sshift, go);
   const DenseLayerDesc* __restrict__ layers = gsh(a.layers, go);
   unsigned* sync = gsh(a.sync, go);
-  unsigned* fail = sync + 1 + 2 * a.nlayers;  // this launch gave up (zeroed with the counters)
+  // counters: [0] ticket; layer l: A_l (8 shards) at 1 + 16l, B_l (8 shards) at 9 + 16l; then the
+  // last layer's unsharded arrival count (its last tile writes the last slice's statistics), fail
+  auto cntA = [&](int l) { return sync + 1 + 16 * l; };
+  auto cntB = [&](int l) { return sync + 9 + 16 * l; };
+  unsigned* lastfin = sync + 1 + 16 * a.nlayers;
+  unsigned* fail = lastfin + 1;  // this launch gave up (zeroed with the counters)
   int* err = gsh(a.err, go);
+  float* scratch = gsh(a.scratch, go);
+  unsigned long long* stamps = gsh(a.stamps, go);
+  const unsigned max_polls = a.max_polls ? a.max_polls : DEFAULT_POLLS;
 
   __shared__ __attribute__((aligned(16))) Smem s;
-  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform: scalar branches on it
   const int fr = lane & 15, fk = (lane >> 4) * 8;
   const int HW = a.H * a.W, M = a.N * HW;
-  const int mtA = (M + 31) / 32, nA = mtA * 2;
-  const int nB = (M + 15) / 16;
+  const int nmt = (M + 31) / 32;
+  const int nA = 2 * nmt, nB = nmt;
   const int per = nA + nB, total = per * a.nlayers;
   const int taps = a.k2 * a.k2, pad = a.k2 >> 1;
   const float lo1 = act_lo(a.act1), hi1 = act_hi(a.act1);
   const float lo2 = act_lo(a.act2), hi2 = act_hi(a.act2);
-  const bool coh = (a.coh & 2) != 0;  // coherent loads, no acquire fence (dense_stage.h)
+  // the zero row past the staged t rows (never written by a tile: the A-phase buffers end before it)
+  static_assert(sizeof(bf16_t) * 2 * 32 * APITCH <= sizeof(bf16_t) * DS_MAX_STAGE_ROWS * TPITCH, "zero row");
+  for (int i = tid; i < TPITCH / 2; i += NT) reinterpret_cast<uint32_t*>(s.u.t + DS_MAX_STAGE_ROWS * TPITCH)[i] = 0u;
 
   for (;;) {
-    // The ticket fetch is a thread-0 region enclosed by barriers on both sides.  Without the
-    // leading barrier hipcc merged it with the previous tile's thread-0 publish (no convergent op
-    // between them) and structurised the loop so that the other lanes of wave 0 and waves 1-3 went
-    // round again to the barrier before thread 0 had fetched the next ticket: they re-ran the stale
-    // tile forever (observed as a hang).
+    // The ticket fetch is a thread-0 region enclosed by barriers on both sides (without the
+    // leading barrier hipcc merged it with the previous tile's thread-0 publish and the other
+    // waves re-ran the stale tile).  The LDS broadcast goes through readfirstlane so every control
+    // decision of the loop is workgroup-uniform (no barrier in exec-masked flow).
     __syncthreads();
     if (tid == 0) s.task = (int)__hip_atomic_fetch_add(sync, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     __syncthreads();
-    // LDS broadcasts read through readfirstlane: the compiler then knows every control decision of
-    // the loop is workgroup-uniform (scalar branches), so no barrier ever sits in exec-masked flow
     const int task = __builtin_amdgcn_readfirstlane(s.task);
-    if (task >= total) {
-      // the last workgroup out reports a failed launch into the persistent error counter
-      if (tid == 0 && err && task == total + (int)gridDim.x - 1 &&
-          __hip_atomic_fetch_add(fail, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0)
-        atomicAdd(err, 1);
-      return;
-    }
+    if (task >= total) return;
+    stamp(stamps, task, 0);
     const int l = task / per, r = task - l * per;
-    DenseLayerDesc d = layers[l];
-    const bf16_t* __restrict__ w1 = gsh(d.w1, go);
-    const bf16_t* __restrict__ w2 = gsh(d.w2, go);
-    bf16_t* __restrict__ tb = gsh(d.t, go);
-    float* __restrict__ tst = gsh(d.tstats, go);
-    const float* __restrict__ tsh = gsh(d.tshift, go);
+    const DenseLayerDesc d = layers[l];
+    float* lslots = scratch + (size_t)l * DS_SCRATCH_PER_LAYER;  // [S][2][32] stats of B_l's slice
+    float* tslots = lslots + S * 64;                              // [S][2][128] stats of A_l's t
 
     if (r < nA) {
-      // ------------------------------------------------ 1x1 phase: t = conv1x1(relu(bn1(x)))
-      // 32 rows x 64 channels per tile (2 tiles across the 128 channels: a 2,304-row stage is 144
-      // tiles, one round on 256 CUs); each wave owns every 4th k-step and runs them in chunks of
-      // KC, a chunk's A and B fragments all in flight at once (cin <= 512: one chunk)
+      // ================================================= A_l: t = conv1x1(relu(bn1(x[:, :cin])))
+      const bf16_t* __restrict__ w1 = gsh(d.w1, go);
+      bf16_t* __restrict__ tb = gsh(d.t, go);
+      const float* __restrict__ tsh = gsh(d.tshift, go);
+      const float* __restrict__ g1 = gsh(d.g1, go);
+      const float* __restrict__ b1 = gsh(d.b1, go);
       const int mt = r >> 1, n0 = (r & 1) * 64, m0 = mt * 32;
-      const int cin = d.cin, nks = cin >> 5;
-      v8bf bq[KC][4];
-      auto load_b = [&](int c0k) {
-#pragma unroll
-        for (int i = 0; i < KC; ++i) {
-          const int ks = wid + 4 * (c0k + i);
-#pragma unroll
-          for (int j = 0; j < 4; ++j)
-            bq[i][j] = ks < nks ? *reinterpret_cast<const v8bf*>(w1 + (size_t)(n0 + j * 16 + fr) * cin + ks * 32 + fk)
-                                : v8bf{};
-        }
-      };
-      uint4 ar[KC][2];
-      auto load_a = [&](int c0k) {
-#pragma unroll
-        for (int i = 0; i < KC; ++i) {
-          const int ks = wid + 4 * (c0k + i);
-#pragma unroll
-          for (int h = 0; h < 2; ++h) {
-            const int m = m0 + h * 16 + fr;
-            const bf16_t* src = buf + (size_t)m * a.ld + ks * 32 + fk;
-            ar[i][h] = (ks < nks && m < M) ? (coh ? ld_coh16(src) : *reinterpret_cast<const uint4*>(src))
-                                           : make_uint4(0, 0, 0, 0);
-          }
-        }
-      };
-      load_b(0);  // weights do not depend on earlier phases: in flight before the wait
+      const int cin = d.cin;
+      const int cold = l == 0 ? cin : cin - 32;  // channels final before B_{l-1}
+      const bf16_t* wrow = w1 + (size_t)(n0 + wid * 16 + fr) * cin;  // this lane's B column
+      const v8bf bnew = l > 0 ? *reinterpret_cast<const v8bf*>(wrow + cold + fk) : v8bf{};
       const int erow = tid >> 3, ecol = (tid & 7) * 8;
       float kq[8];
 #pragma unroll
       for (int q = 0; q < 8; ++q) kq[q] = tsh ? tsh[n0 + ecol + q] : 0.f;
-      if (l > 0) {
-        if (tid == 0) s.bad = !wait_count(&sync[2 * l], (unsigned)nB, fail, coh);  // 3x3 phase of layer l-1
+      v4f acc[2] = {v4f{0.f, 0.f, 0.f, 0.f}, v4f{0.f, 0.f, 0.f, 0.f}};
+
+      // ---- channels [0, cold): final once B_{l-2} is complete.  Their statistics: single-copy
+      // rows for [0, cold-32) (written by A_{l-1}'s tile 0 at the latest -- A_{l-2} for the slice
+      // of B_{l-3} -- hence complete before B_{l-2} started), B_{l-2}'s slots for [cold-32, cold)
+      if (l >= 2) {
+        if (wid == 0) {
+          const bool ok = wait_sum8(cntB(l - 2), (unsigned)nB, fail, err, max_polls);
+          if (lane == 0) s.bad = !ok;
+        }
         __syncthreads();
         if (__builtin_amdgcn_readfirstlane(s.bad)) return;
       }
-      load_a(0);
-      bn_table(sstats, a.ld, sshift, gsh(d.g1, go), gsh(d.b1, go), a.inv_count, d.eps1, cin, s.sc, s.sh, coh);
-      __syncthreads();
-      v4f acc[2][4];
+      stamp(stamps, task, 1);
+      const int srow = m0 + (tid >> 3), sseg = (tid & 7) * 32;  // staging: a row, 32 channels
+      uint4 ar[4];
+      auto load_a = [&](int ch) {
 #pragma unroll
-      for (int h = 0; h < 2; ++h)
-#pragma unroll
-        for (int j = 0; j < 4; ++j) acc[h][j] = v4f{0.f, 0.f, 0.f, 0.f};
-      const int nchunks = (nks + 4 * KC - 1) / (4 * KC);
-      for (int ch = 0; ch < nchunks; ++ch) {
-        if (ch > 0) {
-          load_b(ch * KC);
-          load_a(ch * KC);
+        for (int u = 0; u < 4; ++u) {
+          const int c = ch * ACH + sseg + u * 8;
+          ar[u] = (srow < M && c < cold) ? ld_coh16(buf + (size_t)srow * a.ld + c) : make_uint4(0, 0, 0, 0);
         }
+      };
+      auto load_b = [&](int ch, v8bf (&bq)[8]) {
 #pragma unroll
-        for (int i = 0; i < KC; ++i) {
-          const int ks = wid + 4 * (ch * KC + i);
-          if (ks < nks) {
-            const int c0 = ks * 32 + fk;
+        for (int i = 0; i < 8; ++i) {
+          const int k = ch * ACH + i * 32;
+          bq[i] = k < cold ? *reinterpret_cast<const v8bf*>(wrow + k + fk) : v8bf{};
+        }
+      };
+      auto stage = [&](int ch) {
+        bf16_t* ab = s.u.a[ch & 1] + (tid >> 3) * APITCH + sseg;
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          const int c = ch * ACH + sseg + u * 8;
+          const bool keep = srow < M && c < cold;
+          const int cc = keep ? c : 0;
+          *reinterpret_cast<v8bf*>(ab + u * 8) = bn_act8(ar[u], s.sc + cc, s.sh + cc, lo1, hi1, keep);
+        }
+      };
+      auto mfma_chunk = [&](int ch, const v8bf (&bq)[8]) {
+        const bf16_t* ab = s.u.a[ch & 1];
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+          if (ch * ACH + i * 32 < cold) {
 #pragma unroll
             for (int h = 0; h < 2; ++h) {
-              const v8bf af = bn_act8(ar[i][h], s.sc + c0, s.sh + c0, lo1, hi1, true);
-#pragma unroll
-              for (int j = 0; j < 4; ++j)
-                acc[h][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, bq[i][j], acc[h][j], 0, 0, 0);
+              const v8bf af = *reinterpret_cast<const v8bf*>(ab + (h * 16 + fr) * APITCH + i * 32 + fk);
+              acc[h] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, bq[i], acc[h], 0, 0, 0);
             }
           }
         }
+      };
+      const int nch = (cold + ACH - 1) / ACH;
+      v8bf bq0[8], bq1[8];
+      load_a(0);
+      load_b(0, bq0);
+      const int ccanon = l >= 2 ? cold - 32 : cold;
+      bn_table(sstats, a.ld, sshift, g1, b1, a.inv_count, d.eps1, ccanon, s.sc, s.sh);
+      if (l >= 2 && tid < 32) {
+        float s0, s1, mean, var;
+        slot_sum<S>(lslots - 2 * DS_SCRATCH_PER_LAYER, 32, tid, s0, s1);
+        const int c = ccanon + tid;
+        shifted_mean_var(sshift ? sshift[c] : 0.f, s0, s1, a.inv_count, mean, var);
+        const float rr = g1[c] * rsqrtf(var + d.eps1);
+        s.sc[c] = rr;
+        s.sh[c] = b1[c] - mean * rr;
       }
-      float* red = s.red[wid];
+      __syncthreads();
+      // chunk ch: stage it (BN1+ReLU into LDS buffer ch&1), barrier, put the next chunk's loads in
+      // flight, then its MFMAs; the double buffer makes one barrier per chunk sufficient
+      for (int ch = 0; ch < nch; ch += 2) {
+        stage(ch);
+        __syncthreads();
+        if (ch + 1 < nch) {
+          load_a(ch + 1);
+          load_b(ch + 1, bq1);
+        }
+        mfma_chunk(ch, bq0);
+        if (ch + 1 < nch) {
+          stage(ch + 1);
+          __syncthreads();
+          if (ch + 2 < nch) {
+            load_a(ch + 2);
+            load_b(ch + 2, bq0);
+          }
+          mfma_chunk(ch + 1, bq1);
+        }
+      }
+
+      stamp(stamps, task, 2);
+      // ---- the newest slice [cold, cin): wait for B_{l-1}
+      if (l > 0) {
+        if (wid == 0) {
+          const bool ok = wait_sum8(cntB(l - 1), (unsigned)nB, fail, err, max_polls);
+          if (lane == 0) s.bad = !ok;
+        }
+        __syncthreads();
+        if (__builtin_amdgcn_readfirstlane(s.bad)) return;
+      }
+      stamp(stamps, task, 3);
+      if (l > 0) {
+        const float* pslots = lslots - DS_SCRATCH_PER_LAYER;  // B_{l-1}'s slice statistics
+        const int nrow = m0 + (tid >> 2), nseg = (tid & 3) * 8;
+        const uint4 an = (tid < 128 && nrow < M) ? ld_coh16(buf + (size_t)nrow * a.ld + cold + nseg)
+                                                 : make_uint4(0, 0, 0, 0);
+        if (tid < 32) {
+          float s0, s1, mean, var;
+          slot_sum<S>(pslots, 32, tid, s0, s1);
+          const int c = cold + tid;
+          shifted_mean_var(sshift ? sshift[c] : 0.f, s0, s1, a.inv_count, mean, var);
+          const float rr = g1[c] * rsqrtf(var + d.eps1);
+          s.sc[c] = rr;
+          s.sh[c] = b1[c] - mean * rr;
+          if (r == 0) {  // the slice's single-copy statistics (read by later layers' tables)
+            st_coh(sstats + c, s0);
+            st_coh(sstats + a.ld + c, s1);
+          }
+        }
+        __syncthreads();
+        if (tid < 128)
+          *reinterpret_cast<v8bf*>(s.u.a[0] + (tid >> 2) * APITCH + nseg) =
+              bn_act8(an, s.sc + cold + nseg, s.sh + cold + nseg, lo1, hi1, nrow < M);
+        __syncthreads();
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+          const v8bf af = *reinterpret_cast<const v8bf*>(s.u.a[0] + (h * 16 + fr) * APITCH + fk);
+          acc[h] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, bnew, acc[h], 0, 0, 0);
+        }
+      }
+      stamp(stamps, task, 4);
+
+      // ---- epilogue: bf16 t tile (16-B sc1 stores), shifted statistics into slot mt % S
+      float* red = s.red[0];
 #pragma unroll
       for (int h = 0; h < 2; ++h)
 #pragma unroll
-        for (int j = 0; j < 4; ++j)
-#pragma unroll
-          for (int q = 0; q < 4; ++q) red[(h * 16 + (lane >> 4) * 4 + q) * RLDA + j * 16 + fr] = acc[h][j][q];
+        for (int q = 0; q < 4; ++q) red[(h * 16 + (lane >> 4) * 4 + q) * RLDA + wid * 16 + fr] = acc[h][q];
       __syncthreads();
+      stamp(stamps, task, 5);
       {
         float v[8];
 #pragma unroll
-        for (int q = 0; q < 8; ++q) {
-          const int o = erow * RLDA + ecol + q;
-          v[q] = s.red[0][o] + s.red[1][o] + s.red[2][o] + s.red[3][o];
-        }
+        for (int q = 0; q < 8; ++q) v[q] = red[erow * RLDA + ecol + q];
         const int m = m0 + erow;
         const uint4 pk = pack8(v);
-        if (m < M) {
-          uint32_t* o = reinterpret_cast<uint32_t*>(tb + (size_t)m * 128 + n0 + ecol);
-          if ((a.coh & 1)) {  // agent-coherent (sc1) stores: no release fence needed
-            unsigned long long* o2 = reinterpret_cast<unsigned long long*>(o);
-            __hip_atomic_store(o2, ((unsigned long long)pk.y << 32) | pk.x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            __hip_atomic_store(o2 + 1, ((unsigned long long)pk.w << 32) | pk.z, __ATOMIC_RELAXED,
-                               __HIP_MEMORY_SCOPE_AGENT);
-          } else {
-            *reinterpret_cast<uint4*>(o) = pk;
-          }
-        }
+        if (m < M) st_coh16(tb + (size_t)m * 128 + n0 + ecol, pk);
         float rv[8];
         unpack8(pk, rv);
 #pragma unroll
-        for (int q = 0; q < 8; ++q) s.red[0][erow * RLDA + ecol + q] = m < M ? rv[q] - kq[q] : 0.f;
+        for (int q = 0; q < 8; ++q) red[erow * RLDA + ecol + q] = m < M ? rv[q] - kq[q] : 0.f;
       }
       __syncthreads();
       if (tid < 128) {
@@ -301,127 +345,219 @@ __global__ __launch_bounds__(NT) void dense_stage_kernel(DenseStageArgs a, Group
         float sum = 0.f;
 #pragma unroll 8
         for (int row = 0; row < 32; ++row) {
-          const float x = s.red[0][row * RLDA + c];
+          const float x = red[row * RLDA + c];
           sum += which ? x * x : x;
         }
-        atomicAdd(&tst[which * 128 + n0 + c], sum);
+        atomicAdd(&tslots[(mt % S) * 256 + which * 128 + n0 + c], sum);
       }
-      publish(&sync[1 + 2 * l], (a.coh & 1));
+      stamp(stamps, task, 6);
+      {
+        const unsigned o = publish_shard(cntA(l), r);
+        if (stamps && tid == 0) stamps[(size_t)task * NSTAMP + 7] = __builtin_amdgcn_s_memrealtime() + (o & 0u);
+      }
     } else {
-      // ------------------------------------------------ 3x3 phase: buf[:, cin:cin+32] = conv3x3(relu(bn2(t)))
-      const int m0 = (r - nA) * 16;
+      // ================================================= B_l: buf[:, cin:cin+32] = conv3x3(relu(bn2(t)))
+      const bf16_t* __restrict__ w2 = gsh(d.w2, go);
+      const bf16_t* __restrict__ tb = gsh(d.t, go);
+      float* __restrict__ tst = gsh(d.tstats, go);
+      const float* __restrict__ tsh = gsh(d.tshift, go);
+      const int j = r - nA, m0 = j * 32;
       const int cin = d.cin, Kc = taps * 128, nks = taps * 4;
-      v8bf bq[KB][2];
+      // weight fragments do not depend on earlier phases: in flight before the wait
+      v8bf bq[9][2];
 #pragma unroll
-      for (int i = 0; i < KB; ++i) {
+      for (int i = 0; i < 9; ++i) {
         const int ks = wid + 4 * i;
         const int tap = ks >> 2, c = (ks & 3) * 32 + fk;
 #pragma unroll
-        for (int j = 0; j < 2; ++j)
-          bq[i][j] = ks < nks ? *reinterpret_cast<const v8bf*>(w2 + (size_t)(j * 16 + fr) * Kc + tap * 128 + c)
-                              : v8bf{};
+        for (int jj = 0; jj < 2; ++jj)
+          bq[i][jj] = ks < nks ? *reinterpret_cast<const v8bf*>(w2 + (size_t)(jj * 16 + fr) * Kc + tap * 128 + c)
+                               : v8bf{};
       }
-      const int erow = tid >> 4, ecol = (tid & 15) * 2;
-      float kq[2];
+      const int erow = tid >> 3, ecol = (tid & 7) * 4;
+      float kq[4];
 #pragma unroll
-      for (int q = 0; q < 2; ++q) kq[q] = sshift ? sshift[cin + ecol + q] : 0.f;
-      const int m = m0 + fr;
-      const int mm = m < M ? m : M - 1;
-      const int img = mm / HW, rem = mm - img * HW;
-      const int ph = rem / a.W, pw = rem - ph * a.W;
-      if (tid == 0) s.bad = !wait_count(&sync[1 + 2 * l], (unsigned)nA, fail, coh);  // 1x1 phase of layer l
-      __syncthreads();
-      if (__builtin_amdgcn_readfirstlane(s.bad)) return;
-      uint4 ar[KB];
-      bool okr[KB];
-#pragma unroll
-      for (int i = 0; i < KB; ++i) {
-        const int ks = wid + 4 * i;
-        const int tap = ks >> 2;
-        const int kr = tap / a.k2, kc = tap - kr * a.k2;
-        const int hh = ph + kr - pad, ww = pw + kc - pad;
-        okr[i] = ks < nks && m < M && hh >= 0 && hh < a.H && ww >= 0 && ww < a.W;
-        const bf16_t* src = tb + ((size_t)(img * a.H + hh) * a.W + ww) * 128 + (ks & 3) * 32 + fk;
-        ar[i] = okr[i] ? (coh ? ld_coh16(src) : *reinterpret_cast<const uint4*>(src)) : make_uint4(0, 0, 0, 0);
-      }
+      for (int q = 0; q < 4; ++q) kq[q] = sshift ? sshift[cin + ecol + q] : 0.f;
+      float g2c = 0.f, b2c = 0.f, ksh = 0.f;
       if (tid < 128) {
-        // 128 channels: one per thread (the 4-way table builder's other slots stay idle)
-        const int c = tid;
-        float mean, var;
-        shifted_mean_var(tsh ? tsh[c] : 0.f, coh ? ld_coh(tst + c) : tst[c], coh ? ld_coh(tst + 128 + c) : tst[128 + c],
-                         a.inv_count, mean, var);
-        const float rr = gsh(d.g2, go)[c] * rsqrtf(var + d.eps2);
-        s.sc[c] = rr;
-        s.sh[c] = gsh(d.b2, go)[c] - mean * rr;
+        g2c = gsh(d.g2, go)[tid];
+        b2c = gsh(d.b2, go)[tid];
+        ksh = tsh ? tsh[tid] : 0.f;
       }
-      __syncthreads();
-      v4f acc[2];
+      const int mend = min(m0 + 32, M);
+      const int img_lo = m0 / HW, img_hi = (mend - 1) / HW;
+      const int row_lo = img_lo * HW, R = (img_hi - img_lo + 1) * HW;
+      // LDS element offsets of this lane's A fragments (k-step wid + 4i, row fragment h) in the
+      // staged t rows; zero padding is applied AFTER the activation (Keras 'same' conv of
+      // relu(bn(t))), so padding taps read the all-zero row
+      int aoff[2][9];
 #pragma unroll
-      for (int j = 0; j < 2; ++j) acc[j] = v4f{0.f, 0.f, 0.f, 0.f};
+      for (int h = 0; h < 2; ++h) {
+        const int m = m0 + h * 16 + fr;
+        const int mm = m < M ? m : M - 1;
+        const int img = mm / HW, rem = mm - img * HW;
+        const int ph = rem / a.W, pw = rem - ph * a.W;
+        const int ibase = img * HW - row_lo;
 #pragma unroll
-      for (int i = 0; i < KB; ++i) {
-        const int ks = wid + 4 * i;
-        if (ks < nks) {
-          const int c0 = (ks & 3) * 32 + fk;
-          // zero padding is applied AFTER the activation (Keras 'same' conv of relu(bn(t)))
-          const v8bf af = bn_act8(ar[i], s.sc + c0, s.sh + c0, lo2, hi2, okr[i]);
-#pragma unroll
-          for (int j = 0; j < 2; ++j) acc[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, bq[i][j], acc[j], 0, 0, 0);
+        for (int i = 0; i < 9; ++i) {
+          const int ks = wid + 4 * i;
+          const int tap = ks >> 2;
+          const int kr = tap / a.k2, kc = tap - kr * a.k2;
+          const int hh = ph + kr - pad, ww = pw + kc - pad;
+          const bool ok = ks < nks && m < M && hh >= 0 && hh < a.H && ww >= 0 && ww < a.W;
+          const int lrow = ok ? ibase + hh * a.W + ww : DS_MAX_STAGE_ROWS;
+          aoff[h][i] = lrow * TPITCH + (ks & 3) * 32 + fk;
         }
       }
+      stamp(stamps, task, 1);
+      if (wid == 0) {
+        const bool ok = wait_sum8(cntA(l), (unsigned)nA, fail, err, max_polls);
+        if (lane == 0) s.bad = !ok;
+      }
+      __syncthreads();
+      if (__builtin_amdgcn_readfirstlane(s.bad)) return;
+      stamp(stamps, task, 2);
+      // t rows under the tile's windows (raw) and the t statistics, all loads in flight together
+      constexpr int TU = DS_MAX_STAGE_ROWS * 16 / NT;
+      uint4 traw[TU];
+#pragma unroll
+      for (int u = 0; u < TU; ++u) {
+        const int idx = tid + u * NT;
+        traw[u] = idx < R * 16 ? ld_coh16(tb + (size_t)(row_lo + (idx >> 4)) * 128 + (idx & 15) * 8)
+                               : make_uint4(0, 0, 0, 0);
+      }
+      if (tid < 128) {
+        float s0, s1, mean, var;
+        slot_sum<S>(tslots, 128, tid, s0, s1);
+        shifted_mean_var(ksh, s0, s1, a.inv_count, mean, var);
+        const float rr = g2c * rsqrtf(var + d.eps2);
+        s.sc[tid] = rr;
+        s.sh[tid] = b2c - mean * rr;
+        if (j == 0) {  // t's single-copy statistics (backward, moving averages)
+          tst[tid] = s0;
+          tst[128 + tid] = s1;
+        }
+      }
+      __syncthreads();
+#pragma unroll
+      for (int u = 0; u < TU; ++u) {
+        const int idx = tid + u * NT;
+        if (idx < R * 16) {
+          const int c = (idx & 15) * 8;
+          *reinterpret_cast<v8bf*>(s.u.t + (idx >> 4) * TPITCH + c) = bn_act8(traw[u], s.sc + c, s.sh + c, lo2, hi2, true);
+        }
+      }
+      __syncthreads();
+      stamp(stamps, task, 3);
+      // every LDS read of the tile first (offsets computed before the wait), then the MFMAs
+      v8bf af[2][9];
+#pragma unroll
+      for (int h = 0; h < 2; ++h)
+#pragma unroll
+        for (int i = 0; i < 9; ++i)
+          if (wid + 4 * i < nks) af[h][i] = *reinterpret_cast<const v8bf*>(s.u.t + aoff[h][i]);
+      v4f acc[2][2];
+#pragma unroll
+      for (int h = 0; h < 2; ++h)
+#pragma unroll
+        for (int jj = 0; jj < 2; ++jj) acc[h][jj] = v4f{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int i = 0; i < 9; ++i)
+        if (wid + 4 * i < nks) {
+#pragma unroll
+          for (int h = 0; h < 2; ++h)
+#pragma unroll
+            for (int jj = 0; jj < 2; ++jj)
+              acc[h][jj] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[h][i], bq[i][jj], acc[h][jj], 0, 0, 0);
+        }
       float* red = s.red[wid];
 #pragma unroll
-      for (int j = 0; j < 2; ++j)
+      for (int h = 0; h < 2; ++h)
 #pragma unroll
-        for (int q = 0; q < 4; ++q) red[((lane >> 4) * 4 + q) * RLD + j * 16 + fr] = acc[j][q];
+        for (int jj = 0; jj < 2; ++jj)
+#pragma unroll
+          for (int q = 0; q < 4; ++q) red[(h * 16 + (lane >> 4) * 4 + q) * RLD + jj * 16 + fr] = acc[h][jj][q];
       __syncthreads();
+      stamp(stamps, task, 4);
       {
-        float v[2];
+        float v[4];
 #pragma unroll
-        for (int q = 0; q < 2; ++q) {
+        for (int q = 0; q < 4; ++q) {
           const int o = erow * RLD + ecol + q;
           v[q] = s.red[0][o] + s.red[1][o] + s.red[2][o] + s.red[3][o];
         }
         const int mo = m0 + erow;
-        const uint32_t p = pack2bf(v[0], v[1]);
-        if (mo < M) {
-          uint32_t* o = reinterpret_cast<uint32_t*>(buf + (size_t)mo * a.ld + cin + ecol);
-          if ((a.coh & 1)) __hip_atomic_store(o, p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          else *o = p;
-        }
-        const float rv[2] = {__uint_as_float(p << 16), __uint_as_float(p & 0xffff0000u)};
+        const uint32_t p0 = pack2bf(v[0], v[1]), p1 = pack2bf(v[2], v[3]);
+        if (mo < M) st_coh8(buf + (size_t)mo * a.ld + cin + ecol, p0, p1);
+        const float rv[4] = {__uint_as_float(p0 << 16), __uint_as_float(p0 & 0xffff0000u),
+                             __uint_as_float(p1 << 16), __uint_as_float(p1 & 0xffff0000u)};
 #pragma unroll
-        for (int q = 0; q < 2; ++q) s.red[0][erow * RLD + ecol + q] = mo < M ? rv[q] - kq[q] : 0.f;
+        for (int q = 0; q < 4; ++q) s.red[0][erow * RLD + ecol + q] = mo < M ? rv[q] - kq[q] : 0.f;
       }
       __syncthreads();
+      stamp(stamps, task, 5);
       if (tid < 64) {
         const int c = tid & 31, which = tid >> 5;
         float sum = 0.f;
-#pragma unroll
-        for (int row = 0; row < 16; ++row) {
+#pragma unroll 8
+        for (int row = 0; row < 32; ++row) {
           const float x = s.red[0][row * RLD + c];
           sum += which ? x * x : x;
         }
-        atomicAdd(&sstats[which * a.ld + cin + c], sum);
+        atomicAdd(&lslots[(j % S) * 64 + which * 32 + c], sum);
       }
-      publish(&sync[2 + 2 * l], (a.coh & 1));
+      stamp(stamps, task, 6);
+      {
+        const unsigned o = publish_shard(cntB(l), j);
+        if (stamps && tid == 0) stamps[(size_t)task * NSTAMP + 7] = __builtin_amdgcn_s_memrealtime() + (o & 0u);
+      }
+      if (l == a.nlayers - 1) {
+        // the last slice has no in-launch consumer: the last tile to complete writes its
+        // single-copy statistics
+        if (tid == 0)
+          s.bad = __hip_atomic_fetch_add(lastfin, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == (unsigned)(nB - 1);
+        __syncthreads();
+        if (__builtin_amdgcn_readfirstlane(s.bad) && tid < 32) {
+          float s0, s1;
+          slot_sum<S>(lslots, 32, tid, s0, s1);
+          sstats[cin + tid] = s0;
+          sstats[a.ld + cin + tid] = s1;
+        }
+      }
     }
   }
 }
 
+void dense_stage_phase_tiles(int M, int& nA, int& nB) {
+  const int nmt = (M + 31) / 32;
+  nA = 2 * nmt;
+  nB = nmt;
+}
+
 int dense_stage_tasks(const DenseStageArgs& a) {
-  const long long M = (long long)a.N * a.H * a.W;
-  return (int)(a.nlayers * (((M + 31) / 32) * 2 + (M + 15) / 16));
+  int nA, nB;
+  dense_stage_phase_tiles(a.N * a.H * a.W, nA, nB);
+  return a.nlayers * (nA + nB);
+}
+
+bool dense_stage_shape_ok(int N, int H, int W, int max_cin) {
+  if (N < 1 || H < 1 || W < 1 || max_cin > DS_MAX_CIN) return false;
+  const int HW = H * W, M = N * HW;
+  for (int m0 = 0; m0 < M; m0 += 32) {  // rows staged by each 3x3 tile
+    const int mend = m0 + 32 < M ? m0 + 32 : M;
+    if ((((mend - 1) / HW) - m0 / HW + 1) * HW > DS_MAX_STAGE_ROWS) return false;
+  }
+  return true;
 }
 
 hipError_t dense_stage_fwd(const DenseStageArgs& a, int grid, hipStream_t st) {
   if (a.nlayers < 1 || (a.k2 != 1 && a.k2 != 3) || a.ld % 8 != 0 || a.N < 1 || a.H < 1 || a.W < 1 ||
-      a.buf == nullptr || a.sstats == nullptr || a.layers == nullptr || a.sync == nullptr)
+      a.buf == nullptr || a.sstats == nullptr || a.layers == nullptr || a.sync == nullptr ||
+      a.scratch == nullptr || !dense_stage_shape_ok(a.N, a.H, a.W, 0))
     return hipErrorInvalidValue;
   const int tasks = dense_stage_tasks(a);
   if (grid <= 0) grid = 256;
-  // a grouped launch (K copies, each with its own queue) shares the CUs: one resident workgroup
-  // per CU (256 VGPRs), so K copies of a full-chip grid would run one copy after another
+  // a grouped launch (K copies, each with its own queue) shares the CUs
   const int k = launch_groups().k;
   if (k > 1) grid = grid / k > 8 ? grid / k : 8;
   if (grid > tasks) grid = tasks;

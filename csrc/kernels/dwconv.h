@@ -30,7 +30,7 @@ struct DwArgs {
 };
 
 __device__ __forceinline__ void gshift(DwArgs& a, long long o) {
-  if (!o) return;
+  // (no early return at o == 0: gsh also moves every pointer into the global address space)
   a.x = gsh(a.x, o); gshift(a.pro, o); a.w = gsh(a.w, o); a.y = gsh(a.y, o); a.stats = gsh(a.stats, o);
   a.dy = gsh(a.dy, o); a.dx = gsh(a.dx, o); a.gsum = gsh(a.gsum, o); a.gsumx = gsh(a.gsumx, o);
   a.dw = gsh(a.dw, o); a.ws = gsh(a.ws, o); gshift(a.dyaff, o); a.stats_shift = gsh(a.stats_shift, o);

@@ -31,7 +31,7 @@ struct Mlp2Args {
 };
 
 __device__ __forceinline__ void gshift(Mlp2Args& a, long long o) {
-  if (!o) return;
+  // (no early return at o == 0: gsh also moves every pointer into the global address space)
   a.x = gsh(a.x, o); a.w1 = gsh(a.w1, o); a.b1 = gsh(a.b1, o); a.w2 = gsh(a.w2, o); a.b2 = gsh(a.b2, o);
   a.step = gsh(a.step, o); a.labels = gsh(a.labels, o); a.logits = gsh(a.logits, o); a.h1 = gsh(a.h1, o);
   a.loss = gsh(a.loss, o); a.dlogits = gsh(a.dlogits, o); a.dw1 = gsh(a.dw1, o); a.db1 = gsh(a.db1, o);

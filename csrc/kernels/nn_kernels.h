@@ -111,45 +111,45 @@ struct CastEntry {
 
 // grouped-execution pointer shifts (common.h GroupArg)
 __device__ __forceinline__ void gshift(BnBwdApplyArgs& a, long long o) {
-  if (!o) return;
+  // (no early return at o == 0: gsh also moves every pointer into the global address space)
   a.dz = gsh(a.dz, o); a.x = gsh(a.x, o); gshift(a.bn, o); a.gsum = gsh(a.gsum, o); a.gsumx = gsh(a.gsumx, o);
   a.dst = gsh(a.dst, o); a.fold_sum = gsh(a.fold_sum, o); a.fold_sumx = gsh(a.fold_sumx, o);
 }
 __device__ __forceinline__ void gshift(BnBwdReduceArgs& a, long long o) {
-  if (!o) return;
+  // (no early return at o == 0: gsh also moves every pointer into the global address space)
   a.dy = gsh(a.dy, o); a.x = gsh(a.x, o); gshift(a.bn, o); a.dz = gsh(a.dz, o); a.gsum = gsh(a.gsum, o);
   a.gsumx = gsh(a.gsumx, o);
 }
 __device__ __forceinline__ void gshift(PoolArgs& a, long long o) {
-  if (!o) return;
+  // (no early return at o == 0: gsh also moves every pointer into the global address space)
   a.x = gsh(a.x, o); gshift(a.pro, o); a.y = gsh(a.y, o); a.argmax = gsh(a.argmax, o);
   a.stats = gsh(a.stats, o); a.stats_shift = gsh(a.stats_shift, o);
 }
 __device__ __forceinline__ void gshift(PoolBwdArgs& a, long long o) {
-  if (!o) return;
+  // (no early return at o == 0: gsh also moves every pointer into the global address space)
   a.dy = gsh(a.dy, o); a.argmax = gsh(a.argmax, o); a.x = gsh(a.x, o); gshift(a.bn, o); a.dx = gsh(a.dx, o);
   a.gsum = gsh(a.gsum, o); a.gsumx = gsh(a.gsumx, o); gshift(a.dyaff, o);
 }
 __device__ __forceinline__ void gshift(BnMovingDesc& a, long long o) {
-  if (!o) return;
+  // (no early return at o == 0: gsh also moves every pointer into the global address space)
   a.stats = gsh(a.stats, o); a.mmean = gsh(a.mmean, o); a.mvar = gsh(a.mvar, o); a.shift = gsh(a.shift, o);
 }
 __device__ __forceinline__ void gshift(ShiftDesc& a, long long o) {
-  if (!o) return;
+  // (no early return at o == 0: gsh also moves every pointer into the global address space)
   a.stats = gsh(a.stats, o); a.shift = gsh(a.shift, o);
 }
 __device__ __forceinline__ void gshift(HeadArgs& a, long long o) {
-  if (!o) return;
+  // (no early return at o == 0: gsh also moves every pointer into the global address space)
   a.x = gsh(a.x, o); gshift(a.pro, o); a.w = gsh(a.w, o); a.b = gsh(a.b, o); a.labels = gsh(a.labels, o);
   a.logits = gsh(a.logits, o); a.feats = gsh(a.feats, o); a.dlogits = gsh(a.dlogits, o); a.loss = gsh(a.loss, o);
 }
 __device__ __forceinline__ void gshift(HeadBwdArgs& a, long long o) {
-  if (!o) return;
+  // (no early return at o == 0: gsh also moves every pointer into the global address space)
   a.feats = gsh(a.feats, o); a.dlogits = gsh(a.dlogits, o); a.w = gsh(a.w, o); a.dw = gsh(a.dw, o);
   a.db = gsh(a.db, o); a.dA = gsh(a.dA, o);
 }
 __device__ __forceinline__ void gshift(CastEntry& a, long long o) {
-  if (!o) return;
+  // (no early return at o == 0: gsh also moves every pointer into the global address space)
   a.src = gsh(a.src, o); a.fwd = gsh(a.fwd, o); a.dgrad = gsh(a.dgrad, o);
 }
 

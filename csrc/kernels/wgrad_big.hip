@@ -105,7 +105,8 @@ __global__ __launch_bounds__(512) void wgrad_big_kernel(WgradArgs a, GroupArg ga
   constexpr int NW = C::NW, TM = C::TM, TN = C::TN, NGA = C::NGA, NGG = C::NGG;
   extern __shared__ __attribute__((aligned(16))) char smem[];
 
-  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform: scalar branches on it
   const int wr = wid / C::WN, wc = wid % C::WN;
   const int M = a.N * a.Ho * a.Wo;
   const int K = a.KH * a.KW * a.Cin;

@@ -84,6 +84,8 @@ enum OpKind : int {
   OP_WGRAD_BATCH = 27,
   // persistent dense-stage forward (dense_stage.hip): payload DenseStageArgs, i[0] = grid
   OP_DENSE_STAGE = 28,
+  // persistent dense-stage backward (dense_stage_bwd.hip): payload DenseBwdArgs, i[0] = grid
+  OP_DENSE_STAGE_BWD = 29,
 };
 
 struct Op {
@@ -438,9 +440,10 @@ class Plan {
                                   "pool_bwd", "bn_moving", "head_fwd", "head_bwd", "rmsprop", "cast",
                                   "input", "memset", "bn_stats", "bn_apply", "dw_fwd", "dw_bwd_data",
                                   "dw_wgrad", "copy", "finite_check", "mlp_fwd", "mlp_bwd", "mlp_step",
-                                  "collapse", "stats_shift", "allreduce", "wgrad_batch", "dense_stage"};
+                                  "collapse", "stats_shift", "allreduce", "wgrad_batch", "dense_stage",
+                                  "dense_stage_bwd"};
     int k = ops_.at(idx).kind;
-    return (k >= 0 && k < 29) ? names[k] : "?";
+    return (k >= 0 && k < (int)(sizeof(names) / sizeof(names[0]))) ? names[k] : "?";
   }
 
  private:
@@ -630,6 +633,7 @@ class Plan {
               "wgrad_batch");
         break;
       case OP_DENSE_STAGE: check(dense_stage_fwd(as<DenseStageArgs>(op), op.i[0], st), "dense_stage_fwd"); break;
+      case OP_DENSE_STAGE_BWD: check(dense_stage_bwd(as<DenseBwdArgs>(op), op.i[0], st), "dense_stage_bwd"); break;
       case OP_STATS_SHIFT:
         check(stats_shift(reinterpret_cast<const ShiftDesc*>(op.p[0]), op.i[0], op.i[1], st), "stats_shift");
         break;
@@ -739,6 +743,9 @@ py::dict struct_sizes() {
   d["ShiftDesc"] = sizeof(ShiftDesc);
   d["DenseStageArgs"] = sizeof(DenseStageArgs);
   d["DenseLayerDesc"] = sizeof(DenseLayerDesc);
+  d["DenseBwdArgs"] = sizeof(DenseBwdArgs);
+  d["DenseBwdLayerDesc"] = sizeof(DenseBwdLayerDesc);
+  d["DenseBwdPhase"] = sizeof(DenseBwdPhase);
   d["BnArgs.shift"] = offsetof(BnArgs, shift);
   d["ConvArgs.stats_shift"] = offsetof(ConvArgs, stats_shift);
   d["PoolArgs.stats_shift"] = offsetof(PoolArgs, stats_shift);
@@ -772,13 +779,6 @@ py::dict struct_sizes() {
 
 int py_pick_tile(int M, int Cout) { return conv_pick_tile(M, Cout); }
 
-bool py_halo_ok(py::bytes payload) {
-  std::string s = payload;
-  if (s.size() != sizeof(ConvArgs)) throw std::runtime_error("ConvArgs size mismatch");
-  ConvArgs a;
-  std::memcpy(&a, s.data(), sizeof(a));
-  return conv3x3_halo_ok(a);
-}
 bool py_big_ok(py::bytes payload, int a_f32) {
   std::string s = payload;
   if (s.size() != sizeof(ConvArgs)) throw std::runtime_error("ConvArgs size mismatch");
@@ -787,13 +787,6 @@ bool py_big_ok(py::bytes payload, int a_f32) {
   return conv_big_ok(a, a_f32 != 0);
 }
 int py_pick_splits(int M, int K, int Cout) { return wgrad_pick_splits(M, K, Cout); }
-bool py_ring_ok(py::bytes payload, int a_f32) {
-  std::string s = payload;
-  if (s.size() != sizeof(ConvArgs)) throw std::runtime_error("ConvArgs size mismatch");
-  ConvArgs a;
-  std::memcpy(&a, s.data(), sizeof(a));
-  return conv_ring_ok(a, a_f32 != 0);
-}
 
 int py_effective_splits(py::bytes payload, int splits) {
   std::string s = payload;
@@ -970,18 +963,13 @@ PYBIND11_MODULE(_idc_native, m) {
   m.def("wgrad_num_variants", &wgrad_num_variants);
   m.def("struct_sizes", &struct_sizes);
   m.def("pick_tile", &py_pick_tile);
-  m.def("halo_ok", &py_halo_ok);
   m.def("dw_wgrad_ws_floats", &dwconv_wgrad_ws_floats);
-  m.attr("TILE_HALO") = TILE_HALO;
   m.def("big_ok", &py_big_ok);
   m.attr("TILE_BIG128") = TILE_BIG128;
   m.attr("TILE_BIG256") = TILE_BIG256;
   m.attr("TILE_BIG64") = TILE_BIG64;
   m.attr("TILE_BIG128D") = TILE_BIG128D;
   m.def("pick_splits", &py_pick_splits);
-  m.def("ring_ok", &py_ring_ok);
-  m.attr("TILE_RING") = TILE_RING;
-  m.attr("TILE_RING_N") = TILE_RING_N;
   m.def("effective_splits", &py_effective_splits);
   m.def("wgrad_batch_sig", &py_wgrad_batch_sig);
   m.def("wgrad_batch_pack", &py_wgrad_batch_pack);
@@ -996,9 +984,22 @@ PYBIND11_MODULE(_idc_native, m) {
   m.def("secagg_unmask", &py_secagg_unmask);
   m.attr("OP_CONV") = (int)OP_CONV;
   m.attr("OP_DENSE_STAGE") = (int)OP_DENSE_STAGE;
+  m.attr("OP_DENSE_STAGE_BWD") = (int)OP_DENSE_STAGE_BWD;
+  m.attr("DSB_KG") = DSB_KG;
+  m.attr("DSB_MAX_CG") = DSB_MAX_CG;
+  m.def("dsb_sync_words", &dsb_sync_words);
+  m.attr("DS_SLOTS") = DS_SLOTS;
   m.def("dense_stage_tasks", [](py::bytes payload) {
     std::string s = payload;
     if (s.size() != sizeof(DenseStageArgs)) throw std::runtime_error("dense_stage_tasks: bad payload");
     return dense_stage_tasks(*reinterpret_cast<const DenseStageArgs*>(s.data()));
   });
+  m.def("dense_stage_phase_tiles", [](int M) {
+    int nA, nB;
+    dense_stage_phase_tiles(M, nA, nB);
+    return py::make_tuple(nA, nB);
+  });
+  m.def("dense_stage_shape_ok", &dense_stage_shape_ok);
+  m.attr("DS_SCRATCH_PER_LAYER") = DS_SCRATCH_PER_LAYER;
+  m.attr("DS_MAX_CIN") = DS_MAX_CIN;
 }

@@ -141,8 +141,28 @@ class DenseLayerDesc(C.Structure):
 
 class DenseStageArgs(C.Structure):
     _fields_ = [("buf", vp), ("sstats", vp), ("sshift", vp), ("layers", vp), ("sync", vp), ("err", vp),
+                ("scratch", vp), ("stamps", vp),
                 ("N", ci), ("H", ci), ("W", ci), ("ld", ci), ("nlayers", ci), ("k2", ci),
-                ("act1", ci), ("act2", ci), ("inv_count", cf), ("coh", ci)]
+                ("act1", ci), ("act2", ci), ("inv_count", cf), ("max_polls", C.c_uint)]
+
+
+class DenseBwdLayerDesc(C.Structure):
+    """One dense layer of a persistent dense-stage backward launch (dense_stage.h)."""
+    _fields_ = [(n, vp) for n in ("w1d", "w2d", "g1", "b1", "g2", "b2", "t", "tstats", "tshift", "dO16", "dt",
+                                  "dbeta1", "dgamma1", "dbeta2", "dgamma2", "r1", "r2")] + \
+               [("eps1", cf), ("eps2", cf), ("cin", ci), ("pad_", ci)]
+
+
+class DenseBwdPhase(C.Structure):
+    _fields_ = [("first", ci), ("kind", ci), ("layer", ci), ("tiles", ci)]
+
+
+class DenseBwdArgs(C.Structure):
+    _fields_ = [(n, vp) for n in ("buf", "sstats", "sshift", "dbuf", "dnew", "dx16", "z2")] + \
+               [("pend", BwdAff)] + \
+               [(n, vp) for n in ("layers", "phases", "sync", "btot", "err", "stamps")] + \
+               [(n, ci) for n in ("N", "H", "W", "ld", "c0", "nlayers", "k2", "act", "nphases", "ntickets")] + \
+               [("inv_count", cf), ("max_polls", C.c_uint)]
 
 
 _STRUCTS = {"BnArgs": BnArgs, "BwdAff": BwdAff, "ConvArgs": ConvArgs, "WgradArgs": WgradArgs,
@@ -151,7 +171,8 @@ _STRUCTS = {"BnArgs": BnArgs, "BwdAff": BwdAff, "ConvArgs": ConvArgs, "WgradArgs
             "PoolArgs": PoolArgs, "PoolBwdArgs": PoolBwdArgs, "BnMovingDesc": BnMovingDesc,
             "HeadArgs": HeadArgs, "HeadBwdArgs": HeadBwdArgs, "CastEntry": CastEntry,
             "DwArgs": DwArgs, "Mlp2Args": Mlp2Args, "ShiftDesc": ShiftDesc,
-            "DenseStageArgs": DenseStageArgs, "DenseLayerDesc": DenseLayerDesc}
+            "DenseStageArgs": DenseStageArgs, "DenseLayerDesc": DenseLayerDesc,
+            "DenseBwdArgs": DenseBwdArgs, "DenseBwdLayerDesc": DenseBwdLayerDesc, "DenseBwdPhase": DenseBwdPhase}
 
 # op kinds (csrc/runtime/plan.cpp)
 OP_CONV, OP_WGRAD, OP_BN_BWD_APPLY, OP_BN_BWD_REDUCE, OP_MAXPOOL, OP_AVGPOOL, OP_POOL_BWD = range(7)
@@ -159,6 +180,7 @@ OP_BN_MOVING, OP_HEAD_FWD, OP_HEAD_BWD, OP_RMSPROP, OP_CAST, OP_INPUT, OP_MEMSET
 OP_BN_STATS, OP_BN_APPLY, OP_DW_FWD, OP_DW_BWD_DATA, OP_DW_WGRAD, OP_COPY, OP_FINITE_CHECK = range(14, 21)
 OP_MLP_FWD, OP_MLP_BWD, OP_MLP_STEP, OP_COLLAPSE, OP_STATS_SHIFT, OP_ALLREDUCE, OP_WGRAD_BATCH = range(21, 28)
 OP_DENSE_STAGE = 28
+OP_DENSE_STAGE_BWD = 29
 
 ACT = {None: 0, "none": 0, "linear": 0, "relu": 1, "relu6": 2}
 OUT_BF16, OUT_F32, OUT_F32_ACC = 0, 1, 2

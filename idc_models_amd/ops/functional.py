@@ -428,15 +428,19 @@ def bn_moments(stats: torch.Tensor, count: int, shift: Optional[torch.Tensor] = 
 
 
 def dense_stage(buf: torch.Tensor, sstats: torch.Tensor, layers, sshift: Optional[torch.Tensor] = None,
-                act: int = RELU, grid: int = 256, k2: int = 3, coherent: int = 0):
+                act: int = RELU, grid: int = 256, k2: int = 3, max_polls: int = 0, stamps: bool = False):
     """All dense layers of a DenseNet stage in one persistent launch (csrc/kernels/dense_stage.hip).
 
     ``buf``: NHWC bf16 stage buffer [N, H, W, ld] whose channels [0, c0) are filled and whose
     ``sstats`` ([2*ld] fp32, shifted by ``sshift``) hold their statistics; ``layers``: dicts with
     w1 ([128][cin] bf16 kernel layout), w2 ([32][k2][k2][128] bf16), g1, b1 ([cin]), g2, b2 ([128]),
     t ([N,H,W,128] bf16 output), tstats ([256] zeroed fp32), tshift ([128] or None), eps1, eps2, cin.
-    Returns (sync counters, err flag) for inspection."""
+    ``max_polls``: bound on each wait (0: the kernel's default; tests force timeouts with 1).
+    Returns (sync counters, err counter, stamps or None) for inspection."""
     N, H, W, ld = buf.shape
+    ext = nat.require()
+    if max(L["cin"] for L in layers) > int(ext.DS_MAX_CIN) or not ext.dense_stage_shape_ok(N, H, W, 0):
+        raise ValueError("dense_stage: shape outside the persistent launch's limits")
     arr = (nat.DenseLayerDesc * len(layers))()
     for d, L in zip(arr, layers):
         d.w1, d.w2 = L["w1"].data_ptr(), L["w2"].data_ptr()
@@ -446,15 +450,104 @@ def dense_stage(buf: torch.Tensor, sstats: torch.Tensor, layers, sshift: Optiona
     import ctypes
     tab = torch.frombuffer(bytearray(ctypes.string_at(ctypes.addressof(arr), ctypes.sizeof(arr))),
                            dtype=torch.uint8).to(buf.device)
-    sync = torch.zeros(2 + 2 * len(layers), dtype=torch.int32, device=buf.device)
+    sync = torch.zeros(3 + 16 * len(layers), dtype=torch.int32, device=buf.device)
     err = torch.zeros(1, dtype=torch.int32, device=buf.device)
+    scratch = torch.zeros(int(ext.DS_SCRATCH_PER_LAYER) * len(layers), dtype=torch.float32, device=buf.device)
     a = nat.DenseStageArgs()
     a.buf, a.sstats, a.sshift = buf.data_ptr(), sstats.data_ptr(), nat.ptr(sshift)
     a.layers, a.sync, a.err = tab.data_ptr(), sync.data_ptr(), err.data_ptr()
+    a.scratch = scratch.data_ptr()
     a.N, a.H, a.W, a.ld, a.nlayers, a.k2 = N, H, W, ld, len(layers), k2
     a.act1 = a.act2 = act
     a.inv_count = 1.0 / float(N * H * W)
-    a.coh = coherent
+    a.max_polls = max_polls
+    st = None
+    if stamps:
+        st = torch.zeros(8 * int(ext.dense_stage_tasks(nat.raw(a))), dtype=torch.int64, device=buf.device)
+        a.stamps = st.data_ptr()
     _plan1(nat.OP_DENSE_STAGE, a, ints=(grid, len(layers)), ptrs=(tab.data_ptr(),))
     torch.cuda.current_stream().synchronize()
-    return sync, err
+    return sync, err, st
+
+
+def dense_bwd_queue(L: int, nmt: int, c0: int, kg: int):
+    """Work queue of a persistent dense-stage backward launch (dense_stage_bwd.hip), in ticket
+    order: (first ticket, kind, layer, tiles).  Kinds: 1 P, 2 QN, 3 G, 4 GIN, 5 FIN1, 6 FIN2."""
+    ph = []
+
+    def add(kind, layer, tiles):
+        ph.append((ph[-1][0] + ph[-1][3] if ph else 0, kind, layer, tiles))
+
+    ncg = c0 // 32
+    for l in range(L - 1, -1, -1):
+        add(1, l, nmt)
+        add(2, l, nmt)
+        if l >= 2:
+            add(3, l - 2, nmt * -(-(L - l) // kg))
+        if l == 1:
+            add(4, 0, nmt * ncg * -(-(L - 1) // kg))
+    add(5, 0, nmt * ncg)
+    add(6, 0, nmt * -(-c0 // 64))
+    return ph
+
+
+def dense_stage_bwd(buf: torch.Tensor, sstats: torch.Tensor, layers, dbuf: torch.Tensor, pend: nat.BwdAff,
+                    sshift: Optional[torch.Tensor] = None, act: int = RELU, grid: int = 256, k2: int = 3,
+                    max_polls: int = 0):
+    """Data gradients of all dense layers of a DenseNet stage in one persistent launch
+    (csrc/kernels/dense_stage_bwd.hip).
+
+    ``buf`` / ``sstats`` / ``sshift``: the forward stage buffer [N,H,W,ld] (bf16) and its shifted
+    statistics; ``dbuf``: fp32 [N,H,W,ld], A*dZ of the stage's consumer BatchNorm (updated in place);
+    ``pend``: that BatchNorm's pending backward affine (``bwd_aff(buf, ..., unit_alpha=True)``);
+    ``layers``: dicts with w1d ([cin][128] bf16), w2d ([128][k2][k2][32] bf16, flipped), g1, b1,
+    g2, b2, t ([N,H,W,128] bf16), tstats, tshift, eps1, eps2, cin, and outputs dO16 ([N,H,W,32]
+    bf16), dt ([N,H,W,128] bf16), dbeta1 / dgamma1 ([cin]), dbeta2 / dgamma2 ([128]).
+    Returns (dx16 [N,H,W,c0] bf16, sync counters, err counter)."""
+    ext = nat.require()
+    N, H, W, ld = buf.shape
+    M = N * H * W
+    L = len(layers)
+    c0 = layers[0]["cin"]
+    S = int(ext.DS_SLOTS)
+    nmt = -(-M // 32)
+    dev = buf.device
+    arr = (nat.DenseBwdLayerDesc * L)()
+    keep = []
+    for d, Ly in zip(arr, layers):
+        cin = Ly["cin"]
+        for k in ("w1d", "w2d", "g1", "b1", "g2", "b2", "t", "tstats", "dO16", "dt", "dbeta1", "dgamma1",
+                  "dbeta2", "dgamma2"):
+            setattr(d, k, Ly[k].data_ptr())
+        d.tshift = nat.ptr(Ly.get("tshift"))
+        r1 = torch.zeros(S * 2 * cin, device=dev)
+        r2 = torch.zeros(S * 256, device=dev)
+        keep += [r1, r2]
+        d.r1, d.r2 = r1.data_ptr(), r2.data_ptr()
+        d.eps1, d.eps2, d.cin = Ly["eps1"], Ly["eps2"], cin
+    ph = dense_bwd_queue(L, nmt, c0, int(ext.DSB_KG))
+    parr = (nat.DenseBwdPhase * len(ph))(*[nat.DenseBwdPhase(*p) for p in ph])
+    import ctypes
+    blob = ctypes.string_at(ctypes.addressof(arr), ctypes.sizeof(arr)) + \
+        ctypes.string_at(ctypes.addressof(parr), ctypes.sizeof(parr))
+    tab = torch.frombuffer(bytearray(blob), dtype=torch.uint8).to(dev)
+    sync = torch.zeros(int(ext.dsb_sync_words(L)), dtype=torch.int32, device=dev)
+    err = torch.zeros(1, dtype=torch.int32, device=dev)
+    btot = torch.zeros(2 * ld, device=dev)
+    dnew = torch.zeros(2 * M * 32, device=dev)
+    z2 = torch.zeros(M * 128, dtype=torch.bfloat16, device=dev)
+    dx16 = torch.zeros(N, H, W, c0, dtype=torch.bfloat16, device=dev)
+    a = nat.DenseBwdArgs()
+    a.buf, a.sstats, a.sshift = buf.data_ptr(), sstats.data_ptr(), nat.ptr(sshift)
+    a.dbuf, a.dnew, a.dx16, a.z2 = dbuf.data_ptr(), dnew.data_ptr(), dx16.data_ptr(), z2.data_ptr()
+    a.pend = pend
+    a.layers, a.phases = tab.data_ptr(), tab.data_ptr() + ctypes.sizeof(arr)
+    a.sync, a.btot, a.err = sync.data_ptr(), btot.data_ptr(), err.data_ptr()
+    a.N, a.H, a.W, a.ld, a.c0, a.nlayers = N, H, W, ld, c0, L
+    a.k2, a.act, a.nphases, a.ntickets = k2, act, len(ph), ph[-1][0] + ph[-1][3]
+    a.inv_count = 1.0 / float(M)
+    a.max_polls = max_polls
+    _plan1(nat.OP_DENSE_STAGE_BWD, a, ints=(grid, L), ptrs=(tab.data_ptr(),))
+    torch.cuda.current_stream().synchronize()
+    del keep
+    return dx16, sync, err

@@ -73,7 +73,7 @@ def _time_op(plan, i, stream, reps=4) -> float:
     return e0.elapsed_time(e1) / reps
 
 
-def _conv_candidates(ext, M: int, cout: int, payload: bytes = None, halo: bool = False, a_f32: int = 0):
+def _conv_candidates(ext, M: int, cout: int, payload: bytes = None, a_f32: int = 0):
     ntile = ext.num_tiles()
     cap = 32 if cout <= 32 else (64 if cout <= 64 else 128)
     out = []
@@ -87,15 +87,6 @@ def _conv_candidates(ext, M: int, cout: int, payload: bytes = None, halo: bool =
         if bm > 64 and M <= 2 * 64:
             continue
         out.append(t)
-    if payload is not None and (halo or os.environ.get("IDC_HALO", "0") == "1") and ext.halo_ok(payload):
-        out.append(ext.TILE_HALO)
-    # deep-ring LDS-DMA small tiles (conv_ring.hip): forward convs with a bf16 operand
-    # (opt-in: measured 20-100 % slower than the best general tile on every DenseNet-121 forward
-    # shape, tools/bench_ring.py)
-    if payload is not None and os.environ.get("IDC_CONV_RING", "0") == "1" and ext.ring_ok(payload, a_f32):
-        for v, bn in ((0, 32), (1, 64), (2, 32), (3, 64), (4, 128)):
-            if bn <= cap:
-                out.append(ext.TILE_RING + v)
     # 256 x {128, 256} global_load_lds tiles for plain wide layers (conv_big.hip), when they
     # still make >= 128 workgroups
     if payload is not None and os.environ.get("IDC_CONV_BIG", "1") != "0" and ext.big_ok(payload, a_f32):
@@ -106,7 +97,7 @@ def _conv_candidates(ext, M: int, cout: int, payload: bytes = None, halo: bool =
 
 
 def _tile_shape(ext, t: int):
-    """(BM, BN, BK) of conv tile ``t``; None for the halo kernel (no split-K)."""
+    """(BM, BN, BK) of conv tile ``t``; None for a tile id outside the tables."""
     if t in (ext.TILE_BIG128, ext.TILE_BIG128D):
         return 256, 128, 64
     if t == ext.TILE_BIG256:
@@ -134,16 +125,9 @@ def _splits_for(ext, a, t: int, M: int, slab_floats: int):
     return [s for s in (2, 4, 8) if tiles * s * bm * bn <= slab_floats and nk >= 2 * s]
 
 
-def _autotune_plan_unlocked(plan, stream, verbose: bool = False, reset_tickets=None, slab_floats: int = 0,
-                  halo_ops=()) -> int:
+def _autotune_plan_unlocked(plan, stream, verbose: bool = False, reset_tickets=None, slab_floats: int = 0) -> int:
     """Tune every conv / wgrad op of ``plan`` in place: tile shape, then the split-K factor of the
-    best few tiles (ops whose payload carries a split-K workspace).  Returns the number tuned.
-
-    ``halo_ops``: op indices that may also use the direct 3x3 halo kernel (conv3x3_halo.hip).  The
-    program passes its forward segment: there no side-lane kernel competes for LDS, so the
-    isolated timing is the in-situ one (in the backward the halo kernel's 90-150 KB LDS footprint
-    starves the concurrent weight-gradient kernels)."""
-    halo_ops = set(halo_ops)
+    best few tiles (ops whose payload carries a split-K workspace).  Returns the number tuned."""
     _load_cache()
     ext = nat.load()
     n = 0
@@ -155,12 +139,12 @@ def _autotune_plan_unlocked(plan, stream, verbose: bool = False, reset_tickets=N
             M = a.N * a.Ho * a.Wo
             pro = 2 if a.bpro.mode != 0 else int(a.pro.mode != 0 or a.pro.act != 0)
             key = ("conv", M, a.Cout, a.Cin, a.KH, a.KW, a.SH, a.PT, a.ldx, f32, pro, a.epi_mode,
-                   a.out_mode, int(bool(a.bias)), a.H, a.W, int(i in halo_ops))
+                   a.out_mode, int(bool(a.bias)), a.H, a.W)
             best = _CACHE.get(key)
             if best is None:
                 times = {}
                 plan.set_int(i, 2, 1)
-                for t in _conv_candidates(ext, M, a.Cout, plan.payload(i), i in halo_ops, f32) or [ext.pick_tile(M, a.Cout)]:
+                for t in _conv_candidates(ext, M, a.Cout, plan.payload(i), f32) or [ext.pick_tile(M, a.Cout)]:
                     plan.set_int(i, 0, t)
                     times[(t, 1)] = _time_op(plan, i, stream)
                 if a.slab and a.tickets and reset_tickets is not None and \

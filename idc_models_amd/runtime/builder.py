@@ -143,9 +143,6 @@ class Builder:
         self.segment = "fwd"
         self.side_lane = os.environ.get("IDC_SIDE_LANE", "1") != "0"
         self.guard = os.environ.get("IDC_GUARD") == "1"
-        # direct 3x3 kernel (conv3x3_halo.hip): opt-in — ~25% faster per kernel in isolation, but
-        # its 90-150 KB LDS footprint blocks the side-lane wgrads from sharing CUs (net loss)
-        self.use_halo = os.environ.get("IDC_HALO", "0") == "1"
         # statistics slots (stat_slots_for): opt-in (IDC_STAT_SLOTS=1).  Spreading the per-channel
         # adds over copies paid while the statistics were plain sums; with the shifted statistics,
         # the batched table loads and the consumer-applied BN backward, single-copy reductions
@@ -164,7 +161,9 @@ class Builder:
         self.bwd_marks: List[Tuple[int, int]] = []  # (op index, lowest arena param index ready)
         # stats arena is allocated lazily with a generous capacity; views are handed out in order
         # (the deterministic mode's per-workgroup private slots need ~10-40x more)
-        self._stats_cap = (1 << 25) if self.det else (1 << 20)
+        # (only the used prefix is cleared each step, so the capacity itself costs nothing per step;
+        # the persistent dense-stage launches keep their statistics slots here too)
+        self._stats_cap = (1 << 25) if self.det else (1 << 23)
         self.stats_arena = torch.zeros(self._stats_cap, dtype=F32, device=device)
         self.all_stats: List[Stats] = []
         # shifted statistics (IDC_STATS_SHIFT=0: plain E[y^2] - E[y]^2, for comparisons)
@@ -527,10 +526,7 @@ class Builder:
             t.zero_()
 
     def _default_tile(self, a, M: int, cout: int) -> int:
-        ext = nat.load()
-        if self.use_halo and ext.halo_ok(nat.raw(a)):
-            return ext.TILE_HALO
-        return ext.pick_tile(M, cout)
+        return nat.load().pick_tile(M, cout)
 
     def dgrad(self, dy: Tensor4, layer, dx: Tensor4, *, pads=(0, 0), mx: Optional[Tensor4] = None,
               mbn: Optional[nat.BnArgs] = None, gsum=None, gsumx=None, gbn: Optional["BNRef"] = None,
@@ -673,20 +669,23 @@ class Builder:
     def dense_stage_ok(self, sbuf: Optional[Stats], layers, H: int, W: int) -> bool:
         """Whether the dense layers of one stage can run as ONE persistent launch
         (csrc/kernels/dense_stage.hip): training-mode BatchNorms on single-copy statistics,
-        1x1 inputs of <= 1024 channels in multiples of 32, 128-channel bottlenecks, 32 new channels
-        per layer, and no fixed-order (deterministic) reductions."""
+        1x1 inputs of <= DS_MAX_CIN (2,048) channels in multiples of 32 (DenseNet-121/169/201),
+        128-channel bottlenecks, 32 new channels per layer, maps whose 3x3 windows fit the
+        launch's staging rows, and no fixed-order (deterministic) reductions."""
         if os.environ.get("IDC_DENSE_STAGE", "1") == "0" or not self.training or self.det:
             return False
         if sbuf is None or sbuf.slots != 1:
             return False
+        ext = nat.load()
         for lay in layers:
             if lay["bn1"].mode != 1 or lay["bn2"].mode != 1 or lay["stt"].slots != 1:
                 return False
-            if lay["cin"] % 32 or lay["cin"] > 1024 or lay["cv1"].filters != 128 or lay["cv2"].filters != 32:
+            if lay["cin"] % 32 or lay["cin"] > int(ext.DS_MAX_CIN) or lay["cv1"].filters != 128 \
+                    or lay["cv2"].filters != 32:
                 return False
             if tuple(lay["cv2"].kernel_size) != (3, 3) or tuple(lay["cv1"].kernel_size) != (1, 1):
                 return False
-        return True
+        return bool(ext.dense_stage_shape_ok(self.B, H, W, max(lay["cin"] for lay in layers)))
 
     def dense_stage(self, buf: Tensor4, sbuf: Stats, layers, act: int):
         """Emit ONE persistent launch for the dense layers ``layers`` of a stage (dicts with cin,
@@ -708,20 +707,111 @@ class Builder:
         tab = host.to(self.device)
         self.keep.append(tab)
         if getattr(self, "dense_err", None) is None:
-            # sticky timeout flag of every dense-stage launch of this program (tests read it)
+            # count of dense-stage launches of this program that gave up on a wait (FusedProgram
+            # checks it under IDC_VALIDATE; tests read it)
             self.dense_err = self.alloc((4,), torch.int32)
-        sync = self._stats_floats(2 + 2 * len(layers))  # zeroed with the stats arena every step
+        ext = nat.load()
+        # counters and the in-launch statistics slots live in the stats arena: zeroed every step
+        sync = self._stats_floats(3 + 16 * len(layers))  # ticket, sharded phase counters, fail
+        scratch = self._stats_floats(int(ext.DS_SCRATCH_PER_LAYER) * len(layers))
         a = nat.DenseStageArgs()
         a.buf, a.sstats, a.sshift = buf.ptr, sbuf.ptr, sbuf.shift_ptr()
         a.layers, a.sync, a.err = tab.data_ptr(), sync.data_ptr(), self.dense_err.data_ptr()
+        a.scratch = scratch.data_ptr()
         a.N, a.H, a.W, a.ld, a.nlayers, a.k2 = buf.N, H, W, buf.ld, len(layers), 1 if center else 3
         a.act1 = a.act2 = act
         a.inv_count = 1.0 / float(buf.N * H * W)
-        # cross-workgroup hand-off (dense_stage.h): agent-coherent (sc1) stores and loads by default
-        # (no L2 writeback / invalidate per phase boundary); IDC_DS_COHERENT=0: release/acquire fences
-        a.coh = int(os.environ.get("IDC_DS_COHERENT", "3"))
+        a.max_polls = int(os.environ.get("IDC_DS_MAX_POLLS", "0"))
+        if os.environ.get("IDC_DS_STAMPS", "0") == "1":
+            # per-work-item s_memrealtime stamps (tools/dense_stamps.py reads them after a step)
+            stamps = self.alloc((8 * int(ext.dense_stage_tasks(nat.raw(a))),), torch.int64)
+            a.stamps = stamps.data_ptr()
+            self.dense_stamps = getattr(self, "dense_stamps", []) + [(stamps, len(layers), buf.N * H * W)]
         grid = int(os.environ.get("IDC_DS_GRID", "256"))
         self.emit(nat.OP_DENSE_STAGE, a, ints=(grid, len(layers)), ptrs=(tab.data_ptr(),))
+
+    def dense_stage_bwd_ok(self, buf: Tensor4, layers, pend: "BNRef") -> bool:
+        """Whether a stage's dense-layer backward can run as ONE persistent launch
+        (csrc/kernels/dense_stage_bwd.hip): every layer and BatchNorm trainable in batch mode, the
+        stage's consumer BatchNorm in batch mode with single-copy reductions, shapes within the
+        launch's limits, no fixed-order (deterministic) reductions."""
+        if os.environ.get("IDC_DENSE_STAGE_BWD", "1") == "0" or not self.training or self.det:
+            return False
+        if pend.mode != 1 or getattr(pend, "gsums", None) is None or pend.gsums[2] != 1 or pend.stats.slots != 1:
+            return False
+        ext = nat.load()
+        c0 = layers[0]["cin"]
+        if c0 % 32 or c0 <= 32 or c0 // 32 > int(ext.DSB_MAX_CG) or buf.ld % 8:
+            return False
+        for lay in layers:
+            for bn in (lay["bn1"], lay["bn2"]):
+                if bn.mode != 1 or bn.dbeta is None or bn.stats.slots != 1:
+                    return False
+            if lay["cin"] > int(ext.DS_MAX_CIN) or lay["cv1"].filters != 128 or lay["cv2"].filters != 32:
+                return False
+        return bool(ext.dense_stage_shape_ok(buf.N, buf.H, buf.W, max(lay["cin"] for lay in layers)))
+
+    def dense_stage_bwd(self, buf: Tensor4, sbuf: Stats, layers, pend: "BNRef", dbuf: Tensor4, act: int):
+        """Emit ONE persistent launch for the data gradients of a stage's dense layers (dicts as in
+        lower_densenet, each with its wgrad operand buffers ``dO16`` / ``dt`` allocated).  ``dbuf``
+        holds A*dZ of the stage's consumer BatchNorm ``pend`` on entry.  Returns the bf16 final
+        gradient of the stage input channels [0, c0) (the transition's / stem's operand)."""
+        ext = nat.load()
+        N, H, W = buf.N, buf.H, buf.W
+        M = N * H * W
+        L = len(layers)
+        c0 = layers[0]["cin"]
+        center = self.is_center_only(layers[0]["cv2"], H, W, (1, 1), (1, 1))
+        S = int(ext.DS_SLOTS)
+        nmt = -(-M // 32)
+        arr = (nat.DenseBwdLayerDesc * L)()
+        for d, lay in zip(arr, layers):
+            cin, bn1, bn2 = lay["cin"], lay["bn1"], lay["bn2"]
+            d.w1d = self.conv_weight(lay["cv1"], cin_pad=cin, need_dgrad=True)["dgrad"].data_ptr()
+            d.w2d = self.conv_weight(lay["cv2"], cin_pad=128, need_dgrad=True, center=center)["dgrad"].data_ptr()
+            d.g1, d.b1 = bn1.gamma.data_ptr(), bn1.beta.data_ptr()
+            d.g2, d.b2 = bn2.gamma.data_ptr(), bn2.beta.data_ptr()
+            d.t, d.tstats, d.tshift = lay["t"].ptr, lay["stt"].ptr, lay["stt"].shift_ptr()
+            d.dO16, d.dt = lay["dO16"].ptr, lay["dt"].ptr
+            d.dbeta1, d.dgamma1 = bn1.dbeta.data_ptr(), bn1.dgamma.data_ptr()
+            d.dbeta2, d.dgamma2 = bn2.dbeta.data_ptr(), bn2.dgamma.data_ptr()
+            d.r1 = self._stats_floats(S * 2 * cin).data_ptr()
+            d.r2 = self._stats_floats(S * 256).data_ptr()
+            d.eps1, d.eps2 = bn1.layer.epsilon, bn2.layer.epsilon
+            d.cin = cin
+        # work queue: for l = L-1 .. 0: P_l, QN_l, G_{l-2}, GIN (l == 1); FIN1; FIN2
+        from ..ops.functional import dense_bwd_queue
+        ph = dense_bwd_queue(L, nmt, c0, int(ext.DSB_KG))
+        parr = (nat.DenseBwdPhase * len(ph))(*[nat.DenseBwdPhase(*p) for p in ph])
+        ntickets = ph[-1][0] + ph[-1][3]
+        blob = C.string_at(C.addressof(arr), C.sizeof(arr)) + C.string_at(C.addressof(parr), C.sizeof(parr))
+        tab = torch.frombuffer(bytearray(blob), dtype=torch.uint8).to(self.device)
+        self.keep.append(tab)
+        if getattr(self, "dense_err", None) is None:
+            self.dense_err = self.alloc((4,), torch.int32)
+        sync = self._stats_floats(int(ext.dsb_sync_words(L)))
+        btot = self._stats_floats(2 * buf.ld)
+        dnew = self.alloc((2 * M * 32,), F32)
+        z2 = self.alloc((M * 128,), BF16)
+        dx16 = self.nhwc(N, H, W, c0)
+        a = nat.DenseBwdArgs()
+        a.buf, a.sstats, a.sshift = buf.ptr, sbuf.ptr, sbuf.shift_ptr()
+        a.dbuf, a.dnew, a.dx16, a.z2 = dbuf.ptr, dnew.data_ptr(), dx16.ptr, z2.data_ptr()
+        a.pend = self.bwd_aff(pend, buf, unit_alpha=True)
+        a.layers = tab.data_ptr()
+        a.phases = tab.data_ptr() + C.sizeof(arr)
+        a.sync, a.btot, a.err = sync.data_ptr(), btot.data_ptr(), self.dense_err.data_ptr()
+        a.N, a.H, a.W, a.ld, a.c0, a.nlayers = N, H, W, buf.ld, c0, L
+        a.k2, a.act, a.nphases, a.ntickets = 1 if center else 3, act, len(ph), ntickets
+        a.inv_count = 1.0 / float(M)
+        a.max_polls = int(os.environ.get("IDC_DS_MAX_POLLS", "0"))
+        if os.environ.get("IDC_DS_STAMPS", "0") == "1":
+            stamps = self.alloc((8 * ntickets,), torch.int64)
+            a.stamps = stamps.data_ptr()
+            self.dense_bwd_stamps = getattr(self, "dense_bwd_stamps", []) + [(stamps, ph, M)]
+        grid = int(os.environ.get("IDC_DS_GRID", "256"))
+        self.emit(nat.OP_DENSE_STAGE_BWD, a, ints=(grid, L), ptrs=(tab.data_ptr(),))
+        return dx16
 
     def bn_bwd_apply(self, dz: Tensor4, x: Tensor4, bn: BNRef, dst: Tensor4, accumulate: bool):
         a = nat.BnBwdApplyArgs()

@@ -158,13 +158,36 @@ def lower_densenet(b: Builder, net, U: int, input_dtype):
     # the stage issues them as one OP_WGRAD_BATCH per kernel shape that fills the GPU beside the
     # previous stage's data gradients (builder.flush_wgrad_batch).
     batch_maxm = int(os.environ.get("IDC_WG_BATCH_MAXM", "9216"))
+    # Late stages (M <= IDC_DENSE_STAGE_BWD_MAXM pixels, default 2304: stages 3-4 at bs 256) run the
+    # data gradients of all their dense layers as ONE persistent launch (builder.dense_stage_bwd,
+    # dense_stage_bwd.hip); it hands the stage input's final gradient (bf16) to the transition
+    bwd_maxm = int(os.environ.get("IDC_DENSE_STAGE_BWD_MAXM", "2304"))
     for si in range(len(stages) - 1, -1, -1):
         st = stages[si]
         buf = st["buf"]
         N, Hs, Ws = buf.N, st["H"], st["W"]
         wb = N * Hs * Ws <= batch_maxm
-        z2 = b.nhwc(N, Hs, Ws, 128)  # dZ of bn2, consumed by the next dgrad only
-        for lay in reversed(st["layers"]):
+        dx16 = None
+        lays = st["layers"]
+        if N * Hs * Ws <= bwd_maxm and fz.before(lays[0]["bn1"].layer) and \
+                all(fz.trainable(lay[k]) for lay in lays for k in ("cv1", "cv2")) and \
+                all(fz.trainable(lay[k].layer) for lay in lays for k in ("bn1", "bn2")) and \
+                b.dense_stage_bwd_ok(buf, lays, pend):
+            for lay in lays:
+                lay["dO16"] = b.nhwc(N, Hs, Ws, 32)
+                lay["dt"] = b.nhwc(N, Hs, Ws, 128)
+            dx16 = b.dense_stage_bwd(buf, st["stats"], lays, pend, dbuf, RELU)
+            for lay in lays:
+                b.wgrad(lay["t"], lay["cv2"], lay["dO16"], b.arena.grad_of(lay["cv2"].kernel), pads=(1, 1),
+                        pro=lay["bn2"].args(), lane=1, batch=wb)
+                b.wgrad(buf.slice(0, lay["cin"]), lay["cv1"], lay["dt"], b.arena.grad_of(lay["cv1"].kernel),
+                        pro=lay["bn1"].args(), lane=1, batch=wb)
+                b.mark_grads_ready([lay["cv2"].kernel, lay["cv1"].kernel, lay["bn2"].gamma, lay["bn2"].beta,
+                                    lay["bn1"].gamma, lay["bn1"].beta])
+            b.mark_grads_ready(pend_params())
+            pend = lays[0]["bn1"]
+        z2 = b.nhwc(N, Hs, Ws, 128) if dx16 is None else None  # dZ of bn2, consumed by the next dgrad
+        for lay in (reversed(st["layers"]) if dx16 is None else ()):
             cin, bn1, cv1, bn2, cv2, t = lay["cin"], lay["bn1"], lay["cv1"], lay["bn2"], lay["cv2"], lay["t"]
             dO = dbuf.slice(cin, 32)
             xO = buf.slice(cin, 32)
@@ -217,14 +240,21 @@ def lower_densenet(b: Builder, net, U: int, input_dtype):
         dO = dbuf.slice(0, c0)
         xO = buf.slice(0, c0)
         if not fz.before(cvt):
-            if fz.trainable(cvt):
+            if fz.trainable(cvt) and dx16 is not None:
+                b.wgrad(p, cvt, dx16, b.arena.grad_of(cvt.kernel), lane=1)
+            elif fz.trainable(cvt):
                 b.wgrad(p, cvt, dO, b.arena.grad_of(cvt.kernel), lane=1,
                         gpro=b.bwd_aff(pend, xO, unit_alpha=True))
             b.mark_grads_ready([cvt.kernel] + pend_params())
             return
         dp = b.nhwc(p.N, p.H, p.W, p.C)
-        dO16 = b.nhwc(N, Hs, Ws, c0)
-        b.dgrad(dO, cvt, dp, bpro=b.bwd_aff(pend, xO, unit_alpha=True, fold=True), aout=dO16)
+        if dx16 is not None:
+            # the persistent backward finished these channels' gradient (every pending affine included)
+            dO16 = dx16
+            b.dgrad(dO16, cvt, dp)
+        else:
+            dO16 = b.nhwc(N, Hs, Ws, c0)
+            b.dgrad(dO, cvt, dp, bpro=b.bwd_aff(pend, xO, unit_alpha=True, fold=True), aout=dO16)
         if fz.trainable(cvt):
             b.wgrad(p, cvt, dO16, b.arena.grad_of(cvt.kernel), lane=1)
         b.mark_grads_ready(pend_params())
@@ -243,8 +273,11 @@ def lower_densenet(b: Builder, net, U: int, input_dtype):
         return
     st0 = stages[0]
     zs = b.nhwc(B, H1, W1, 64)
-    b.pool_bwd(dbuf.slice(0, 64), zs, k=3, s=2, pt=1, pl=1, is_max=True, argmax=argmax, x=ys,
-               bn=bn_stem, dyaff=b.bwd_aff(pend, st0["buf"].slice(0, 64), unit_alpha=True, fold=True))
+    if dx16 is not None:  # stage 1 ran the persistent backward: its input gradient is final
+        b.pool_bwd(dx16, zs, k=3, s=2, pt=1, pl=1, is_max=True, argmax=argmax, x=ys, bn=bn_stem)
+    else:
+        b.pool_bwd(dbuf.slice(0, 64), zs, k=3, s=2, pt=1, pl=1, is_max=True, argmax=argmax, x=ys,
+                   bn=bn_stem, dyaff=b.bwd_aff(pend, st0["buf"].slice(0, 64), unit_alpha=True, fold=True))
     if fz.trainable(conv1):
         # the stem wgrad consumes the LAST main-lane op's output, so it can never overlap the
         # dgrad chain; on the main lane it starts at once and overlaps the side lane's backlog of

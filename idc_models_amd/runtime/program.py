@@ -231,11 +231,8 @@ class FusedProgram:
         # program keeps the fixed default tiles (and no split-K)
         if os.environ.get("IDC_AUTOTUNE", "1") != "0" and not b.det:
             from .autotune import autotune_plan
-            halo = ()
-            if "fwd" in self.seg and os.environ.get("IDC_HALO_FWD", "0") == "1":
-                halo = range(*self.seg["fwd"])
             autotune_plan(self.plan, self.stream, verbose=os.environ.get("IDC_TUNE_VERBOSE") == "1",
-                          reset_tickets=b.reset_tickets, slab_floats=b.SLAB_FLOATS, halo_ops=halo)
+                          reset_tickets=b.reset_tickets, slab_floats=b.SLAB_FLOATS)
         b.reset_tickets()  # split-K tickets count modulo the op's split: start every op aligned
 
     # ------------------------------------------------------------------ execution

@@ -150,55 +150,6 @@ def test_conv_prologue_bn_relu_and_stats(fn):
     assert relerr(stats_out[Cout:], (yf * yf).sum((0, 1, 2))) < 1e-3
 
 
-@pytest.mark.parametrize("H", [13, 6, 3, 1])
-def test_conv3x3_halo_fwd_bn_prologue_stats(fn, H):
-    """One-image-per-workgroup direct 3x3 kernel (DenseNet growth conv) == reference conv."""
-    N, Cin, Cout = 5, 128, 32
-    ext = fn.nat.require()
-    x = bf(torch.randn(N, H, H, Cin, device=DEV) * 2 + 0.5)
-    st = torch.cat([x.sum((0, 1, 2)), (x * x).sum((0, 1, 2))])
-    gamma = torch.rand(Cin, device=DEV) + 0.5
-    beta = torch.randn(Cin, device=DEV) * 0.1
-    w = bf(torch.randn(3, 3, Cin, Cout, device=DEV) * 0.05)
-    stats_out = torch.zeros(2 * Cout, device=DEV)
-    cnt = N * H * H
-    y = fn.conv2d(x.to(torch.bfloat16), w, pads=(1, 1), tile=ext.TILE_HALO, stats=stats_out,
-                  pro=fn.BN(stats=st, gamma=gamma, beta=beta, count=cnt, eps=1.001e-5, act=1))
-    ref = ref_conv(bf(bn_ref(x, st, gamma, beta, cnt, 1.001e-5, 1)), w, 1, (1, 1, 1, 1))
-    assert relerr(y, ref) < 1e-2
-    yf = y.float()
-    assert relerr(stats_out[:Cout], yf.sum((0, 1, 2))) < 1e-3
-    assert relerr(stats_out[Cout:], (yf * yf).sum((0, 1, 2))) < 1e-3
-
-
-@pytest.mark.parametrize("H", [13, 6, 3])
-def test_conv3x3_halo_dgrad_fp32_bn_epilogue(fn, H):
-    """dgrad of the growth conv from the fp32 concat gradient, BN-backward epilogue."""
-    N, Cin, Cout = 3, 128, 32
-    ext = fn.nat.require()
-    mx = bf(torch.randn(N, H, H, Cin, device=DEV))
-    st = torch.cat([mx.sum((0, 1, 2)), (mx * mx).sum((0, 1, 2))])
-    gamma = torch.rand(Cin, device=DEV) + 0.5
-    beta = torch.randn(Cin, device=DEV) * 0.1
-    cnt = N * H * H
-    dy = torch.randn(N, H, H, Cout, device=DEV)
-    w = bf(torch.randn(3, 3, Cin, Cout, device=DEV) * 0.1)
-    gsum = torch.zeros(Cin, device=DEV)
-    gsumx = torch.zeros(Cin, device=DEV)
-    dz = fn.conv2d_dgrad(dy, w, (H, H), pads=(1, 1), mx=mx.to(torch.bfloat16), tile=ext.TILE_HALO,
-                         mbn=fn.BN(stats=st, gamma=gamma, beta=beta, count=cnt, eps=1e-3, act=1),
-                         gsum=gsum, gsumx=gsumx)
-    dA = torch.nn.grad.conv2d_input((N, Cin, H, H), w.permute(3, 2, 0, 1), bf(dy).permute(0, 3, 1, 2),
-                                    padding=1).permute(0, 2, 3, 1)
-    mean = st[:Cin] / cnt
-    var = st[Cin:] / cnt - mean ** 2
-    xhat = (mx - mean) * torch.rsqrt(var + 1e-3)
-    dZ = dA * ((xhat * gamma + beta) > 0).float()
-    assert relerr(dz, dZ) < 1e-2
-    assert relerr(gsum, dZ.sum((0, 1, 2))) < 2e-2
-    assert relerr(gsumx, (dZ * xhat).sum((0, 1, 2))) < 2e-2
-
-
 def test_conv_fp32_operand(fn):
     N, H, Cin, Cout = 2, 13, 32, 128
     x = torch.randn(N, H, H, Cin, device=DEV)
@@ -740,47 +691,6 @@ def test_avgpool_bwd_scatter_bn_epilogue_f32(fn, H):
     assert relerr(gsumx, (dZ * xhat).sum((0, 1, 2))) < 2e-2
 
 
-@pytest.mark.parametrize("variant", range(5))
-@pytest.mark.parametrize("case", ["1x1_ktail_bn", "3x3_bn", "1x1_plain_bias"])
-def test_conv_ring_tiles_match_reference(fn, variant, case):
-    """Deep-ring LDS-DMA tiles (conv_ring.hip): 1x1 with a K tail (Cin = 544, DenseNet's 64+32k)
-    and 3x3 'same' (padding zero AFTER the activation), both through the pending-BN prologue with
-    shifted output statistics; and a plain 1x1 with bias + ReLU epilogue."""
-    from idc_models_amd.ops import _native as nat
-    tile = nat.load().TILE_RING + variant
-    g0 = torch.Generator(device="cpu").manual_seed(variant)
-    if case == "1x1_ktail_bn":
-        N, H, Cin, Cout, k, pads = 16, 6, 544, 128, 1, (0, 0)
-    elif case == "3x3_bn":
-        N, H, Cin, Cout, k, pads = 8, 13, 128, 32, 3, (1, 1)
-    else:
-        N, H, Cin, Cout, k, pads = 16, 9, 96, 64, 1, (0, 0)
-    x = bf(torch.randn(N, H, H, Cin, generator=g0).to(DEV) * 2 + 0.5)
-    w = bf(torch.randn(k, k, Cin, Cout, generator=g0).to(DEV) * (0.5 / (k * Cin ** 0.5)))
-    if case == "1x1_plain_bias":
-        bias = torch.randn(Cout, generator=g0).to(DEV) * 0.1
-        y = fn.conv2d(x.to(torch.bfloat16), w, pads=pads, bias=bias, act=1, tile=tile)
-        ref = torch.relu(ref_conv(x, w, 1, (0, 0, 0, 0)) + bias)
-        assert relerr(y.float(), ref) < 1e-2
-        return
-    st_in = torch.cat([x.sum((0, 1, 2)), (x * x).sum((0, 1, 2))])
-    g = torch.rand(Cin, generator=g0).to(DEV) + 0.5
-    be = torch.randn(Cin, generator=g0).to(DEV) * 0.1
-    bn = fn.BN(stats=st_in, gamma=g, beta=be, count=N * H * H, eps=1e-3, act=1)
-    mean = x.mean((0, 1, 2))
-    var = (x * x).mean((0, 1, 2)) - mean * mean
-    xa = torch.relu((x - mean) / torch.sqrt(var + 1e-3) * g + be)
-    ref = ref_conv(xa, w, 1, (pads[0], pads[0], pads[1], pads[1]))
-    shift = torch.randn(Cout, generator=g0).to(DEV) * 0.1
-    for _ in range(2):
-        st = torch.zeros(2 * Cout, device=DEV)
-        y = fn.conv2d(x.to(torch.bfloat16), w, pads=pads, pro=bn, tile=tile, stats=st, stats_shift=shift)
-        assert relerr(y.float(), ref) < 1e-2, case
-        yb = y.float()
-        assert relerr(st[:Cout], (yb - shift).sum((0, 1, 2))) < 1e-3
-        assert relerr(st[Cout:], ((yb - shift) ** 2).sum((0, 1, 2))) < 1e-3
-
-
 @pytest.mark.parametrize("N,H,Cin,Cout,k,s,pads", [
     (2, 25, 64, 128, 3, 1, (1, 1)),     # VGG block 2 conv 1: K = 576 (a partial 256-row k tile)
     (4, 12, 128, 256, 3, 1, (1, 1)),    # block 3
@@ -868,15 +778,17 @@ def test_wgrad_batch_matches_single_launches(fn, kind, N, H):
         assert relerr(o, r) < 1.5e-2
 
 
-@pytest.mark.parametrize("N,H,c0,L,grid,coh", [(4, 3, 64, 3, 256, 0), (6, 1, 96, 4, 7, 0), (3, 5, 32, 2, 1, 0),
-                                              (4, 3, 64, 3, 256, 3), (8, 6, 64, 3, 64, 3)])
-def test_dense_stage_persistent_matches_reference(fn, N, H, c0, L, grid, coh):
-    """The persistent dense-stage launch (work queue + per-phase completion counters) vs a PyTorch
-    fp32 reference of the same dense layers: BN1(shifted batch stats)->ReLU->1x1(128) stored bf16
-    with its shifted statistics, BN2->ReLU->3x3(32) (centre tap on 1x1 maps) into the stage buffer
-    slice with its statistics.  grid 7 / 1: far fewer workgroups than tiles (the queue must still
-    drain: every wait depends only on earlier tickets).  coh 3: the fence-free hand-off (agent-
-    coherent stores and loads)."""
+@pytest.mark.parametrize("N,H,c0,L,grid", [(4, 3, 64, 3, 256), (6, 1, 96, 4, 7), (3, 5, 32, 2, 1),
+                                          (8, 6, 64, 3, 64), (2, 1, 1120, 3, 256), (5, 2, 256, 4, 256)])
+def test_dense_stage_persistent_matches_reference(fn, N, H, c0, L, grid):
+    """The persistent dense-stage launch (work queue + per-phase completion counters, 1x1 partial
+    sums over the finished channels accumulated before the newest slice is waited for, slotted
+    in-launch statistics) vs a PyTorch fp32 reference of the same dense layers:
+    BN1(shifted batch stats)->ReLU->1x1(128) stored bf16 with its shifted statistics,
+    BN2->ReLU->3x3(32) (centre tap on 1x1 maps) into the stage buffer slice with its statistics.
+    grid 7 / 1: far fewer workgroups than tiles (the queue must still drain: every wait depends only
+    on earlier tickets).  c0 1120: DenseNet-201-wide inputs (cin > 1024, several 256-channel
+    staging chunks); 2x2 maps: DenseNet-201 @ 32x32's stage 3."""
     W = H
     ld = c0 + 32 * L
     g = torch.Generator(device="cpu").manual_seed(N * 100 + H)
@@ -927,11 +839,12 @@ def test_dense_stage_persistent_matches_reference(fn, N, H, c0, L, grid, coh):
         rst[ld + cin:ld + cin + 32] = (yk * yk).sum(0)
         rts.append(t)
         rtst.append(tst)
-    sync, err = fn.dense_stage(buf, sst, lays, sshift=K, grid=grid, k2=k2, coherent=coh)
+    sync, err, _ = fn.dense_stage(buf, sst, lays, sshift=K, grid=grid, k2=k2)
     M = N * H * W
-    nA, nB = -(-M // 32) * 2, -(-M // 16)
+    nA, nB = -(-M // 32) * 2, -(-M // 32)
     assert int(err[0].item()) == 0 and int(sync[-1].item()) == 0
-    assert sync[1:-1:2].tolist() == [nA] * L and sync[2:-1:2].tolist() == [nB] * L, sync.tolist()
+    cnt = sync[1:1 + 16 * L].reshape(L, 2, 8).sum(-1)  # per layer: A_l, B_l sharded counters
+    assert cnt[:, 0].tolist() == [nA] * L and cnt[:, 1].tolist() == [nB] * L, sync.tolist()
     errs = {}
     for i, d in enumerate(lays):
         errs[f"t{i}"] = relerr(d["t"].float(), rts[i])
@@ -939,3 +852,128 @@ def test_dense_stage_persistent_matches_reference(fn, N, H, c0, L, grid, coh):
     errs["buf"] = relerr(buf.float(), rbuf)
     errs["sst"] = relerr(sst, rst)
     assert all(v < 2e-2 for v in errs.values()), errs
+
+
+def test_dense_stage_timeout_is_counted(fn):
+    """A wait that gives up (poll bound forced to 1) fails the launch: every workgroup leaves and
+    the persistent error counter records it (dense_stage.hip wait_count)."""
+    N, H, c0, L = 64, 3, 64, 4
+    ld = c0 + 32 * L
+    buf = (torch.randn(N, H, H, ld, device=DEV) * 0.5).to(torch.bfloat16)
+    buf[..., c0:] = 0
+    x0 = buf[..., :c0].float().reshape(-1, c0)
+    sst = torch.zeros(2 * ld, device=DEV)
+    sst[:c0], sst[ld:ld + c0] = x0.sum(0), (x0 * x0).sum(0)
+    lays = []
+    for i in range(L):
+        cin = c0 + 32 * i
+        lays.append(dict(w1=torch.randn(128 * cin, device=DEV).to(torch.bfloat16) * 0.05,
+                         w2=torch.randn(32 * 9 * 128, device=DEV).to(torch.bfloat16) * 0.03,
+                         g1=torch.ones(cin, device=DEV), b1=torch.zeros(cin, device=DEV),
+                         g2=torch.ones(128, device=DEV), b2=torch.zeros(128, device=DEV),
+                         t=torch.zeros(N, H, H, 128, dtype=torch.bfloat16, device=DEV),
+                         tstats=torch.zeros(256, device=DEV), tshift=None, eps1=1e-5, eps2=1e-5, cin=cin))
+    sync, err, _ = fn.dense_stage(buf, sst, lays, grid=256, k2=3, max_polls=1)
+    assert int(sync[-1].item()) == 1 and int(err[0].item()) == 1, (sync.tolist(), err.tolist())
+    # the same launch with the default bound completes
+    sst2 = torch.zeros(2 * ld, device=DEV)
+    sst2[:c0], sst2[ld:ld + c0] = x0.sum(0), (x0 * x0).sum(0)
+    for d in lays:
+        d["tstats"].zero_()
+    sync, err, _ = fn.dense_stage(buf, sst2, lays, grid=256, k2=3)
+    assert int(sync[-1].item()) == 0 and int(err[0].item()) == 0
+
+
+def _bn_train(x, g, b, eps):
+    mean = x.mean((0, 1, 2))
+    var = x.var((0, 1, 2), unbiased=False)
+    return (x - mean) * torch.rsqrt(var + eps) * g + b
+
+
+@pytest.mark.parametrize("N,H,c0,L,grid", [(16, 3, 64, 3, 256), (64, 1, 96, 4, 256), (8, 3, 128, 2, 5),
+                                          (6, 2, 256, 3, 64), (4, 1, 1120, 2, 256), (64, 3, 256, 4, 256)])
+def test_dense_stage_bwd_matches_autograd(fn, N, H, c0, L, grid):
+    """The persistent dense-stage BACKWARD launch (dense_stage_bwd.hip: 3x3 dgrad, dT, newest-slice
+    and older-channel 1x1 dgrads, every BatchNorm backward through the summed pending affines,
+    d gamma / d beta) vs fp32 autograd of the same dense layers, forward values rounded to bf16
+    where the kernels store them (straight-through).  Upstream: a consumer BatchNorm + ReLU over the
+    whole stage buffer with a random output gradient (the transition / final BatchNorm of
+    lower_densenet).  grid 5: far fewer workgroups than tickets (queue order must still drain);
+    c0 1120: DenseNet-201-wide inputs; 1x1 maps: centre-tap 3x3."""
+    torch.manual_seed(N * 1000 + c0 + L)
+    W = H
+    ld = c0 + 32 * L
+    k2 = 1 if H == 1 else 3
+    eps = 1.001e-5
+
+    def rnd(v):  # round the value to bf16, gradient straight through
+        return v + (bf(v) - v).detach()
+
+    x0 = bf(torch.randn(N, H, W, c0, device=DEV) * 1.5 + 0.3).requires_grad_(True)
+    params, lays = [], []
+    for i in range(L):
+        cin = c0 + 32 * i
+        p = dict(W1=bf(torch.randn(1, 1, cin, 128, device=DEV) * (2.0 / cin) ** 0.5),
+                 W2=bf(torch.randn(3, 3, 128, 32, device=DEV) * (2.0 / 1152) ** 0.5),
+                 g1=(torch.rand(cin, device=DEV) + 0.5).requires_grad_(True),
+                 b1=(torch.randn(cin, device=DEV) * 0.1).requires_grad_(True),
+                 g2=(torch.rand(128, device=DEV) + 0.5).requires_grad_(True),
+                 b2=(torch.randn(128, device=DEV) * 0.1).requires_grad_(True))
+        params.append(p)
+    gc = torch.rand(ld, device=DEV) + 0.5
+    bc = torch.randn(ld, device=DEV) * 0.1
+    G = torch.randn(N, H, W, ld, device=DEV)
+    parts, ts, ys = [x0], [], []
+    for i, p in enumerate(params):
+        x = torch.cat(parts, -1)
+        a1 = rnd(torch.relu(_bn_train(x, p["g1"], p["b1"], eps)))
+        t = rnd(ref_conv(a1, p["W1"], 1, (0, 0, 0, 0)))
+        t.retain_grad()
+        a2 = rnd(torch.relu(_bn_train(t, p["g2"], p["b2"], eps)))
+        y = rnd(ref_conv(a2, p["W2"], 1, (1, 1, 1, 1)))
+        y.retain_grad()
+        ts.append(t)
+        ys.append(y)
+        parts.append(y)
+    xb = torch.cat(parts, -1)
+    zc = _bn_train(xb, gc, bc, eps)
+    (torch.relu(zc) * G).sum().backward()
+    # kernel inputs from the same forward values
+    cnt = N * H * W
+    buf = xb.detach().to(torch.bfloat16).contiguous()
+    xf = buf.float().reshape(-1, ld)
+    K = torch.randn(ld, device=DEV) * 0.2
+    sst = torch.cat([(xf - K).sum(0), ((xf - K) ** 2).sum(0)])
+    mean_c, var_c = xf.mean(0), xf.var(0, unbiased=False)
+    rstd_c = torch.rsqrt(var_c + eps)
+    zcv = ((xf - mean_c) * rstd_c * gc + bc)
+    dZc = G.reshape(-1, ld) * (zcv > 0).float()
+    xh_c = (xf - mean_c) * rstd_c
+    dbuf = (dZc * gc * rstd_c).reshape(N, H, W, ld).contiguous()
+    gsum, gsumx = dZc.sum(0), (dZc * xh_c).sum(0)
+    pend = fn.bwd_aff(buf, fn.BN(stats=sst, gamma=gc, beta=bc, count=cnt, eps=eps, shift=K, ld=ld),
+                      gsum=gsum, gsumx=gsumx, unit_alpha=True)
+    for i, p in enumerate(params):
+        cin = c0 + 32 * i
+        t = ts[i].detach().to(torch.bfloat16).contiguous()
+        tsh = torch.randn(128, device=DEV) * 0.1
+        tk = t.float().reshape(-1, 128) - tsh
+        w2 = p["W2"][1:2, 1:2] if k2 == 1 else p["W2"]
+        lays.append(dict(w1d=fn.weight_dgrad_layout(p["W1"]), w2d=fn.weight_dgrad_layout(w2),
+                         g1=p["g1"].detach(), b1=p["b1"].detach(), g2=p["g2"].detach(), b2=p["b2"].detach(),
+                         t=t, tstats=torch.cat([tk.sum(0), (tk * tk).sum(0)]), tshift=tsh, eps1=eps, eps2=eps,
+                         cin=cin, dO16=torch.zeros(N, H, W, 32, dtype=torch.bfloat16, device=DEV),
+                         dt=torch.zeros(N, H, W, 128, dtype=torch.bfloat16, device=DEV),
+                         dbeta1=torch.zeros(cin, device=DEV), dgamma1=torch.zeros(cin, device=DEV),
+                         dbeta2=torch.zeros(128, device=DEV), dgamma2=torch.zeros(128, device=DEV)))
+    dx16, sync, err = fn.dense_stage_bwd(buf, sst, lays, dbuf, pend, sshift=K, grid=grid, k2=k2)
+    assert int(err[0].item()) == 0 and int(sync[-1].item()) == 0, sync.tolist()
+    errs = {"dx": relerr(dx16, x0.grad)}
+    for i, (p, d) in enumerate(zip(params, lays)):
+        errs[f"dO{i}"] = relerr(d["dO16"], ys[i].grad)
+        errs[f"dt{i}"] = relerr(d["dt"], ts[i].grad)
+        errs[f"db2_{i}"] = relerr(d["dbeta2"], p["b2"].grad)
+        errs[f"dg2_{i}"] = relerr(d["dgamma2"], p["g2"].grad)
+        errs[f"db1_{i}"] = relerr(d["dbeta1"], p["b1"].grad)
+        errs[f"dg1_{i}"] = relerr(d["dgamma1"], p["g1"].grad)
+    assert all(v < 3e-2 for v in errs.values()), errs

@@ -42,7 +42,8 @@ STRUCTS = {nat.OP_CONV: nat.ConvArgs, nat.OP_WGRAD: nat.WgradArgs, nat.OP_BN_BWD
            nat.OP_AVGPOOL: nat.PoolArgs, nat.OP_POOL_BWD: nat.PoolBwdArgs, nat.OP_HEAD_FWD: nat.HeadArgs,
            nat.OP_HEAD_BWD: nat.HeadBwdArgs, nat.OP_DW_FWD: nat.DwArgs, nat.OP_DW_BWD_DATA: nat.DwArgs,
            nat.OP_DW_WGRAD: nat.DwArgs, nat.OP_BN_APPLY: nat.BnArgs, nat.OP_MLP_FWD: nat.Mlp2Args,
-           nat.OP_MLP_BWD: nat.Mlp2Args, nat.OP_DENSE_STAGE: nat.DenseStageArgs}
+           nat.OP_MLP_BWD: nat.Mlp2Args, nat.OP_DENSE_STAGE: nat.DenseStageArgs,
+           nat.OP_DENSE_STAGE_BWD: nat.DenseBwdArgs}
 
 
 def _pointers(obj, out):
@@ -159,3 +160,24 @@ def test_dense_stage_lowering(monkeypatch):
     assert count({"IDC_DENSE_STAGE": "1", "IDC_DETERMINISTIC": "1"})[0] == 0
     monkeypatch.delenv("IDC_DETERMINISTIC")
     assert count({"IDC_STAT_SLOTS": "1"})[0] == 2  # stage 3/4 rows (<= 4096) keep one copy
+
+
+def test_dense_stage_bwd_lowering(monkeypatch):
+    """The late stages' dense-layer data gradients lower to one OP_DENSE_STAGE_BWD each (stages 3
+    and 4 at bs 256; with fine_tune_at=150 stage 3 is partly frozen and keeps the per-layer
+    dgrads); the deterministic mode keeps the per-layer dgrads everywhere."""
+    def count(ft=None, **env):
+        for k, v in env.items():
+            monkeypatch.setenv(k, v)
+        _, _, b = _lower("densenet121", ft, True, B=256)
+        kinds = [k for (_, k, *_r) in b.ops]
+        for k in env:
+            monkeypatch.delenv(k)
+        return kinds.count(nat.OP_DENSE_STAGE_BWD), kinds.count(nat.OP_CONV)
+    n_on, conv_on = count()
+    n_off, conv_off = count(IDC_DENSE_STAGE_BWD="0")
+    assert (n_on, n_off) == (2, 0)
+    assert conv_off - conv_on == 2 * (24 + 16)  # two dgrads per dense layer of stages 3 and 4
+    assert count(150)[0] == 1
+    assert count(IDC_DETERMINISTIC="1")[0] == 0
+    assert count(IDC_DENSE_STAGE_BWD_MAXM="9216")[0] == 3  # stage 2 (6x6 maps) fits the launch too

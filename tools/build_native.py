@@ -32,13 +32,12 @@ SOURCES = [
     "kernels/conv_igemm_g3.hip",
     "kernels/conv_igemm_g4.hip",
     "kernels/conv_igemm_g5.hip",
-    "kernels/conv3x3_halo.hip",
     "kernels/conv_big.hip",
-    "kernels/conv_ring.hip",
     "kernels/conv_wgrad.hip", "kernels/wgrad_big.hip",
     "kernels/nn_kernels.hip",
     "kernels/dwconv.hip",
     "kernels/dense_stage.hip",
+    "kernels/dense_stage_bwd.hip",
     "kernels/mlp_head.hip",
     "kernels/secagg.hip",
     "comm/communicator.cpp",

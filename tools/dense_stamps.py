@@ -1,0 +1,135 @@
+"""Per-phase timing of the persistent dense-stage launches (csrc/kernels/dense_stage.hip forward,
+dense_stage_bwd.hip backward) from the kernels' own s_memrealtime stamps (IDC_DS_STAMPS=1: 8
+stamps per work item, 100 MHz clock; persist.h NSTAMP).
+
+    python tools/dense_stamps.py [--model densenet121] [--batch 256] [--steps 5] [--md out.md]
+
+Forward stamp points:
+  A (1x1):  0 ticket | 1 older slices ready (B_{l-2}) | 2 older-channel partial sums done |
+            3 newest slice ready (B_{l-1}) | 4 newest operands staged + MFMA | 5 tile in LDS |
+            6 stores + statistics issued | 7 published
+  B (3x3):  0 ticket | 1 weights issued | 2 t ready (A_l) | 3 operands staged | 4 MFMA done |
+            5 stores issued | 6 statistics issued | 7 published
+Backward (dense_stage_bwd.hip): 0 ticket | 1 dependencies ready | 2 operands staged | 3 before publish.
+
+For every phase it reports (us): the chain step (this phase's last publish - the previous phase's),
+the hand-off (first tile's dependency cleared - previous phase's last publish), and the median of
+every stamp-to-stamp interval over the phase's tiles.
+"""
+from __future__ import annotations
+
+import argparse
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+NSTAMP = 8
+
+
+def _phase_rows(a, spans, ready_idx, end_idx):
+    """spans: [(name, lo, hi)] ticket ranges in queue order."""
+    import numpy as np
+    rows = []
+    prev_end = 0.0
+    for name, lo, hi in spans:
+        blk = a[lo:hi]
+        kind = name.rstrip("0123456789")
+        ri, ei = ready_idx.get(kind, 1), end_idx.get(kind, NSTAMP - 1)
+        end = float(blk[:, ei].max())
+        iv = []
+        for k in range(1, ei + 1):
+            d = blk[:, k] - blk[:, k - 1]
+            iv.append(float(np.median(d)))
+        rows.append({"phase": name, "end": end, "step": end - prev_end,
+                     "handoff": float(blk[:, ri].min()) - prev_end, "iv": iv})
+        prev_end = end
+    return rows
+
+
+def _table(rows, title):
+    import statistics as stt
+    out = [title, ""]
+    kinds = sorted({r["phase"].rstrip("0123456789") for r in rows})
+    for k in kinds:
+        rr = [r for r in rows if r["phase"].rstrip("0123456789") == k][1:] or \
+             [r for r in rows if r["phase"].rstrip("0123456789") == k]
+        n = len(rr[0]["iv"])
+        ivs = " / ".join(f"{stt.mean(r['iv'][i] for r in rr):.2f}" for i in range(n))
+        out.append(f"- {k}: {len(rr)} phases, mean step {stt.mean(r['step'] for r in rr):.2f} us, hand-off "
+                   f"{stt.mean(r['handoff'] for r in rr):.2f}, median stamp intervals {ivs}")
+    out += ["", "| phase | end | step | handoff | stamp intervals (median over tiles) |", "|---|---:|---:|---:|---|"]
+    for r in rows:
+        out.append(f"| {r['phase']} | {r['end']:.1f} | {r['step']:.2f} | {r['handoff']:.2f} | "
+                   + " ".join(f"{v:.2f}" for v in r["iv"]) + " |")
+    out.append("")
+    return out
+
+
+def analyse_fwd(st, nlayers: int, M: int):
+    import numpy as np
+    nmt = (M + 31) // 32
+    nA, nB = 2 * nmt, nmt
+    per = nA + nB
+    a = st.reshape(nlayers * per, NSTAMP).astype(np.int64)
+    a = (a - a[:, 0].min()) * 0.01  # 10 ns ticks -> us
+    spans = []
+    for l in range(nlayers):
+        spans.append((f"A{l}", l * per, l * per + nA))
+        spans.append((f"B{l}", l * per + nA, (l + 1) * per))
+    return _phase_rows(a, spans, {"A": 3, "B": 2}, {"A": 7, "B": 7})
+
+
+def analyse_bwd(st, phases):
+    import numpy as np
+    n = phases[-1][0] + phases[-1][3]
+    a = st.reshape(-1, NSTAMP)[:n].astype(np.int64)
+    a = (a - a[:, 0].min()) * 0.01
+    names = {1: "P", 2: "QN", 3: "G", 4: "GIN", 5: "FIN1", 6: "FIN2"}
+    spans = [(f"{names[k]}{l}", f, f + t) for f, k, l, t in phases]
+    return _phase_rows(a, spans, {k: 1 for k in names.values()}, {k: 3 for k in names.values()})
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--model", default="densenet121")
+    ap.add_argument("--batch", type=int, default=256)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--md", default=None)
+    args = ap.parse_args()
+    os.environ["IDC_DS_STAMPS"] = "1"
+    import torch
+
+    from idc_models_amd.engine import Model, RMSprop
+    from idc_models_amd.models import build_model
+
+    dev = torch.device("cuda", 0)
+    net = build_model(args.model, num_outputs=1, seed=1234)
+    m = Model(net, device=dev)
+    m.compile(RMSprop(1e-4), "binary_crossentropy", [], backend="fused")
+    H, W, C = net.input_shape
+    x = torch.randint(0, 256, (args.batch, H, W, C), dtype=torch.uint8, device=dev)
+    y = torch.randint(0, 2, (args.batch,), device=dev)
+    for _ in range(args.steps):
+        m.impl.train_step(x, y)
+    torch.cuda.synchronize()
+    p = m.impl._prog(args.batch, True, torch.uint8)
+    out = []
+    for si, (stamps, nl, M) in enumerate(getattr(p.b, "dense_stamps", [])):
+        rows = analyse_fwd(stamps.cpu().numpy(), nl, M)
+        out += _table(rows, f"## forward launch {si}: {nl} layers, M = {M} rows, span {rows[-1]['end']:.1f} us "
+                            f"(err counter {int(p.b.dense_err[0])})")
+    for si, (stamps, phases, M) in enumerate(getattr(p.b, "dense_bwd_stamps", [])):
+        rows = analyse_bwd(stamps.cpu().numpy(), phases)
+        out += _table(rows, f"## backward launch {si}: M = {M} rows, span {max(r['end'] for r in rows):.1f} us")
+    text = "\n".join(out)
+    print(text)
+    if args.md:
+        with open(args.md, "w") as f:
+            f.write(f"# Dense-stage phase timing ({args.model}, batch {args.batch}, in-kernel s_memrealtime stamps, "
+                    f"last of {args.steps} steps)\n\n" + text + "\n")
+
+
+if __name__ == "__main__":
+    main()
