@@ -735,7 +735,11 @@ class Builder:
         (csrc/kernels/dense_stage_bwd.hip): every layer and BatchNorm trainable in batch mode, the
         stage's consumer BatchNorm in batch mode with single-copy reductions, shapes within the
         launch's limits, no fixed-order (deterministic) reductions."""
-        if os.environ.get("IDC_DENSE_STAGE_BWD", "1") == "0" or not self.training or self.det:
+        # opt-in (IDC_DENSE_STAGE_BWD=1): correct (tests/test_kernels_gpu.py vs autograd) but its
+        # gather tiles wait on agent-coherent loads of ~3 us each under load, so stages 3-4 took
+        # 761 + 234 us against ~720 us for the per-layer dgrad chain (DenseNet-121 bs 256: 4.14 vs
+        # 4.00 ms/step, round 4); see tools/dense_stamps.py
+        if os.environ.get("IDC_DENSE_STAGE_BWD", "0") != "1" or not self.training or self.det:
             return False
         if pend.mode != 1 or getattr(pend, "gsums", None) is None or pend.gsums[2] != 1 or pend.stats.slots != 1:
             return False

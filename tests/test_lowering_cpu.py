@@ -174,10 +174,11 @@ def test_dense_stage_bwd_lowering(monkeypatch):
         for k in env:
             monkeypatch.delenv(k)
         return kinds.count(nat.OP_DENSE_STAGE_BWD), kinds.count(nat.OP_CONV)
-    n_on, conv_on = count()
-    n_off, conv_off = count(IDC_DENSE_STAGE_BWD="0")
+    n_on, conv_on = count(IDC_DENSE_STAGE_BWD="1")
+    n_off, conv_off = count()  # opt-in
     assert (n_on, n_off) == (2, 0)
     assert conv_off - conv_on == 2 * (24 + 16)  # two dgrads per dense layer of stages 3 and 4
-    assert count(150)[0] == 1
-    assert count(IDC_DETERMINISTIC="1")[0] == 0
-    assert count(IDC_DENSE_STAGE_BWD_MAXM="9216")[0] == 3  # stage 2 (6x6 maps) fits the launch too
+    assert count(150, IDC_DENSE_STAGE_BWD="1")[0] == 1
+    assert count(IDC_DENSE_STAGE_BWD="1", IDC_DETERMINISTIC="1")[0] == 0
+    # stage 2 (6x6 maps) fits the launch too
+    assert count(IDC_DENSE_STAGE_BWD="1", IDC_DENSE_STAGE_BWD_MAXM="9216")[0] == 3
