@@ -13,11 +13,12 @@ namespace idc {
 // cannot compute it).  Summed over all clients (an RCCL int32 SUM all-reduce, which wraps mod 2^32)
 // the masks cancel EXACTLY and only the fixed-point sum is revealed.  `alive` is the bitmask of
 // participating clients (<= 64): a client that dropped out before masking is excluded from every
-// pair, so the survivors' masks still cancel (re-keyed round).
+// pair, so the survivors' masks still cancel (re-keyed round).  `accumulate`: out[i] += value
+// instead of out[i] = value (a rank's running masked sum over its clients).
 hipError_t secagg_quantize_mask(const float* x, uint32_t* out, long long n, const float* seg_scale,
                                 const long long* seg_end, int nseg, float clip, int nclients, int rank,
                                 const uint32_t* keys, unsigned long long round_, unsigned long long alive,
-                                hipStream_t st);
+                                hipStream_t st, int accumulate = 0);
 // out[i] = (int32)sum[i] / (scale_s * divisor)
 hipError_t secagg_dequantize(const uint32_t* sum, float* out, long long n, const float* seg_scale,
                              const long long* seg_end, int nseg, float divisor, hipStream_t st);

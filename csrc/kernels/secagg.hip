@@ -49,7 +49,7 @@ __global__ __launch_bounds__(256) void secagg_mask_kernel(const float* __restric
                                                           const long long* __restrict__ seg_end, int nseg,
                                                           float clip, int K, int rank,
                                                           const uint32_t* __restrict__ keys, unsigned long long rnd,
-                                                          unsigned long long alive) {
+                                                          unsigned long long alive, int accumulate) {
   const long long stride = (long long)gridDim.x * blockDim.x;
   long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x;
   if (i >= n) return;
@@ -69,7 +69,10 @@ __global__ __launch_bounds__(256) void secagg_mask_kernel(const float* __restric
                                 keys[2 * j], keys[2 * j + 1]);
       acc += (rank < j) ? m : (0u - m);
     }
-    out[i] = acc;
+    // accumulate: add into the running masked sum of this rank's clients (uint32 wraps mod 2^32,
+    // exactly the ring the all-reduce sums in), no per-client int32 temporary and no host-side
+    // widen / add / modulo passes
+    out[i] = accumulate ? out[i] + acc : acc;
   }
 }
 
@@ -100,11 +103,11 @@ static int grid_for(long long n) {
 hipError_t secagg_quantize_mask(const float* x, uint32_t* out, long long n, const float* seg_scale,
                                 const long long* seg_end, int nseg, float clip, int K, int rank,
                                 const uint32_t* keys, unsigned long long rnd, unsigned long long alive,
-                                hipStream_t st) {
+                                hipStream_t st, int accumulate) {
   if (K > 64 || nseg < 1 || (K > 1 && keys == nullptr)) return hipErrorInvalidValue;
   if (n == 0) return hipSuccess;
   hipLaunchKernelGGL(secagg_mask_kernel, dim3(grid_for(n)), dim3(256), 0, st, x, out, n, seg_scale, seg_end, nseg,
-                     clip, K, rank, keys, rnd, alive);
+                     clip, K, rank, keys, rnd, alive, accumulate);
   return hipGetLastError();
 }
 

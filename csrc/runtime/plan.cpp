@@ -835,11 +835,11 @@ py::tuple py_wgrad_batch_pack(py::list payloads, py::list splits) {
 
 void py_secagg_mask(uintptr_t x, uintptr_t out, long long n, uintptr_t seg_scale, uintptr_t seg_end, int nseg,
                     float clip, int nclients, int rank, uintptr_t keys, unsigned long long round_,
-                    unsigned long long alive, uintptr_t stream) {
+                    unsigned long long alive, uintptr_t stream, int accumulate) {
   check(secagg_quantize_mask(reinterpret_cast<const float*>(x), reinterpret_cast<uint32_t*>(out), n,
                              reinterpret_cast<const float*>(seg_scale), reinterpret_cast<const long long*>(seg_end),
                              nseg, clip, nclients, rank, reinterpret_cast<const uint32_t*>(keys), round_, alive,
-                             reinterpret_cast<hipStream_t>(stream)),
+                             reinterpret_cast<hipStream_t>(stream), accumulate),
         "secagg_quantize_mask");
 }
 
@@ -980,7 +980,9 @@ PYBIND11_MODULE(_idc_native, m) {
   m.def("tile_bn", &conv_tile_bn);
   m.def("tile_bk", &conv_tile_bk);
   m.def("rmsprop", &py_rmsprop);
-  m.def("secagg_mask", &py_secagg_mask);
+  m.def("secagg_mask", &py_secagg_mask, py::arg("x"), py::arg("out"), py::arg("n"), py::arg("seg_scale"),
+        py::arg("seg_end"), py::arg("nseg"), py::arg("clip"), py::arg("nclients"), py::arg("rank"), py::arg("keys"),
+        py::arg("round_"), py::arg("alive"), py::arg("stream"), py::arg("accumulate") = 0);
   m.def("secagg_unmask", &py_secagg_unmask);
   m.attr("OP_CONV") = (int)OP_CONV;
   m.attr("OP_DENSE_STAGE") = (int)OP_DENSE_STAGE;

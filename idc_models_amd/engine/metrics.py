@@ -143,7 +143,8 @@ class AUC(Metric):
         self.batch_aucs: List[float] = []
 
     def update(self, logits, y, loss=None):
-        s = logits.detach().float().reshape(-1)
+        # a copy: the fused backend returns VIEWS of its output buffer, rewritten by the next step
+        s = logits.detach().float().reshape(-1).clone()
         l = y.detach().reshape(-1).float()
         if self.mode == "per_batch":
             a = exact_auc(s, l)

@@ -297,22 +297,25 @@ class FedAvgProcess:
             delta = flat - flat_server
             # TFF gives a client weight 0 when its update is non-finite; the BatchNorm statistics
             # that get averaged too (average_bn_stats) must be finite as well, or they would poison
-            # the mean (plain) or the masked segment ranges (secure)
-            finite = bool(torch.isfinite(delta).all()) and (
-                flat_ntr is None or ntr_sum is None or bool(torch.isfinite(flat_ntr).all()))
+            # the mean (plain) or the masked segment ranges (secure).  The decision stays on the
+            # device (a 0/1 weight, NaNs replaced by where()): no host sync per client -- the round
+            # reads its totals once, after the all-reduce
+            fin = torch.isfinite(delta).all()
+            if flat_ntr is not None and ntr_sum is not None:
+                fin = fin & torch.isfinite(flat_ntr).all()
+            w = fin.to(torch.float64)
+            zero = delta.new_zeros(())
             if self.secure:
                 v = [n_k * delta] + ([n_k * flat_ntr] if ntr_sum is not None else [])
-                masked[k] = torch.cat(v) if finite else torch.zeros(sum(x.numel() for x in v), device=m.device)
-            if not finite:
-                continue  # TFF: non-finite client update gets weight 0
-            if not self.secure:
-                delta_sum += n_k * delta
+                masked[k] = torch.where(fin, torch.cat(v), zero)
+            else:
+                delta_sum += torch.where(fin, n_k * delta, zero)
                 if ntr_sum is not None:
-                    ntr_sum += n_k * flat_ntr
-            n_sum += n_k
-            met[0] += n_k * logs.get("loss", 0.0)
+                    ntr_sum += torch.where(fin, n_k * flat_ntr, zero)
+            n_sum += n_k * w
+            met[0] += n_k * logs.get("loss", 0.0) * w
             for i, name in enumerate(self.metric_names):
-                met[1 + i] += n_k * logs.get(name if name in logs else "accuracy", 0.0)
+                met[1 + i] += n_k * logs.get(name if name in logs else "accuracy", 0.0) * w
         if self.secure:
             # the weighted deltas cross ranks only masked; counts and metrics in the clear
             if self._agg is None or self._agg.K != K:

@@ -75,9 +75,10 @@ def _key_table(nclients: int, keys) -> np.ndarray:
 
 
 def mask_quantize(x: torch.Tensor, scales, seg_end, nclients: int, rank: int, keys, round_: int,
-                  clip: float = None, participants=None) -> torch.Tensor:
+                  clip: float = None, participants=None, out: torch.Tensor = None) -> torch.Tensor:
     """Fixed-point quantise ``x`` (segment s scaled by ``scales[s]``) and add this client's
-    pairwise masks -> int32 tensor.  ``keys``: {peer client -> (k0, k1)} pair keys of this round
+    pairwise masks -> int32 tensor.  ``out`` (GPU, int32): ADD into it instead (mod 2^32) and
+    return it -- a rank's running masked sum over its clients.  ``keys``: {peer client -> (k0, k1)} pair keys of this round
     (``keyagree.ClientKeys.round_keys``).  ``participants``: the clients taking part (default all);
     masks are only exchanged between participants, so a round re-keyed after a dropout still
     cancels exactly."""
@@ -98,13 +99,17 @@ def mask_quantize(x: torch.Tensor, scales, seg_end, nclients: int, rank: int, ke
     if x.is_cuda:
         from ..ops import _native as nat
         dev = x.device
-        out = torch.empty(n, dtype=torch.int32, device=dev)
+        accumulate = out is not None
+        if out is None:
+            out = torch.empty(n, dtype=torch.int32, device=dev)
+        elif out.dtype != torch.int32 or out.numel() != n or out.device != dev:
+            raise ValueError("mask_quantize: out must be an int32 tensor of the vector's size on its device")
         sc = torch.from_numpy(scales).to(dev)
         se = torch.from_numpy(seg_end).to(dev)
         kt = torch.from_numpy(table.view(np.int32)).to(dev)
         nat.require().secagg_mask(x.data_ptr(), out.data_ptr(), n, sc.data_ptr(), se.data_ptr(), len(seg_end),
                                   float(clip), int(nclients), int(rank), kt.data_ptr(), int(round_), alive,
-                                  nat.stream_handle())
+                                  nat.stream_handle(), 1 if accumulate else 0)
         # no host sync: the small tables above were allocated on this stream, so the caching
         # allocator hands their memory out again only to work ordered after this kernel
         return out
@@ -208,14 +213,19 @@ class MaskedAggregator:
             import torch.distributed as dist
             comm.all_reduce_(mx, op=dist.ReduceOp.MAX)
         scales = choose_scales(mx.cpu().numpy(), self.K)
-        total = torch.zeros(n, dtype=torch.int64, device=dev)
+        gpu = dev.type == "cuda"
+        total = torch.zeros(n, dtype=torch.int32 if gpu else torch.int64, device=dev)
         for k, v in sorted(vecs.items()):
             with Timer(f"Encryption for client {k}", printer):
                 keys = self.keys[k].round_keys(self.publics, round_, parts)
-                masked = mask_quantize(v.reshape(-1).to(dev), scales, seg_end, self.K, k, keys, round_,
-                                       participants=parts)
-                total = (total + masked.to(dev).to(torch.int64)) % (1 << 32)
-        t32 = torch.where(total >= (1 << 31), total - (1 << 32), total).to(torch.int32)
+                if gpu:  # the mask kernel adds into the rank's int32 ring sum (wraps mod 2^32)
+                    mask_quantize(v.reshape(-1).to(dev), scales, seg_end, self.K, k, keys, round_,
+                                  participants=parts, out=total)
+                else:
+                    masked = mask_quantize(v.reshape(-1).to(dev), scales, seg_end, self.K, k, keys, round_,
+                                           participants=parts)
+                    total = (total + masked.to(torch.int64)) % (1 << 32)
+        t32 = total if gpu else torch.where(total >= (1 << 31), total - (1 << 32), total).to(torch.int32)
         comm.all_reduce_(t32)  # int32 SUM wraps mod 2^32 on RCCL / gloo
         t0 = time.perf_counter()
         out = unmask(t32, scales, seg_end, 1.0).to(dev)

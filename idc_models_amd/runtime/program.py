@@ -350,9 +350,9 @@ class FusedProgram:
 def _labels_to(io_labels: torch.Tensor, y: torch.Tensor, U: int):
     y = y.to(io_labels.device, non_blocking=True)
     if U == 1:
-        io_labels.copy_(y.reshape(-1).float())
+        io_labels.copy_(y.reshape(-1))  # one conversion kernel (no float temporary)
     elif y.dim() == 2 and y.shape[1] == U:
-        io_labels.copy_(y.float())
+        io_labels.copy_(y)
     else:
         io_labels.zero_()
         io_labels.scatter_(1, y.reshape(-1, 1).long(), 1.0)
@@ -467,7 +467,14 @@ class FusedStep:
         if validate:
             self._validate(p, "after opt")
         torch.cuda.current_stream(m.device).wait_stream(p.stream)
-        return p.io.loss.reshape(()).clone(), p.io.logits.clone()
+        return self._outputs(p)
+
+    @staticmethod
+    def _outputs(p: FusedProgram):
+        """(loss, logits) as VIEWS of the program's output buffers, ordered after the step on the
+        caller's stream and valid until the next step of the same program (copies would add two
+        dependent launches to every step; Model.fit consumes them before the next step is issued)."""
+        return p.io.loss.reshape(()), p.io.logits
 
     def _central_storage_step(self, p: FusedProgram, validate: bool):
         """CentralStorageStrategy (``dist_model_tf_dense.py:24``): gradients are reduced to rank 0,
@@ -491,7 +498,7 @@ class FusedStep:
             st.broadcast_from_root(m.arena.data, p.stream)
             p.run_range(cast_lo, hi, graph=False)
         torch.cuda.current_stream(m.device).wait_stream(p.stream)
-        return p.io.loss.reshape(()).clone(), p.io.logits.clone()
+        return self._outputs(p)
 
     def skipped_steps(self) -> int:
         """Training steps whose update was skipped for non-finite gradients (skip_nonfinite)."""
@@ -507,7 +514,7 @@ class FusedStep:
         self._stage_inputs(p, x, y)
         p.run_segment("fwd")
         torch.cuda.current_stream(self.m.device).wait_stream(p.stream)
-        return p.io.loss.reshape(()).clone(), p.io.logits.clone()
+        return self._outputs(p)
 
     def reset_stats_shift(self):
         """Every program back to a first step's statistics shifts (a federated client starts

@@ -1,0 +1,81 @@
+"""Gradient fidelity of a bf16 training step against an fp32 eager reference.
+
+A randomly initialised DenseNet-121 in training mode (batch-statistics BN) has an ill-conditioned
+gradient: in fp32 eager, perturbing its 50x50 inputs by 1e-6 moves the whole gradient by 2.5 %
+(relative L2), rounding the inputs to bf16 moves it by 45 %, and PyTorch's own bf16 autocast is
+79 % away from fp32 (batch 64, seed 7; see profiles/densenet121_gradient_spread.md). So "close to
+fp32" can only be judged per parameter RELATIVE to what bf16 rounding does to that parameter:
+the yardsticks here are bf16 autocast and fp32-on-bf16-rounded-inputs, both computed by this
+module on the same network and batch.
+
+Used by tests/rccl_worker.py (data-parallel step), tests/test_fused_gpu.py (bench-batch
+fused-vs-eager) and tools/grad_fidelity.py (the committed measurement).
+"""
+from __future__ import annotations
+
+import copy
+from typing import Dict, List, Sequence
+
+import torch
+import torch.nn.functional as F
+
+
+def eager_grads(net, x_u8: torch.Tensor, y: torch.Tensor, mode: str = "fp32") -> List[torch.Tensor]:
+    """Gradients of BCE-with-logits wrt every trainable Parameter of a deep copy of ``net``
+    (training mode), on uint8 NHWC inputs scaled by 1/255. ``mode``: ``fp32``; ``autocast``
+    (bf16 autocast forward); ``bf16in`` (fp32 network on inputs rounded to bf16)."""
+    ref = copy.deepcopy(net)
+    dev = next(iter(ref.parameters())).device
+    xs = x_u8.to(dev).float() / 255.0
+    if mode == "bf16in":
+        xs = xs.bfloat16().float()
+    yy = y.to(dev).float().reshape(-1)
+    ref.train()
+    with torch.autocast(dev.type, dtype=torch.bfloat16, enabled=(mode == "autocast")):
+        lg = ref(xs)
+    loss = F.binary_cross_entropy_with_logits(lg.float().reshape(-1), yy)
+    ps = [p for p in ref.trainable_weights if isinstance(p, torch.nn.Parameter)]
+    return [g.detach().double() for g in torch.autograd.grad(loss, ps)]
+
+
+def _cos(a: torch.Tensor, b: torch.Tensor) -> float:
+    a, b = a.reshape(-1).double(), b.reshape(-1).double()
+    return float(a @ b / (a.norm() * b.norm() + 1e-300))
+
+
+def _rel(a: torch.Tensor, ref: torch.Tensor) -> float:
+    a, ref = a.reshape(-1).double(), ref.reshape(-1).double()
+    return float((a - ref).norm() / ref.norm().clamp_min(1e-300))
+
+
+def param_report(arena, grad: torch.Tensor, g32: Sequence[torch.Tensor],
+                 yardsticks: Dict[str, Sequence[torch.Tensor]]) -> List[dict]:
+    """Per parameter: cosine and relative error of the fused gradient (flat ``grad`` in
+    ``arena`` layout) vs fp32, and the same two numbers for every yardstick gradient."""
+    rows = []
+    for i, gr in enumerate(g32):
+        if float(gr.norm()) < 1e-12:
+            continue
+        gf = arena.view(grad, i).to(gr.device)
+        row = {"param": i, "shape": list(gr.shape), "cos": _cos(gf, gr), "rel": _rel(gf, gr)}
+        for k, gs in yardsticks.items():
+            row[f"cos_{k}"] = _cos(gs[i], gr)
+            row[f"rel_{k}"] = _rel(gs[i], gr)
+        rows.append(row)
+    return rows
+
+
+def whole_rel(arena, grad: torch.Tensor, g32: Sequence[torch.Tensor]) -> float:
+    """Relative L2 error of the whole fused gradient vs fp32."""
+    num = den = 0.0
+    for i, gr in enumerate(g32):
+        gf = arena.view(grad, i).to(gr.device).double()
+        num += float((gf.reshape(-1) - gr.reshape(-1)).pow(2).sum())
+        den += float(gr.pow(2).sum())
+    return (num / max(den, 1e-300)) ** 0.5
+
+
+def whole_rel_list(gs: Sequence[torch.Tensor], g32: Sequence[torch.Tensor]) -> float:
+    num = sum(float((a - b).pow(2).sum()) for a, b in zip(gs, g32))
+    den = sum(float(b.pow(2).sum()) for b in g32)
+    return (num / max(den, 1e-300)) ** 0.5

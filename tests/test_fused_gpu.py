@@ -227,6 +227,7 @@ def test_tinycnn_fused_dropout_trains_and_eval_is_deterministic():
     losses = [m.impl.train_step(x, y)[0].item() for _ in range(30)]
     assert losses[-1] < losses[0], losses
     l1, g1 = m.impl.eval_step(x, y)
+    g1 = g1.clone()  # the fused backend returns views of its output buffer
     l2, g2 = m.impl.eval_step(x, y)
     assert torch.equal(g1, g2)  # no dropout at inference
 

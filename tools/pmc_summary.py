@@ -1,10 +1,14 @@
-"""Per-kernel PMC summary of a ``rocprofv3 --pmc ... --kernel-trace --output-format csv`` run.
+"""Per-kernel PMC summary of one or more ``rocprofv3 --pmc ... --output-format csv`` passes.
 
-usage: python tools/pmc_summary.py DIR/PREFIX --steps 3 [--marker input_stage] [--md out.md]
+usage: python tools/pmc_summary.py DIR/PREFIX [DIR/PREFIX2 ...] --steps 3 [--marker input_stage] [--md out.md]
 
-Counters expected: SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_VALU_MFMA_BUSY_CYCLES SQ_LDS_BANK_CONFLICT
-SQ_LDS_IDX_ACTIVE SQ_WAIT_INST_LDS SQ_INSTS_MFMA SQ_WAIT_ANY.  Only the last ``--steps`` training
-steps are used (a step starts at the ``--marker`` kernel), so autotuning and warm-up are excluded.
+Counters expected (over all passes): SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_VALU_MFMA_BUSY_CYCLES
+SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_WAIT_INST_LDS SQ_INSTS_MFMA SQ_WAIT_ANY.  Only the last
+``--steps`` training steps of each pass are used (a step starts at the ``--marker`` kernel), so
+autotuning and warm-up are excluded; the passes' selected dispatch sequences must match kernel for
+kernel (same program, same tune cache) and are merged by position.  Collect at most 4 SQ counters
+per pass and no tracing domain beside --pmc: a round-3 pass of all 8 SQ counters together with
+--kernel-trace segfaulted inside rocprofv3 at the first dispatch (tools/pmc_session.sh).
 
 Derived (per kernel class, summed over its dispatches):
   MFMA util   = SQ_VALU_MFMA_BUSY_CYCLES / (kernel time x 2.4 GHz x 1024 SIMDs)
@@ -29,27 +33,39 @@ def short(name):
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("prefix")
+    ap.add_argument("prefix", nargs="+")
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--marker", default="input_stage")
     ap.add_argument("--md", default=None)
     a = ap.parse_args()
-    disp = {}
-    order = []
-    with open(a.prefix + "_counter_collection.csv") as f:
-        for r in csv.DictReader(f):
-            d = int(r["Dispatch_Id"])
-            if d not in disp:
-                disp[d] = {"name": r["Kernel_Name"], "t": int(r["End_Timestamp"]) - int(r["Start_Timestamp"])}
-                order.append(d)
-            disp[d][r["Counter_Name"]] = disp[d].get(r["Counter_Name"], 0.0) + float(r["Counter_Value"])
-    order.sort()
-    marks = [d for d in order if a.marker in disp[d]["name"]]
-    first = marks[-a.steps]
-    sel = [d for d in order if d >= first]
+    merged = None
+    for prefix in a.prefix:
+        disp = {}
+        order = []
+        with open(prefix + "_counter_collection.csv") as f:
+            for r in csv.DictReader(f):
+                d = int(r["Dispatch_Id"])
+                if d not in disp:
+                    disp[d] = {"name": r["Kernel_Name"], "t": int(r["End_Timestamp"]) - int(r["Start_Timestamp"])}
+                    order.append(d)
+                disp[d][r["Counter_Name"]] = disp[d].get(r["Counter_Name"], 0.0) + float(r["Counter_Value"])
+        order.sort()
+        marks = [d for d in order if a.marker in disp[d]["name"]]
+        first = marks[-a.steps]
+        sel = [disp[d] for d in order if d >= first]
+        if merged is None:
+            merged = sel
+            continue
+        if [e["name"] for e in sel] != [e["name"] for e in merged]:
+            raise SystemExit(f"{prefix}: dispatch sequence differs from the first pass")
+        for e0, e in zip(merged, sel):
+            e0["t"] = min(e0["t"], e["t"])
+            for k, v in e.items():
+                if k not in ("name", "t"):
+                    e0[k] = v
+    sel = merged
     agg = collections.OrderedDict()
-    for d in sel:
-        e = disp[d]
+    for e in sel:
         k = short(e["name"])
         s = agg.setdefault(k, collections.Counter())
         s["n"] += 1
@@ -66,6 +82,9 @@ def main():
         wait = s["SQ_WAIT_ANY"] / s["SQ_WAVE_CYCLES"] if s["SQ_WAVE_CYCLES"] else 0.0
         ldsw = s["SQ_WAIT_INST_LDS"] / s["SQ_WAVE_CYCLES"] if s["SQ_WAVE_CYCLES"] else 0.0
         rows.append((s["t"], k, s["n"] / a.steps, s["t"] / 1e3 / a.steps, util, lds, wait, ldsw))
+    for key in ("SQ_VALU_MFMA_BUSY_CYCLES", "SQ_LDS_IDX_ACTIVE", "SQ_WAVE_CYCLES"):
+        if not any(s[key] for s in agg.values()):
+            print(f"warning: no {key} in any pass")
     rows.sort(reverse=True)
     lines = [f"# PMC summary per kernel ({a.steps} steps, rocprofv3 --pmc, serialised dispatches)", "",
              f"- kernel time per step under PMC: {tot_t / 1e6 / a.steps:.3f} ms",
