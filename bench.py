@@ -77,15 +77,19 @@ def rccl_version_of(strategy):
         return "unknown"
 
 
-def stock_img_s_per_gpu(model: str):
-    """Best stock PyTorch-ROCm images/sec on one GPU for ``model`` (benchmarks/stock_baseline.json)."""
+def stock_img_s_per_gpu(model: str, size: int = 50, classes: int = 1, phase: str = "full"):
+    """Best stock PyTorch-ROCm images/sec on one GPU for ``model`` at this input size / class
+    count / training phase (benchmarks/stock_baseline.json; entries without those keys are the
+    default 50x50x3, 1 logit, every layer trained)."""
     p = os.path.join(ROOT, "benchmarks", "stock_baseline.json")
     try:
         with open(p) as f:
             runs = json.load(f)
     except (OSError, ValueError):
         return None
-    vals = [r["images_per_sec"] for r in runs.get("results", []) if r.get("model") == model]
+    vals = [r["images_per_sec"] for r in runs.get("results", []) if r.get("model") == model
+            and r.get("input", [50])[0] == size and r.get("classes", 1) == classes
+            and r.get("phase", "full") == phase]
     return max(vals) if vals else None
 
 
@@ -174,6 +178,14 @@ def main():
     ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--model", default="densenet121")
     ap.add_argument("--batch", type=int, default=256, help="per-GPU batch")
+    ap.add_argument("--input", type=int, default=None, help="square input size (default: the model's, 50)")
+    ap.add_argument("--classes", type=int, default=1,
+                    help="logits: 1 = binary IDC head (BCE); >1 = softmax head (categorical CE), "
+                         "e.g. --model densenet201 --input 32 --classes 10 (dist_model_tf_dense.py)")
+    ap.add_argument("--phase", default="full", choices=["full", "frozen", "finetune"],
+                    help="frozen: reference phase 1 (base_model.trainable = False, head only); "
+                         "finetune: phase 2 (layers[:fine_tune_at] frozen, 150 DenseNet / 100 "
+                         "MobileNetV2, lr/10); full: every layer trains (the headline)")
     ap.add_argument("--lr", type=float, default=1e-4)
     ap.add_argument("--no-graphs", action="store_true")
     ap.add_argument("--backend", default="fused")
@@ -243,15 +255,26 @@ def main():
     rccl = rccl_version_of(strategy) if comm_backend == "nccl" else None
     torch.manual_seed(1234)
 
+    size = args.input or 50
+    if args.phase == "finetune":
+        args.lr /= 10  # the reference recompiles phase 2 with base_learning_rate / 10
     with strategy.scope():
-        net = build_model(args.model, num_outputs=1, seed=1234)
+        net = build_model(args.model, (size, size, 3) if args.input else None, num_outputs=args.classes, seed=1234)
+        if args.phase == "frozen":
+            net.base.trainable = False
+        elif args.phase == "finetune":
+            net.base.trainable = True
+            for layer in net.base.layers[:150 if args.model.startswith("densenet") else 100]:
+                layer.trainable = False
         model = Model(net, strategy)
-        model.compile(RMSprop(args.lr), "binary_crossentropy", ["accuracy", "auc"], backend=args.backend,
+        binary = args.classes == 1
+        model.compile(RMSprop(args.lr), "binary_crossentropy" if binary else "categorical_crossentropy",
+                      ["accuracy", "auc"] if binary else ["accuracy"], backend=args.backend,
                       **({"use_graphs": False} if args.no_graphs and args.backend == "fused" else {}))
     H, W, C = net.input_shape
     g = torch.Generator(device="cpu").manual_seed(1000 + rank)
     x = torch.randint(0, 256, (args.batch, H, W, C), generator=g, dtype=torch.uint8).to(dev)
-    y = torch.randint(0, 2, (args.batch,), generator=g).to(dev)
+    y = torch.randint(0, max(2, args.classes), (args.batch,), generator=g).to(dev)
 
     step = model.impl.train_step
 
@@ -290,8 +313,9 @@ def main():
         gb = args.batch * world
         # weak class signal and 20 % re-drawn labels: the held-out AUC ceiling is 0.90, so the
         # number says how well the fit learned rather than saturating at 1.0
-        train = synthetic_dataset(gb * args.fit_steps, (H, W, C), 2, seed=11, signal=6.0, label_noise=0.2)
-        held = synthetic_dataset(max(gb * 2, 1024), (H, W, C), 2, seed=12, signal=6.0, label_noise=0.2)
+        nc = max(2, args.classes)
+        train = synthetic_dataset(gb * args.fit_steps, (H, W, C), nc, seed=11, signal=6.0, label_noise=0.2)
+        held = synthetic_dataset(max(gb * 2, 1024), (H, W, C), nc, seed=12, signal=6.0, label_noise=0.2)
         meter = ThroughputMeter()
         model.fit(train.batch(gb, True, 1000, True, seed=5), epochs=args.fit_epochs, callbacks=[meter],
                   verbose=0)
@@ -300,13 +324,16 @@ def main():
         t_ep = all_reduce_max(t_ep, dev) if strategy.active else t_ep  # slowest rank sets the pace
         fit_ips = gb * args.fit_steps / t_ep
         logs = model.evaluate(held.batch(gb, False, 1000, False), return_dict=True)
-        val_auc, val_acc = float(logs["auc"]), float(logs["accuracy"])
+        val_auc, val_acc = (float(logs["auc"]) if "auc" in logs else None), float(logs["accuracy"])
 
-    base = stock_img_s_per_gpu(args.model)
+    base = stock_img_s_per_gpu(args.model, size, args.classes, args.phase)
+    headline = args.model == "densenet121" and size == 50 and args.classes == 1 and args.phase == "full"
     if rank == 0:
         print(json.dumps({
             "metric": "images/sec (whole node) DenseNet-121 50x50x3 bs=256 at 1/2/4/8 MI355X; val AUC"
-            if args.model == "densenet121" else f"images/sec (whole node) {args.model} 50x50x3",
+            if headline else (f"images/sec (whole node) {args.model} {size}x{size}x3"
+                              + (f" {args.classes}-class" if args.classes > 1 else "")
+                              + (f" phase={args.phase}" if args.phase != "full" else "")),
             "value": round(value, 1),
             "unit": "images/sec",
             "n_gpus": world if dev.type == "cuda" else 0,
@@ -317,15 +344,18 @@ def main():
             "scaling": "weak",
             "vs_baseline": round(value / (base * world), 3) if base and dev.type == "cuda" else None,
             "dtype": "bf16" if dev.type == "cuda" else "fp32",
-            "data": "synthetic uint8 50x50x3 patches, random-init weights",
+            "data": f"synthetic uint8 {size}x{size}x3 images, random-init weights",
             "val_auc": round(val_auc, 4) if val_auc is not None else None,
             "val_accuracy": round(val_acc, 4) if val_acc is not None else None,
             "fit_images_per_sec": round(fit_ips, 1) if fit_ips is not None else None,
             "config": {"model": "DenseNet-121" if args.model == "densenet121" else args.model,
                        "global_batch": args.batch * world, "seq_len": None,
-                       "input": [H, W, C], "per_gpu_batch": args.batch,
+                       "input": [H, W, C], "per_gpu_batch": args.batch, "classes": args.classes,
+                       "phase": args.phase, "trainable_params": sum(int(t.numel()) for t in model.arena.params)
+                       if hasattr(model, "arena") else None,
                        "parallelism": f"dp{world}", "optimizer": "RMSprop(lr=%g)" % args.lr,
-                       "loss": "BCE(from_logits)", "final_loss": round(lossv, 5),
+                       "loss": "BCE(from_logits)" if args.classes == 1 else "CategoricalCE(from_logits)",
+                       "final_loss": round(lossv, 5),
                        "backend": args.backend, "comm_backend": comm_backend, "rccl_version": rccl,
                        "world_size": world,
                        "grad_allreduce": ("native RCCL communicator, bucket ops in the C++ plan"

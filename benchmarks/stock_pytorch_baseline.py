@@ -1,4 +1,4 @@
-"""In-situ comparison point: stock PyTorch-ROCm DenseNet-121 / VGG16 / MobileNetV2 training step.
+"""In-situ comparison point: stock PyTorch-ROCm DenseNet-121/201 / VGG16 / MobileNetV2 training step.
 
 BASELINE.md: the reference publishes no numbers, so the point to beat is "stock PyTorch-ROCm
 (MIOpen convolutions, bf16 autocast, channels_last)" on the same MI355X and config.  This is a
@@ -6,6 +6,12 @@ plain ``torch.nn`` implementation (torchvision is not installed) — NOT part of
 hot path; it exists only to produce that number.
 
     python benchmarks/stock_pytorch_baseline.py --model densenet121 --batch 256 --steps 20
+    python benchmarks/stock_pytorch_baseline.py --model densenet201 --input 32 --classes 10 --phase finetune
+
+``--phase``: ``full`` (every layer trains), ``frozen`` (reference phase 1, ``base_model.trainable =
+False``: only the head trains, frozen BatchNorms in inference mode) or ``finetune`` (reference
+phase 2, ``fine_tune_at`` = 150 for DenseNet / 100 for MobileNetV2 Keras layers frozen: the same
+number of leading weighted layers -- Keras order = this module order -- is frozen here).
 """
 from __future__ import annotations
 
@@ -33,7 +39,7 @@ class DenseLayer(nn.Module):
 
 
 class DenseNet121(nn.Module):
-    def __init__(self, blocks=(6, 12, 24, 16)):
+    def __init__(self, blocks=(6, 12, 24, 16), classes=1):
         super().__init__()
         layers = [nn.ZeroPad2d(3), nn.Conv2d(3, 64, 7, 2, bias=False),
                   nn.BatchNorm2d(64, eps=1.001e-5, momentum=0.01), nn.ReLU(), nn.ZeroPad2d(1),
@@ -48,14 +54,18 @@ class DenseNet121(nn.Module):
                            nn.Conv2d(ch, ch // 2, 1, bias=False), nn.AvgPool2d(2, 2)]
                 ch //= 2
         layers += [nn.BatchNorm2d(ch, eps=1.001e-5, momentum=0.01), nn.ReLU(),
-                   nn.AdaptiveAvgPool2d(1), nn.Flatten(), nn.Linear(ch, 1)]
+                   nn.AdaptiveAvgPool2d(1), nn.Flatten(), nn.Linear(ch, classes)]
         self.net = nn.Sequential(*layers)
 
     def forward(self, x):
         return self.net(x)
 
 
-def vgg16():
+def densenet201(classes=1):
+    return DenseNet121((6, 12, 48, 32), classes)
+
+
+def vgg16(classes=1):
     cfg = [(64, 2), (128, 2), (256, 3), (512, 3), (512, 3)]
     layers, cin = [], 3
     for c, n in cfg:
@@ -63,7 +73,7 @@ def vgg16():
             layers += [nn.Conv2d(cin, c, 3, padding=1), nn.ReLU()]
             cin = c
         layers.append(nn.MaxPool2d(2, 2))
-    layers += [nn.AdaptiveAvgPool2d(1), nn.Flatten(), nn.Linear(512, 1)]
+    layers += [nn.AdaptiveAvgPool2d(1), nn.Flatten(), nn.Linear(512, classes)]
     return nn.Sequential(*layers)
 
 
@@ -91,7 +101,7 @@ class InvRes(nn.Module):
         return x + y if self.res else y
 
 
-def mobilenetv2():
+def mobilenetv2(classes=1):
     cfg = [(16, 1, 1), (24, 2, 6), (24, 1, 6), (32, 2, 6), (32, 1, 6), (32, 1, 6), (64, 2, 6), (64, 1, 6),
            (64, 1, 6), (64, 1, 6), (96, 1, 6), (96, 1, 6), (96, 1, 6), (160, 2, 6), (160, 1, 6),
            (160, 1, 6), (320, 1, 6)]
@@ -102,28 +112,60 @@ def mobilenetv2():
         layers.append(InvRes(cin, _div8(c), s, t))
         cin = _div8(c)
     layers += [nn.Conv2d(cin, 1280, 1, bias=False), nn.BatchNorm2d(1280, eps=1e-3, momentum=1e-3),
-               nn.ReLU6(), nn.AdaptiveAvgPool2d(1), nn.Flatten(), nn.Linear(1280, 1)]
+               nn.ReLU6(), nn.AdaptiveAvgPool2d(1), nn.Flatten(), nn.Linear(1280, classes)]
     return nn.Sequential(*layers)
 
 
-def run(model_name: str, batch: int, steps: int, warmup: int, graph: bool, channels_last: bool = True) -> dict:
+def _keras_frozen_weighted(model_name: str, phase: str, size: int, classes: int):
+    """How many leading weighted (conv / BN) layers the reference freezes in ``phase``: counted on
+    the framework's Keras-order layer list, so both sides freeze the same layers."""
+    if phase == "full":
+        return 0
+    import os
+    import sys
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    from idc_models_amd.models import build_model
+    net = build_model(model_name, (size, size, 3), classes, seed=0)
+    layers = net.base.layers
+    if phase == "finetune":
+        layers = layers[:150 if model_name.startswith("densenet") else 100]
+    return sum(1 for l in layers if l.keras_class in ("Conv2D", "BatchNormalization", "DepthwiseConv2D"))
+
+
+def run(model_name: str, batch: int, steps: int, warmup: int, graph: bool, channels_last: bool = True,
+        size: int = 50, classes: int = 1, phase: str = "full") -> dict:
     """Time one stock training step (bf16 autocast forward, fp32 loss, backward, RMSprop).
     ``graph``: the whole step captured once into a HIP graph (torch.cuda.graphs, capturable
     RMSprop) and replayed — the strongest stock configuration (no per-kernel host launches)."""
     dev = torch.device("cuda")
     torch.backends.cudnn.benchmark = True
     torch.manual_seed(0)
-    model = {"densenet121": DenseNet121, "vgg16": vgg16, "mobilenetv2": mobilenetv2}[model_name]().to(dev)
+    ctor = {"densenet121": DenseNet121, "densenet201": densenet201, "vgg16": vgg16, "mobilenetv2": mobilenetv2}
+    model = ctor[model_name](classes=classes).to(dev)
+    nfreeze = _keras_frozen_weighted(model_name, phase, size, classes)
+    weighted = [mod for mod in model.modules() if isinstance(mod, (nn.Conv2d, nn.BatchNorm2d))]
+    for mod in weighted[:nfreeze]:
+        for prm in mod.parameters():
+            prm.requires_grad_(False)
+    frozen_bn = [mod for mod in weighted[:nfreeze] if isinstance(mod, nn.BatchNorm2d)]
     fmt = torch.channels_last if channels_last else torch.contiguous_format
     model = model.to(memory_format=fmt)
-    opt = torch.optim.RMSprop(model.parameters(), lr=1e-4, alpha=0.9, eps=1e-7, capturable=graph)
-    x = torch.rand(batch, 3, 50, 50, device=dev).to(memory_format=fmt)
-    y = torch.randint(0, 2, (batch, 1), device=dev).float()
+    model.train()
+    for mod in frozen_bn:  # Keras: a non-trainable BatchNormalization runs in inference mode
+        mod.eval()
+    opt = torch.optim.RMSprop([q for q in model.parameters() if q.requires_grad], lr=1e-4, alpha=0.9,
+                              eps=1e-7, capturable=graph)
+    x = torch.rand(batch, 3, size, size, device=dev).to(memory_format=fmt)
+    if classes == 1:
+        y = torch.randint(0, 2, (batch, 1), device=dev).float()
+    else:
+        y = torch.randint(0, classes, (batch,), device=dev)
 
     def step():
         with torch.autocast("cuda", dtype=torch.bfloat16):
             out = model(x)
-        loss = F.binary_cross_entropy_with_logits(out.float(), y)
+        loss = (F.binary_cross_entropy_with_logits(out.float(), y) if classes == 1
+                else F.cross_entropy(out.float(), y))
         loss.backward()
         opt.step()
         return loss
@@ -154,7 +196,8 @@ def run(model_name: str, batch: int, steps: int, warmup: int, graph: bool, chann
     torch.cuda.synchronize()
     dt = (time.perf_counter() - t) / steps
     return {"baseline": "stock_pytorch_%s_bf16_autocast" % ("hipgraph" if graph else "eager"),
-            "model": model_name, "batch": batch, "ms_per_step": round(dt * 1e3, 3),
+            "model": model_name, "batch": batch, "input": [size, size, 3], "classes": classes, "phase": phase,
+            "frozen_weighted_layers": nfreeze, "ms_per_step": round(dt * 1e3, 3),
             "images_per_sec": round(batch / dt, 1), "channels_last": channels_last,
             "torch": torch.__version__, "device": torch.cuda.get_device_name()}
 
@@ -167,8 +210,23 @@ def main():
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--no-channels-last", action="store_true")
     ap.add_argument("--graph", action="store_true", help="HIP-graph-captured step")
+    ap.add_argument("--input", type=int, default=50, help="square input size")
+    ap.add_argument("--classes", type=int, default=1)
+    ap.add_argument("--phase", default="full", choices=["full", "frozen", "finetune"])
     ap.add_argument("--all", metavar="OUT_JSON", help="every model, eager and graph; write JSON")
+    ap.add_argument("--append", metavar="JSON", help="append this run's eager and graph results to JSON")
     args = ap.parse_args()
+    if args.append:
+        with open(args.append) as f:
+            doc = json.load(f)
+        for graph in (False, True):
+            r = run(args.model, args.batch, args.steps, args.warmup, graph, not args.no_channels_last,
+                    args.input, args.classes, args.phase)
+            print(json.dumps(r), flush=True)
+            doc["results"].append(r)
+        with open(args.append, "w") as f:
+            json.dump(doc, f, indent=1)
+        return
     if args.all:
         results = []
         for m in ("densenet121", "vgg16", "mobilenetv2"):
@@ -187,7 +245,7 @@ def main():
                        "results": results}, f, indent=1)
         return
     print(json.dumps(run(args.model, args.batch, args.steps, args.warmup, args.graph,
-                         not args.no_channels_last)))
+                         not args.no_channels_last, args.input, args.classes, args.phase)))
 
 
 if __name__ == "__main__":

@@ -681,7 +681,7 @@ struct RegionState {
 };
 std::mutex g_region_mu;
 std::unordered_map<uintptr_t, RegionState> g_regions;
-uintptr_t g_region_active = 0;
+thread_local uintptr_t g_region_active = 0;  // per thread, as allocating() routes per thread
 
 void region_activate(uintptr_t base, long long cap) {
   std::lock_guard<std::mutex> l(g_region_mu);

@@ -187,9 +187,19 @@ class FedAvgProcess:
         from .grouped import GroupedClientTrainer
         g = self._grouped
         if g is None or g.k < n_clients or g.B != batch:
+            # a region stays reserved for the whole process (runtime/grouped.py _KEEP_ALIVE): the
+            # old one stops allocating and the re-creation is reported (idle copies cost compute,
+            # so the group is not over-sized speculatively; it only grows, never shrinks for a
+            # smaller round)
+            k = n_clients if g is None else max(n_clients, g.k)
+            if g is not None:
+                g.region.close()
+                import warnings
+                warnings.warn(f"client batching: re-creating the grouped trainer (K {g.k}->{k}, batch "
+                              f"{g.B}->{batch}); the old {g.k} x {g.region.stride >> 20} MiB region stays reserved")
             m = self.worker()
             g = GroupedClientTrainer(self.model_fn, self.client_optimizer_fn, self.loss, self.metric_names,
-                                     n_clients, batch, m.device)
+                                     k, batch, m.device)
             self._grouped = g
         return g
 

@@ -28,6 +28,10 @@ def eligible(datasets: Sequence, model) -> bool:
         return False
     if not all(isinstance(d, BatchedDataset) and d.drop_remainder and d.repeat == 1 for d in datasets):
         return False
+    # the grouped program takes uint8 pixels (its xin is [K, B, H, W, C] uint8): float or other
+    # integer client data would be silently truncated by the index_select copy into it
+    if not all(str(getattr(d.ds.x, "dtype", "")) in ("uint8", "torch.uint8") for d in datasets):
+        return False
     bs = {d.batch_size for d in datasets}
     steps = {len(d) for d in datasets}
     return len(bs) == 1 and len(steps) == 1 and next(iter(steps)) > 0

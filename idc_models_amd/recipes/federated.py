@@ -138,8 +138,12 @@ def run_fedavg(cfg: FedConfig, printer=print):
         state = fed_avg.initialize()
         fp = _fed_fingerprint(cfg, state)
         if cfg.resume and os.path.exists(state_path):
-            saved = load_server_extra(state_path)
-            diff = {k: (saved.get(k), v) for k, v in fp.items() if saved.get(k) != v}
+            saved = load_server_extra(state_path) or {}
+            # a state written before fingerprints were saved carries none: unknown, not different
+            # (load_server_state still checks every tensor shape against the model)
+            diff = {k: (saved[k], v) for k, v in fp.items() if k in saved and saved[k] != v}
+            if not saved:
+                printer(f"{state_path} carries no configuration fingerprint; resuming without the check")
             if diff:
                 raise ValueError(f"{state_path} was written by a different federated configuration "
                                  f"(saved, current): {diff}; use another path or resume=False")

@@ -33,3 +33,20 @@ def test_bench_refuses_mismatched_world():
               "--warmup", "0", "--fit-steps", "0"], {"WORLD_SIZE": "1", "RANK": "0", "LOCAL_RANK": "0"})
     assert r.returncode == 3
     assert "error" in json.loads(r.stdout.strip().splitlines()[-1])
+
+
+def test_bench_densenet201_cifar_phases_on_cpu():
+    """``--model densenet201 --input 32 --classes 10 --phase frozen|finetune`` (dist_model_tf_dense.py
+    phases 1 and 2): the softmax head, the frozen parameter counts and the per-phase metric name."""
+    counts = {}
+    for ph in ("frozen", "finetune"):
+        r = _run(["--device", "cpu", "--model", "densenet201", "--input", "32", "--classes", "10",
+                  "--phase", ph, "--batch", "2", "--steps", "1", "--warmup", "0", "--fit-steps", "0"])
+        assert r.returncode == 0, r.stderr[-3000:]
+        out = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][-1])
+        assert f"phase={ph}" in out["metric"] and "10-class" in out["metric"]
+        assert out["config"]["input"] == [32, 32, 3] and out["config"]["classes"] == 10
+        assert out["config"]["loss"].startswith("CategoricalCE")
+        counts[ph] = out["config"]["trainable_params"]
+    assert counts["frozen"] == 1920 * 10 + 10  # GAP(1920) -> Dense(10) only
+    assert counts["frozen"] < counts["finetune"]
