@@ -17,6 +17,7 @@ from __future__ import annotations
 
 import argparse
 import json
+import sys
 import time
 
 import torch
@@ -173,9 +174,11 @@ def run(model_name: str, batch: int, steps: int, warmup: int, graph: bool, chann
     side = torch.cuda.Stream()
     side.wait_stream(torch.cuda.current_stream())
     with torch.cuda.stream(side):
-        for _ in range(warmup):
+        for i in range(warmup):
             opt.zero_grad(set_to_none=True)
             step()
+            torch.cuda.synchronize()  # MIOpen's first-call searches can take minutes: show progress
+            print(f"# warmup step {i} done", file=sys.stderr, flush=True)
     torch.cuda.current_stream().wait_stream(side)
     if graph:
         g = torch.cuda.CUDAGraph()

@@ -681,6 +681,32 @@ __global__ __launch_bounds__(256) void conv_igemm_kernel(ConvArgs a, GroupArg ga
         }
         *reinterpret_cast<float4*>(yp) = make_float4(o[0], o[1], o[2], o[3]);
         *reinterpret_cast<float4*>(yp + 4) = make_float4(o[4], o[5], o[6], o[7]);
+      } else if (a.out_mode != OUT_BF16) {
+        // fp32 gradient of a BatchNorm OUTPUT that also feeds a residual (MobileNetV2 block
+        // outputs): store (or accumulate into) dL/dy in fp32 and reduce that final value against
+        // the BN input mx -- the BN's backward reductions without a separate reduce pass
+        uint4 xv;
+        if constexpr (EPF) xv = ep_x[pass * EPI_IT + it];
+        else xv = *reinterpret_cast<const uint4*>(a.mx + (size_t)m * a.ldmx + n);
+        float* yp = reinterpret_cast<float*>(a.y) + (size_t)m * a.ldy + n;
+        if (a.out_mode == OUT_F32_ACC) {
+          const float4 o0 = *reinterpret_cast<const float4*>(yp);
+          const float4 o1 = *reinterpret_cast<const float4*>(yp + 4);
+          v[0] += o0.x; v[1] += o0.y; v[2] += o0.z; v[3] += o0.w;
+          v[4] += o1.x; v[5] += o1.y; v[6] += o1.z; v[7] += o1.w;
+        }
+        float xf[8];
+        unpack8(xv, xf);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const int cj = c8 * 8 + j;
+          const float z = xf[j] * (HOIST ? t_e0[j] : s_e0[cj]) + (HOIST ? t_e1[j] : s_e1[cj]);
+          v[j] = (z > msk_lo && z < msk_hi) ? v[j] : 0.f;
+          psum[j] += v[j];
+          psq[j] += v[j] * (xf[j] - (HOIST ? t_e2[j] : s_e2[cj])) * (HOIST ? t_e3[j] : s_e3[cj]);
+        }
+        *reinterpret_cast<float4*>(yp) = make_float4(v[0], v[1], v[2], v[3]);
+        *reinterpret_cast<float4*>(yp + 4) = make_float4(v[4], v[5], v[6], v[7]);
       } else {
         uint4 xv;
         if constexpr (EPF) xv = ep_x[pass * EPI_IT + it];

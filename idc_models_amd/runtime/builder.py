@@ -571,6 +571,13 @@ class Builder:
             a.epi_mode = 2 if bepi is not None else 1
             a.mx, a.ldmx = mx.ptr, mx.ld
             a.mbn = mbn
+            if bepi is None and dx.is_f32:
+                # epilogue 1 into fp32: dL/dy (accumulated for OUT_F32_ACC) stored unmasked-rounded
+                # and reduced against mx -- a BatchNorm OUTPUT's gradient (block outputs with a
+                # residual); an activation mask on an accumulated sum would be meaningless
+                if out_mode not in (nat.OUT_F32, nat.OUT_F32_ACC) or (out_mode == nat.OUT_F32_ACC and mbn.act):
+                    raise RuntimeError("fp32 epilogue-1 dgrad needs OUT_F32 / OUT_F32_ACC without activation")
+                a.out_mode = out_mode
             if gbn is not None:
                 a.gsum, a.gsumx, a.gsum_slots, a.gsum_ld = self.grad_sums(gbn, dx.M, self._conv_row_tiles(dx.M))
             elif self.det and (gsum is not None or gsumx is not None):

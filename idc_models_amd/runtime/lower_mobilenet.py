@@ -8,7 +8,9 @@ MI355X structure:
   apply the pending expand-BN + ReLU6 on load and reduce their own output statistics;
 * each block output ``BN_project(p) [+ residual]`` is materialised ONCE by ``bn_apply`` (it is the
   next block's expand input AND, for identity blocks, its residual);
-* backward: every BatchNorm backward is reduced once by its producer and APPLIED BY ITS CONSUMERS
+* backward: every BatchNorm backward is reduced once by its producer and APPLIED BY ITS CONSUMERS;
+  the project BN's reductions come from the epilogue of the dgrad that produces the block-output
+  gradient G (next expand / Conv_1, fp32, residual-accumulated), so no reduce pass runs for them
   (common.h BwdAff: A*dZ + B*x + C staged while loading dZ) — the pointwise dgrads for the
   Conv_1, project and expand BNs (they also write the staged operand for the side-lane weight
   gradient); only the depthwise BN keeps an apply pass (its depthwise consumers re-read dZ ~4.5x,
@@ -140,8 +142,20 @@ def lower_mobilenet(b: Builder, net, U: int, input_dtype):
     # the BatchNorm backward of Conv_1_bn is staged by its consumer: the dgrad applies
     # A*dZ + B*x + C while loading dZ (and folds the BN's reductions), and writes the staged
     # operand for the side-lane weight gradient (no separate apply pass)
+    def fold_ok(blk):
+        # the block-output gradient G's producer (the next expand dgrad, or Conv_1's) reduces the
+        # project BN's backward sums in its epilogue when the block continues into its project
+        # dgrad (which then reads G in fp32 through the BN-backward prologue): no reduce pass
+        return fz.before(blk["bn_p"].layer) and fz.before(blk["prj"])
+
+    def g_epilogue(blk):
+        if not fold_ok(blk):
+            return {}
+        return {"mx": blk["p"], "mbn": blk["bn_p"].args(), "gbn": blk["bn_p"]}
+
     G = b.nhwc(h_last.N, h_last.H, h_last.W, h_last.C, F32)
-    b.dgrad(zc, c1l, G, out_mode=nat.OUT_F32, bpro=b.bwd_aff(bn_c1, c1, fold=True), aout=dc1)
+    b.dgrad(zc, c1l, G, out_mode=nat.OUT_F32, bpro=b.bwd_aff(bn_c1, c1, fold=True), aout=dc1,
+            **g_epilogue(blocks[-1]))
     b.mark_grads_ready([bn_c1.gamma, bn_c1.beta])
     if fz.trainable(c1l):
         b.wgrad(h_last, c1l, dc1, b.arena.grad_of(c1l.kernel), lane=1)
@@ -151,8 +165,11 @@ def lower_mobilenet(b: Builder, net, U: int, input_dtype):
         p, bn_p, d, bn_d = blk["p"], blk["bn_p"], blk["d"], blk["bn_d"]
         prj, dwl = blk["prj"], blk["dwl"]
         # project BN (no activation): G is the gradient of BN_p(p) (+ residual passthrough)
-        zp = b.nhwc(p.N, p.H, p.W, p.C)
-        b.bn_bwd_reduce(G, p, bn_p, zp)
+        if fold_ok(blk):
+            zp = G  # reduced by G's producer; the project dgrad stages A*G + B*p + C from fp32
+        else:
+            zp = b.nhwc(p.N, p.H, p.W, p.C)
+            b.bn_bwd_reduce(G, p, bn_p, zp)
         if not fz.before(bn_p.layer):
             b.mark_grads_ready([bn_p.gamma, bn_p.beta])
             return
@@ -210,12 +227,13 @@ def lower_mobilenet(b: Builder, net, U: int, input_dtype):
             return
         h_prev = blk["h_in"]
         aff_in = b.bwd_aff(bn_in, e, fold=True)
+        gep = g_epilogue(blocks[blk["bid"] - 1])
         if blk["residual"]:
             # dL/dh_prev = G (identity shortcut) + expand^T de: accumulate into G in place
-            b.dgrad(ze, ex, G, out_mode=nat.OUT_F32_ACC, bpro=aff_in, aout=de)
+            b.dgrad(ze, ex, G, out_mode=nat.OUT_F32_ACC, bpro=aff_in, aout=de, **gep)
         else:
             G = b.nhwc(h_prev.N, h_prev.H, h_prev.W, h_prev.C, F32)
-            b.dgrad(ze, ex, G, out_mode=nat.OUT_F32, bpro=aff_in, aout=de)
+            b.dgrad(ze, ex, G, out_mode=nat.OUT_F32, bpro=aff_in, aout=de, **gep)
         b.mark_grads_ready([bn_in.gamma, bn_in.beta])
         if fz.trainable(ex):
             b.wgrad(h_prev, ex, de, b.arena.grad_of(ex.kernel), lane=1)
