@@ -87,9 +87,12 @@ struct HeadArgs {
   float* logits;    // [N][U]
   float* feats;     // [N][C]
   float* dlogits;   // [N][U]
-  float* loss;      // scalar, += mean loss
+  float* loss;      // scalar: mean loss (+= per sample when loss_vec is null)
   float loss_scale; // 1/N_global-batch-mean factor (1/N local)
   int training;
+  float* loss_vec;  // [N] per-sample losses: the last block sums them in sample order and WRITES
+                    // loss (run-to-run identical, no zero-fill before the head)
+  unsigned* ticket; // arrival counter of loss_vec (counts modulo N, never reset)
 };
 
 struct HeadBwdArgs {
@@ -142,6 +145,7 @@ __device__ __forceinline__ void gshift(HeadArgs& a, long long o) {
   // (no early return at o == 0: gsh also moves every pointer into the global address space)
   a.x = gsh(a.x, o); gshift(a.pro, o); a.w = gsh(a.w, o); a.b = gsh(a.b, o); a.labels = gsh(a.labels, o);
   a.logits = gsh(a.logits, o); a.feats = gsh(a.feats, o); a.dlogits = gsh(a.dlogits, o); a.loss = gsh(a.loss, o);
+  a.loss_vec = gsh(a.loss_vec, o); a.ticket = gsh(a.ticket, o);
 }
 __device__ __forceinline__ void gshift(HeadBwdArgs& a, long long o) {
   // (no early return at o == 0: gsh also moves every pointer into the global address space)
@@ -169,7 +173,7 @@ hipError_t finite_check(const float* g, long long n, int* flag, hipStream_t st);
 hipError_t finite_flag_reset(int* flag, int* status, hipStream_t st);
 hipError_t cast_weights(const CastEntry* d_entries, const int* tile_entry, long long ntiles, hipStream_t st);
 hipError_t input_stage(const void* x, int x_u8, int N, int H, int W, int C, bf16_t* y, int Cpad,
-                       hipStream_t st);
+                       const void* lab, int lab_code, int U, float* lab_out, hipStream_t st);
 hipError_t bn_stats(const bf16_t* x, int ldx, int M, int C, float* stats, int stats_ld,
                     int stats_off, int stats_slots, hipStream_t st);
 hipError_t bn_apply(const bf16_t* x, int ldx, BnArgs bn, const bf16_t* res, int ldres,

@@ -20,6 +20,7 @@
 #include <cstdlib>
 
 #include "nn_kernels.h"
+#include "persist.h"
 
 namespace idc {
 
@@ -843,7 +844,20 @@ __global__ __launch_bounds__(256) void head_fwd_kernel(HeadArgs a, GroupArg ga) 
           if (a.dlogits) a.dlogits[n * a.U + u] = (expf(lg[u] - lse) * tsum - y) * a.loss_scale;
         }
       }
-      if (a.loss) atomicAdd(a.loss, loss * a.loss_scale);
+      if (a.loss && a.loss_vec) {
+        // agent-scope store of this sample's loss, then one arrival; the block that completes the
+        // step's N arrivals sums them in sample order (agent-scope loads: other XCDs' L2s)
+        idc::persist::st_coh(a.loss_vec + n, loss);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        const unsigned t = __hip_atomic_fetch_add(a.ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if ((t + 1u) % (unsigned)a.N == 0u) {
+          float s = 0.f;
+          for (int i = 0; i < a.N; ++i) s += idc::persist::ld_coh(a.loss_vec + i);
+          *a.loss = s * a.loss_scale;
+        }
+      } else if (a.loss) {
+        atomicAdd(a.loss, loss * a.loss_scale);
+      }
     }
   }
 }
@@ -1104,12 +1118,28 @@ hipError_t cast_weights(const CastEntry* d_entries, const int* tile_entry, long 
 }
 
 // ------------------------------------------------------------------------------------------
+// Input staging, the first op of every training / inference step: uint8 (x/255) or fp32 NHWC
+// pixels -> bf16 [.., Cpad] operand, and (lab_code != 0) the labels -> fp32 head labels in the same
+// launch (the caller's own tensors are read directly: no staging copies before the step).
+// lab_code: 1 fp32, 2 int64, 3 int32, 4 uint8; U == 1: out[i] = y[i]; U > 1: integer class ids
+// become one-hot rows, fp32 input is an [N, U] matrix copied as is.
+__device__ __forceinline__ float load_label(const void* y, int code, long long i) {
+  switch (code) {
+    case 1: return reinterpret_cast<const float*>(y)[i];
+    case 2: return (float)reinterpret_cast<const long long*>(y)[i];
+    case 3: return (float)reinterpret_cast<const int*>(y)[i];
+    default: return (float)reinterpret_cast<const uint8_t*>(y)[i];
+  }
+}
+
 __global__ __launch_bounds__(256) void input_stage_kernel(const void* x, int u8, long long npix, int C,
-                                                          bf16_t* y, int Cpad, GroupArg ga) {
+                                                          bf16_t* y, int Cpad, const void* lab, int lab_code,
+                                                          int N, int U, float* lab_out, GroupArg ga) {
   x = gsh(x, goff(ga));
   y = gsh(y, goff(ga));
-  for (long long p = blockIdx.x * (long long)blockDim.x + threadIdx.x; p < npix;
-       p += (long long)gridDim.x * blockDim.x) {
+  const long long tid0 = blockIdx.x * (long long)blockDim.x + threadIdx.x;
+  const long long nthr = (long long)gridDim.x * blockDim.x;
+  for (long long p = tid0; p < npix; p += nthr) {
     float v[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     for (int c = 0; c < C && c < 8; ++c) {
       v[c] = u8 ? (float)reinterpret_cast<const uint8_t*>(x)[p * C + c] * (1.f / 255.f)
@@ -1120,14 +1150,31 @@ __global__ __launch_bounds__(256) void input_stage_kernel(const void* x, int u8,
       *reinterpret_cast<uint4*>(y + p * Cpad + c0) = q;
     }
   }
+  if (lab_code) {
+    lab_out = gsh(lab_out, goff(ga));
+    const long long nl = (long long)N * U;
+    for (long long q = tid0; q < nl; q += nthr) {
+      float o;
+      if (U == 1 || lab_code == 1) {
+        o = load_label(lab, lab_code, q);
+      } else {
+        const long long i = q / U;
+        o = (long long)load_label(lab, lab_code, i) == q - i * U ? 1.f : 0.f;
+      }
+      lab_out[q] = o;
+    }
+  }
 }
 
 hipError_t input_stage(const void* x, int x_u8, int N, int H, int W, int C, bf16_t* y, int Cpad,
-                       hipStream_t st) {
+                       const void* lab, int lab_code, int U, float* lab_out, hipStream_t st) {
+  if (lab_code && (lab == nullptr || lab_out == nullptr || U < 1 || lab_code > 4)) return hipErrorInvalidValue;
   long long npix = (long long)N * H * W;
   long long blocks = (npix + 255) / 256;
   if (blocks > 4096) blocks = 4096;
-  hipLaunchKernelGGL(input_stage_kernel, ggrid((int)blocks), dim3(256), 0, st, x, x_u8, npix, C, y, Cpad, garg());
+  if (blocks < 1) blocks = 1;
+  hipLaunchKernelGGL(input_stage_kernel, ggrid((int)blocks), dim3(256), 0, st, x, x_u8, npix, C, y, Cpad, lab,
+                     lab_code, N, U, lab_out, garg());
   return hipGetLastError();
 }
 

@@ -150,6 +150,9 @@ class Plan {
   }
 
   uintptr_t get_ptr(int idx, int slot) const { return ops_.at(idx).p[slot & 7]; }
+  // per-step operands of a directly issued op (the input stage reads the caller's tensors); an op
+  // inside a captured graph keeps the pointers it was captured with
+  void set_ptr(int idx, int slot, uintptr_t v) { ops_.at(idx).p[slot & 7] = v; }
   long long get_long(int idx, int slot) const { return ops_.at(idx).l[slot & 3]; }
   void set_float(int idx, int slot, float v) { ops_.at(idx).f[slot] = v; }
   void set_int(int idx, int slot, int v) { ops_.at(idx).i[slot] = v; }
@@ -588,7 +591,8 @@ class Plan {
         break;
       case OP_INPUT:
         check(input_stage(reinterpret_cast<const void*>(op.p[0]), op.i[0], op.i[1], op.i[2], op.i[3], op.i[4],
-                          reinterpret_cast<bf16_t*>(op.p[1]), op.i[5], st),
+                          reinterpret_cast<bf16_t*>(op.p[1]), op.i[5], reinterpret_cast<const void*>(op.p[2]),
+                          op.i[6], op.i[7], reinterpret_cast<float*>(op.p[3]), st),
               "input_stage");
         break;
       case OP_MEMSET:
@@ -926,6 +930,7 @@ PYBIND11_MODULE(_idc_native, m) {
       .def("set_comm", &Plan::set_comm, py::keep_alive<1, 2>())
       .def("set_groups", &Plan::set_groups)
       .def("get_ptr", &Plan::get_ptr)
+      .def("set_ptr", &Plan::set_ptr)
       .def("get_long", &Plan::get_long)
       .def("groups", &Plan::groups)
       .def("has_comm_ops", &Plan::has_comm_ops)

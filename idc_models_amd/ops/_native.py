@@ -98,7 +98,8 @@ class ShiftDesc(C.Structure):
 class HeadArgs(C.Structure):
     _fields_ = [("x", vp), ("ldx", ci), ("N", ci), ("HW", ci), ("C", ci), ("U", ci),
                 ("pro", BnArgs), ("w", vp), ("b", vp), ("labels", vp), ("logits", vp),
-                ("feats", vp), ("dlogits", vp), ("loss", vp), ("loss_scale", cf), ("training", ci)]
+                ("feats", vp), ("dlogits", vp), ("loss", vp), ("loss_scale", cf), ("training", ci),
+                ("loss_vec", vp), ("ticket", vp)]
 
 
 class HeadBwdArgs(C.Structure):

@@ -78,7 +78,9 @@ def emit_head(b: Builder, feat: Tensor4, pro: Optional[nat.BnArgs], dense, U: in
     a.loss = io.loss.data_ptr()
     a.loss_scale = 1.0 / float(feat.N)
     a.training = 1 if training else 0
-    b.memset(io.loss)
+    # per-sample losses summed in sample order by the last block (deterministic, no zero-fill op)
+    a.loss_vec = b.alloc((feat.N,), F32).data_ptr()
+    a.ticket = b.alloc((1,), torch.int32).data_ptr()
     b.emit(nat.OP_HEAD_FWD, a)
     io.feats_ptr = a.feats
     return a

@@ -86,6 +86,20 @@ class FusedProgram:
         self.b = b
         self.xin = b.xin
         self.io = b.io
+        # the input stage (OP_INPUT) becomes the program's first op and is issued directly (never
+        # captured): each step points it at the caller's own x / y tensors, so staging the inputs
+        # costs one launch and no copies (FusedStep._stage_inputs)
+        self.input_op = None
+        k = next((i for i, op in enumerate(b.ops) if op[1] == nat.OP_INPUT), None)
+        if k is not None and all(op[0] == "fwd" and op[1] == nat.OP_MEMSET for op in b.ops[:k]) \
+                and b.ops[k][0] == "fwd" and not any(pos <= k for pos, _ in b.bwd_marks):
+            seg, kind, raw, ints, floats, longs, ptrs, lane = b.ops.pop(k)
+            ints = list(ints) + [0] * (8 - len(ints))
+            ints[6], ints[7] = 0, self.U
+            ptrs = list(ptrs) + [0] * (4 - len(ptrs))
+            ptrs[2], ptrs[3] = 0, self.io.labels.data_ptr()
+            b.ops.insert(0, (seg, kind, raw, ints, floats, longs, ptrs, lane))
+            self.input_op = 0
         b.finalize_casts()
         b.finalize_moving()
         # optimizer segment
@@ -334,7 +348,16 @@ class FusedProgram:
     def run_segment(self, name: str):
         if name in self.seg:
             with trace.range("seg:" + name):
-                self.run_range(*self.seg[name])
+                lo, hi = self.seg[name]
+                if name == "fwd" and self.input_op == lo:
+                    # direct issue with this step's operands, then back to the program's own
+                    # buffers (a later forward without staging reads xin, as before)
+                    self.plan.run(lo, lo + 1, self._sh(), True)
+                    self.plan.set_ptr(lo, 0, self.xin.data_ptr())
+                    self.plan.set_ptr(lo, 2, 0)
+                    self.plan.set_int(lo, 6, 0)
+                    lo += 1
+                self.run_range(lo, hi)
 
     def set_lr(self, lr: float):
         if self.rms_index is not None:
@@ -345,6 +368,31 @@ class FusedProgram:
 
     def close(self):
         self.plan.clear_graphs()
+
+
+_LABEL_CODES = {torch.float32: 1, torch.int64: 2, torch.int32: 3, torch.uint8: 4}
+
+
+def _direct_input_codes(p: "FusedProgram", x, y):
+    """None: stage through copies.  Else the input op's label code (0: no labels) for reading the
+    caller's x / y in place: same device, dtype and shape as the program's input, contiguous;
+    labels as the head takes them (U == 1: [B]; U > 1: [B] class ids or an [B, U] fp32 matrix)."""
+    if p.input_op is None or p.group is not None or not isinstance(x, torch.Tensor):
+        return None
+    xin = p.xin
+    if x.device != xin.device or x.dtype != xin.dtype or x.shape != xin.shape or not x.is_contiguous():
+        return None
+    if y is None:
+        return 0
+    if not isinstance(y, torch.Tensor) or y.device != xin.device or not y.is_contiguous():
+        return None
+    code = _LABEL_CODES.get(y.dtype)
+    if code is None:
+        return None
+    B, U = xin.shape[0], p.U
+    if U == 1 or code != 1:
+        return code if y.numel() == B else None
+    return code if tuple(y.shape) == (B, U) else None
 
 
 def _labels_to(io_labels: torch.Tensor, y: torch.Tensor, U: int):
@@ -386,6 +434,17 @@ class FusedStep:
     def _stage_inputs(self, p: FusedProgram, x, y):
         cur = torch.cuda.current_stream(self.m.device)
         p.stream.wait_stream(cur)
+        code = _direct_input_codes(p, x, y)
+        if code is not None:
+            # the input op reads x and y where they are (one launch, no copies); they stay
+            # allocated until it has run on the program stream
+            p.plan.set_ptr(p.input_op, 0, x.data_ptr())
+            x.record_stream(p.stream)
+            if code:
+                p.plan.set_ptr(p.input_op, 2, y.data_ptr())
+                p.plan.set_int(p.input_op, 6, code)
+                y.record_stream(p.stream)
+            return
         with torch.cuda.stream(p.stream):
             p.xin.copy_(x.to(p.xin.device, non_blocking=True).to(p.xin.dtype))
             if y is not None:

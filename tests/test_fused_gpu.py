@@ -49,8 +49,10 @@ def _cos(a, b):
 
 def _check(m, ref, x, y, slack=0.03, loss_slack=None):
     """Fused (bf16) vs eager fp32, judged against the eager bf16-autocast drift from fp32 (the
-    precision floor of bf16 training): per parameter, 1-cos(fused,fp32) must stay within
-    3x the autocast deficit + ``slack``; logits within 2x the autocast deviation + 0.05."""
+    precision floor of bf16 training) on the same net and batch: per parameter, the relative L2
+    error vs fp32 must stay within 1.5x autocast's + 0.02 (idc_models_amd/utils/fidelity.py;
+    direction and magnitude); logits within 2x the autocast deviation + 0.05."""
+    from idc_models_amd.utils.fidelity import grad_failures
     ref16 = copy.deepcopy(ref)
     p = m.impl._prog(x.shape[0], True, torch.uint8)
     m.impl._stage_inputs(p, x, y)
@@ -67,13 +69,8 @@ def _check(m, ref, x, y, slack=0.03, loss_slack=None):
     dev_fused = (lg - logits_ref.reshape(-1)).abs().max().item()
     dev_auto = (logits16.reshape(-1) - logits_ref.reshape(-1)).abs().max().item()
     assert dev_fused < 2 * dev_auto + 0.05, (dev_fused, dev_auto)
-    arena = m.arena
-    for i, (pm, gr, g16) in enumerate(zip(arena.params, grads_ref, grads16)):
-        gf = arena.view(arena.grad, i)
-        if gr.norm() < 1e-12:
-            continue
-        c, c16 = _cos(gf, gr), _cos(g16, gr)
-        assert (1 - c) <= 3 * (1 - c16) + slack, (i, tuple(pm.shape), c, c16)
+    bad = grad_failures(m.arena, m.arena.grad, [g.double() for g in grads_ref], [g.double() for g in grads16])
+    assert not bad, bad[:8]
 
 
 def test_densenet121_fused_matches_eager():
@@ -279,22 +276,30 @@ def test_moving_statistics_match_eager_every_bn(arch):
     assert not bad, bad[:12]
 
 
+def _fp32_yardsticks(seed, x, y):
+    """fp32 and bf16-autocast eager gradients of the seed's DenseNet-121 (first step)."""
+    from idc_models_amd.models import build_model
+    from idc_models_amd.utils.fidelity import eager_grads
+    net = build_model("densenet121", None, num_outputs=1, seed=seed).to(DEV)
+    return eager_grads(net, x, y, "fp32"), eager_grads(net, x, y, "autocast")
+
+
 @pytest.mark.parametrize("maxm", ["2304", "9216"])
 def test_batched_weight_gradients_match_per_layer(monkeypatch, maxm):
     """DenseNet-121 at the bench batch: the late stages' weight gradients launched as one batched
-    kernel per shape (OP_WGRAD_BATCH, the default for M <= 2304 pixels; here also stage 2) against
-    the per-layer launches.  Without IDC_DETERMINISTIC the statistics' float-atomic order already
-    makes two identical per-layer programs differ (bf16 roundings flip and propagate through 120
-    layers), so the batched program must sit within the per-layer run-to-run spread; the kernel
+    kernel per shape (OP_WGRAD_BATCH, the default for M <= 2304 pixels; here also stage 2) and the
+    per-layer launches, EACH against the fp32 eager gradient of the same weights and batch: every
+    parameter within 1.5x bf16 autocast's relative error + 0.02 (utils/fidelity.py).  The kernel
     itself is checked exactly in test_kernels_gpu.py::test_wgrad_batch_matches_single_launches."""
     from idc_models_amd.engine import Model, RMSprop
     from idc_models_amd.models import build_model
     from idc_models_amd.ops import _native as nat
+    from idc_models_amd.utils.fidelity import grad_failures, whole_rel
     g = torch.Generator().manual_seed(17)
     x = torch.randint(0, 256, (256, 50, 50, 3), generator=g, dtype=torch.uint8)
     y = torch.randint(0, 2, (256,), generator=g)
-    grads = []
-    for mm in ("0", "0", maxm):
+    g32, g16 = _fp32_yardsticks(3, x, y)
+    for mm in ("0", maxm):
         monkeypatch.setenv("IDC_WG_BATCH_MAXM", mm)
         net = build_model("densenet121", None, num_outputs=1, seed=3)
         m = Model(net, device=DEV)
@@ -304,32 +309,31 @@ def test_batched_weight_gradients_match_per_layer(monkeypatch, maxm):
         p = m.impl._prog(256, True, torch.uint8)
         nb = sum(1 for i in range(p.plan.size()) if p.plan.kind(i) == nat.OP_WGRAD_BATCH)
         assert (nb > 0) == (mm != "0"), (mm, nb)
-        grads.append(m.arena.grad.clone())
-    g0, g1, gb = grads
-
-    def rel(a, b):
-        return float((a - b).norm() / (b.norm() + 1e-12))
-
-    noise, dev = rel(g1, g0), rel(gb, g0)
-    assert dev <= 3 * noise + 1e-3, (dev, noise)
+        bad = grad_failures(m.arena, m.arena.grad, g32, g16)
+        print("maxm", mm, "whole rel vs fp32", whole_rel(m.arena, m.arena.grad, g32))
+        assert not bad, (mm, bad[:8])
+        m.impl.close()
 
 
 @pytest.mark.parametrize("B,maxm", [(8, "2304"), (256, "512"), (256, "9216"), (256, "2304")])
 def test_dense_stage_matches_per_layer(monkeypatch, B, maxm):
-    """DenseNet-121 at the bench batch: the late stages' dense layers as ONE persistent work-queue
-    launch each (OP_DENSE_STAGE, csrc/kernels/dense_stage.hip; default for M <= 2304 pixels, here
-    also stage 2; both hand-off modes) against the per-layer convs on the same weights and input.  Forward stage buffers
-    and every statistics array must agree to the per-layer program's own run-to-run spread (float
-    atomics order), the timeout flag must stay clear, and the training step's gradients too."""
+    """DenseNet-121: the late stages' dense layers as ONE persistent work-queue launch each
+    (OP_DENSE_STAGE, csrc/kernels/dense_stage.hip; default for M <= 2304 pixels, here also stage 2)
+    against the per-layer convs on the same weights and input.  Forward stage buffers and every
+    statistics array agree with the per-layer program to a FIXED bf16-level bound, the timeout
+    counter stays zero, and both programs' training-step gradients pass the fp32 check
+    (utils/fidelity.py: per parameter within 1.5x bf16 autocast's relative error + 0.02)."""
     from idc_models_amd.engine import Model, RMSprop
     from idc_models_amd.models import build_model
     from idc_models_amd.ops import _native as nat
+    from idc_models_amd.utils.fidelity import grad_failures
     g = torch.Generator().manual_seed(5)
     x = torch.randint(0, 256, (B, 50, 50, 3), generator=g, dtype=torch.uint8)
     y = torch.randint(0, 2, (B,), generator=g)
+    g32, g16 = _fp32_yardsticks(4, x, y)
     outs = []
     want = {8: 4, 256: {"512": 1, "2304": 2, "9216": 3}[maxm]}[B]
-    for on in ("0", "0", "1"):
+    for on in ("0", "1"):
         monkeypatch.setenv("IDC_DENSE_STAGE", on)
         monkeypatch.setenv("IDC_DENSE_STAGE_MAXM", maxm)
         net = build_model("densenet121", None, num_outputs=1, seed=4)
@@ -349,19 +353,65 @@ def test_dense_stage_matches_per_layer(monkeypatch, B, maxm):
             assert int(p.b.dense_err[0]) == 0
         p.run_segment("bwd")
         torch.cuda.synchronize()
-        outs.append((bufs, stats, m.arena.grad.clone(), float(p.io.loss.item())))
+        bad = grad_failures(m.arena, m.arena.grad, g32, g16)
+        assert not bad, (on, bad[:8])
+        outs.append((bufs, stats, float(p.io.loss.item())))
+        m.impl.close()
 
     def rel(a, b):
         return float((a - b).norm() / (b.norm() + 1e-12))
 
-    (b0, s0, g0, l0), (b1, s1, g1, l1), (bd, sd, gd, ld) = outs
-    print("stage buf noise/dev", [(round(rel(b1[i], b0[i]), 5), round(rel(bd[i], b0[i]), 5)) for i in range(len(b0))])
-    print("stats", rel(s1, s0), rel(sd, s0), "grads", rel(g1, g0), rel(gd, g0), "loss", l0, l1, ld)
+    (b0, s0, l0), (bd, sd, ld) = outs
+    print("stage buf rel", [round(rel(bd[i], b0[i]), 5) for i in range(len(b0))], "stats", rel(sd, s0),
+          "loss", l0, ld)
+    # bf16 rounding flips between two summation orders move a stage buffer by ~1e-3 relative
     for i in range(len(b0)):
-        noise, dev = rel(b1[i], b0[i]), rel(bd[i], b0[i])
-        assert dev <= 3 * noise + 2e-3, ("stage", i, dev, noise)
-    assert rel(sd, s0) <= 3 * rel(s1, s0) + 2e-3, (rel(sd, s0), rel(s1, s0))
-    assert rel(gd, g0) <= 3 * rel(g1, g0) + 2e-3, (rel(gd, g0), rel(g1, g0))
-    # the loss: within the run-to-run spread or 1% (two identical per-layer runs can agree to 3e-4
-    # by chance while bf16 rounding flips move it by ~0.3%)
-    assert abs(ld - l0) <= max(3 * abs(l1 - l0), 0.01 * abs(l0)) + 1e-3, (ld, l0, l1)
+        assert rel(bd[i], b0[i]) <= 1e-2, ("stage", i, rel(bd[i], b0[i]))
+    assert rel(sd, s0) <= 1e-2, rel(sd, s0)
+    assert abs(ld - l0) <= 0.01 * abs(l0) + 1e-3, (ld, l0)
+
+
+@pytest.mark.parametrize("ydt", [torch.int64, torch.int32, torch.float32, torch.uint8])
+def test_direct_input_staging_matches_copies(monkeypatch, ydt):
+    """The input op reads the caller's device x / y in place (one launch, labels converted inside
+    it): deterministic forward+backward bitwise equal to the staged-copy path (host tensors)."""
+    monkeypatch.setenv("IDC_DETERMINISTIC", "1")
+    from idc_models_amd.engine import Model, RMSprop
+    from idc_models_amd.models import build_model
+    from idc_models_amd.runtime.program import _direct_input_codes
+    g = torch.Generator().manual_seed(2)
+    x = torch.randint(0, 256, (8, 50, 50, 3), generator=g, dtype=torch.uint8)
+    y = torch.randint(0, 2, (8,), generator=g).to(ydt)
+    outs = []
+    for direct in (False, True):
+        m = Model(build_model("densenet121", None, 1, seed=6), device=DEV)
+        m.compile(RMSprop(1e-4), "binary_crossentropy", [], backend="fused")
+        p = m.impl._prog(8, True, torch.uint8)
+        xs, ys = (x.to(DEV), y.to(DEV)) if direct else (x, y)
+        assert (_direct_input_codes(p, xs, ys) is not None) == direct
+        m.impl._stage_inputs(p, xs, ys)
+        p.run_segment("fwd")
+        p.run_segment("bwd")
+        torch.cuda.synchronize()
+        outs.append((p.io.loss.clone(), p.io.logits.clone(), m.arena.grad.clone(), p.io.labels.clone()))
+        m.impl.close()
+    for a, b in zip(*outs):
+        assert torch.equal(a, b)
+
+
+def test_direct_input_staging_one_hot_labels(monkeypatch):
+    """U > 1: integer class ids become one-hot label rows inside the input op."""
+    monkeypatch.setenv("IDC_DETERMINISTIC", "1")
+    from idc_models_amd.engine import Model, RMSprop
+    from idc_models_amd.models import build_model
+    m = Model(build_model("densenet201", (32, 32, 3), 10, seed=6), device=DEV)
+    m.compile(RMSprop(1e-4), "categorical_crossentropy", [], backend="fused")
+    g = torch.Generator().manual_seed(2)
+    x = torch.randint(0, 256, (16, 32, 32, 3), generator=g, dtype=torch.uint8).to(DEV)
+    y = torch.randint(0, 10, (16,), generator=g).to(DEV)
+    p = m.impl._prog(16, True, torch.uint8)
+    m.impl._stage_inputs(p, x, y)
+    p.run_segment("fwd")
+    torch.cuda.synchronize()
+    assert torch.equal(p.io.labels.reshape(16, 10), torch.nn.functional.one_hot(y, 10).float())
+    m.impl.close()
