@@ -133,13 +133,25 @@ def _keras_frozen_weighted(model_name: str, phase: str, size: int, classes: int)
     return sum(1 for l in layers if l.keras_class in ("Conv2D", "BatchNormalization", "DepthwiseConv2D"))
 
 
+def _heartbeat(stop):
+    """MIOpen compiles (and with benchmark mode searches) every new conv shape on first use: a
+    201-layer network on a fresh box stays inside its first step for minutes.  Say so."""
+    t0 = time.time()
+    while not stop.wait(30):
+        print(f"# still in MIOpen first-use compilation / search after {time.time() - t0:.0f} s",
+              file=sys.stderr, flush=True)
+
+
 def run(model_name: str, batch: int, steps: int, warmup: int, graph: bool, channels_last: bool = True,
-        size: int = 50, classes: int = 1, phase: str = "full") -> dict:
+        size: int = 50, classes: int = 1, phase: str = "full", benchmark: bool = True) -> dict:
     """Time one stock training step (bf16 autocast forward, fp32 loss, backward, RMSprop).
     ``graph``: the whole step captured once into a HIP graph (torch.cuda.graphs, capturable
     RMSprop) and replayed — the strongest stock configuration (no per-kernel host launches)."""
+    import threading
     dev = torch.device("cuda")
-    torch.backends.cudnn.benchmark = True
+    torch.backends.cudnn.benchmark = benchmark
+    stop = threading.Event()
+    threading.Thread(target=_heartbeat, args=(stop,), daemon=True).start()
     torch.manual_seed(0)
     ctor = {"densenet121": DenseNet121, "densenet201": densenet201, "vgg16": vgg16, "mobilenetv2": mobilenetv2}
     model = ctor[model_name](classes=classes).to(dev)
@@ -198,9 +210,10 @@ def run(model_name: str, batch: int, steps: int, warmup: int, graph: bool, chann
         run_step()
     torch.cuda.synchronize()
     dt = (time.perf_counter() - t) / steps
+    stop.set()
     return {"baseline": "stock_pytorch_%s_bf16_autocast" % ("hipgraph" if graph else "eager"),
             "model": model_name, "batch": batch, "input": [size, size, 3], "classes": classes, "phase": phase,
-            "frozen_weighted_layers": nfreeze, "ms_per_step": round(dt * 1e3, 3),
+            "frozen_weighted_layers": nfreeze, "miopen_benchmark": benchmark, "ms_per_step": round(dt * 1e3, 3),
             "images_per_sec": round(batch / dt, 1), "channels_last": channels_last,
             "torch": torch.__version__, "device": torch.cuda.get_device_name()}
 
@@ -216,6 +229,8 @@ def main():
     ap.add_argument("--input", type=int, default=50, help="square input size")
     ap.add_argument("--classes", type=int, default=1)
     ap.add_argument("--phase", default="full", choices=["full", "frozen", "finetune"])
+    ap.add_argument("--no-benchmark", action="store_true",
+                    help="MIOpen immediate mode (PyTorch's default) instead of benchmark-mode search")
     ap.add_argument("--all", metavar="OUT_JSON", help="every model, eager and graph; write JSON")
     ap.add_argument("--append", metavar="JSON", help="append this run's eager and graph results to JSON")
     args = ap.parse_args()
@@ -224,7 +239,7 @@ def main():
             doc = json.load(f)
         for graph in (False, True):
             r = run(args.model, args.batch, args.steps, args.warmup, graph, not args.no_channels_last,
-                    args.input, args.classes, args.phase)
+                    args.input, args.classes, args.phase, not args.no_benchmark)
             print(json.dumps(r), flush=True)
             doc["results"].append(r)
         with open(args.append, "w") as f:
@@ -248,7 +263,8 @@ def main():
                        "results": results}, f, indent=1)
         return
     print(json.dumps(run(args.model, args.batch, args.steps, args.warmup, args.graph,
-                         not args.no_channels_last, args.input, args.classes, args.phase)))
+                         not args.no_channels_last, args.input, args.classes, args.phase,
+                         not args.no_benchmark)))
 
 
 if __name__ == "__main__":

@@ -38,6 +38,26 @@ def eager_grads(net, x_u8: torch.Tensor, y: torch.Tensor, mode: str = "fp32") ->
     return [g.detach().double() for g in torch.autograd.grad(loss, ps)]
 
 
+def eager_activations(net, x_u8: torch.Tensor, names: Sequence[str], mode: str = "fp32") -> Dict[str, torch.Tensor]:
+    """Outputs of the named layers of a deep copy of ``net`` (training-mode forward, ``mode`` as
+    in ``eager_grads``), as float64 NHWC tensors."""
+    ref = copy.deepcopy(net)
+    dev = next(iter(ref.parameters())).device
+    xs = x_u8.to(dev).float() / 255.0
+    if mode == "bf16in":
+        xs = xs.bfloat16().float()
+    base = getattr(ref, "base", ref)
+    out: Dict[str, torch.Tensor] = {}
+    hooks = [base.get_layer(n).register_forward_hook(
+        lambda _m, _i, o, n=n: out.__setitem__(n, o.detach().double())) for n in names]
+    ref.train()
+    with torch.no_grad(), torch.autocast(dev.type, dtype=torch.bfloat16, enabled=(mode == "autocast")):
+        ref(xs)
+    for h in hooks:
+        h.remove()
+    return out
+
+
 def _cos(a: torch.Tensor, b: torch.Tensor) -> float:
     a, b = a.reshape(-1).double(), b.reshape(-1).double()
     return float(a @ b / (a.norm() * b.norm() + 1e-300))
