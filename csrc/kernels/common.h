@@ -467,6 +467,10 @@ __device__ __forceinline__ void bn_full_table(const BnArgs& b, int C, float* s_s
 // All pointers are pre-offset to the operand's first channel.  Optionally one workgroup of the
 // consumer folds the statistics-slot copies of the reductions into the BatchNorm's d beta / d gamma
 // (fold_*: channels [0, fold_C) from gsum/gsumx bases fgsum/fgsumx).
+// mode 1: pending BatchNorm BACKWARD (v' = A*dZ + B*x + C, A/B/C from the BN's statistics and
+// gradient sums; unit_alpha: A = 1).  mode 2: a BatchNorm FORWARD applied while a consumer stages
+// its operand, plus an optional residual tensor x (unit_alpha = 1: v' = sc*v + sh + x) -- the
+// MobileNetV2 block output BN_project(p) [+ h_in] built inside the next expand conv.
 struct BwdAff {
   const bf16_t* x; int ldx;
   BnArgs bn;
@@ -506,7 +510,7 @@ __device__ __forceinline__ void bwd_aff_table(const BwdAff& b, int c0, int n, in
     const float g = b.bn.gamma ? b.bn.gamma[c] : 1.f;
     if (b.bn.mode == 1) {
       slot_sums_1(b.bn.stats, b.bn.stats + b.bn.C, SS, 2 * (size_t)b.bn.C, c, m0, m1);
-      slot_sums_1(b.gsum, b.gsumx, SG, (size_t)b.gsum_ld, c, q0, q1);
+      if (b.mode == 1) slot_sums_1(b.gsum, b.gsumx, SG, (size_t)b.gsum_ld, c, q0, q1);
     } else {
       m0 = b.bn.mmean[c];
       m1 = b.bn.mvar[c];
@@ -514,6 +518,12 @@ __device__ __forceinline__ void bwd_aff_table(const BwdAff& b, int c0, int n, in
     float mean = m0, var = m1;
     if (b.bn.mode == 1) shifted_mean_var(bn_shift(b.bn, c), m0, m1, b.bn.inv_count, mean, var);
     const float rstd = rsqrtf(var + b.bn.eps);
+    if (b.mode == 2) {  // forward BatchNorm (+ residual x): v' = g*rstd*v + [x] + beta - mean*g*rstd
+      sA[i] = g * rstd;
+      sB[i] = b.unit_alpha ? 1.f : 0.f;
+      sC[i] = (b.bn.beta ? b.bn.beta[c] : 0.f) - mean * g * rstd;
+      continue;
+    }
     const float sd = q0 * b.inv_n, sdx = q1 * b.inv_n;
     const float Bc = -g * rstd * rstd * sdx;
     sA[i] = b.unit_alpha ? 1.f : g * rstd;
@@ -557,21 +567,28 @@ __device__ __forceinline__ bool bwd_aff_slots4(const BwdAff& b) {
 // raw inputs of one channel of a BwdAff table (training-mode BatchNorm, <= 4 slots)
 struct BwdAffRaw {
   Raw4 st, gs;
-  float g, k;
+  float g, k, be;
 };
 __device__ __forceinline__ void bwd_aff_load(const BwdAff& b, int c, BwdAffRaw& r) {
   load4(b.bn.stats, b.bn.stats + b.bn.C, stat_slots(b.bn.slots), 2 * (size_t)b.bn.C, c, r.st);
-  load4(b.gsum, b.gsumx, stat_slots(b.gsum_slots), (size_t)b.gsum_ld, c, r.gs);
+  if (b.mode == 1) load4(b.gsum, b.gsumx, stat_slots(b.gsum_slots), (size_t)b.gsum_ld, c, r.gs);
   r.g = b.bn.gamma ? b.bn.gamma[c] : 1.f;
   r.k = bn_shift(b.bn, c);
+  r.be = (b.mode == 2 && b.bn.beta) ? b.bn.beta[c] : 0.f;
 }
 __device__ __forceinline__ void bwd_aff_finish(const BwdAff& b, const BwdAffRaw& r, float& A, float& B, float& C) {
   float m0, m1, q0, q1;
   sum4(r.st, stat_slots(b.bn.slots), m0, m1);
-  sum4(r.gs, stat_slots(b.gsum_slots), q0, q1);
   float mean, var;
   shifted_mean_var(r.k, m0, m1, b.bn.inv_count, mean, var);
   const float rstd = rsqrtf(var + b.bn.eps);
+  if (b.mode == 2) {  // forward BatchNorm (+ residual), see bwd_aff_table
+    A = r.g * rstd;
+    B = b.unit_alpha ? 1.f : 0.f;
+    C = r.be - mean * A;
+    return;
+  }
+  sum4(r.gs, stat_slots(b.gsum_slots), q0, q1);
   const float Bc = -r.g * rstd * rstd * (q1 * b.inv_n);
   A = b.unit_alpha ? 1.f : r.g * rstd;
   B = Bc;

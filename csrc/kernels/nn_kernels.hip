@@ -846,24 +846,30 @@ __global__ __launch_bounds__(256) void head_fwd_kernel(HeadArgs a, GroupArg ga) 
       }
       if (a.loss && a.loss_vec) {
         // agent-scope store of this sample's loss, then one arrival; the block that completes the
-        // step's N arrivals sums them in sample order (agent-scope loads: other XCDs' L2s)
+        // step's N arrivals sums them (agent-scope loads: other XCDs' L2s) in a fixed order
         idc::persist::st_coh(a.loss_vec + n, loss);
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         const unsigned t = __hip_atomic_fetch_add(a.ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        if ((t + 1u) % (unsigned)a.N == 0u) {
-          float s = 0.f;
-          for (int i = 0; i < a.N; ++i) s += idc::persist::ld_coh(a.loss_vec + i);
-          *a.loss = s * a.loss_scale;
-        }
+        s_red[4 * a.U] = ((t + 1u) % (unsigned)a.N == 0u) ? 1.f : 0.f;
       } else if (a.loss) {
         atomicAdd(a.loss, loss * a.loss_scale);
       }
     }
   }
+  if (!(a.loss && a.loss_vec && (a.training || a.loss))) return;
+  __syncthreads();
+  float* s_fin = s_red + 4 * a.U;  // [flag, 4 wave partials] (launch reserves 8 floats)
+  if (s_fin[0] == 0.f) return;     // block-uniform: not the last arrival
+  float v = 0.f;
+  for (int i = threadIdx.x; i < a.N; i += blockDim.x) v += idc::persist::ld_coh(a.loss_vec + i);
+  v = wave_sum(v);
+  if (lane == 0) s_fin[1 + wid] = v;
+  __syncthreads();
+  if (threadIdx.x == 0) *a.loss = (s_fin[1] + s_fin[2] + s_fin[3] + s_fin[4]) * a.loss_scale;
 }
 
 hipError_t head_fwd(const HeadArgs& a, hipStream_t st) {
-  hipLaunchKernelGGL(head_fwd_kernel, ggrid(a.N), dim3(256), (a.C + 4 * a.U) * 4, st, a, garg());
+  hipLaunchKernelGGL(head_fwd_kernel, ggrid(a.N), dim3(256), (a.C + 4 * a.U + 8) * 4, st, a, garg());
   return hipGetLastError();
 }
 

@@ -464,10 +464,27 @@ class Builder:
         a.mode = 1
         return a
 
+    def fwd_aff(self, bn: "BNRef", p: Tensor4, res: Optional[Tensor4] = None) -> nat.BwdAff:
+        """A BatchNorm FORWARD (+ residual ``res``) applied by a consumer while it stages its
+        operand ``p`` (common.h BwdAff mode 2): v' = sc*p + sh [+ res].  With ``aout`` the consumer
+        also stores v' -- the materialised block output -- from its first column tiles."""
+        a = nat.BwdAff()
+        r = res if res is not None else p
+        if r.C != p.C or r.M != p.M or r.is_f32 or p.is_f32:
+            raise RuntimeError("forward affine needs bf16 operand and residual of one shape")
+        a.x, a.ldx = r.ptr, r.ld
+        a.bn = bn.args()
+        a.inv_n = 1.0
+        a.unit_alpha = 1 if res is not None else 0
+        a.mode = 2
+        return a
+
     def conv(self, x: Tensor4, layer, y: Tensor4, *, stride=(1, 1), pads=(0, 0), pro=None,
              bias=None, epi_act=0, out_mode=nat.OUT_BF16, stats: Optional[Stats] = None,
-             stats_off=0, w=None, cin_override=None, tile=-1, bpro: Optional[nat.BwdAff] = None):
-        """Forward conv (or, with ``w`` given, a generic conv such as a dgrad)."""
+             stats_off=0, w=None, cin_override=None, tile=-1, bpro: Optional[nat.BwdAff] = None,
+             aout: Optional[Tensor4] = None):
+        """Forward conv (or, with ``w`` given, a generic conv such as a dgrad).  ``bpro`` +
+        ``aout``: the staged operand is also stored (bf16, shaped like ``x``)."""
         a = nat.ConvArgs()
         a.x = x.ptr
         a.N, a.H, a.W = x.N, x.H, x.W
@@ -503,6 +520,12 @@ class Builder:
         a.mbn = act_only(0)
         if bpro is not None:
             a.bpro = bpro
+            if aout is not None:
+                if aout.C != x.C or aout.M != x.M or aout.is_f32 or (kh, kw) != (1, 1):
+                    raise RuntimeError("operand side output must be bf16, shaped like x, of a 1x1 conv")
+                a.aout, a.ldaout = aout.ptr, aout.ld
+        elif aout is not None:
+            raise RuntimeError("operand side output needs an operand affine")
         if tile < 0:
             tile = self._default_tile(a, M, y.C)
         self._splitk(a, M, y.C)

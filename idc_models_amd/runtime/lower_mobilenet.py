@@ -6,8 +6,11 @@ MI355X structure:
   pending BN + ReLU6 (expand -> depthwise BN and depthwise -> project BN never materialise);
 * depthwise 3x3 convs are bandwidth kernels (``dwconv.hip``) that read the fp32 master kernel,
   apply the pending expand-BN + ReLU6 on load and reduce their own output statistics;
-* each block output ``BN_project(p) [+ residual]`` is materialised ONCE by ``bn_apply`` (it is the
-  next block's expand input AND, for identity blocks, its residual);
+* each block output ``BN_project(p) [+ residual]`` is built by its consumer -- the next expand
+  conv (or Conv_1) applies the project BN and adds the residual while staging its operand
+  (common.h BwdAff mode 2) and stores the result from its first column tiles, because it is also
+  the next identity block's residual and the expand weight gradient's input (IDC_MBV2_FOLD_OUT=0:
+  a separate ``bn_apply`` pass);
 * backward: every BatchNorm backward is reduced once by its producer and APPLIED BY ITS CONSUMERS;
   the project BN's reductions come from the epilogue of the dgrad that produces the block-output
   gradient G (next expand / Conv_1, fp32, residual-accumulated), so no reduce pass runs for them
@@ -20,6 +23,8 @@ MI355X structure:
 Keras ``correct_pad`` asymmetric padding of stride-2 layers = top/left pad + implicit bottom/right.
 """
 from __future__ import annotations
+
+import os
 
 import torch
 
@@ -66,6 +71,18 @@ def lower_mobilenet(b: Builder, net, U: int, input_dtype):
     blocks = []
     h_in = None                 # materialised block input (None for block 0: pending y0/bn0)
     cin, h, w = conv1.filters, H1, W1
+    # a block output BN_project(p) [+ h_in] is built by its consumer (the next expand conv or
+    # Conv_1) while staging its operand, and stored from there (no separate apply pass)
+    pending_out = None          # (p, bn_p, residual tensor or None) of the block just lowered
+    fold_out = os.environ.get("IDC_MBV2_FOLD_OUT", "1") != "0"
+
+    def consume(layer, out, stats):
+        """1x1 conv of the current block input; materialises it first if it is pending."""
+        if pending_out is None:
+            b.conv(h_in, layer, out, stats=stats)
+            return
+        p_, bnp_, res_ = pending_out
+        b.conv(p_, layer, out, stats=stats, bpro=b.fwd_aff(bnp_, p_, res_), aout=h_in)
     for bid, (filters, stride, t) in enumerate(MBV2_BLOCKS):
         pre = f"block_{bid}_" if bid else "expanded_conv_"
         blk = {"bid": bid, "stride": stride, "h_in": h_in}
@@ -73,7 +90,8 @@ def lower_mobilenet(b: Builder, net, U: int, input_dtype):
             ex, exbn = L[pre + "expand"], L[pre + "expand_BN"]
             e = b.nhwc(B, h, w, ex.filters)
             se = b.stats(ex.filters, B * h * w) if training else None
-            b.conv(h_in, ex, e, stats=se)
+            consume(ex, e, se)
+            pending_out = None
             bn_e = BNRef(exbn, b, se, RELU6)
             b.add_moving(bn_e)
             blk.update(ex=ex, e=e, bn_in=bn_e)
@@ -98,7 +116,10 @@ def lower_mobilenet(b: Builder, net, U: int, input_dtype):
         b.add_moving(bn_p)
         residual = (cin == pw and stride == 1)
         hout = b.nhwc(B, ho, wo, pw)
-        b.bn_apply(p, bn_p, hout, res=h_in if residual else None)
+        if fold_out:
+            pending_out = (p, bn_p, h_in if residual else None)
+        else:
+            b.bn_apply(p, bn_p, hout, res=h_in if residual else None)
         blk.update(dwl=dwl, pads=pads, d=d, bn_d=bn_d, prj=prj, p=p, bn_p=bn_p, residual=residual,
                    h_out=hout)
         blocks.append(blk)
@@ -107,7 +128,8 @@ def lower_mobilenet(b: Builder, net, U: int, input_dtype):
     c1l, c1bnl = L["Conv_1"], L["Conv_1_bn"]
     c1 = b.nhwc(B, h, w, c1l.filters)
     sc1 = b.stats(c1l.filters, B * h * w) if training else None
-    b.conv(h_in, c1l, c1, stats=sc1)
+    consume(c1l, c1, sc1)
+    pending_out = None
     bn_c1 = BNRef(c1bnl, b, sc1, RELU6)
     b.add_moving(bn_c1)
     emit_head(b, c1, bn_c1.args(), dense, U, io, training)
