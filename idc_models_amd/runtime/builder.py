@@ -211,8 +211,10 @@ class Builder:
         self._stats_size += n
         return v
 
-    def stats(self, ld: int, count: int) -> Stats:
-        slots = stat_slots_for(count) if (self.stat_slots_on and not self.det) else 1
+    def stats(self, ld: int, count: int, slotted: bool = False) -> Stats:
+        """``slotted``: this producer spreads its adds over slot copies even when IDC_STAT_SLOTS
+        is off (producers with ~1k workgroups per channel, e.g. the depthwise convs)."""
+        slots = stat_slots_for(count) if ((self.stat_slots_on or slotted) and not self.det) else 1
         st = Stats(self._stats_floats(2 * ld * slots), ld, count, slots,
                    self.alloc((ld,), F32) if self.shift_stats else None)
         self.all_stats.append(st)
@@ -237,7 +239,7 @@ class Builder:
         self.emit(nat.OP_STATS_SHIFT, ints=(len(descs), max(st.ld for st in descs)), ptrs=(dev.data_ptr(),),
                   lane=1 if self.side_lane else 0)
 
-    def grad_sums(self, bn: Optional["BNRef"], rows: int, grid: int = 0):
+    def grad_sums(self, bn: Optional["BNRef"], rows: int, grid: int = 0, slotted: bool = False):
         """(gsum, gsumx, slots, ld) for the producer of a BatchNorm backward's reductions
         (sum dZ -> d beta, sum dZ*xhat -> d gamma).  With several row blocks the producer adds
         into slot copies in the stats arena and ``finish_grad_sums`` folds them into the gradient
@@ -251,7 +253,7 @@ class Builder:
             # into d beta / d gamma follows it; consumers read the collapsed sums
             bn.gsums = (bn.dbeta.data_ptr(), bn.dgamma.data_ptr(), 1, 0)
             return self._det_gsum_slots(bn.C, max(int(grid), 1), bn.dbeta.data_ptr(), bn.dgamma.data_ptr())
-        S = stat_slots_for(rows) if self.stat_slots_on else 1
+        S = stat_slots_for(rows) if (self.stat_slots_on or slotted) else 1
         if S == 1:
             bn.gsums = (bn.dbeta.data_ptr(), bn.dgamma.data_ptr(), 1, 0)
         else:
@@ -987,7 +989,9 @@ class Builder:
         a.dy, a.lddy = dy.ptr, dy.ld
         a.dx, a.lddx = dz.ptr, dz.ld
         if bn is not None:
-            a.gsum, a.gsumx, a.gsum_slots, a.gsum_ld = self.grad_sums(bn, dz.M)
+            # slot copies: the depthwise backward runs hundreds of workgroups per channel chunk
+            a.gsum, a.gsumx, a.gsum_slots, a.gsum_ld = self.grad_sums(
+                bn, dz.M, slotted=os.environ.get("IDC_DW_STAT_SLOTS", "1") != "0")
         self.emit(nat.OP_DW_BWD_DATA, a)
         self.finish_grad_sums(bn)
 

@@ -75,6 +75,7 @@ def lower_mobilenet(b: Builder, net, U: int, input_dtype):
     # Conv_1) while staging its operand, and stored from there (no separate apply pass)
     pending_out = None          # (p, bn_p, residual tensor or None) of the block just lowered
     fold_out = os.environ.get("IDC_MBV2_FOLD_OUT", "1") != "0"
+    dw_slots = os.environ.get("IDC_DW_STAT_SLOTS", "1") != "0"
 
     def consume(layer, out, stats):
         """1x1 conv of the current block input; materialises it first if it is pending."""
@@ -103,7 +104,10 @@ def lower_mobilenet(b: Builder, net, U: int, input_dtype):
         pads, ho, wo = _dw_geometry(h, w, stride)
         ch = dw_in.C
         d = b.nhwc(B, ho, wo, ch)
-        sd = b.stats(ch, B * ho * wo) if training else None
+        # the depthwise kernels run ~300-700 workgroups per channel chunk: one statistics copy took
+        # that many float atomics per address (H=25 C=32: 28.6 us with, 14.5 us without the
+        # statistics epilogue; 16.9 us with slot copies, tools/bench_dw.py)
+        sd = b.stats(ch, B * ho * wo, slotted=dw_slots) if training else None
         b.dwconv(dw_in, dwl, d, stride=stride, pads=pads, pro=bn_in.args(), stats=sd)
         bn_d = BNRef(dwbn, b, sd, RELU6)
         b.add_moving(bn_d)
