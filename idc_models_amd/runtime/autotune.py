@@ -90,7 +90,8 @@ def _conv_candidates(ext, M: int, cout: int, payload: bytes = None, a_f32: int =
     # 256 x {128, 256} global_load_lds tiles for plain wide layers (conv_big.hip), when they
     # still make >= 128 workgroups
     if payload is not None and os.environ.get("IDC_CONV_BIG", "1") != "0" and ext.big_ok(payload, a_f32):
-        for t, bn in ((ext.TILE_BIG128, 128), (ext.TILE_BIG128D, 128), (ext.TILE_BIG256, 256)):
+        # (BIG64: 4 waves of 64 x 64, the 64-channel layers -- VGG16's 50x50 dgrads)
+        for t, bn in ((ext.TILE_BIG64, 64), (ext.TILE_BIG128, 128), (ext.TILE_BIG128D, 128), (ext.TILE_BIG256, 256)):
             if cout >= bn and -(-M // 256) * -(-cout // bn) >= 8:
                 out.append(t)
     return out
@@ -98,6 +99,8 @@ def _conv_candidates(ext, M: int, cout: int, payload: bytes = None, a_f32: int =
 
 def _tile_shape(ext, t: int):
     """(BM, BN, BK) of conv tile ``t``; None for a tile id outside the tables."""
+    if t == ext.TILE_BIG64:
+        return 256, 64, 64
     if t in (ext.TILE_BIG128, ext.TILE_BIG128D):
         return 256, 128, 64
     if t == ext.TILE_BIG256:
@@ -111,7 +114,7 @@ def _splits_for(ext, a, t: int, M: int, slab_floats: int):
     """Feasible split-K factors for conv tile ``t``: the partial slabs must fit the workspace, each
     slice must keep >= 2 K-steps, and only grids that leave the GPU under-filled are split."""
     shape = _tile_shape(ext, t)
-    if shape is None:
+    if shape is None or t == ext.TILE_BIG64:  # (BIG64 split-K: no exactness test, not offered)
         return []
     bm, bn, bk = shape
     tiles = -(-M // bm) * -(-a.Cout // bn)
