@@ -767,11 +767,14 @@ class Builder:
         (csrc/kernels/dense_stage_bwd.hip): every layer and BatchNorm trainable in batch mode, the
         stage's consumer BatchNorm in batch mode with single-copy reductions, shapes within the
         launch's limits, no fixed-order (deterministic) reductions."""
-        # opt-in (IDC_DENSE_STAGE_BWD=1): correct (tests/test_kernels_gpu.py vs autograd) but its
-        # gather tiles wait on agent-coherent loads of ~3 us each under load, so stages 3-4 took
-        # 761 + 234 us against ~720 us for the per-layer dgrad chain (DenseNet-121 bs 256: 4.14 vs
-        # 4.00 ms/step, round 4); see tools/dense_stamps.py
-        if os.environ.get("IDC_DENSE_STAGE_BWD", "0") != "1" or not self.training or self.det:
+        # Default on for the smallest maps only (lower_densenet: IDC_DENSE_STAGE_BWD_MAXM=256, stage
+        # 4 at bs 256): there its one launch beats 32 latency-bound per-layer dgrads (3.94 vs 4.00-4.02
+        # ms/step); on stage 3 as well its gather tiles wait on agent-coherent loads of ~3 us each
+        # under load (761 + 234 us against ~720 us per-layer: 4.12 ms/step, round 4, see
+        # tools/dense_stamps.py).  Not in grouped (client-batched) programs.
+        if os.environ.get("IDC_DENSE_STAGE_BWD", "1") != "1" or not self.training or self.det:
+            return False
+        if getattr(self, "grouped", False):
             return False
         if pend.mode != 1 or getattr(pend, "gsums", None) is None or pend.gsums[2] != 1 or pend.stats.slots != 1:
             return False

@@ -158,10 +158,10 @@ def lower_densenet(b: Builder, net, U: int, input_dtype):
     # the stage issues them as one OP_WGRAD_BATCH per kernel shape that fills the GPU beside the
     # previous stage's data gradients (builder.flush_wgrad_batch).
     batch_maxm = int(os.environ.get("IDC_WG_BATCH_MAXM", "9216"))
-    # Late stages (M <= IDC_DENSE_STAGE_BWD_MAXM pixels, default 2304: stages 3-4 at bs 256) run the
-    # data gradients of all their dense layers as ONE persistent launch (builder.dense_stage_bwd,
+    # The smallest stages (M <= IDC_DENSE_STAGE_BWD_MAXM pixels, default 256: stage 4 at bs 256) run
+    # the data gradients of all their dense layers as ONE persistent launch (builder.dense_stage_bwd,
     # dense_stage_bwd.hip); it hands the stage input's final gradient (bf16) to the transition
-    bwd_maxm = int(os.environ.get("IDC_DENSE_STAGE_BWD_MAXM", "2304"))
+    bwd_maxm = int(os.environ.get("IDC_DENSE_STAGE_BWD_MAXM", "256"))
     for si in range(len(stages) - 1, -1, -1):
         st = stages[si]
         buf = st["buf"]

@@ -72,6 +72,7 @@ class FusedProgram:
         net = model.net
         self.U = net.num_outputs
         b = Builder(net, model.arena, model.device, batch, training)
+        b.grouped = group is not None
         _lowering_for(net)(b, net, self.U, input_dtype)
         if b.has_wgrad_batch():  # a lowering that returned early (frozen layers) mid-batch
             b.segment = "bwd"

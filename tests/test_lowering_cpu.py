@@ -163,9 +163,10 @@ def test_dense_stage_lowering(monkeypatch):
 
 
 def test_dense_stage_bwd_lowering(monkeypatch):
-    """The late stages' dense-layer data gradients lower to one OP_DENSE_STAGE_BWD each (stages 3
-    and 4 at bs 256; with fine_tune_at=150 stage 3 is partly frozen and keeps the per-layer
-    dgrads); the deterministic mode keeps the per-layer dgrads everywhere."""
+    """The smallest stages' dense-layer data gradients lower to one OP_DENSE_STAGE_BWD each (by
+    default stage 4 at bs 256, M <= 256; with IDC_DENSE_STAGE_BWD_MAXM=2304 stages 3 and 4; with
+    fine_tune_at=150 stage 3 is partly frozen and keeps the per-layer dgrads); the deterministic
+    mode and IDC_DENSE_STAGE_BWD=0 keep the per-layer dgrads everywhere."""
     def count(ft=None, **env):
         for k, v in env.items():
             monkeypatch.setenv(k, v)
@@ -174,11 +175,13 @@ def test_dense_stage_bwd_lowering(monkeypatch):
         for k in env:
             monkeypatch.delenv(k)
         return kinds.count(nat.OP_DENSE_STAGE_BWD), kinds.count(nat.OP_CONV)
-    n_on, conv_on = count(IDC_DENSE_STAGE_BWD="1")
-    n_off, conv_off = count()  # opt-in
-    assert (n_on, n_off) == (2, 0)
-    assert conv_off - conv_on == 2 * (24 + 16)  # two dgrads per dense layer of stages 3 and 4
-    assert count(150, IDC_DENSE_STAGE_BWD="1")[0] == 1
-    assert count(IDC_DENSE_STAGE_BWD="1", IDC_DETERMINISTIC="1")[0] == 0
+    n_def, conv_def = count()
+    n_on, conv_on = count(IDC_DENSE_STAGE_BWD_MAXM="2304")
+    n_off, conv_off = count(IDC_DENSE_STAGE_BWD="0")
+    assert (n_def, n_on, n_off) == (1, 2, 0)
+    assert conv_off - conv_def == 2 * 16  # two dgrads per dense layer of stage 4
+    assert conv_off - conv_on == 2 * (24 + 16)  # ... and of stage 3
+    assert count(150, IDC_DENSE_STAGE_BWD_MAXM="2304")[0] == 1
+    assert count(IDC_DETERMINISTIC="1")[0] == 0
     # stage 2 (6x6 maps) fits the launch too
-    assert count(IDC_DENSE_STAGE_BWD="1", IDC_DENSE_STAGE_BWD_MAXM="9216")[0] == 3
+    assert count(IDC_DENSE_STAGE_BWD_MAXM="9216")[0] == 3
