@@ -20,6 +20,9 @@ hipError_t secagg_quantize_mask(const float* x, uint32_t* out, long long n, cons
                                 const uint32_t* keys, unsigned long long round_, unsigned long long alive,
                                 hipStream_t st, int accumulate = 0);
 // out[i] = (int32)sum[i] / (scale_s * divisor)
+// max |x| per segment, merged into out[] (float bits, zero-initialised by the caller)
+hipError_t secagg_absmax(const float* x, long long n, const long long* seg_end, int nseg, unsigned* out,
+                         hipStream_t st);
 hipError_t secagg_dequantize(const uint32_t* sum, float* out, long long n, const float* seg_scale,
                              const long long* seg_end, int nseg, float divisor, hipStream_t st);
 

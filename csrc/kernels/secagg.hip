@@ -94,6 +94,47 @@ __global__ __launch_bounds__(256) void secagg_unmask_kernel(const uint32_t* __re
   }
 }
 
+// Per-segment max |x| (the quantisation ranges of secure aggregation), OR-ed into out[] as float
+// bits (non-negative floats order like their bit patterns): block b owns the contiguous chunk
+// [b*per, (b+1)*per), each thread keeps one running max per segment it walks through and merges it
+// into the block's LDS bins when it leaves the segment; the block then adds its bins to out[] with
+// one global atomic per segment it touched (a handful per block, not one per element).
+constexpr int kAbsMaxBins = 4096;
+__global__ __launch_bounds__(256) void secagg_absmax_kernel(const float* __restrict__ x, long long n,
+                                                            const long long* __restrict__ seg_end, int nseg,
+                                                            unsigned* __restrict__ out) {
+  __shared__ unsigned bins[kAbsMaxBins];
+  const long long per = (n + gridDim.x - 1) / gridDim.x;
+  const long long c0 = blockIdx.x * per, c1 = c0 + per < n ? c0 + per : n;
+  if (c0 >= c1) return;  // block-uniform
+  const int s0 = segment_from(c0, seg_end, 0, nseg);
+  const int s1 = segment_from(c1 - 1, seg_end, s0, nseg);
+  const int nb = s1 - s0 + 1;
+  for (int j = threadIdx.x; j < nb && j < kAbsMaxBins; j += blockDim.x) bins[j] = 0u;
+  __syncthreads();
+  auto flush = [&](int sg, unsigned m) {
+    if (m == 0u) return;
+    if (sg - s0 < kAbsMaxBins) atomicMax(&bins[sg - s0], m);
+    else atomicMax(&out[sg], m);
+  };
+  long long i = c0 + threadIdx.x;
+  int sg = s0;
+  unsigned m = 0u;
+  for (; i < c1; i += blockDim.x) {
+    if (i >= seg_end[sg]) {
+      flush(sg, m);
+      m = 0u;
+      sg = segment_from(i, seg_end, sg, nseg);
+    }
+    const unsigned b = __float_as_uint(fabsf(x[i]));
+    m = b > m ? b : m;
+  }
+  flush(sg, m);
+  __syncthreads();
+  for (int j = threadIdx.x; j < nb && j < kAbsMaxBins; j += blockDim.x)
+    if (bins[j]) atomicMax(&out[s0 + j], bins[j]);
+}
+
 static int grid_for(long long n) {
   long long b = (n + 255) / 256;
   if (b > 2048) b = 2048;
@@ -108,6 +149,14 @@ hipError_t secagg_quantize_mask(const float* x, uint32_t* out, long long n, cons
   if (n == 0) return hipSuccess;
   hipLaunchKernelGGL(secagg_mask_kernel, dim3(grid_for(n)), dim3(256), 0, st, x, out, n, seg_scale, seg_end, nseg,
                      clip, K, rank, keys, rnd, alive, accumulate);
+  return hipGetLastError();
+}
+
+hipError_t secagg_absmax(const float* x, long long n, const long long* seg_end, int nseg, unsigned* out,
+                         hipStream_t st) {
+  if (nseg < 1) return hipErrorInvalidValue;
+  if (n == 0) return hipSuccess;
+  hipLaunchKernelGGL(secagg_absmax_kernel, dim3(grid_for(n)), dim3(256), 0, st, x, n, seg_end, nseg, out);
   return hipGetLastError();
 }
 

@@ -847,6 +847,12 @@ void py_secagg_mask(uintptr_t x, uintptr_t out, long long n, uintptr_t seg_scale
         "secagg_quantize_mask");
 }
 
+void py_secagg_absmax(uintptr_t x, long long n, uintptr_t seg_end, int nseg, uintptr_t out, uintptr_t stream) {
+  check(secagg_absmax(reinterpret_cast<const float*>(x), n, reinterpret_cast<const long long*>(seg_end), nseg,
+                      reinterpret_cast<unsigned*>(out), reinterpret_cast<hipStream_t>(stream)),
+        "secagg_absmax");
+}
+
 void py_secagg_unmask(uintptr_t sum, uintptr_t out, long long n, uintptr_t seg_scale, uintptr_t seg_end, int nseg,
                       float divisor, uintptr_t stream) {
   check(secagg_dequantize(reinterpret_cast<const uint32_t*>(sum), reinterpret_cast<float*>(out), n,
@@ -989,6 +995,7 @@ PYBIND11_MODULE(_idc_native, m) {
         py::arg("seg_end"), py::arg("nseg"), py::arg("clip"), py::arg("nclients"), py::arg("rank"), py::arg("keys"),
         py::arg("round_"), py::arg("alive"), py::arg("stream"), py::arg("accumulate") = 0);
   m.def("secagg_unmask", &py_secagg_unmask);
+  m.def("secagg_absmax", &py_secagg_absmax);
   m.attr("OP_CONV") = (int)OP_CONV;
   m.attr("OP_DENSE_STAGE") = (int)OP_DENSE_STAGE;
   m.attr("OP_DENSE_STAGE_BWD") = (int)OP_DENSE_STAGE_BWD;

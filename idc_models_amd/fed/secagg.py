@@ -151,6 +151,31 @@ def unmask(total: torch.Tensor, scales, seg_end, divisor: float = 1.0) -> torch.
     return total.float() / (torch.from_numpy(scales[sidx]) * divisor)
 
 
+def segment_absmax(vecs, seg_end, nseg: int, dev) -> torch.Tensor:
+    """max |x| per segment over all vectors in ``vecs`` (float32 [nseg]); GPU: the native
+    ``secagg_absmax`` kernel, one launch per vector."""
+    seg_end = np.asarray(seg_end, dtype=np.int64)
+    dev = torch.device(dev)
+    if dev.type == "cuda" and vecs:
+        from ..ops import _native as nat
+        bits = torch.zeros(nseg, dtype=torch.int32, device=dev)
+        se = torch.from_numpy(seg_end).to(dev)
+        ext = nat.require()
+        for v in vecs:
+            v = v.reshape(-1).contiguous()
+            if v.numel() != int(seg_end[-1]):
+                raise ValueError("segments do not cover the vector")
+            ext.secagg_absmax(v.data_ptr(), v.numel(), se.data_ptr(), nseg, bits.data_ptr(), nat.stream_handle())
+        return bits.view(torch.float32)
+    mx = torch.zeros(nseg, dtype=torch.float32, device=dev)
+    starts = np.concatenate([[0], seg_end[:-1]])
+    for v in vecs:
+        a = v.reshape(-1).float().abs()
+        mx = torch.maximum(mx, torch.stack([a[int(s0):int(s1)].max() if s1 > s0 else a.new_zeros(())
+                                            for s0, s1 in zip(starts, seg_end)]).to(dev))
+    return mx
+
+
 def choose_scales(max_abs, nclients: int, headroom: float = 2.0) -> np.ndarray:
     """Per segment: the largest power-of-two scale with K * max|x| * scale < 2^31 (with headroom),
     so each protected tensor keeps the resolution its own range allows."""
@@ -205,10 +230,9 @@ class MaskedAggregator:
         dev = self.device
         n = int(sum(sizes))
         seg_end = segment_ends(sizes)
-        mx = torch.zeros(len(sizes), dtype=torch.float32, device=dev)
-        for v in vecs.values():
-            segs = torch.split(v.reshape(-1).to(dev).float().abs(), list(sizes))
-            mx = torch.maximum(mx, torch.stack([s.max() if s.numel() else s.new_zeros(()) for s in segs]))
+        # per-segment |max| over every local client: one native launch per client (not one torch
+        # reduction per client and segment: ~600 segments x 8 clients per DenseNet-121 round)
+        mx = segment_absmax([v.reshape(-1).to(dev).float() for v in vecs.values()], seg_end, len(sizes), dev)
         if comm.world_size() > 1:
             import torch.distributed as dist
             comm.all_reduce_(mx, op=dist.ReduceOp.MAX)

@@ -977,3 +977,16 @@ def test_dense_stage_bwd_matches_autograd(fn, N, H, c0, L, grid):
         errs[f"db1_{i}"] = relerr(d["dbeta1"], p["b1"].grad)
         errs[f"dg1_{i}"] = relerr(d["dgamma1"], p["g1"].grad)
     assert all(v < 3e-2 for v in errs.values()), errs
+
+
+def test_secagg_segment_absmax_matches_torch():
+    """Native per-segment max |x| (secure-aggregation ranges): segments from 1 element to more
+    than a block's chunk, several vectors merged, exactly the torch reduction."""
+    from idc_models_amd.fed.secagg import segment_absmax, segment_ends
+    g = torch.Generator().manual_seed(4)
+    sizes = [1, 7, 64, 3000, 1, 200000, 17, 4096, 5, 123457]
+    vecs = [torch.randn(sum(sizes), generator=g) * (i + 1) for i in range(3)]
+    se = segment_ends(sizes)
+    got = segment_absmax([v.to(DEV) for v in vecs], se, len(sizes), DEV).cpu()
+    ref = segment_absmax(vecs, se, len(sizes), "cpu")
+    assert torch.equal(got, ref), (got, ref)
