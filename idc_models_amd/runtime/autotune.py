@@ -118,7 +118,7 @@ def _splits_for(ext, a, t: int, M: int, slab_floats: int):
         return []
     bm, bn, bk = shape
     tiles = -(-M // bm) * -(-a.Cout // bn)
-    if tiles >= 256:
+    if tiles >= int(os.environ.get("IDC_SPLITK_MAX_TILES", "256")):
         return []
     K = a.KH * a.KW * a.Cin
     nk = -(-K // bk)
