@@ -45,6 +45,8 @@ struct DenseStageArgs {
   int act1, act2;
   float inv_count;              // 1 / (N*H*W)
   unsigned max_polls;           // bound on one wait's polls (0: default, ~0.5 s)
+  int lookahead;                // queue order (set by dense_stage_fwd): 0 [A0][B0][A1][B1]...,
+                                // 1 [A0][A1][B0][A2][B1]...[B_{L-1}] (see dense_stage.hip)
 };
 
 // number of work items of one launch (the grid never needs more workgroups than this)

@@ -8,10 +8,14 @@
 //
 // One launch walks the stage as a WORK QUEUE of tiles:
 //     [layer 0: 1x1 tiles (A_0)][layer 0: 3x3 tiles (B_0)][layer 1: 1x1 tiles (A_1)] ...
-// A workgroup takes the next ticket (one agent-scope atomic) and waits, where it must, until an
-// earlier phase's completion counter is full.  Tickets are handed out in queue order, so every
-// tile a waiting workgroup depends on was taken earlier by a workgroup that is already running
-// (or done): the queue cannot deadlock whatever number of workgroups is resident.  Every wait is
+// or, when more than one A phase's worth of workgroups is resident (lookahead order),
+//     [A_0][A_1][B_0][A_2][B_1] ... [A_{L-1}][B_{L-2}][B_{L-1}]
+// A workgroup takes the next ticket (one agent-scope atomic) and waits, where it must, until a
+// phase's completion counter is full.  In layer order every tile a waiting workgroup depends on
+// was taken earlier by a workgroup that is already running (or done): that queue cannot deadlock
+// whatever number of workgroups is resident.  In lookahead order only A_{l+1}'s last k-step waits
+// on a later ticket (B_l, queued right after it), so the queue progresses whenever more than nA
+// workgroups are resident -- the launcher uses it only then.  Every wait is
 // poll-bounded; a workgroup that gives up sets the launch's fail flag (all others then leave) and
 // the first one to set it counts the launch in the persistent error counter.
 //
@@ -46,6 +50,8 @@
 // cleared / operands staged / before publish for every work item (tools/dense_stamps.py).
 #include "dense_stage.h"
 #include "persist.h"
+
+#include <cstdlib>
 
 namespace idc {
 namespace {
@@ -166,7 +172,27 @@ __global__ __launch_bounds__(NT) void dense_stage_kernel(DenseStageArgs a, Group
     const int task = __builtin_amdgcn_readfirstlane(s.task);
     if (task >= total) return;
     stamp(stamps, task, 0);
-    const int l = task / per, r = task - l * per;
+    int l, r;  // layer and phase-local item (r < nA: A_l, else B_l item r - nA)
+    if (!a.lookahead) {
+      l = task / per;
+      r = task - l * per;
+    } else if (task < nA) {
+      l = 0;
+      r = task;
+    } else {
+      // lookahead order [A0][A1 B0][A2 B1]...[A_{L-1} B_{L-2}][B_{L-1}]: A_{l+1} is queued before
+      // B_l, so its older-channel accumulation (needs B_{l-1} only) runs beside B_l instead of
+      // after it; its newest-slice step then waits on B_l, a LATER ticket -- safe while more than
+      // nA workgroups are resident (dense_stage_fwd enables it only then)
+      const int t2 = task - nA, j = t2 / per + 1, rr = t2 - (j - 1) * per;
+      if (j < a.nlayers && rr < nA) {
+        l = j;
+        r = rr;
+      } else {
+        l = j - 1;
+        r = j < a.nlayers ? rr : nA + rr;
+      }
+    }
     const DenseLayerDesc d = layers[l];
     float* lslots = scratch + (size_t)l * DS_SCRATCH_PER_LAYER;  // [S][2][32] stats of B_l's slice
     float* tslots = lslots + S * 64;                              // [S][2][128] stats of A_l's t
@@ -561,7 +587,18 @@ hipError_t dense_stage_fwd(const DenseStageArgs& a, int grid, hipStream_t st) {
   const int k = launch_groups().k;
   if (k > 1) grid = grid / k > 8 ? grid / k : 8;
   if (grid > tasks) grid = tasks;
-  hipLaunchKernelGGL(dense_stage_kernel, ggrid(grid), dim3(NT), 0, st, a, garg());
+  // the lookahead queue order lets an A phase wait on the B phase queued after it: it needs more
+  // than nA workgroups of this queue resident at once, so it is used for one ungrouped launch
+  // whose grid (one workgroup per CU, 2 fit) exceeds nA with margin (IDC_DS_LOOKAHEAD=0: off)
+  static const bool la_on = [] {
+    const char* e = std::getenv("IDC_DS_LOOKAHEAD");
+    return !(e && e[0] == '0');
+  }();
+  int nA, nB;
+  dense_stage_phase_tiles(a.N * a.H * a.W, nA, nB);
+  DenseStageArgs b = a;
+  b.lookahead = (la_on && k == 1 && a.nlayers > 1 && grid >= nA + 16) ? 1 : 0;
+  hipLaunchKernelGGL(dense_stage_kernel, ggrid(grid), dim3(NT), 0, st, b, garg());
   return hipGetLastError();
 }
 

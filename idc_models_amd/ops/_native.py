@@ -144,7 +144,7 @@ class DenseStageArgs(C.Structure):
     _fields_ = [("buf", vp), ("sstats", vp), ("sshift", vp), ("layers", vp), ("sync", vp), ("err", vp),
                 ("scratch", vp), ("stamps", vp),
                 ("N", ci), ("H", ci), ("W", ci), ("ld", ci), ("nlayers", ci), ("k2", ci),
-                ("act1", ci), ("act2", ci), ("inv_count", cf), ("max_polls", C.c_uint)]
+                ("act1", ci), ("act2", ci), ("inv_count", cf), ("max_polls", C.c_uint), ("lookahead", ci)]
 
 
 class DenseBwdLayerDesc(C.Structure):

@@ -37,13 +37,13 @@ def _phase_rows(a, spans, ready_idx, end_idx):
         blk = a[lo:hi]
         kind = name.rstrip("0123456789")
         ri, ei = ready_idx.get(kind, 1), end_idx.get(kind, NSTAMP - 1)
-        end = float(blk[:, ei].max())
+        end = float(np.nanmax(blk[:, ei]))
         iv = []
         for k in range(1, ei + 1):
-            d = blk[:, k] - blk[:, k - 1]
-            iv.append(float(np.median(d)))
+            d = blk[:, k] - blk[:, k - 1]  # NaN where a stamp point is not reached by this phase kind
+            iv.append(float(np.nanmedian(d)) if np.isfinite(d).any() else float("nan"))
         rows.append({"phase": name, "end": end, "step": end - prev_end,
-                     "handoff": float(blk[:, ri].min()) - prev_end, "iv": iv})
+                     "handoff": float(np.nanmin(blk[:, ri])) - prev_end, "iv": iv})
         prev_end = end
     return rows
 
@@ -56,13 +56,16 @@ def _table(rows, title):
         rr = [r for r in rows if r["phase"].rstrip("0123456789") == k][1:] or \
              [r for r in rows if r["phase"].rstrip("0123456789") == k]
         n = len(rr[0]["iv"])
-        ivs = " / ".join(f"{stt.mean(r['iv'][i] for r in rr):.2f}" for i in range(n))
+        def mean_iv(i):
+            v = [r["iv"][i] for r in rr if r["iv"][i] == r["iv"][i]]
+            return f"{stt.mean(v):.2f}" if v else "-"
+        ivs = " / ".join(mean_iv(i) for i in range(n))
         out.append(f"- {k}: {len(rr)} phases, mean step {stt.mean(r['step'] for r in rr):.2f} us, hand-off "
                    f"{stt.mean(r['handoff'] for r in rr):.2f}, median stamp intervals {ivs}")
     out += ["", "| phase | end | step | handoff | stamp intervals (median over tiles) |", "|---|---:|---:|---:|---|"]
     for r in rows:
         out.append(f"| {r['phase']} | {r['end']:.1f} | {r['step']:.2f} | {r['handoff']:.2f} | "
-                   + " ".join(f"{v:.2f}" for v in r["iv"]) + " |")
+                   + " ".join(f"{v:.2f}" if v == v else "-" for v in r["iv"]) + " |")
     out.append("")
     return out
 
@@ -72,20 +75,31 @@ def analyse_fwd(st, nlayers: int, M: int):
     nmt = (M + 31) // 32
     nA, nB = 2 * nmt, nmt
     per = nA + nB
-    a = st.reshape(nlayers * per, NSTAMP).astype(np.int64)
-    a = (a - a[:, 0].min()) * 0.01  # 10 ns ticks -> us
+    a = st.reshape(nlayers * per, NSTAMP).astype(np.float64)
+    a[a == 0] = np.nan  # stamp points a tile never reaches stay 0
+    a = (a - np.nanmin(a[:, 0])) * 0.01  # 10 ns ticks -> us
     spans = []
-    for l in range(nlayers):
-        spans.append((f"A{l}", l * per, l * per + nA))
-        spans.append((f"B{l}", l * per + nA, (l + 1) * per))
+    lookahead = os.environ.get("IDC_DS_LOOKAHEAD", "1") != "0" and nlayers > 1 and 256 >= nA + 16
+    if not lookahead:
+        for l in range(nlayers):
+            spans.append((f"A{l}", l * per, l * per + nA))
+            spans.append((f"B{l}", l * per + nA, (l + 1) * per))
+    else:  # dense_stage.hip lookahead order [A0][A1 B0][A2 B1]...[B_{L-1}]
+        spans.append(("A0", 0, nA))
+        for j in range(1, nlayers):
+            b0 = nA + (j - 1) * per
+            spans.append((f"A{j}", b0, b0 + nA))
+            spans.append((f"B{j - 1}", b0 + nA, b0 + per))
+        spans.append((f"B{nlayers - 1}", nA + (nlayers - 1) * per, nlayers * per))
     return _phase_rows(a, spans, {"A": 3, "B": 2}, {"A": 7, "B": 7})
 
 
 def analyse_bwd(st, phases):
     import numpy as np
     n = phases[-1][0] + phases[-1][3]
-    a = st.reshape(-1, NSTAMP)[:n].astype(np.int64)
-    a = (a - a[:, 0].min()) * 0.01
+    a = st.reshape(-1, NSTAMP)[:n].astype(np.float64)
+    a[a == 0] = np.nan
+    a = (a - np.nanmin(a[:, 0])) * 0.01
     names = {1: "P", 2: "QN", 3: "G", 4: "GIN", 5: "FIN1", 6: "FIN2"}
     spans = [(f"{names[k]}{l}", f, f + t) for f, k, l, t in phases]
     return _phase_rows(a, spans, {k: 1 for k in names.values()}, {k: 3 for k in names.values()})
