@@ -19,6 +19,10 @@ struct DenseLayerDesc {
   float eps1, eps2;
   int cin;              // input channels = this layer's slice offset in the stage buffer
   int pad_;
+  const float* mm1;     // moving mean / variance of _0_bn [cin] and _1_bn [128]: the inference-mode
+  const float* mv1;     // (DenseStageArgs::infer) BatchNorms normalise with these
+  const float* mm2;
+  const float* mv2;
 };
 
 // Slot copies of the in-launch statistics (the per-channel float atomics of one phase are spread
@@ -47,6 +51,8 @@ struct DenseStageArgs {
   unsigned max_polls;           // bound on one wait's polls (0: default, ~0.5 s)
   int lookahead;                // queue order (set by dense_stage_fwd): 0 [A0][B0][A1][B1]...,
                                 // 1 [A0][A1][B0][A2][B1]...[B_{L-1}] (see dense_stage.hip)
+  int infer;                    // inference-mode BatchNorms (moving statistics; frozen layers,
+                                // evaluation): no statistics are produced, only data hand-offs
 };
 
 // number of work items of one launch (the grid never needs more workgroups than this)

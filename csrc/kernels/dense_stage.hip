@@ -271,8 +271,18 @@ __global__ __launch_bounds__(NT) void dense_stage_kernel(DenseStageArgs a, Group
       load_a(0);
       load_b(0, bq0);
       const int ccanon = l >= 2 ? cold - 32 : cold;
-      bn_table(sstats, a.ld, sshift, g1, b1, a.inv_count, d.eps1, ccanon, s.sc, s.sh);
-      if (l >= 2 && tid < 32) {
+      if (a.infer) {  // inference mode: the layer's own moving statistics, every channel at once
+        const float* __restrict__ mm = gsh(d.mm1, go);
+        const float* __restrict__ mv = gsh(d.mv1, go);
+        for (int c = tid; c < cin; c += NT) {
+          const float rr = g1[c] * rsqrtf(mv[c] + d.eps1);
+          s.sc[c] = rr;
+          s.sh[c] = b1[c] - mm[c] * rr;
+        }
+      } else {
+        bn_table(sstats, a.ld, sshift, g1, b1, a.inv_count, d.eps1, ccanon, s.sc, s.sh);
+      }
+      if (!a.infer && l >= 2 && tid < 32) {
         float s0, s1, mean, var;
         slot_sum<S>(lslots - 2 * DS_SCRATCH_PER_LAYER, 32, tid, s0, s1);
         const int c = ccanon + tid;
@@ -319,7 +329,7 @@ __global__ __launch_bounds__(NT) void dense_stage_kernel(DenseStageArgs a, Group
         const int nrow = m0 + (tid >> 2), nseg = (tid & 3) * 8;
         const uint4 an = (tid < 128 && nrow < M) ? ld_coh16(buf + (size_t)nrow * a.ld + cold + nseg)
                                                  : make_uint4(0, 0, 0, 0);
-        if (tid < 32) {
+        if (!a.infer && tid < 32) {
           float s0, s1, mean, var;
           slot_sum<S>(pslots, 32, tid, s0, s1);
           const int c = cold + tid;
@@ -366,7 +376,7 @@ __global__ __launch_bounds__(NT) void dense_stage_kernel(DenseStageArgs a, Group
         for (int q = 0; q < 8; ++q) red[erow * RLDA + ecol + q] = m < M ? rv[q] - kq[q] : 0.f;
       }
       __syncthreads();
-      if (tid < 128) {
+      if (!a.infer && tid < 128) {
         const int c = tid & 63, which = tid >> 6;
         float sum = 0.f;
 #pragma unroll 8
@@ -452,7 +462,12 @@ __global__ __launch_bounds__(NT) void dense_stage_kernel(DenseStageArgs a, Group
         traw[u] = idx < R * 16 ? ld_coh16(tb + (size_t)(row_lo + (idx >> 4)) * 128 + (idx & 15) * 8)
                                : make_uint4(0, 0, 0, 0);
       }
-      if (tid < 128) {
+      if (tid < 128 && a.infer) {
+        const float mean = gsh(d.mm2, go)[tid], var = gsh(d.mv2, go)[tid];
+        const float rr = g2c * rsqrtf(var + d.eps2);
+        s.sc[tid] = rr;
+        s.sh[tid] = b2c - mean * rr;
+      } else if (tid < 128) {
         float s0, s1, mean, var;
         slot_sum<S>(tslots, 128, tid, s0, s1);
         shifted_mean_var(ksh, s0, s1, a.inv_count, mean, var);
@@ -522,7 +537,7 @@ __global__ __launch_bounds__(NT) void dense_stage_kernel(DenseStageArgs a, Group
       }
       __syncthreads();
       stamp(stamps, task, 5);
-      if (tid < 64) {
+      if (!a.infer && tid < 64) {
         const int c = tid & 31, which = tid >> 5;
         float sum = 0.f;
 #pragma unroll 8
@@ -537,7 +552,7 @@ __global__ __launch_bounds__(NT) void dense_stage_kernel(DenseStageArgs a, Group
         const unsigned o = publish_shard(cntB(l), j);
         if (stamps && tid == 0) stamps[(size_t)task * NSTAMP + 7] = __builtin_amdgcn_s_memrealtime() + (o & 0u);
       }
-      if (l == a.nlayers - 1) {
+      if (l == a.nlayers - 1 && !a.infer) {
         // the last slice has no in-launch consumer: the last tile to complete writes its
         // single-copy statistics
         if (tid == 0)
@@ -578,8 +593,8 @@ bool dense_stage_shape_ok(int N, int H, int W, int max_cin) {
 
 hipError_t dense_stage_fwd(const DenseStageArgs& a, int grid, hipStream_t st) {
   if (a.nlayers < 1 || (a.k2 != 1 && a.k2 != 3) || a.ld % 8 != 0 || a.N < 1 || a.H < 1 || a.W < 1 ||
-      a.buf == nullptr || a.sstats == nullptr || a.layers == nullptr || a.sync == nullptr ||
-      a.scratch == nullptr || !dense_stage_shape_ok(a.N, a.H, a.W, 0))
+      a.buf == nullptr || a.layers == nullptr || a.sync == nullptr ||
+      (!a.infer && (a.sstats == nullptr || a.scratch == nullptr)) || !dense_stage_shape_ok(a.N, a.H, a.W, 0))
     return hipErrorInvalidValue;
   const int tasks = dense_stage_tasks(a);
   if (grid <= 0) grid = 256;

@@ -137,14 +137,16 @@ class WgBatchEntry(C.Structure):
 class DenseLayerDesc(C.Structure):
     """One dense layer of a persistent dense-stage launch (dense_stage.h)."""
     _fields_ = [("w1", vp), ("w2", vp), ("g1", vp), ("b1", vp), ("g2", vp), ("b2", vp), ("t", vp),
-                ("tstats", vp), ("tshift", vp), ("eps1", cf), ("eps2", cf), ("cin", ci), ("pad_", ci)]
+                ("tstats", vp), ("tshift", vp), ("eps1", cf), ("eps2", cf), ("cin", ci), ("pad_", ci),
+                ("mm1", vp), ("mv1", vp), ("mm2", vp), ("mv2", vp)]
 
 
 class DenseStageArgs(C.Structure):
     _fields_ = [("buf", vp), ("sstats", vp), ("sshift", vp), ("layers", vp), ("sync", vp), ("err", vp),
                 ("scratch", vp), ("stamps", vp),
                 ("N", ci), ("H", ci), ("W", ci), ("ld", ci), ("nlayers", ci), ("k2", ci),
-                ("act1", ci), ("act2", ci), ("inv_count", cf), ("max_polls", C.c_uint), ("lookahead", ci)]
+                ("act1", ci), ("act2", ci), ("inv_count", cf), ("max_polls", C.c_uint), ("lookahead", ci),
+                ("infer", ci)]
 
 
 class DenseBwdLayerDesc(C.Structure):

@@ -428,7 +428,8 @@ def bn_moments(stats: torch.Tensor, count: int, shift: Optional[torch.Tensor] = 
 
 
 def dense_stage(buf: torch.Tensor, sstats: torch.Tensor, layers, sshift: Optional[torch.Tensor] = None,
-                act: int = RELU, grid: int = 256, k2: int = 3, max_polls: int = 0, stamps: bool = False):
+                act: int = RELU, grid: int = 256, k2: int = 3, max_polls: int = 0, stamps: bool = False,
+                infer: bool = False):
     """All dense layers of a DenseNet stage in one persistent launch (csrc/kernels/dense_stage.hip).
 
     ``buf``: NHWC bf16 stage buffer [N, H, W, ld] whose channels [0, c0) are filled and whose
@@ -436,6 +437,8 @@ def dense_stage(buf: torch.Tensor, sstats: torch.Tensor, layers, sshift: Optiona
     w1 ([128][cin] bf16 kernel layout), w2 ([32][k2][k2][128] bf16), g1, b1 ([cin]), g2, b2 ([128]),
     t ([N,H,W,128] bf16 output), tstats ([256] zeroed fp32), tshift ([128] or None), eps1, eps2, cin.
     ``max_polls``: bound on each wait (0: the kernel's default; tests force timeouts with 1).
+    ``infer``: inference-mode BatchNorms from each layer's mm1 / mv1 ([cin]) and mm2 / mv2 ([128])
+    moving statistics; no statistics are produced (``sstats`` may be None).
     Returns (sync counters, err counter, stamps or None) for inspection."""
     N, H, W, ld = buf.shape
     ext = nat.require()
@@ -447,6 +450,8 @@ def dense_stage(buf: torch.Tensor, sstats: torch.Tensor, layers, sshift: Optiona
         d.g1, d.b1, d.g2, d.b2 = (L[k].data_ptr() for k in ("g1", "b1", "g2", "b2"))
         d.t, d.tstats, d.tshift = L["t"].data_ptr(), L["tstats"].data_ptr(), nat.ptr(L.get("tshift"))
         d.eps1, d.eps2, d.cin = L["eps1"], L["eps2"], L["cin"]
+        if infer:
+            d.mm1, d.mv1, d.mm2, d.mv2 = (L[k].data_ptr() for k in ("mm1", "mv1", "mm2", "mv2"))
     import ctypes
     tab = torch.frombuffer(bytearray(ctypes.string_at(ctypes.addressof(arr), ctypes.sizeof(arr))),
                            dtype=torch.uint8).to(buf.device)
@@ -454,7 +459,8 @@ def dense_stage(buf: torch.Tensor, sstats: torch.Tensor, layers, sshift: Optiona
     err = torch.zeros(1, dtype=torch.int32, device=buf.device)
     scratch = torch.zeros(int(ext.DS_SCRATCH_PER_LAYER) * len(layers), dtype=torch.float32, device=buf.device)
     a = nat.DenseStageArgs()
-    a.buf, a.sstats, a.sshift = buf.data_ptr(), sstats.data_ptr(), nat.ptr(sshift)
+    a.buf, a.sstats, a.sshift = buf.data_ptr(), nat.ptr(sstats), nat.ptr(sshift)
+    a.infer = 1 if infer else 0
     a.layers, a.sync, a.err = tab.data_ptr(), sync.data_ptr(), err.data_ptr()
     a.scratch = scratch.data_ptr()
     a.N, a.H, a.W, a.ld, a.nlayers, a.k2 = N, H, W, ld, len(layers), k2

@@ -704,13 +704,20 @@ class Builder:
         1x1 inputs of <= DS_MAX_CIN (2,048) channels in multiples of 32 (DenseNet-121/169/201),
         128-channel bottlenecks, 32 new channels per layer, maps whose 3x3 windows fit the
         launch's staging rows, and no fixed-order (deterministic) reductions."""
-        if os.environ.get("IDC_DENSE_STAGE", "1") == "0" or not self.training or self.det:
+        if os.environ.get("IDC_DENSE_STAGE", "1") == "0" or self.det:
             return False
-        if sbuf is None or sbuf.slots != 1:
-            return False
+        infer = all(lay["bn1"].mode == 2 and lay["bn2"].mode == 2 for lay in layers)
+        if infer:
+            # inference-mode BatchNorms (evaluation programs, a frozen base): moving statistics,
+            # nothing produced but the stage buffer and t (IDC_DENSE_STAGE_INFER=0: per layer)
+            if os.environ.get("IDC_DENSE_STAGE_INFER", "1") == "0":
+                return False
+        else:
+            if not self.training or sbuf is None or sbuf.slots != 1:
+                return False
         ext = nat.load()
         for lay in layers:
-            if lay["bn1"].mode != 1 or lay["bn2"].mode != 1 or lay["stt"].slots != 1:
+            if not infer and (lay["bn1"].mode != 1 or lay["bn2"].mode != 1 or lay["stt"].slots != 1):
                 return False
             if lay["cin"] % 32 or lay["cin"] > int(ext.DS_MAX_CIN) or lay["cv1"].filters != 128 \
                     or lay["cv2"].filters != 32:
@@ -725,6 +732,7 @@ class Builder:
         the per-layer convs, so everything downstream (backward included) is unchanged."""
         H, W = buf.H, buf.W
         center = self.is_center_only(layers[0]["cv2"], H, W, (1, 1), (1, 1))
+        infer = all(lay["bn1"].mode == 2 and lay["bn2"].mode == 2 for lay in layers)
         arr = (nat.DenseLayerDesc * len(layers))()
         for d, lay in zip(arr, layers):
             cin, bn1, bn2 = lay["cin"], lay["bn1"], lay["bn2"]
@@ -732,9 +740,13 @@ class Builder:
             d.w2 = self.conv_weight(lay["cv2"], cin_pad=128, center=center)["fwd"].data_ptr()
             d.g1, d.b1 = bn1.gamma.data_ptr(), bn1.beta.data_ptr()
             d.g2, d.b2 = bn2.gamma.data_ptr(), bn2.beta.data_ptr()
-            d.t, d.tstats, d.tshift = lay["t"].ptr, lay["stt"].ptr, lay["stt"].shift_ptr()
+            if lay["stt"] is not None:
+                d.tstats, d.tshift = lay["stt"].ptr, lay["stt"].shift_ptr()
+            d.t = lay["t"].ptr
             d.eps1, d.eps2 = bn1.layer.epsilon, bn2.layer.epsilon
             d.cin = cin
+            d.mm1, d.mv1 = bn1.layer.moving_mean.data_ptr(), bn1.layer.moving_variance.data_ptr()
+            d.mm2, d.mv2 = bn2.layer.moving_mean.data_ptr(), bn2.layer.moving_variance.data_ptr()
         host = torch.frombuffer(bytearray(C.string_at(C.addressof(arr), C.sizeof(arr))), dtype=torch.uint8)
         tab = host.to(self.device)
         self.keep.append(tab)
@@ -744,12 +756,18 @@ class Builder:
             self.dense_err = self.alloc((4,), torch.int32)
         ext = nat.load()
         # counters and the in-launch statistics slots live in the stats arena: zeroed every step
+        # (a program without a stats-arena reset -- evaluation -- zeroes its counters itself)
         sync = self._stats_floats(3 + 16 * len(layers))  # ticket, sharded phase counters, fail
-        scratch = self._stats_floats(int(ext.DS_SCRATCH_PER_LAYER) * len(layers))
+        if not self.training:
+            self.memset(sync)
+        scratch = self._stats_floats(int(ext.DS_SCRATCH_PER_LAYER) * len(layers)) if not infer else None
         a = nat.DenseStageArgs()
-        a.buf, a.sstats, a.sshift = buf.ptr, sbuf.ptr, sbuf.shift_ptr()
+        a.buf = buf.ptr
+        if sbuf is not None and not infer:
+            a.sstats, a.sshift = sbuf.ptr, sbuf.shift_ptr()
+        a.infer = 1 if infer else 0
         a.layers, a.sync, a.err = tab.data_ptr(), sync.data_ptr(), self.dense_err.data_ptr()
-        a.scratch = scratch.data_ptr()
+        a.scratch = scratch.data_ptr() if scratch is not None else 0
         a.N, a.H, a.W, a.ld, a.nlayers, a.k2 = buf.N, H, W, buf.ld, len(layers), 1 if center else 3
         a.act1 = a.act2 = act
         a.inv_count = 1.0 / float(buf.N * H * W)

@@ -990,3 +990,47 @@ def test_secagg_segment_absmax_matches_torch():
     got = segment_absmax([v.to(DEV) for v in vecs], se, len(sizes), DEV).cpu()
     ref = segment_absmax(vecs, se, len(sizes), "cpu")
     assert torch.equal(got, ref), (got, ref)
+
+
+@pytest.mark.parametrize("N,H,c0,L,grid", [(4, 3, 64, 3, 256), (6, 1, 96, 4, 7), (2, 1, 1120, 3, 256)])
+def test_dense_stage_inference_mode_matches_reference(fn, N, H, c0, L, grid):
+    """Inference-mode dense stage (frozen base / evaluation): BN1 and BN2 from each layer's own
+    moving statistics, nothing produced but t and the stage-buffer slices, vs a PyTorch reference."""
+    W = H
+    ld = c0 + 32 * L
+    g = torch.Generator(device="cpu").manual_seed(N * 7 + H)
+    buf = torch.zeros(N, H, W, ld)
+    buf[..., :c0] = torch.randn(N, H, W, c0, generator=g) * 1.5 + 0.3
+    buf = buf.to(torch.bfloat16).to(DEV)
+    k2 = 1 if H == 1 else 3
+    lays, refs = [], []
+    for i in range(L):
+        cin = c0 + 32 * i
+        w1 = bf(torch.randn(1, 1, cin, 128, generator=g) * (2.0 / cin) ** 0.5).to(DEV)
+        w2 = bf(torch.randn(3, 3, 128, 32, generator=g) * (2.0 / 1152) ** 0.5).to(DEV)
+        w2l = fn.weight_fwd_layout(w2[1:2, 1:2] if k2 == 1 else w2, 128)
+        d = dict(w1=fn.weight_fwd_layout(w1, cin), w2=w2l,
+                 g1=(torch.rand(cin, generator=g) + 0.5).to(DEV), b1=(torch.randn(cin, generator=g) * 0.1).to(DEV),
+                 g2=(torch.rand(128, generator=g) + 0.5).to(DEV), b2=(torch.randn(128, generator=g) * 0.1).to(DEV),
+                 mm1=(torch.randn(cin, generator=g) * 0.3).to(DEV), mv1=(torch.rand(cin, generator=g) * 2 + 0.2).to(DEV),
+                 mm2=(torch.randn(128, generator=g) * 0.3).to(DEV), mv2=(torch.rand(128, generator=g) * 2 + 0.2).to(DEV),
+                 t=torch.zeros(N, H, W, 128, dtype=torch.bfloat16, device=DEV),
+                 tstats=torch.zeros(256, device=DEV), tshift=None, eps1=1e-3, eps2=1.001e-5, cin=cin)
+        lays.append(d)
+        refs.append((w1, w2))
+    rbuf = buf.float().clone()
+    rts = []
+    for i, d in enumerate(lays):
+        cin = d["cin"]
+        w1, w2 = refs[i]
+        a1 = bf(torch.relu((rbuf[..., :cin] - d["mm1"]) * torch.rsqrt(d["mv1"] + d["eps1"]) * d["g1"] + d["b1"]))
+        t = bf(ref_conv(a1, w1, 1, (0, 0, 0, 0)))
+        a2 = bf(torch.relu((t - d["mm2"]) * torch.rsqrt(d["mv2"] + d["eps2"]) * d["g2"] + d["b2"]))
+        rbuf[..., cin:cin + 32] = bf(ref_conv(a2, w2, 1, (1, 1, 1, 1)))
+        rts.append(t)
+    sync, err, _ = fn.dense_stage(buf, None, lays, grid=grid, k2=k2, infer=True)
+    assert int(err[0].item()) == 0 and int(sync[-1].item()) == 0
+    errs = {f"t{i}": relerr(d["t"].float(), rts[i]) for i, d in enumerate(lays)}
+    errs["buf"] = relerr(buf.float(), rbuf)
+    assert all(v < 2e-2 for v in errs.values()), errs
+    assert all(float(d["tstats"].abs().sum()) == 0.0 for d in lays)  # no statistics produced
