@@ -18,7 +18,8 @@ struct DenseLayerDesc {
   const float* tshift;  // [128] statistics shift of t (nullable)
   float eps1, eps2;
   int cin;              // input channels = this layer's slice offset in the stage buffer
-  int pad_;
+  int pad_;             // bit 0 / bit 1: _0_bn / _1_bn in inference mode (frozen layer of a
+                        // fine-tuned stage; the launch still produces the statistics)
   const float* mm1;     // moving mean / variance of _0_bn [cin] and _1_bn [128]: the inference-mode
   const float* mv1;     // (DenseStageArgs::infer) BatchNorms normalise with these
   const float* mm2;

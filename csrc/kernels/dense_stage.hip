@@ -271,7 +271,11 @@ __global__ __launch_bounds__(NT) void dense_stage_kernel(DenseStageArgs a, Group
       load_a(0);
       load_b(0, bq0);
       const int ccanon = l >= 2 ? cold - 32 : cold;
-      if (a.infer) {  // inference mode: the layer's own moving statistics, every channel at once
+      // inference-mode BN1 (a frozen layer in a fine-tuned stage, or the whole launch): the
+      // layer's own moving statistics; the statistics of the stage buffer are still produced
+      // for the trainable layers after it (unless the whole launch is inference mode)
+      const bool inf1 = a.infer || (d.pad_ & 1);
+      if (inf1) {  // inference mode: the layer's own moving statistics, every channel at once
         const float* __restrict__ mm = gsh(d.mm1, go);
         const float* __restrict__ mv = gsh(d.mv1, go);
         for (int c = tid; c < cin; c += NT) {
@@ -282,7 +286,7 @@ __global__ __launch_bounds__(NT) void dense_stage_kernel(DenseStageArgs a, Group
       } else {
         bn_table(sstats, a.ld, sshift, g1, b1, a.inv_count, d.eps1, ccanon, s.sc, s.sh);
       }
-      if (!a.infer && l >= 2 && tid < 32) {
+      if (!inf1 && l >= 2 && tid < 32) {
         float s0, s1, mean, var;
         slot_sum<S>(lslots - 2 * DS_SCRATCH_PER_LAYER, 32, tid, s0, s1);
         const int c = ccanon + tid;
@@ -334,9 +338,11 @@ __global__ __launch_bounds__(NT) void dense_stage_kernel(DenseStageArgs a, Group
           slot_sum<S>(pslots, 32, tid, s0, s1);
           const int c = cold + tid;
           shifted_mean_var(sshift ? sshift[c] : 0.f, s0, s1, a.inv_count, mean, var);
-          const float rr = g1[c] * rsqrtf(var + d.eps1);
-          s.sc[c] = rr;
-          s.sh[c] = b1[c] - mean * rr;
+          if (!inf1) {
+            const float rr = g1[c] * rsqrtf(var + d.eps1);
+            s.sc[c] = rr;
+            s.sh[c] = b1[c] - mean * rr;
+          }
           if (r == 0) {  // the slice's single-copy statistics (read by later layers' tables)
             st_coh(sstats + c, s0);
             st_coh(sstats + a.ld + c, s1);
@@ -462,18 +468,22 @@ __global__ __launch_bounds__(NT) void dense_stage_kernel(DenseStageArgs a, Group
         traw[u] = idx < R * 16 ? ld_coh16(tb + (size_t)(row_lo + (idx >> 4)) * 128 + (idx & 15) * 8)
                                : make_uint4(0, 0, 0, 0);
       }
-      if (tid < 128 && a.infer) {
+      const bool inf2 = a.infer || (d.pad_ & 2);
+      if (tid < 128 && inf2) {
         const float mean = gsh(d.mm2, go)[tid], var = gsh(d.mv2, go)[tid];
         const float rr = g2c * rsqrtf(var + d.eps2);
         s.sc[tid] = rr;
         s.sh[tid] = b2c - mean * rr;
-      } else if (tid < 128) {
+      }
+      if (tid < 128 && !a.infer) {
         float s0, s1, mean, var;
         slot_sum<S>(tslots, 128, tid, s0, s1);
         shifted_mean_var(ksh, s0, s1, a.inv_count, mean, var);
-        const float rr = g2c * rsqrtf(var + d.eps2);
-        s.sc[tid] = rr;
-        s.sh[tid] = b2c - mean * rr;
+        if (!inf2) {
+          const float rr = g2c * rsqrtf(var + d.eps2);
+          s.sc[tid] = rr;
+          s.sh[tid] = b2c - mean * rr;
+        }
         if (j == 0) {  // t's single-copy statistics (backward, moving averages)
           tst[tid] = s0;
           tst[128 + tid] = s1;

@@ -713,11 +713,14 @@ class Builder:
             if os.environ.get("IDC_DENSE_STAGE_INFER", "1") == "0":
                 return False
         else:
+            # a training program: every slice's statistics are produced; a frozen layer (fine-tuning
+            # cut inside the stage) normalises with its moving statistics (per-layer mode bits)
             if not self.training or sbuf is None or sbuf.slots != 1:
                 return False
         ext = nat.load()
         for lay in layers:
-            if not infer and (lay["bn1"].mode != 1 or lay["bn2"].mode != 1 or lay["stt"].slots != 1):
+            if not infer and (lay["bn1"].mode not in (1, 2) or lay["bn2"].mode not in (1, 2)
+                              or lay["stt"] is None or lay["stt"].slots != 1):
                 return False
             if lay["cin"] % 32 or lay["cin"] > int(ext.DS_MAX_CIN) or lay["cv1"].filters != 128 \
                     or lay["cv2"].filters != 32:
@@ -747,6 +750,7 @@ class Builder:
             d.cin = cin
             d.mm1, d.mv1 = bn1.layer.moving_mean.data_ptr(), bn1.layer.moving_variance.data_ptr()
             d.mm2, d.mv2 = bn2.layer.moving_mean.data_ptr(), bn2.layer.moving_variance.data_ptr()
+            d.pad_ = 0 if infer else (1 if bn1.mode == 2 else 0) | (2 if bn2.mode == 2 else 0)
         host = torch.frombuffer(bytearray(C.string_at(C.addressof(arr), C.sizeof(arr))), dtype=torch.uint8)
         tab = host.to(self.device)
         self.keep.append(tab)

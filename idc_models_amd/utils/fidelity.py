@@ -38,6 +38,17 @@ def eager_grads(net, x_u8: torch.Tensor, y: torch.Tensor, mode: str = "fp32") ->
     return [g.detach().double() for g in torch.autograd.grad(loss, ps)]
 
 
+def eager_loss(net, x_u8: torch.Tensor, y: torch.Tensor, mode: str = "fp32") -> float:
+    """Training-mode BCE-with-logits loss of a deep copy of ``net`` (``mode`` as in eager_grads)."""
+    ref = copy.deepcopy(net)
+    dev = next(iter(ref.parameters())).device
+    xs = x_u8.to(dev).float() / 255.0
+    ref.train()
+    with torch.no_grad(), torch.autocast(dev.type, dtype=torch.bfloat16, enabled=(mode == "autocast")):
+        lg = ref(xs)
+    return float(F.binary_cross_entropy_with_logits(lg.float().reshape(-1), y.to(dev).float().reshape(-1)))
+
+
 def eager_activations(net, x_u8: torch.Tensor, names: Sequence[str], mode: str = "fp32") -> Dict[str, torch.Tensor]:
     """Outputs of the named layers of a deep copy of ``net`` (training-mode forward, ``mode`` as
     in ``eager_grads``), as float64 NHWC tensors."""
