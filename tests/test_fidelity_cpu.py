@@ -65,3 +65,18 @@ def test_segment_absmax_cpu():
     v2 = torch.tensor([-5., 1., 0., -0.25, 1., 1., 9., 0., -1.])
     got = segment_absmax([v1, v2], segment_ends(sizes), 3, "cpu")
     assert torch.equal(got, torch.tensor([5., 0.5, 9.]))
+
+
+def test_one_noise_draw_past_the_soft_bound_is_tolerated_many_are_not():
+    g = torch.Generator().manual_seed(5)
+    shapes = [(32,)] * 10
+    ar = _Arena(shapes)
+    g32 = [torch.randn(s, generator=g, dtype=torch.float64) for s in shapes]
+    e = [torch.randn(s, generator=g, dtype=torch.float64) for s in shapes]
+    g16 = [a + 0.2 * a.norm() / b.norm() * b for a, b in zip(g32, e)]  # autocast: rel 0.2 each
+
+    def fused(scales):  # rel(fused) = scale * 0.2 along the same noise direction
+        return torch.cat([(a + s * (b - a)).reshape(-1) for a, b, s in zip(g32, g16, scales)]).float()
+    assert fd.grad_failures(ar, fused([2.0] + [1.0] * 9), g32, g16) == []        # one soft draw
+    assert len(fd.grad_failures(ar, fused([2.0] * 3 + [1.0] * 7), g32, g16)) == 3  # several: fail
+    assert len(fd.grad_failures(ar, fused([4.0] + [1.0] * 9), g32, g16)) == 1     # past the hard bound
