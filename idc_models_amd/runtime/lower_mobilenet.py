@@ -76,6 +76,7 @@ def lower_mobilenet(b: Builder, net, U: int, input_dtype):
     pending_out = None          # (p, bn_p, residual tensor or None) of the block just lowered
     fold_out = os.environ.get("IDC_MBV2_FOLD_OUT", "1") != "0"
     dw_slots = os.environ.get("IDC_DW_STAT_SLOTS", "1") != "0"
+    dw_aff = os.environ.get("IDC_MBV2_DW_AFF", "0") == "1"
 
     def consume(layer, out, stats):
         """1x1 conv of the current block input; materialises it first if it is pending."""
@@ -221,18 +222,26 @@ def lower_mobilenet(b: Builder, net, U: int, input_dtype):
         e, bn_in = blk["e"], blk["bn_in"]
         # depthwise BN backward: materialised once (the depthwise kernels re-read dZ ~4.5x; staging
         # the affine there re-reads the BN input as often and rebuilds the slot-summed A/B/C table
-        # in every workgroup, measured slower than this pass)
-        dd = b.nhwc(d.N, d.H, d.W, d.C)
-        b.bn_bwd_apply(zd, d, bn_d, dd, accumulate=False)
-        b.mark_grads_ready([bn_d.gamma, bn_d.beta])
+        # in every workgroup, measured slower than this pass; IDC_MBV2_DW_AFF=1: staged)
+        if dw_aff and bn_d.mode == 1:
+            dd, aff_d = zd, b.bwd_aff(bn_d, d, fold=True)
+        else:
+            dd, aff_d = b.nhwc(d.N, d.H, d.W, d.C), None
+            b.bn_bwd_apply(zd, d, bn_d, dd, accumulate=False)
+            b.mark_grads_ready([bn_d.gamma, bn_d.beta])
+        if fz.before(dwl) or aff_d is not None:
+            ze = b.nhwc(e.N, e.H, e.W, e.C)
+            if fz.before(dwl):
+                b.dw_bwd_data(e, dwl, dd, ze, stride=blk["stride"], pads=blk["pads"], bn=bn_in, dyaff=aff_d)
+        if aff_d is not None:
+            b.mark_grads_ready([bn_d.gamma, bn_d.beta])
         if fz.trainable(dwl):
             b.dw_wgrad(e, dwl, dd, b.arena.grad_of(dwl.depthwise_kernel), stride=blk["stride"],
-                       pads=blk["pads"], pro=bn_in.args(), lane=1)
+                       pads=blk["pads"], pro=bn_in.args(), lane=1,
+                       dyaff=b.bwd_aff(bn_d, d) if aff_d is not None else None)
         b.mark_grads_ready([dwl.depthwise_kernel])
         if not fz.before(dwl):
             return
-        ze = b.nhwc(e.N, e.H, e.W, e.C)
-        b.dw_bwd_data(e, dwl, dd, ze, stride=blk["stride"], pads=blk["pads"], bn=bn_in)
         if not fz.before(bn_in.layer):
             b.mark_grads_ready([bn_in.gamma, bn_in.beta])
             return
