@@ -168,6 +168,20 @@ class Model:
             n += self.impl.skipped_steps()
         return n
 
+    def _check_persistent(self):
+        """Once per epoch: a persistent launch that gave up on a wait (fail flag, error counter)
+        left stale outputs -- say so instead of training on silently."""
+        fn = getattr(self.impl, "persistent_failures", None)
+        if fn is None:
+            return
+        n = fn()
+        if n > getattr(self, "_persist_fail_seen", 0):
+            import warnings
+            warnings.warn(f"{n - getattr(self, '_persist_fail_seen', 0)} persistent dense-stage launch(es) timed "
+                          "out this epoch: their outputs are stale (IDC_DENSE_STAGE=0 / IDC_DENSE_STAGE_BWD=0 "
+                          "run the per-layer kernels)", RuntimeWarning)
+            self._persist_fail_seen = n
+
     def reset_optimizer(self):
         """Fresh optimizer slot state without re-lowering (TFF re-creates the client optimizer
         every round, ``fed_model.py:208``)."""
@@ -233,6 +247,7 @@ class Model:
             cbs.on_epoch_begin(epoch)
             logs = self._run_epoch(x, steps_per_epoch, True, cbs)
             cbs.on_epoch_train_end(epoch, logs)
+            self._check_persistent()
             self.strategy.sync_bn_stats(self)
             if validation_data is not None:
                 vlogs = self.evaluate(validation_data, steps=validation_steps, verbose=0,

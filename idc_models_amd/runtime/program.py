@@ -459,6 +459,9 @@ class FusedStep:
         named += [(f"keep[{i}]{tuple(t.shape)}", t) for i, t in enumerate(p.b.keep) if t.is_floating_point()]
         named.append(("stats_arena", p.b.stats_arena))
         bad = []
+        err = getattr(p.b, "dense_err", None)
+        if err is not None and int(err[0].item()):
+            bad.append(f"dense_err={int(err[0].item())} (a persistent dense-stage launch timed out)")
         for name, t in named:
             if t.numel() and (not bool(torch.isfinite(t).all()) or t.float().abs().max().item() > 1e8):
                 bad.append(f"{name} max={t.float().abs().max().item():.3g}")
@@ -559,6 +562,16 @@ class FusedStep:
             p.run_range(cast_lo, hi, graph=False)
         torch.cuda.current_stream(m.device).wait_stream(p.stream)
         return self._outputs(p)
+
+    def persistent_failures(self) -> int:
+        """Persistent dense-stage launches (forward or backward) of this backend's programs that
+        gave up on a wait: their outputs are stale (one small device read per call)."""
+        n = 0
+        for p in self.progs.values():
+            err = getattr(p.b, "dense_err", None)
+            if err is not None:
+                n += int(err[0].item())
+        return n
 
     def skipped_steps(self) -> int:
         """Training steps whose update was skipped for non-finite gradients (skip_nonfinite)."""

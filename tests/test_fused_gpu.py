@@ -435,3 +435,14 @@ def test_direct_input_staging_one_hot_labels(monkeypatch):
     torch.cuda.synchronize()
     assert torch.equal(p.io.labels.reshape(16, 10), torch.nn.functional.one_hot(y, 10).float())
     m.impl.close()
+
+
+def test_persistent_timeout_is_reported(monkeypatch):
+    """A persistent dense-stage launch that gives up on a wait (poll bound forced to 1) is
+    reported by the backend and by fit() (a RuntimeWarning once per epoch), not silent."""
+    monkeypatch.setenv("IDC_DS_MAX_POLLS", "1")
+    from idc_models_amd.data import prepare_for_training, synthetic_dataset
+    m, ref, x, y = _setup("densenet121", 16)
+    with pytest.warns(RuntimeWarning, match="persistent dense-stage"):
+        m.fit(prepare_for_training(synthetic_dataset(32, seed=2), 16, drop_remainder=True), epochs=1, verbose=0)
+    assert m.impl.persistent_failures() > 0
