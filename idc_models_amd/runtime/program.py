@@ -140,8 +140,12 @@ class FusedProgram:
         # 89 main ops: 2.47 ms/step at 4 vs 2.56 at 0, 3 A/B pairs in round 3); a backward of few
         # long kernels (VGG16: 20 main ops of 45-220 us) forks every side op at once (0), or its
         # weight gradients would wait for the next dgrads to finish before starting
+        # round 4 (DenseNet-121: 97 main backward ops after the persistent stage-4 backward):
+        # 2 -> 3.894-3.901 ms/step, 3 -> 3.915-3.923, 4 -> 3.953-3.964; MobileNetV2 (73 ops): 2 ->
+        # 2.394-2.395, 3 -> 2.318, 4 -> 2.322-2.329
         n_bwd_main = sum(1 for op in b.ops if op[0] == "bwd" and op[7] == 0)
-        self.plan.set_side_flush(int(os.environ.get("IDC_SIDE_FLUSH", "4" if n_bwd_main >= 64 else "0")))
+        default_flush = "2" if n_bwd_main >= 90 else "4" if n_bwd_main >= 64 else "0"
+        self.plan.set_side_flush(int(os.environ.get("IDC_SIDE_FLUSH", default_flush)))
         self.seg: Dict[str, Tuple[int, int]] = {}
         self.rms_index = None
         cur, start = None, 0
