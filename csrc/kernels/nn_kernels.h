@@ -172,6 +172,8 @@ hipError_t finite_check(const float* g, long long n, int* flag, hipStream_t st);
 // status[0] = flag (last step skipped?), status[1] += flag (skipped steps), flag = 0
 hipError_t finite_flag_reset(int* flag, int* status, hipStream_t st);
 hipError_t cast_weights(const CastEntry* d_entries, const int* tile_entry, long long ntiles, hipStream_t st);
+hipError_t group_metrics(const float* loss, const float* logits, const float* labels, long long stride, int K,
+                         int B, float thr, double* acc, hipStream_t st);
 hipError_t input_stage(const void* x, int x_u8, int N, int H, int W, int C, bf16_t* y, int Cpad,
                        const void* lab, int lab_code, int U, float* lab_out, hipStream_t st);
 hipError_t bn_stats(const bf16_t* x, int ldx, int M, int C, float* stats, int stats_ld,

@@ -1143,6 +1143,9 @@ __global__ __launch_bounds__(256) void input_stage_kernel(const void* x, int u8,
                                                           int N, int U, float* lab_out, GroupArg ga) {
   x = gsh(x, goff(ga));
   y = gsh(y, goff(ga));
+  // labels read in place: in a grouped program they live in the region like x (client batching
+  // stages each client's epoch in its own copy); goff is 0 otherwise
+  lab = gsh(lab, goff(ga));
   const long long tid0 = blockIdx.x * (long long)blockDim.x + threadIdx.x;
   const long long nthr = (long long)gridDim.x * blockDim.x;
   for (long long p = tid0; p < npix; p += nthr) {
@@ -1181,6 +1184,36 @@ hipError_t input_stage(const void* x, int x_u8, int N, int H, int W, int C, bf16
   if (blocks < 1) blocks = 1;
   hipLaunchKernelGGL(input_stage_kernel, ggrid((int)blocks), dim3(256), 0, st, x, x_u8, npix, C, y, Cpad, lab,
                      lab_code, N, U, lab_out, garg());
+  return hipGetLastError();
+}
+
+// ------------------------------------------------------------------------------------------
+// Per-copy training metrics of a grouped (client-batched) step: workgroup g reads copy g of the
+// program's loss [1], logits [B] and labels [B] (copy 0 + g * stride bytes) and adds the loss and
+// the number of correct predictions (logit > thr vs label > 0.5) into acc[2g], acc[2g + 1].  One
+// launch per step instead of torch ops over [K]-views of the region, which TensorIterator splits
+// per copy (the views span more than 2^31 bytes).
+__global__ __launch_bounds__(64) void group_metrics_kernel(const float* loss, const float* logits,
+                                                           const float* labels, long long stride, int B,
+                                                           float thr, double* acc) {
+  const int g = blockIdx.x;
+  const long long off = (long long)g * stride;
+  const float* lg = reinterpret_cast<const float*>(reinterpret_cast<const char*>(logits) + off);
+  const float* lb = reinterpret_cast<const float*>(reinterpret_cast<const char*>(labels) + off);
+  int c = 0;
+  for (int i = threadIdx.x; i < B; i += 64) c += ((lg[i] > thr) == (lb[i] > 0.5f)) ? 1 : 0;
+  for (int o = 32; o > 0; o >>= 1) c += __shfl_xor(c, o, 64);
+  if (threadIdx.x == 0) {
+    const float l = *reinterpret_cast<const float*>(reinterpret_cast<const char*>(loss) + off);
+    acc[2 * g] += (double)l;
+    acc[2 * g + 1] += (double)c;
+  }
+}
+
+hipError_t group_metrics(const float* loss, const float* logits, const float* labels, long long stride, int K,
+                         int B, float thr, double* acc, hipStream_t st) {
+  if (K < 1 || B < 1 || !loss || !logits || !labels || !acc) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(group_metrics_kernel, dim3(K), dim3(64), 0, st, loss, logits, labels, stride, B, thr, acc);
   return hipGetLastError();
 }
 

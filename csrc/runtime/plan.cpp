@@ -847,6 +847,14 @@ void py_secagg_mask(uintptr_t x, uintptr_t out, long long n, uintptr_t seg_scale
         "secagg_quantize_mask");
 }
 
+void py_group_metrics(uintptr_t loss, uintptr_t logits, uintptr_t labels, long long stride, int K, int B, float thr,
+                      uintptr_t acc, uintptr_t stream) {
+  check(group_metrics(reinterpret_cast<const float*>(loss), reinterpret_cast<const float*>(logits),
+                      reinterpret_cast<const float*>(labels), stride, K, B, thr, reinterpret_cast<double*>(acc),
+                      reinterpret_cast<hipStream_t>(stream)),
+        "group_metrics");
+}
+
 void py_secagg_absmax(uintptr_t x, long long n, uintptr_t seg_end, int nseg, uintptr_t out, uintptr_t stream) {
   check(secagg_absmax(reinterpret_cast<const float*>(x), n, reinterpret_cast<const long long*>(seg_end), nseg,
                       reinterpret_cast<unsigned*>(out), reinterpret_cast<hipStream_t>(stream)),
@@ -996,6 +1004,7 @@ PYBIND11_MODULE(_idc_native, m) {
         py::arg("round_"), py::arg("alive"), py::arg("stream"), py::arg("accumulate") = 0);
   m.def("secagg_unmask", &py_secagg_unmask);
   m.def("secagg_absmax", &py_secagg_absmax);
+  m.def("group_metrics", &py_group_metrics);
   m.attr("OP_CONV") = (int)OP_CONV;
   m.attr("OP_DENSE_STAGE") = (int)OP_DENSE_STAGE;
   m.attr("OP_DENSE_STAGE_BWD") = (int)OP_DENSE_STAGE_BWD;

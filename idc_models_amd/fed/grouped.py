@@ -13,6 +13,7 @@ that are ``BatchedDataset`` s with ``drop_remainder`` and the same batch size an
 """
 from __future__ import annotations
 
+import os
 from typing import Dict, List, Sequence, Tuple
 
 import torch
@@ -59,6 +60,26 @@ class GroupedClientTrainer:
         self.logit_v = R.view(p.io.logits)   # [K, B, 1]
         self.threshold = 0.5 if getattr(m, "keras_compat_accuracy", False) else 0.0
         self._data: Dict[int, Tuple[torch.Tensor, torch.Tensor]] = {}
+        self._epoch = None  # (rows, X0, Y0): a local epoch's inputs and labels inside the region
+        self.ext = R.ext
+
+    def _epoch_buffers(self, rows: int):
+        """Copy-0 tensors [rows, H, W, C] uint8 / [rows] fp32 INSIDE the region, so copy g holds
+        client g's shuffled epoch and the input op reads step t's batch in place (its pointers
+        are shifted per copy like every other; no per-step staging copies).  None if the region
+        has no room left (the caller stages through copies)."""
+        if self._epoch is not None and self._epoch[0] >= rows:
+            return self._epoch
+        H, W, C = self.m.net.input_shape
+        need = rows * (H * W * C + 4) + (1 << 20)
+        if os.environ.get("IDC_GROUP_EPOCH_INPUT", "1") != "1" or self.prog.input_op != self.prog.seg["fwd"][0] \
+                or self.region.used + need > self.region.stride:
+            return None
+        with self.region.allocating():
+            X0 = torch.empty((rows, H, W, C), dtype=torch.uint8, device=self.device)
+            Y0 = torch.empty((rows,), dtype=torch.float32, device=self.device)
+        self._epoch = (rows, X0, Y0)
+        return self._epoch
 
     def _device_data(self, ds):
         """The client's whole example set on the GPU (uploaded once; 288 GB of HBM)."""
@@ -94,34 +115,50 @@ class GroupedClientTrainer:
         R.replicate(p.stream)                # every copy starts from copy 0
         cur = torch.cuda.current_stream(self.device)
         H, W, C = m.net.input_shape
-        X = torch.empty((K, T * B, H, W, C), dtype=torch.uint8, device=self.device)
-        Y = torch.empty((K, T * B), dtype=torch.float32, device=self.device)
+        ep = self._epoch_buffers(T * B)
+        # replicate() also copies copy 0's epoch buffers (from the second round on they lie in
+        # its used part): the per-copy fills below must come after it
+        cur.wait_stream(p.stream)
+        if ep is not None:
+            X, Y = R.view(ep[1]), R.view(ep[2])    # [K, rows, ...] views of the copies
+        else:
+            X = torch.empty((K, T * B, H, W, C), dtype=torch.uint8, device=self.device)
+            Y = torch.empty((K, T * B), dtype=torch.float32, device=self.device)
         orders = [d.epoch_order()[:T * B] for d in datasets]  # each client's own shuffle
         for g in range(K):
             j = g if g < n else 0  # idle copies (fewer clients than copies) recompute client 0
             xd, yd = self._device_data(datasets[j])
             idx = torch.as_tensor(orders[j], device=self.device)
-            X[g] = xd.index_select(0, idx)
-            Y[g] = yd.index_select(0, idx)
-        loss_sum = torch.zeros(K, dtype=torch.float64, device=self.device)
-        correct = torch.zeros(K, dtype=torch.float64, device=self.device)
+            torch.index_select(xd, 0, idx, out=X[g, :T * B])
+            torch.index_select(yd, 0, idx, out=Y[g, :T * B])
+        # acc[2g], acc[2g+1]: client g's loss sum and correct count (one group_metrics launch a step)
+        acc = torch.zeros(2 * K, dtype=torch.float64, device=self.device)
+        io = p.io
         p.stream.wait_stream(cur)
         lo, hi = p.seg["bwd"]
+        xrow, op = H * W * C, p.input_op
         with torch.cuda.stream(p.stream):
+            sh = p.stream.cuda_stream
             for t in range(T):
-                self.xin_v.copy_(X[:, t * B:(t + 1) * B])
-                self.lab_v.copy_(Y[:, t * B:(t + 1) * B])
+                if ep is not None:
+                    # the input op reads this step's rows of every copy's epoch in place;
+                    # run_segment issues it directly and then restores the program's own xin
+                    p.plan.set_ptr(op, 0, ep[1].data_ptr() + t * B * xrow)
+                    p.plan.set_ptr(op, 2, ep[2].data_ptr() + t * B * 4)
+                    p.plan.set_int(op, 6, 1)
+                else:
+                    self.xin_v.copy_(X[:, t * B:(t + 1) * B])
+                    self.lab_v.copy_(Y[:, t * B:(t + 1) * B])
                 p.run_segment("fwd")
                 p.run_range(lo, hi)
                 p.run_segment("opt")
-                loss_sum += self.loss_v[:, 0].double()
-                pred = self.logit_v[..., 0] > self.threshold
-                correct += (pred == (self.lab_v > 0.5)).sum(1).double()
+                self.ext.group_metrics(io.loss.data_ptr(), io.logits.data_ptr(), io.labels.data_ptr(),
+                                       R.stride, K, B, float(self.threshold), acc.data_ptr(), sh)
         cur.wait_stream(p.stream)
         tr, ntr = self.state_views()
         flat_tr = torch.cat(tr, 1) if tr else torch.zeros(K, 0, device=self.device)
         flat_ntr = torch.cat(ntr, 1) if ntr else None
-        lv, cv = (loss_sum / T).tolist(), (correct / (T * B)).tolist()
+        lv, cv = (acc[0::2] / T).tolist(), (acc[1::2] / (T * B)).tolist()
         out = []
         for g in range(n):
             logs = {"loss": lv[g], "accuracy": cv[g]}
