@@ -350,7 +350,6 @@ class FedAvgProcess:
                 p.copy_(flatp[off:off + p.numel()].view(p.shape).to(p.dtype))
                 off += p.numel()
         total = float(n_sum.item())
-        new_tr = []
         if total > 0:
             mean_delta = delta_sum / total
             new_flat = flat_server + self.server_lr * mean_delta
@@ -359,20 +358,16 @@ class FedAvgProcess:
         # the new server weights are VIEWS of one fresh flat buffer each (trainable / statistics):
         # a per-tensor clone was ~600 copy launches per DenseNet-121 round
         new_flat = new_flat.to(dev)
-        off = 0
-        for w in state.model.trainable:
-            new_tr.append(new_flat[off:off + w.numel()].view(w.shape))
-            off += w.numel()
+        tr_w = state.model.trainable
+        new_tr = [t.view(w.shape) for t, w in zip(new_flat.split([w.numel() for w in tr_w]), tr_w)]
         if ntr_sum is not None and total > 0:
             flat_ntr_new = (ntr_sum / total).to(dev)
         else:
             flat_ntr_new = torch.cat([w.reshape(-1) for w in state.model.non_trainable]) \
                 if state.model.non_trainable else None
-        new_ntr = []
-        off = 0
-        for w in state.model.non_trainable:
-            new_ntr.append(flat_ntr_new[off:off + w.numel()].view(w.shape).to(w.dtype))
-            off += w.numel()
+        ntr_w = state.model.non_trainable
+        new_ntr = [t.view(w.shape).to(w.dtype)
+                   for t, w in zip(flat_ntr_new.split([w.numel() for w in ntr_w]), ntr_w)] if ntr_w else []
         metrics = collections.OrderedDict()
         for i, name in enumerate(self.metric_names):
             metrics[name] = float(met[1 + i].item() / total) if total else 0.0

@@ -92,11 +92,14 @@ class GroupedClientTrainer:
         return hit
 
     def state_views(self):
-        """[K, n] views of every copy's flat trainable / non-trainable weights."""
-        R = self.region
-        tr = [R.view(t.detach()).reshape(self.k, -1) for t in self.m.net.trainable_weights]
-        ntr = [R.view(t.detach()).reshape(self.k, -1) for t in self.m.net.non_trainable_weights]
-        return tr, ntr
+        """[K, n] views of every copy's flat trainable / non-trainable weights (built once: the
+        worker's weights never move, and ~600 views cost ~2.7 ms of host time per round)."""
+        if getattr(self, "_views", None) is None:
+            R = self.region
+            tr = [R.view(t.detach()).reshape(self.k, -1) for t in self.m.net.trainable_weights]
+            ntr = [R.view(t.detach()).reshape(self.k, -1) for t in self.m.net.non_trainable_weights]
+            self._views = (tr, ntr)
+        return self._views
 
     @torch.no_grad()
     def train(self, load_weights, datasets: Sequence) -> List[tuple]:

@@ -180,18 +180,16 @@ def choose_scales(max_abs, nclients: int, headroom: float = 2.0) -> np.ndarray:
     """Per segment: the largest power-of-two scale with K * max|x| * scale < 2^31 (with headroom),
     so each protected tensor keeps the resolution its own range allows."""
     m = np.asarray(max_abs, dtype=np.float64).reshape(-1)
-    out = np.empty(m.shape, dtype=np.float32)
-    for i, v in enumerate(m):
-        if not np.isfinite(v):
-            raise ValueError("non-finite value in a protected tensor")
-        if v <= 0:
-            out[i] = 2.0 ** 16
-            continue
-        s = (2 ** 31 - 1) / (nclients * v * headroom)
-        # capped at 2^100: a tiny-but-nonzero segment (|x| < ~1e-29) would otherwise overflow the
-        # float32 scale to inf (0*inf = NaN in the kernel, and the decode divides by inf)
-        out[i] = 2.0 ** min(int(np.floor(np.log2(max(s, 1.0)))), 100)
-    return out
+    if not np.isfinite(m).all():
+        raise ValueError("non-finite value in a protected tensor")
+    pos = m > 0
+    with np.errstate(divide="ignore"):
+        s = np.where(pos, (2 ** 31 - 1) / (nclients * np.where(pos, m, 1.0) * headroom), 1.0)
+    # capped at 2^100: a tiny-but-nonzero segment (|x| < ~1e-29) would otherwise overflow the
+    # float32 scale to inf (0*inf = NaN in the kernel, and the decode divides by inf); all-zero
+    # segments get 2^16
+    e = np.minimum(np.floor(np.log2(np.maximum(s, 1.0))), 100.0)
+    return np.where(pos, np.exp2(e), 2.0 ** 16).astype(np.float32)
 
 
 class MaskedAggregator:
