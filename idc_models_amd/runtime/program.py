@@ -144,7 +144,10 @@ class FusedProgram:
         # 2 -> 3.894-3.901 ms/step, 3 -> 3.915-3.923, 4 -> 3.953-3.964; MobileNetV2 (73 ops): 2 ->
         # 2.394-2.395, 3 -> 2.318, 4 -> 2.322-2.329
         n_bwd_main = sum(1 for op in b.ops if op[0] == "bwd" and op[7] == 0)
-        default_flush = "2" if n_bwd_main >= 90 else "4" if n_bwd_main >= 64 else "0"
+        # grouped (client-batched) DenseNet: secure FedAvg 0.410-0.414 s/round at 0 vs 0.416 at 2,
+        # 0.418 at 4; grouped MobileNetV2 FedAvg keeps 4 (0.220-0.222 vs 0.223 at 0)
+        big = n_bwd_main >= 90
+        default_flush = "0" if b.grouped and big else "2" if big else "4" if n_bwd_main >= 64 else "0"
         self.plan.set_side_flush(int(os.environ.get("IDC_SIDE_FLUSH", default_flush)))
         self.seg: Dict[str, Tuple[int, int]] = {}
         self.rms_index = None
