@@ -185,7 +185,7 @@ def main():
     ap.add_argument("--phase", default="full", choices=["full", "frozen", "finetune"],
                     help="frozen: reference phase 1 (base_model.trainable = False, head only); "
                          "finetune: phase 2 (layers[:fine_tune_at] frozen, 150 DenseNet / 100 "
-                         "MobileNetV2, lr/10); full: every layer trains (the headline)")
+                         "MobileNetV2 / 15 VGG16, lr/10); full: every layer trains (the headline)")
     ap.add_argument("--lr", type=float, default=1e-4)
     ap.add_argument("--no-graphs", action="store_true")
     ap.add_argument("--backend", default="fused")
@@ -263,8 +263,9 @@ def main():
         if args.phase == "frozen":
             net.base.trainable = False
         elif args.phase == "finetune":
+            from idc_models_amd.recipes.transfer import fine_tune_at_for
             net.base.trainable = True
-            for layer in net.base.layers[:150 if args.model.startswith("densenet") else 100]:
+            for layer in net.base.layers[:fine_tune_at_for(args.model)]:  # VGG16 15, MBv2 100, DN 150
                 layer.trainable = False
         model = Model(net, strategy)
         binary = args.classes == 1

@@ -29,7 +29,10 @@ enum CommOp : int { CO_SUM = 0, CO_MAX = 1, CO_MIN = 2, CO_AVG = 3 };
 
 class Communicator {
  public:
-  Communicator(int rank, int world, const std::string& unique_id, int device);
+  // init_timeout_s > 0: the communicator is created non-blocking (ncclCommInitRankConfig,
+  // blocking = 0) and the constructor polls its state, aborting and throwing after that many
+  // seconds (a peer that never joins); 0: blocking ncclCommInitRank
+  Communicator(int rank, int world, const std::string& unique_id, int device, double init_timeout_s = 0.0);
   ~Communicator();
   Communicator(const Communicator&) = delete;
   Communicator& operator=(const Communicator&) = delete;
@@ -49,6 +52,13 @@ class Communicator {
   void abort();
   void close();
 
+  // Progress marks for the host watchdog (parallel/watchdog.py): mark() records an event on the
+  // comm stream after the collectives enqueued so far, unless the previous mark is still
+  // outstanding (so the age below is that of the OLDEST unfinished mark); mark_age() is the
+  // seconds since that mark was recorded while it has not completed, 0 when none is pending.
+  void mark();
+  double mark_age();
+
   hipStream_t stream() const { return stream_; }
   int rank() const { return rank_; }
   int world() const { return world_; }
@@ -58,7 +68,13 @@ class Communicator {
 
  private:
   void require_open() const;
+  void settle(ncclResult_t r, const char* what);  // non-blocking comms: wait out ncclInProgress
   ncclComm_t comm_ = nullptr;
+  bool nonblocking_ = false;
+  double settle_timeout_s_ = 0.0;
+  hipEvent_t mark_ev_ = nullptr;
+  bool mark_pending_ = false;
+  double mark_t_ = 0.0;
   hipStream_t stream_ = nullptr;
   int rank_ = 0, world_ = 1, device_ = 0;
   long long ncoll_ = 0;

@@ -51,9 +51,16 @@ struct DenseStageArgs {
   float inv_count;              // 1 / (N*H*W)
   unsigned max_polls;           // bound on one wait's polls (0: default, ~0.5 s)
   int lookahead;                // queue order (set by dense_stage_fwd): 0 [A0][B0][A1][B1]...,
-                                // 1 [A0][A1][B0][A2][B1]...[B_{L-1}] (see dense_stage.hip)
+                                // 1 [A0][A1][B0][A2][B1]...[B_{L-1}] (see dense_stage.hip); the
+                                // caller passes -1 to forbid the lookahead order (another
+                                // persistent launch may share the device: the order needs more
+                                // than one phase of workgroups resident)
   int infer;                    // inference-mode BatchNorms (moving statistics; frozen layers,
                                 // evaluation): no statistics are produced, only data hand-offs
+  int* stepflag;                // nullable: the program's per-step guard word; a launch that gives
+                                // up ORs 2 into it (the optimizer then skips the step's update)
+  int* hostflag;                // nullable: pinned host word set to 1 on a give-up (never shifted
+                                // per group copy; the runtime polls it without a device sync)
 };
 
 // number of work items of one launch (the grid never needs more workgroups than this)
@@ -125,6 +132,8 @@ struct DenseBwdArgs {
   int N, H, W, ld, c0, nlayers, k2, act, nphases, ntickets;
   float inv_count;
   unsigned max_polls;
+  int* stepflag;                  // nullable: per-step guard word (as DenseStageArgs::stepflag)
+  int* hostflag;                  // nullable: pinned host give-up flag (as DenseStageArgs::hostflag)
 };
 
 hipError_t dense_stage_bwd(const DenseBwdArgs& a, int grid, hipStream_t st);

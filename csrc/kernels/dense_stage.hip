@@ -142,6 +142,7 @@ __global__ __launch_bounds__(NT) void dense_stage_kernel(DenseStageArgs a, Group
   unsigned* lastfin = sync + 1 + 16 * a.nlayers;
   unsigned* fail = lastfin + 1;  // this launch gave up (zeroed with the counters)
   int* err = gsh(a.err, go);
+  const persist::FailSink fsink{err, gsh(a.stepflag, go), a.hostflag};
   float* scratch = gsh(a.scratch, go);
   unsigned long long* stamps = gsh(a.stamps, go);
   const unsigned max_polls = a.max_polls ? a.max_polls : DEFAULT_POLLS;
@@ -220,7 +221,7 @@ __global__ __launch_bounds__(NT) void dense_stage_kernel(DenseStageArgs a, Group
       // of B_{l-3} -- hence complete before B_{l-2} started), B_{l-2}'s slots for [cold-32, cold)
       if (l >= 2) {
         if (wid == 0) {
-          const bool ok = wait_sum8(cntB(l - 2), (unsigned)nB, fail, err, max_polls);
+          const bool ok = wait_sum8(cntB(l - 2), (unsigned)nB, fail, fsink, max_polls);
           if (lane == 0) s.bad = !ok;
         }
         __syncthreads();
@@ -321,7 +322,7 @@ __global__ __launch_bounds__(NT) void dense_stage_kernel(DenseStageArgs a, Group
       // ---- the newest slice [cold, cin): wait for B_{l-1}
       if (l > 0) {
         if (wid == 0) {
-          const bool ok = wait_sum8(cntB(l - 1), (unsigned)nB, fail, err, max_polls);
+          const bool ok = wait_sum8(cntB(l - 1), (unsigned)nB, fail, fsink, max_polls);
           if (lane == 0) s.bad = !ok;
         }
         __syncthreads();
@@ -453,7 +454,7 @@ __global__ __launch_bounds__(NT) void dense_stage_kernel(DenseStageArgs a, Group
       }
       stamp(stamps, task, 1);
       if (wid == 0) {
-        const bool ok = wait_sum8(cntA(l), (unsigned)nA, fail, err, max_polls);
+        const bool ok = wait_sum8(cntA(l), (unsigned)nA, fail, fsink, max_polls);
         if (lane == 0) s.bad = !ok;
       }
       __syncthreads();
@@ -622,7 +623,7 @@ hipError_t dense_stage_fwd(const DenseStageArgs& a, int grid, hipStream_t st) {
   int nA, nB;
   dense_stage_phase_tiles(a.N * a.H * a.W, nA, nB);
   DenseStageArgs b = a;
-  b.lookahead = (la_on && k == 1 && a.nlayers > 1 && grid >= nA + 16) ? 1 : 0;
+  b.lookahead = (a.lookahead >= 0 && la_on && k == 1 && a.nlayers > 1 && grid >= nA + 16) ? 1 : 0;
   hipLaunchKernelGGL(dense_stage_kernel, ggrid(grid), dim3(NT), 0, st, b, garg());
   return hipGetLastError();
 }

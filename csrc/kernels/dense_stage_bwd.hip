@@ -119,6 +119,7 @@ __global__ __launch_bounds__(NT) void dense_stage_bwd_kernel(DenseBwdArgs a, Gro
   unsigned* sync = gsh(a.sync, go);
   float* btot = gsh(a.btot, go);
   int* err = gsh(a.err, go);
+  const persist::FailSink fsink{err, gsh(a.stepflag, go), a.hostflag};
   unsigned long long* stamps = gsh(a.stamps, go);
   const unsigned max_polls = a.max_polls ? a.max_polls : DEFAULT_POLLS;
   BwdAff pend = a.pend;
@@ -175,14 +176,14 @@ __global__ __launch_bounds__(NT) void dense_stage_bwd_kernel(DenseBwdArgs a, Gro
     // wait ends the workgroup
 #define DSB_WAIT(cnt, need)                                                                   \
   do {                                                                                        \
-    if (tid == 0) s.bad = !wait_count((cnt), (unsigned)(need), fail, err, max_polls);         \
+    if (tid == 0) s.bad = !wait_count((cnt), (unsigned)(need), fail, fsink, max_polls);         \
     __syncthreads();                                                                          \
     if (__builtin_amdgcn_readfirstlane(s.bad)) return;                                       \
   } while (0)
 #define DSB_WAIT8(cnt, need)                                                                  \
   do {                                                                                        \
     if (wid == 0) {                                                                           \
-      const bool ok_ = wait_sum8((cnt), (unsigned)(need), fail, err, max_polls);              \
+      const bool ok_ = wait_sum8((cnt), (unsigned)(need), fail, fsink, max_polls);              \
       if (lane == 0) s.bad = !ok_;                                                            \
     }                                                                                         \
     __syncthreads();                                                                          \

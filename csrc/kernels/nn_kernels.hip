@@ -850,7 +850,11 @@ __global__ __launch_bounds__(256) void head_fwd_kernel(HeadArgs a, GroupArg ga) 
         idc::persist::st_coh(a.loss_vec + n, loss);
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         const unsigned t = __hip_atomic_fetch_add(a.ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        s_red[4 * a.U] = ((t + 1u) % (unsigned)a.N == 0u) ? 1.f : 0.f;
+        const bool last = (t + 1u) % (unsigned)a.N == 0u;
+        // the last arrival re-arms the ticket for the next launch (every arrival of this one is
+        // in), so the count never depends on N dividing 2^32 or on earlier launches completing
+        if (last) __hip_atomic_store(a.ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        s_red[4 * a.U] = last ? 1.f : 0.f;
       } else if (a.loss) {
         atomicAdd(a.loss, loss * a.loss_scale);
       }
@@ -1026,8 +1030,10 @@ hipError_t finite_check(const float* g, long long n, int* flag, hipStream_t st) 
 __global__ void finite_flag_reset_kernel(int* flag, int* status, GroupArg ga) {
   flag = gsh(flag, goff(ga));
   status = gsh(status, goff(ga));
+  // flag bit 0: non-finite gradients; bit 1: a persistent launch gave up (persist.h note_fail);
+  // summed over data-parallel ranks by the step-guard all-reduce, so any non-zero value skips
   status[0] = flag[0];
-  status[1] += flag[0];  // running count of skipped steps
+  status[1] += flag[0] != 0;  // running count of skipped steps
   flag[0] = 0;
 }
 

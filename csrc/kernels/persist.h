@@ -41,17 +41,37 @@ __device__ __forceinline__ void st_coh16(void* p, const uint4& v) {
 
 constexpr unsigned DEFAULT_POLLS = 1u << 19;  // ~0.5-1 s of polling
 
+// A launch gave up: the first workgroup to set the fail flag counts the launch in the persistent
+// error counter and raises bit 1 of the program's per-step guard word (the flag the optimizer's
+// skip test reads: the step's update is dropped, its stale outputs never reach the weights; the
+// host sees the counter after the step, runtime/program.py FusedStep.check_persistent).
+// ``hostflag`` (nullable) is a word of pinned host memory the runtime polls without a device
+// synchronisation: a plain system-scope store of 1.
+struct FailSink {
+  int* err;
+  int* stepflag;
+  int* hostflag;
+};
+__device__ inline void note_fail(unsigned* fail, const FailSink& fs) {
+  const unsigned old = __hip_atomic_fetch_or(fail, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (old == 0) {
+    if (fs.err) atomicAdd(fs.err, 1);
+    if (fs.stepflag) atomicOr(fs.stepflag, 2);
+    if (fs.hostflag) __hip_atomic_store(fs.hostflag, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
+}
+
 // thread 0: wait until *cnt >= need.  Every 256 polls the fail flag is checked.  On a timeout (or
 // when another workgroup already failed) returns false; the workgroup that first sets the fail
 // flag counts the launch in the persistent error counter.
-__device__ inline bool wait_count(const unsigned* cnt, unsigned need, unsigned* fail, int* err, unsigned max_polls) {
+__device__ inline bool wait_count(const unsigned* cnt, unsigned need, unsigned* fail, const FailSink& fs,
+                                  unsigned max_polls) {
   unsigned polls = 0;
   while (__hip_atomic_load(cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < need) {
     __builtin_amdgcn_s_sleep(1);
     if ((++polls & 255u) == 0 || polls >= max_polls) {
       if (polls >= max_polls || __hip_atomic_load(fail, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0) {
-        const unsigned old = __hip_atomic_fetch_or(fail, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        if (old == 0 && err) atomicAdd(err, 1);
+        note_fail(fail, fs);
         return false;
       }
     }
@@ -84,7 +104,8 @@ __device__ __forceinline__ unsigned publish_shard(unsigned* cnt8, int tile) {
 
 // called by ALL lanes of ONE wave: wait until the shards of cnt8 sum to >= need; returns a
 // wave-uniform result (false: timeout or fail flag, counted like wait_count)
-__device__ inline bool wait_sum8(const unsigned* cnt8, unsigned need, unsigned* fail, int* err, unsigned max_polls) {
+__device__ inline bool wait_sum8(const unsigned* cnt8, unsigned need, unsigned* fail, const FailSink& fs,
+                                 unsigned max_polls) {
   const int lane = threadIdx.x & 63;
   unsigned polls = 0;
   for (;;) {
@@ -99,10 +120,7 @@ __device__ inline bool wait_sum8(const unsigned* cnt8, unsigned need, unsigned* 
       unsigned f = lane == 0 ? __hip_atomic_load(fail, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0u;
       f = __builtin_amdgcn_readfirstlane(f);
       if (polls >= max_polls || f != 0) {
-        if (lane == 0) {
-          const unsigned old = __hip_atomic_fetch_or(fail, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          if (old == 0 && err) atomicAdd(err, 1);
-        }
+        if (lane == 0) note_fail(fail, fs);
         return false;
       }
     }

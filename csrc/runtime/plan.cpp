@@ -876,6 +876,19 @@ void py_rmsprop(uintptr_t w, uintptr_t g, uintptr_t ms, long long n, float lr, f
         "rmsprop");
 }
 
+// Pinned host words the device writes and the host polls without a synchronisation (the
+// persistent launches' give-up flag, DenseStageArgs::hostflag).  hipHostMalloc memory is mapped
+// into the device address space under the same pointer.
+uintptr_t py_host_alloc(long long bytes) {
+  void* p = nullptr;
+  check(hipHostMalloc(&p, (size_t)bytes, hipHostMallocMapped), "hipHostMalloc");
+  std::memset(p, 0, (size_t)bytes);
+  return reinterpret_cast<uintptr_t>(p);
+}
+void py_host_free(uintptr_t p) {
+  if (p) (void)hipHostFree(reinterpret_cast<void*>(p));
+}
+
 }  // namespace
 
 // torch.cuda.memory.CUDAPluggableAllocator entry points (looked up by name with dlsym)
@@ -904,10 +917,15 @@ extern "C" __attribute__((visibility("default"))) void idc_region_free(void* ptr
 PYBIND11_MODULE(_idc_native, m) {
   m.doc() = "idc_models_amd native MI355X (gfx950) kernels and plan executor";
   py::class_<Communicator>(m, "Communicator")
-      .def(py::init([](int rank, int world, py::bytes uid, int device) {
-             return new Communicator(rank, world, std::string(uid), device);
+      .def(py::init([](int rank, int world, py::bytes uid, int device, double init_timeout_s) {
+             std::string u = uid;
+             py::gil_scoped_release nogil;  // a non-blocking init polls for its peers
+             return new Communicator(rank, world, u, device, init_timeout_s);
            }),
-           py::arg("rank"), py::arg("world"), py::arg("unique_id"), py::arg("device"))
+           py::arg("rank"), py::arg("world"), py::arg("unique_id"), py::arg("device"),
+           py::arg("init_timeout_s") = 0.0)
+      .def("mark", &Communicator::mark)
+      .def("mark_age", &Communicator::mark_age)
       .def_static("make_unique_id", []() { return py::bytes(Communicator::make_unique_id()); })
       .def("all_reduce", [](Communicator& c, uintptr_t buf, long long n, int dt, int op, uintptr_t st) {
              c.all_reduce(reinterpret_cast<void*>(buf), n, dt, op, reinterpret_cast<hipStream_t>(st));
@@ -999,6 +1017,8 @@ PYBIND11_MODULE(_idc_native, m) {
   m.def("tile_bn", &conv_tile_bn);
   m.def("tile_bk", &conv_tile_bk);
   m.def("rmsprop", &py_rmsprop);
+  m.def("host_alloc", &py_host_alloc);
+  m.def("host_free", &py_host_free);
   m.def("secagg_mask", &py_secagg_mask, py::arg("x"), py::arg("out"), py::arg("n"), py::arg("seg_scale"),
         py::arg("seg_end"), py::arg("nseg"), py::arg("clip"), py::arg("nclients"), py::arg("rank"), py::arg("keys"),
         py::arg("round_"), py::arg("alive"), py::arg("stream"), py::arg("accumulate") = 0);

@@ -74,7 +74,9 @@ class EagerStep:
         m.arena.zero_grad()
         if m.arena.params:
             m.strategy.bucketer(m.arena)  # installs overlap hooks once (no-op single device)
-            loss.backward()
+            from ..parallel.strategy import current_replica_weight
+            w = current_replica_weight[0]  # uneven split of a global batch (strategy._ShardedBatches)
+            (loss * w if w != 1.0 else loss).backward()
             m.strategy.apply_gradients(m.optimizer, m.arena)
         return loss.detach(), logits.detach()
 
@@ -169,18 +171,16 @@ class Model:
         return n
 
     def _check_persistent(self):
-        """Once per epoch: a persistent launch that gave up on a wait (fail flag, error counter)
-        left stale outputs -- say so instead of training on silently."""
-        fn = getattr(self.impl, "persistent_failures", None)
-        if fn is None:
+        """End of epoch, once every step of it has run: a persistent dense-stage launch that gave
+        up on a wait has already made its step skip the weight update on the device (step guard
+        word); the backend's policy (IDC_DS_ON_FAIL: fall back to per-layer kernels, or raise)
+        applies here at the latest -- train_step polls the same flags before every step."""
+        fn = getattr(self.impl, "check_persistent", None)
+        if fn is None or not getattr(self.impl, "progs", None):
             return
-        n = fn()
-        if n > getattr(self, "_persist_fail_seen", 0):
-            import warnings
-            warnings.warn(f"{n - getattr(self, '_persist_fail_seen', 0)} persistent dense-stage launch(es) timed "
-                          "out this epoch: their outputs are stale (IDC_DENSE_STAGE=0 / IDC_DENSE_STAGE_BWD=0 "
-                          "run the per-layer kernels)", RuntimeWarning)
-            self._persist_fail_seen = n
+        if self.device.type == "cuda":
+            torch.cuda.current_stream(self.device).synchronize()
+        fn()
 
     def reset_optimizer(self):
         """Fresh optimizer slot state without re-lowering (TFF re-creates the client optimizer

@@ -161,12 +161,23 @@ class FedAvgProcess:
         return self._worker
 
     def workers(self, n: int):
-        """``n`` worker models: the primary one plus independently built copies."""
+        """``n`` worker models: the primary one plus independently built copies.  With n > 1 they
+        run concurrently on one device: their programs must not use a persistent launch order that
+        assumes the device to itself (Builder.shared_device)."""
         while len(self._more_workers) < n - 1:
             m = self.model_fn()
             m.compile(self.client_optimizer_fn(), self.loss, list(self.metric_names), backend=self.backend)
             self._more_workers.append(m)
-        return [self.worker()] + self._more_workers[:n - 1]
+        ws = [self.worker()] + self._more_workers[:n - 1]
+        if n > 1:
+            for m in ws:
+                impl = m.impl
+                if impl is not None and not getattr(impl, "shared_device", False):
+                    impl.shared_device = True
+                    if getattr(impl, "progs", None):  # built for exclusive use: rebuild
+                        impl.sync_to_module()
+                        impl.close()
+        return ws
 
     def _train_client(self, m, state: "ServerState", ds):
         """Local training of one client from the server weights: returns its flat trainable
@@ -210,11 +221,25 @@ class FedAvgProcess:
         and kernels never order each other)."""
         if self.client_batching and len(mine) > 0 and self.local_epochs == 1:
             from .grouped import eligible
+            from ..runtime.builder import PersistentLaunchError, disable_persistent
             sets = [data[k] for k in mine]
             if eligible(sets, self.worker()):
                 g = self._grouped_trainer(len(mine), sets[0].batch_size)
-                res = g.train(lambda m: self._load(m, state.model), sets)
-                return dict(zip(mine, res))
+                try:
+                    res = g.train(lambda m: self._load(m, state.model), sets)
+                    return dict(zip(mine, res))
+                except PersistentLaunchError as e:
+                    # a client copy's persistent launch gave up: its skipped steps make the round
+                    # wrong, so the round is re-run on a grouped program without persistent
+                    # launches (IDC_DS_ON_FAIL=raise: propagate)
+                    if os.environ.get("IDC_DS_ON_FAIL", "fallback") == "raise":
+                        raise
+                    disable_persistent(str(e))
+                    g.region.close()
+                    self._grouped = None
+                    g = self._grouped_trainer(len(mine), sets[0].batch_size)
+                    res = g.train(lambda m: self._load(m, state.model), sets)
+                    return dict(zip(mine, res))
         W = min(self.concurrent, len(mine))
         if W <= 1 or not torch.cuda.is_available() or self.worker().device.type != "cuda":
             return {k: self._train_client(self.worker(), state, data[k]) for k in mine}
@@ -323,9 +348,14 @@ class FedAvgProcess:
                 if ntr_sum is not None:
                     ntr_sum += torch.where(fin, n_k * flat_ntr, zero)
             n_sum += n_k * w
-            met[0] += n_k * logs.get("loss", 0.0) * w
+            # a diverged client's metrics are usually non-finite too (NaN * 0 = NaN): select, not
+            # multiply, so its loss never reaches the round's metrics
+            zero64 = met.new_zeros(())
+            met[0] += torch.where(fin, torch.as_tensor(n_k * logs.get("loss", 0.0), dtype=met.dtype,
+                                                       device=met.device), zero64)
             for i, name in enumerate(self.metric_names):
-                met[1 + i] += n_k * logs.get(name if name in logs else "accuracy", 0.0) * w
+                v = logs.get(name if name in logs else "accuracy", 0.0)
+                met[1 + i] += torch.where(fin, torch.as_tensor(n_k * v, dtype=met.dtype, device=met.device), zero64)
         if self.secure:
             # the weighted deltas cross ranks only masked; counts and metrics in the clear
             if self._agg is None or self._agg.K != K:

@@ -158,6 +158,15 @@ class GroupedClientTrainer:
                 self.ext.group_metrics(io.loss.data_ptr(), io.logits.data_ptr(), io.labels.data_ptr(),
                                        R.stride, K, B, float(self.threshold), acc.data_ptr(), sh)
         cur.wait_stream(p.stream)
+        err = getattr(p.b, "dense_err", None)
+        if err is not None:
+            # every copy's persistent-launch error counter (a give-up skipped that client's step)
+            tot = int(R.view(err)[:, 0].sum().item())
+            if tot > getattr(self, "_err_seen", 0):
+                self._err_seen = tot
+                from ..runtime.builder import PersistentLaunchError
+                raise PersistentLaunchError(f"{tot} persistent dense-stage launch(es) of the grouped client "
+                                            "program gave up on a wait")
         tr, ntr = self.state_views()
         flat_tr = torch.cat(tr, 1) if tr else torch.zeros(K, 0, device=self.device)
         flat_ntr = torch.cat(ntr, 1) if ntr else None

@@ -7,7 +7,7 @@ homomorphically, every client decrypts (quirk Q13: every client can decrypt ever
 Here: each client quantises its weights to fixed point (int32 two's complement,
 one power-of-two scale per protected tensor), adds pairwise Philox masks ``+m_ij`` / ``-m_ij`` for
 every other participant, and the masked vectors are summed with ONE integer all-reduce (RCCL over
-xGMI; int32 sums wrap mod 2^32).  The masks cancel exactly, so the result equals the plain
+xGMI over ``ncclUint32``: unsigned sums wrap mod 2^32 by definition).  The masks cancel exactly, so the result equals the plain
 fixed-point sum BIT-EXACTLY, while any single masked vector is uniformly random.  The pair keys come
 from a Diffie-Hellman agreement between the two clients (``keyagree.py``): the aggregator, which
 sees only public keys and masked vectors, cannot regenerate any mask.  ``percent`` keeps its
@@ -156,7 +156,9 @@ def segment_absmax(vecs, seg_end, nseg: int, dev) -> torch.Tensor:
     ``secagg_absmax`` kernel, one launch per vector."""
     seg_end = np.asarray(seg_end, dtype=np.int64)
     dev = torch.device(dev)
-    if dev.type == "cuda" and vecs:
+    if not vecs:
+        return torch.zeros(nseg, dtype=torch.float32, device=dev)
+    if dev.type == "cuda":
         from ..ops import _native as nat
         bits = torch.zeros(nseg, dtype=torch.int32, device=dev)
         se = torch.from_numpy(seg_end).to(dev)
@@ -167,13 +169,16 @@ def segment_absmax(vecs, seg_end, nseg: int, dev) -> torch.Tensor:
                 raise ValueError("segments do not cover the vector")
             ext.secagg_absmax(v.data_ptr(), v.numel(), se.data_ptr(), nseg, bits.data_ptr(), nat.stream_handle())
         return bits.view(torch.float32)
-    mx = torch.zeros(nseg, dtype=torch.float32, device=dev)
-    starts = np.concatenate([[0], seg_end[:-1]])
+    # CPU: one scatter-amax per vector over the element -> segment index (empty segments stay 0)
+    n = int(seg_end[-1]) if len(seg_end) else 0
+    seg_of = torch.from_numpy(_seg_index(n, seg_end))
+    mx = torch.zeros(nseg, dtype=torch.float32)
     for v in vecs:
-        a = v.reshape(-1).float().abs()
-        mx = torch.maximum(mx, torch.stack([a[int(s0):int(s1)].max() if s1 > s0 else a.new_zeros(())
-                                            for s0, s1 in zip(starts, seg_end)]).to(dev))
-    return mx
+        a = v.reshape(-1).float().abs().cpu()
+        if a.numel() != n:
+            raise ValueError("segments do not cover the vector")
+        mx.scatter_reduce_(0, seg_of, a, reduce="amax", include_self=True)
+    return mx.to(dev)
 
 
 def choose_scales(max_abs, nclients: int, headroom: float = 2.0) -> np.ndarray:
@@ -248,7 +253,7 @@ class MaskedAggregator:
                                            participants=parts)
                     total = (total + masked.to(torch.int64)) % (1 << 32)
         t32 = total if gpu else torch.where(total >= (1 << 31), total - (1 << 32), total).to(torch.int32)
-        comm.all_reduce_(t32)  # int32 SUM wraps mod 2^32 on RCCL / gloo
+        comm.ring_sum_u32_(t32)  # SUM mod 2^32 (RCCL: one ncclUint32 all-reduce, defined wrap)
         t0 = time.perf_counter()
         out = unmask(t32, scales, seg_end, 1.0).to(dev)
         dt = time.perf_counter() - t0

@@ -146,7 +146,7 @@ class DenseStageArgs(C.Structure):
                 ("scratch", vp), ("stamps", vp),
                 ("N", ci), ("H", ci), ("W", ci), ("ld", ci), ("nlayers", ci), ("k2", ci),
                 ("act1", ci), ("act2", ci), ("inv_count", cf), ("max_polls", C.c_uint), ("lookahead", ci),
-                ("infer", ci)]
+                ("infer", ci), ("stepflag", vp), ("hostflag", vp)]
 
 
 class DenseBwdLayerDesc(C.Structure):
@@ -165,7 +165,7 @@ class DenseBwdArgs(C.Structure):
                [("pend", BwdAff)] + \
                [(n, vp) for n in ("layers", "phases", "sync", "btot", "err", "stamps")] + \
                [(n, ci) for n in ("N", "H", "W", "ld", "c0", "nlayers", "k2", "act", "nphases", "ntickets")] + \
-               [("inv_count", cf), ("max_polls", C.c_uint)]
+               [("inv_count", cf), ("max_polls", C.c_uint), ("stepflag", vp), ("hostflag", vp)]
 
 
 _STRUCTS = {"BnArgs": BnArgs, "BwdAff": BwdAff, "ConvArgs": ConvArgs, "WgradArgs": WgradArgs,

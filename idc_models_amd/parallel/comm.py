@@ -60,6 +60,7 @@ def backend() -> Optional[str]:
 
 def destroy():
     global _FORCED
+    destroy_native_ring()
     if dist.is_available() and dist.is_initialized():
         dist.destroy_process_group()
     _FORCED = False
@@ -96,6 +97,50 @@ def all_reduce_max(value: float, device) -> float:
     t = torch.tensor([value], dtype=torch.float64, device=device)
     all_reduce_(t, dist.ReduceOp.MAX)
     return float(t.item())
+
+
+_NATIVE_RING = None  # (group identity, NativeCommunicator) for ring sums on RCCL
+
+
+def _native_ring(device):
+    """A native RCCL communicator over the default group (created on first use), or None when the
+    group is not RCCL or native collectives are off (IDC_NATIVE_COMM=0)."""
+    global _NATIVE_RING
+    if backend() != "nccl" or os.environ.get("IDC_NATIVE_COMM", "1") == "0":
+        return None
+    key = id(dist.group.WORLD)
+    if _NATIVE_RING is None or _NATIVE_RING[0] != key:
+        from .native_comm import NativeCommunicator
+        _NATIVE_RING = (key, NativeCommunicator(dist.get_rank(), dist.get_world_size(), device, watchdog=False))
+    return _NATIVE_RING[1]
+
+
+def ring_sum_u32_(t: torch.Tensor) -> torch.Tensor:
+    """In-place SUM over the ranks modulo 2^32 of an int32 tensor that holds uint32 bit patterns
+    (the masked fixed-point vectors of secure aggregation, fed/secagg.py).  On RCCL: ONE native
+    ``ncclUint32`` all-reduce (unsigned wrap is defined; a signed int32 sum that wraps is not); on
+    gloo (or with native collectives off): an exact int64 sum of the unsigned values, reduced mod
+    2^32."""
+    if not is_dist():
+        return t
+    if t.dtype != torch.int32:
+        raise TypeError("ring_sum_u32_: int32 bit patterns expected")
+    nc = _native_ring(t.device) if t.is_cuda else None
+    if nc is not None:
+        nc.all_reduce_u32_(t, stream=torch.cuda.current_stream(t.device))
+        return t
+    wide = t.to(torch.int64) & 0xFFFFFFFF
+    dist.all_reduce(wide)  # < world * 2^32: exact in int64
+    wide &= 0xFFFFFFFF
+    t.copy_(torch.where(wide >= (1 << 31), wide - (1 << 32), wide).to(torch.int32))
+    return t
+
+
+def destroy_native_ring():
+    global _NATIVE_RING
+    if _NATIVE_RING is not None:
+        _NATIVE_RING[1].close()
+        _NATIVE_RING = None
 
 
 def pack_all_reduce(tensors: List[torch.Tensor], op=dist.ReduceOp.SUM) -> List[torch.Tensor]:

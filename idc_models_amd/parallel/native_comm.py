@@ -7,11 +7,17 @@ one Python ``dist.all_reduce`` call per bucket.  Reference: the NCCL all-reduce 
 ``tf.distribute.MirroredStrategy`` runs inside every step (``dist_model_tf_vgg.py:115``).
 
 Bootstrap: rank 0 creates the 128-byte RCCL unique id, publishes it in the ``torch.distributed``
-TCPStore, every rank reads it and joins (``ncclCommInitRank``).  A world of one needs no store.
+TCPStore, every rank reads it and joins.  A world of one needs no store.  With more than one rank
+the communicator is created non-blocking (``ncclCommInitRankConfig``) and a rank whose peers do not
+join within ``IDC_COMM_INIT_TIMEOUT`` seconds (default 300) raises instead of hanging; a
+``CommWatchdog`` (``parallel/watchdog.py``) then aborts the communicator when RCCL reports an
+asynchronous error or a step's collectives make no progress for ``IDC_COMM_TIMEOUT`` seconds
+(default 300; ``IDC_COMM_WATCHDOG=0`` turns it off).
 """
 from __future__ import annotations
 
 import itertools
+import os
 from typing import Optional
 
 import torch
@@ -38,8 +44,12 @@ def _op_code(op) -> int:
 class NativeCommunicator:
     """One RCCL communicator over the ranks of the default process group (or a world of one)."""
 
-    def __init__(self, rank: int, world: int, device, store=None, timeout_s: float = 600.0):
-        ext = nat.require()
+    def __init__(self, rank: int, world: int, device, store=None, timeout_s: float = 600.0, ext=None,
+                 watchdog: Optional[bool] = None, init_timeout_s: Optional[float] = None):
+        """``ext``: the native module (tests pass a fake to exercise the bootstrap on the CPU).
+        ``init_timeout_s``: > 0 creates the communicator non-blocking with that timeout (default:
+        IDC_COMM_INIT_TIMEOUT, 300 s, for a world > 1; blocking for a world of one)."""
+        ext = ext if ext is not None else nat.require()
         self.rank, self.world = int(rank), int(world)
         self.device = torch.device(device)
         if self.device.type != "cuda":
@@ -57,7 +67,18 @@ class NativeCommunicator:
             else:
                 store.wait([key])
                 uid = store.get(key)
-        self.c = ext.Communicator(self.rank, self.world, bytes(uid), self.device.index or 0)
+        if init_timeout_s is not None:
+            init_timeout = float(init_timeout_s)
+        else:
+            init_timeout = float(os.environ.get("IDC_COMM_INIT_TIMEOUT", "300")) if self.world > 1 else 0.0
+        self.c = ext.Communicator(self.rank, self.world, bytes(uid), self.device.index or 0, init_timeout)
+        self.watchdog = None
+        if watchdog is None:
+            watchdog = self.world > 1 and os.environ.get("IDC_COMM_WATCHDOG", "1") != "0"
+        if watchdog:
+            from .watchdog import CommWatchdog
+            self.watchdog = CommWatchdog(self.c, timeout_s=float(os.environ.get("IDC_COMM_TIMEOUT", "300")),
+                                         name=f"rccl rank {self.rank}/{self.world}").start()
 
     # ------------------------------------------------------------------ properties
     @property
@@ -91,6 +112,14 @@ class NativeCommunicator:
         self.c.all_reduce(t.data_ptr(), t.numel(), DTYPES[t.dtype], _op_code(op), self._stream(stream))
         return t
 
+    def all_reduce_u32_(self, t: torch.Tensor, stream: Optional[torch.cuda.Stream] = None):
+        """In-place SUM modulo 2^32 of a 4-byte integer tensor read as uint32 (``ncclUint32``)."""
+        self._check(t)
+        if t.element_size() != 4 or t.dtype.is_floating_point:
+            raise TypeError("all_reduce_u32_ needs a 32-bit integer tensor")
+        self.c.all_reduce(t.data_ptr(), t.numel(), 4, 0, self._stream(stream))
+        return t
+
     def reduce_(self, t: torch.Tensor, root: int = 0, op="sum", stream=None):
         self._check(t)
         self.c.reduce(t.data_ptr(), t.numel(), DTYPES[t.dtype], _op_code(op), int(root), self._stream(stream))
@@ -109,9 +138,26 @@ class NativeCommunicator:
         return out
 
     def check(self):
-        self.c.check_async()
+        """Raise if the watchdog aborted the communicator or RCCL reports an asynchronous error."""
+        if self.watchdog is not None:
+            self.watchdog.raise_if_failed()
+        if self.c is not None:
+            self.c.check_async()
+
+    def step_issued(self):
+        """After a step's collectives were enqueued: a progress mark for the watchdog, and the
+        failure (if any) it detected on an earlier step raised here, on the training thread."""
+        if self.watchdog is not None:
+            self.watchdog.raise_if_failed()
+            self.watchdog.mark()
 
     def close(self):
+        if self.watchdog is not None:
+            self.watchdog.stop()
+            failed = self.watchdog.error is not None
+            self.watchdog = None
+            if failed:  # aborted: nothing left to destroy
+                self.c = None
         if self.c is not None:
             self.c.close()
             self.c = None

@@ -258,6 +258,11 @@ class CentralStorageStrategy(MirroredStrategy):
                 dist.broadcast(t, 0)
 
 
+# weight of the current local batch in the global-batch mean (set by _ShardedBatches while a
+# replica's slice of an unevenly split batch is being trained; read by the training steps)
+current_replica_weight = [1.0]
+
+
 class _ShardedBatches:
     """Fallback for arbitrary iterables of global batches: rank ``r`` takes its contiguous slice
     of every batch.  Uneven batches are split as evenly as possible (the first ``b % world``
@@ -271,6 +276,7 @@ class _ShardedBatches:
         return len(self.data)
 
     def __iter__(self):
+        st = current_replica_weight
         for x, y in self.data:
             b = x.shape[0]
             if b < self.world:
@@ -278,7 +284,15 @@ class _ShardedBatches:
             per, extra = divmod(b, self.world)
             lo = self.rank * per + min(self.rank, extra)
             hi = lo + per + (1 if self.rank < extra else 0)
-            yield x[lo:hi], y[lo:hi]
+            # the global-batch mean (TF scales each replica's loss by 1 / global batch): a replica
+            # holding n of the b rows weighs its local-mean gradient by n * world / b before the
+            # SUM all-reduce and the optimizer's 1 / world (1 when the split is even)
+            st[0] = (hi - lo) * self.world / b
+            try:
+                yield x[lo:hi], y[lo:hi]
+            finally:
+                st[0] = 1.0
+
 
 
 def _all_layers(net):

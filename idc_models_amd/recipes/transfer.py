@@ -61,6 +61,18 @@ PRESETS = {
 }
 
 
+def fine_tune_at_for(arch: str) -> int:
+    """The reference's phase-2 cut for a backbone: VGG16 15 (``dist_model_tf_vgg.py:146``, block5
+    trains), MobileNetV2 100 (``dist_model_tf_mobile.py:146``), DenseNets 150
+    (``dist_model_tf_dense.py:158``)."""
+    for pre in PRESETS.values():
+        if pre["arch"] == arch:
+            return int(pre["fine_tune_at"])
+    if arch.startswith("densenet"):
+        return int(PRESETS["dense"]["fine_tune_at"])
+    raise KeyError(f"no reference fine-tuning cut for {arch!r}")
+
+
 def make_strategy(kind: str):
     from ..parallel import CentralStorageStrategy, MirroredStrategy, OneDeviceStrategy
     if kind == "central":

@@ -123,6 +123,29 @@ def act_only(act: int) -> nat.BnArgs:
 
 IDENT = None
 
+# Persistent dense-stage launches switched off for the rest of the process (a launch gave up on a
+# wait: see disable_persistent); checked by dense_stage_ok / dense_stage_bwd_ok
+_PERSISTENT_OFF: List[str] = []
+
+
+def disable_persistent(reason: str):
+    """Build no more persistent dense-stage launches in this process (programs built from now on
+    run the per-layer kernels).  Called by the runtime when a launch timed out (runtime/program.py
+    FusedStep.check_persistent, fed/fedavg.py client batching)."""
+    if not _PERSISTENT_OFF:
+        import warnings
+        warnings.warn(f"persistent dense-stage launches disabled: {reason}", RuntimeWarning, stacklevel=2)
+    _PERSISTENT_OFF.append(reason)
+
+
+def persistent_disabled() -> bool:
+    return bool(_PERSISTENT_OFF)
+
+
+class PersistentLaunchError(RuntimeError):
+    """A persistent dense-stage launch gave up on a wait (IDC_DS_ON_FAIL=raise); the step it
+    belonged to skipped its weight update."""
+
 
 class Builder:
     def __init__(self, net, arena, device, batch: int, training: bool):
@@ -173,6 +196,15 @@ class Builder:
         # flush_wgrad_batch (DenseNet: the end of a late stage's dense layers)
         self._wg_batch: List[tuple] = []
         self._wg_batch_marks: list = []
+        # fail-safe of the persistent launches (csrc/kernels/persist.h note_fail): a per-step guard
+        # word in the stats arena (zeroed by every training step's arena memset) that a give-up ORs
+        # 2 into and the optimizer's skip test reads, and a pinned host word the runtime polls
+        self.step_flag: Optional[torch.Tensor] = None
+        self.host_flag: int = 0
+        # another program may run concurrently on this device (concurrent federated clients): the
+        # forward launch's lookahead queue order, which needs more than one phase of its own
+        # workgroups resident, is not used
+        self.shared_device = False
 
     # ------------------------------------------------------------------ allocation
     def alloc(self, shape, dtype=BF16) -> torch.Tensor:
@@ -698,13 +730,29 @@ class Builder:
             self.mark_grads_ready(marks)
 
     # ------------------------------------------------------------------ persistent dense stage
+    def _fail_words(self, a):
+        """Point a persistent launch's give-up sinks at this program's step guard (training
+        programs: the optimizer skips a step whose launch gave up) and its pinned host flag."""
+        if self.training:
+            if self.step_flag is None:
+                self.step_flag = self._stats_floats(4).view(torch.int32)
+            a.stepflag = self.step_flag.data_ptr()
+        if getattr(self, "grouped", False):
+            return  # a grouped program's pointers all lie in its region (the trainer reads dense_err)
+        if not self.host_flag and torch.cuda.is_available():  # (CPU-only lowering tests: none)
+            import weakref
+            ext = nat.load()
+            self.host_flag = int(ext.host_alloc(64))
+            weakref.finalize(self, ext.host_free, self.host_flag)
+        a.hostflag = self.host_flag
+
     def dense_stage_ok(self, sbuf: Optional[Stats], layers, H: int, W: int) -> bool:
         """Whether the dense layers of one stage can run as ONE persistent launch
         (csrc/kernels/dense_stage.hip): training-mode BatchNorms on single-copy statistics,
         1x1 inputs of <= DS_MAX_CIN (2,048) channels in multiples of 32 (DenseNet-121/169/201),
         128-channel bottlenecks, 32 new channels per layer, maps whose 3x3 windows fit the
         launch's staging rows, and no fixed-order (deterministic) reductions."""
-        if os.environ.get("IDC_DENSE_STAGE", "1") == "0" or self.det:
+        if os.environ.get("IDC_DENSE_STAGE", "1") == "0" or self.det or persistent_disabled():
             return False
         infer = all(lay["bn1"].mode == 2 and lay["bn2"].mode == 2 for lay in layers)
         if infer:
@@ -776,6 +824,8 @@ class Builder:
         a.act1 = a.act2 = act
         a.inv_count = 1.0 / float(buf.N * H * W)
         a.max_polls = int(os.environ.get("IDC_DS_MAX_POLLS", "0"))
+        a.lookahead = -1 if self.shared_device else 0
+        self._fail_words(a)
         if os.environ.get("IDC_DS_STAMPS", "0") == "1":
             # per-work-item s_memrealtime stamps (tools/dense_stamps.py reads them after a step)
             stamps = self.alloc((8 * int(ext.dense_stage_tasks(nat.raw(a))),), torch.int64)
@@ -794,7 +844,8 @@ class Builder:
         # ms/step); on stage 3 as well its gather tiles wait on agent-coherent loads of ~3 us each
         # under load (761 + 234 us against ~720 us per-layer: 4.12 ms/step, round 4, see
         # tools/dense_stamps.py).  Not in grouped (client-batched) programs.
-        if os.environ.get("IDC_DENSE_STAGE_BWD", "1") != "1" or not self.training or self.det:
+        if os.environ.get("IDC_DENSE_STAGE_BWD", "1") != "1" or not self.training or self.det or \
+                persistent_disabled():
             return False
         if getattr(self, "grouped", False):
             return False
@@ -866,6 +917,7 @@ class Builder:
         a.k2, a.act, a.nphases, a.ntickets = 1 if center else 3, act, len(ph), ntickets
         a.inv_count = 1.0 / float(M)
         a.max_polls = int(os.environ.get("IDC_DS_MAX_POLLS", "0"))
+        self._fail_words(a)
         if os.environ.get("IDC_DS_STAMPS", "0") == "1":
             stamps = self.alloc((8 * ntickets,), torch.int64)
             a.stamps = stamps.data_ptr()

@@ -73,6 +73,7 @@ class FusedProgram:
         self.U = net.num_outputs
         b = Builder(net, model.arena, model.device, batch, training)
         b.grouped = group is not None
+        b.shared_device = bool(getattr(getattr(model, "impl", None), "shared_device", False))
         _lowering_for(net)(b, net, self.U, input_dtype)
         if b.has_wgrad_batch():  # a lowering that returned early (frozen layers) mid-batch
             b.segment = "bwd"
@@ -103,22 +104,36 @@ class FusedProgram:
             self.input_op = 0
         b.finalize_casts()
         b.finalize_moving()
+        strategy = model.strategy
+        if training and model.arena.params and b.step_flag is None and getattr(strategy, "native_comm", None) is not None \
+                and strategy.active and not getattr(strategy, "central_storage", False):
+            # every rank's program carries the step-guard all-reduce (below) and its optimizer reads
+            # the summed word, whether or not its own lowering built persistent launches: the
+            # ranks' collective sequences match and a give-up on any rank skips the step on all
+            b.step_flag = b._stats_floats(4).view(torch.int32)
         # optimizer segment
         self.nonfinite_status = None
         if training and model.arena.params:
             opt = model.optimizer
             self.host_optimizer = not isinstance(opt, RMSprop) or bool(opt.momentum) or bool(opt.centered)
             flag = 0
+            # persistent dense-stage launches OR 2 into the step guard word when they give up
+            # (csrc/kernels/persist.h note_fail): RMSprop then skips the step's update, so stale
+            # stage outputs never reach the weights.  The word lives in the stats arena, which every
+            # training step zeroes first.
+            guard = b.step_flag.data_ptr() if b.step_flag is not None else 0
+            if guard and not self.host_optimizer:
+                flag = guard
             if skip_nonfinite and not self.host_optimizer:
                 # non-finite guard: the gradient arena is checked at the end of the
                 # backward; RMSprop skips the whole update when anything is inf/nan
                 # (opt segment: under data parallelism it runs after the all-reduce, so every
                 # replica sees the same reduced gradients and makes the same decision)
-                fl = b.alloc((4,), torch.int32)
+                if not flag:
+                    flag = b.alloc((4,), torch.int32).data_ptr()
                 self.nonfinite_status = b.alloc((4,), torch.int32)
-                flag = fl.data_ptr()
             b.segment = "opt"
-            if flag:
+            if skip_nonfinite and flag:
                 b.emit(nat.OP_FINITE_CHECK, ints=(0,), longs=(model.arena.numel,),
                        ptrs=(model.arena.grad.data_ptr(), flag))
             if not self.host_optimizer:
@@ -129,7 +144,7 @@ class FusedProgram:
             if b.cast_tr_n:
                 b.emit(nat.OP_CAST, ints=(b.cast_tr_n,), longs=(b.cast_tr_total,),
                        ptrs=(b.cast_tr_dev.data_ptr(), b.cast_tr_map.data_ptr()))
-            if flag:
+            if skip_nonfinite and flag:
                 b.emit(nat.OP_FINITE_CHECK, ints=(1,), ptrs=(0, flag, self.nonfinite_status.data_ptr()))
         else:
             self.host_optimizer = False
@@ -181,10 +196,25 @@ class FusedProgram:
                 op_index += 1
                 self.n_comm_ops += 1
 
+        # under data parallelism a give-up on ONE rank must skip the update on EVERY rank (the
+        # stale gradients were all-reduced into everyone's): the step guard word is summed over
+        # the ranks at the end of the backward, after every persistent launch of the step
+        guard_ar = self.native_comm is not None and b.step_flag is not None
+
+        def add_guard_allreduce():
+            nonlocal op_index, guard_ar
+            if guard_ar:
+                self.plan.add(nat.OP_ALLREDUCE, b"", [2, 0], [], [1], [b.step_flag.data_ptr()], 0)
+                op_index += 1
+                self.n_comm_ops += 1
+                guard_ar = False
+
         for i, (seg, kind, raw, ints, floats, longs, ptrs, lane) in enumerate(b.ops):
             if seg != cur:
                 if cur == "bwd" and pending_buckets:
                     add_ready_buckets(-1)  # buckets no mark released (params without gradient)
+                if cur == "bwd":
+                    add_guard_allreduce()
                 if cur is not None:
                     self.seg[cur] = (start, op_index)
                 cur, start = seg, op_index
@@ -204,6 +234,8 @@ class FusedProgram:
             op_index += 1
         if cur == "bwd" and pending_buckets:
             add_ready_buckets(-1)
+        if cur == "bwd":
+            add_guard_allreduce()
         if cur is not None:
             self.seg[cur] = (start, op_index)
         if self.native_comm is not None:
@@ -428,12 +460,15 @@ class FusedStep:
         self.progs: Dict[tuple, FusedProgram] = {}
         self._lr = model.optimizer.learning_rate if model.optimizer else None
         self.group = None  # runtime.grouped.GroupRegion: programs run K copies (grouped.py)
+        self.shared_device = False  # other programs run concurrently on the device (fedavg workers)
 
     def _prog(self, batch: int, training: bool, dtype) -> FusedProgram:
-        key = (batch, training, dtype)
+        from ..parallel.strategy import current_replica_weight
+        w = current_replica_weight[0] if training else 1.0  # uneven split of a global batch
+        key = (batch, training, dtype) if w == 1.0 else (batch, training, dtype, w)
         p = self.progs.get(key)
         if p is None:
-            gs = 1.0 / self.m.strategy.num_replicas_in_sync
+            gs = w / self.m.strategy.num_replicas_in_sync
             p = FusedProgram(self.m, batch, training, dtype, grad_scale=gs, use_graphs=self.use_graphs,
                              skip_nonfinite=self.skip_nonfinite, group=self.group)
             self.progs[key] = p
@@ -476,8 +511,44 @@ class FusedStep:
             print(f"[validate] {where}: {len(bad)} bad buffers: " + "; ".join(bad[:40]), flush=True)
         return not bad
 
+    # ---- fail-safe of the persistent dense-stage launches -----------------------------------
+    def check_persistent(self) -> int:
+        """Poll the programs' pinned host give-up flags (no device synchronisation).  A set flag
+        means a persistent dense-stage launch of an already finished step gave up on a wait: that
+        step's weight update was skipped on the device (step guard word, csrc/kernels/persist.h).
+        Policy IDC_DS_ON_FAIL: ``fallback`` (default) switches persistent launches off for the
+        process and rebuilds the programs with per-layer kernels; ``raise`` raises
+        PersistentLaunchError.  Returns the number of programs that reported a give-up."""
+        import ctypes
+        from .builder import PersistentLaunchError, disable_persistent
+        hit = []
+        for key, p in self.progs.items():
+            hf = getattr(p.b, "host_flag", 0)
+            if hf and ctypes.c_int.from_address(hf).value:
+                ctypes.c_int.from_address(hf).value = 0
+                hit.append(key)
+        if not hit:
+            return 0
+        policy = os.environ.get("IDC_DS_ON_FAIL", "fallback")
+        msg = (f"a persistent dense-stage launch gave up on a wait in program(s) {hit}; the "
+               "affected step(s) skipped their weight update")
+        if policy == "raise":
+            raise PersistentLaunchError(msg)
+        disable_persistent(msg)
+        torch.cuda.current_stream(self.m.device).wait_stream(next(iter(self.progs.values())).stream)
+        for p in self.progs.values():
+            p.stream.synchronize()
+            p.close()
+        self.progs = {}
+        return len(hit)
+
     def train_step(self, x, y):
+        """One training step.  Returns (loss, logits) as VIEWS of the program's output buffers:
+        the next step of the same program overwrites them (clone() them to keep them; see
+        _outputs)."""
         with trace.range("train_step"):
+            if self.progs:
+                self.check_persistent()
             return self._train_step(x, y)
 
     def _train_step(self, x, y):
@@ -503,6 +574,8 @@ class FusedStep:
                 # the plan itself issues every bucket all-reduce on the communicator's stream and
                 # joins it back into the main lane at the end of the range
                 p.run_bwd()
+                if p.native_comm is not None:
+                    p.native_comm.step_issued()  # watchdog progress mark (parallel/watchdog.py)
             elif bucketer is not None and p.bwd_marks:
                 # backward in bucket-aligned segments: each bucket's all-reduce is issued from
                 # the comm stream as soon as its gradients are final — the comm stream waits for
@@ -530,7 +603,7 @@ class FusedStep:
             trace.pop()
         if p.host_optimizer:
             with torch.cuda.stream(p.stream):
-                m.optimizer.step(m.arena, grad_scale=1.0 / strategy.num_replicas_in_sync)
+                m.optimizer.step(m.arena, grad_scale=p.grad_scale)
         if validate:
             self._validate(p, "after bwd")
         p.run_segment("opt")
@@ -589,6 +662,8 @@ class FusedStep:
         return n
 
     def eval_step(self, x, y):
+        if self.progs:
+            self.check_persistent()
         dtype = torch.uint8 if x.dtype == torch.uint8 else torch.float32
         p = self._prog(x.shape[0], False, dtype)
         self._stage_inputs(p, x, y)

@@ -17,7 +17,9 @@ really runs through RCCL on the MI355X:
                  RMSprop on rank 0 only, broadcast of the parameters, all through the native
                  communicator inside the fused step, under IDC_DETERMINISTIC=1: bit-identical
                  gradients and updated weights to the single-device program;
-* ``masked``   — MaskedAggregator's int32 masked SUM all-reduce and decode;
+* ``masked``   — MaskedAggregator's masked SUM (one ncclUint32 all-reduce) and decode;
+* ``nonblocking`` — a communicator created non-blocking with an init timeout (the world > 1
+                 form), the uint32 ring sum and the watchdog's progress marks;
 * ``fedavg``   — the FedAvg packed all-reduce and the server-state broadcast helpers.
 Prints ``RCCLCASE {json}`` per case.
 """
@@ -93,6 +95,30 @@ def _fp32_check(net0, arena, grad, x, y):
     bad = grad_failures(arena, grad, g32, g16)
     worst = max(bad, key=lambda r: r["rel"] / max(r["rel_autocast"], 1e-12)) if bad else None
     return len(bad), worst
+
+
+def case_nonblocking(st):
+    """A second communicator created NON-blocking (ncclCommInitRankConfig, blocking = 0, init
+    timeout) as every world > 1 is: its collectives settle through ncclInProgress, the uint32 ring
+    sum, the watchdog's progress marks and its poll on a healthy communicator."""
+    from idc_models_amd.parallel.native_comm import NativeCommunicator
+    from idc_models_amd.parallel.watchdog import CommWatchdog
+    dev = st.device
+    nc = NativeCommunicator(0, 1, dev, init_timeout_s=60.0, watchdog=False)
+    x = torch.randn(4097, device=dev)
+    y = x.clone()
+    nc.all_reduce_(y)
+    u = torch.tensor([-1, -(2 ** 31), 2 ** 31 - 1, 7], dtype=torch.int32, device=dev)
+    v = u.clone()
+    nc.all_reduce_u32_(v)
+    wd = CommWatchdog(nc.c, timeout_s=30.0)
+    wd.mark()
+    torch.cuda.synchronize()
+    age = nc.c.mark_age()
+    polled = wd.poll_once()
+    nc.close()
+    ok = torch.equal(x, y) and torch.equal(u, v) and age == 0.0 and polled is None
+    emit({"case": "nonblocking", "ok": bool(ok), "age": age, "polled": polled})
 
 
 def case_dp(det):
@@ -215,13 +241,15 @@ def case_fedavg(dev):
 def main():
     os.environ["IDC_FORCE_COLLECTIVES"] = "1"
     from idc_models_amd.parallel import MirroredStrategy
-    cases = sys.argv[1].split(",") if len(sys.argv) > 1 else ["native", "dp_det", "dp_tuned", "central", "masked",
-                                                              "fedavg"]
+    cases = sys.argv[1].split(",") if len(sys.argv) > 1 else ["native", "nonblocking", "dp_det", "dp_tuned",
+                                                              "central", "masked", "fedavg"]
     st = MirroredStrategy(force_collectives=True)
     assert st.native_comm is not None, "no native communicator on a nccl GPU rank"
     for c in cases:
         if c == "native":
             case_native(st)
+        elif c == "nonblocking":
+            case_nonblocking(st)
         elif c == "dp_det":
             case_dp(True)
         elif c == "dp_tuned":

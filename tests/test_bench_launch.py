@@ -28,6 +28,18 @@ def test_bench_spawns_requested_world_on_cpu():
     assert out["config"]["global_batch"] == 8 and out["steps"] == 1
 
 
+def test_bench_spawns_world4_on_cpu():
+    """The driver's N=4 point, rehearsed on gloo: 4 ranks, one JSON line, dp4, global batch 4x."""
+    r = _run(["--gpus", "4", "--device", "cpu", "--model", "mobilenetv2", "--batch", "2", "--steps", "1",
+              "--warmup", "0", "--fit-steps", "0"])
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [json.loads(l) for l in r.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    out = lines[0]
+    assert out["config"]["world_size"] == 4 and out["config"]["parallelism"] == "dp4"
+    assert out["config"]["global_batch"] == 8
+
+
 def test_bench_refuses_mismatched_world():
     r = _run(["--gpus", "4", "--device", "cpu", "--model", "mobilenetv2", "--batch", "4", "--steps", "1",
               "--warmup", "0", "--fit-steps", "0"], {"WORLD_SIZE": "1", "RANK": "0", "LOCAL_RANK": "0"})
@@ -50,3 +62,15 @@ def test_bench_densenet201_cifar_phases_on_cpu():
         counts[ph] = out["config"]["trainable_params"]
     assert counts["frozen"] == 1920 * 10 + 10  # GAP(1920) -> Dense(10) only
     assert counts["frozen"] < counts["finetune"]
+
+
+def test_bench_finetune_cuts_follow_the_reference():
+    """``--phase finetune`` freezes ``layers[:fine_tune_at]`` with the reference's cut per backbone:
+    VGG16 15 (block5 + head train: 7,079,937), MobileNetV2 100 in the 155-layer build (1,863,873)."""
+    want = {"vgg16": 7079937, "mobilenetv2": 1863873}
+    for model, n in want.items():
+        r = _run(["--device", "cpu", "--model", model, "--phase", "finetune", "--batch", "2", "--steps", "1",
+                  "--warmup", "0", "--fit-steps", "0"])
+        assert r.returncode == 0, r.stderr[-3000:]
+        out = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][-1])
+        assert out["config"]["trainable_params"] == n, (model, out["config"]["trainable_params"])

@@ -189,11 +189,16 @@ def test_fedavg_skips_non_finite_client():
         if calls["n"] == 2:
             with torch.no_grad():
                 m.net.trainable_weights[0].fill_(float("nan"))
+            # a diverged client also reports a non-finite loss / metric: it must not
+            # reach the round's metrics (NaN * weight 0 is still NaN)
+            for k in h.history:
+                h.history[k][-1] = float("nan")
         return h
 
     m.fit = fit
-    new, _ = proc.next(state, clients)
+    new, mets = proc.next(state, clients)
     assert all(torch.isfinite(w).all() for w in new.model.trainable)
+    assert mets and all(np.isfinite(v) for v in mets.values()), mets
 
 
 def test_fedavg_secure_mask_equals_plain_weighted_mean():

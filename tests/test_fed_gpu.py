@@ -199,3 +199,23 @@ def test_fedavg_batched_clients_mobilenetv2_matches_sequential():
     assert rel <= 3 * floor + 2e-2, (rel, floor)
     assert float((ntg - nt_a).norm() / nt_a.norm()) <= 3 * float((nt_b - nt_a).norm() / nt_a.norm()) + 1e-3
     assert mg["loss"] == pytest.approx(m_a["loss"], rel=0.05)
+
+
+@pytest.mark.parametrize("nseg,empty", [(7, False), (5000, True)])
+def test_segment_absmax_gpu_matches_cpu(nseg, empty):
+    """the native per-segment |max| kernel (incl. > 4096 segments: its global-atomic
+    path) equals the CPU scatter-amax, empty segments included (0)."""
+    from idc_models_amd.fed.secagg import segment_absmax, segment_ends
+    g = torch.Generator().manual_seed(nseg)
+    sizes = torch.randint(0 if empty else 1, 40, (nseg,), generator=g).tolist()
+    if empty:
+        sizes[3] = 0
+        sizes[-1] = 0
+    vecs = [torch.randn(sum(sizes), generator=g) * (k + 1) for k in range(3)]
+    se = segment_ends(sizes)
+    cpu = segment_absmax(vecs, se, nseg, "cpu")
+    gpu = segment_absmax([v.to(DEV) for v in vecs], se, nseg, DEV).cpu()
+    assert torch.equal(cpu, gpu)
+    if empty:
+        assert cpu[3].item() == 0.0 and cpu[-1].item() == 0.0
+    assert torch.equal(segment_absmax([], se, nseg, DEV).cpu(), torch.zeros(nseg))

@@ -446,3 +446,58 @@ def test_persistent_timeout_is_reported(monkeypatch):
     with pytest.warns(RuntimeWarning, match="persistent dense-stage"):
         m.fit(prepare_for_training(synthetic_dataset(32, seed=2), 16, drop_remainder=True), epochs=1, verbose=0)
     assert m.impl.persistent_failures() > 0
+
+
+def _giveup_model(monkeypatch, policy):
+    """DenseNet-121 at batch 32 (stages 2-4 run persistent launches) with every wait bounded to ONE
+    poll: the launches give up at their first dependency."""
+    from idc_models_amd.engine import Model, RMSprop
+    from idc_models_amd.models import build_model
+    from idc_models_amd.runtime import builder as bld
+    monkeypatch.setenv("IDC_DS_MAX_POLLS", "1")
+    monkeypatch.setenv("IDC_DS_ON_FAIL", policy)
+    monkeypatch.setenv("IDC_AUTOTUNE", "0")
+    monkeypatch.setattr(bld, "_PERSISTENT_OFF", [])  # restored after the test
+    net = build_model("densenet121", None, num_outputs=1, seed=0)
+    m = Model(net, device=DEV)
+    m.compile(RMSprop(1e-3), "binary_crossentropy", [], backend="fused")
+    g = torch.Generator().manual_seed(2)
+    x = torch.randint(0, 256, (32, 50, 50, 3), generator=g, dtype=torch.uint8).to(DEV)
+    y = torch.randint(0, 2, (32,), generator=g).to(DEV)
+    return m, x, y, bld
+
+
+def test_persistent_giveup_skips_update_then_raises(monkeypatch):
+    """a persistent dense-stage launch that gives up makes its step skip the
+    weight update on the device (weights and RMSprop slots bitwise unchanged), and the runtime
+    raises after the step (IDC_DS_ON_FAIL=raise)."""
+    import ctypes
+    m, x, y, bld = _giveup_model(monkeypatch, "raise")
+    p = m.impl._prog(32, True, torch.uint8)
+    assert any(p.plan.kind(i) in (bld.nat.OP_DENSE_STAGE, bld.nat.OP_DENSE_STAGE_BWD) for i in range(p.plan.size()))
+    torch.cuda.synchronize()
+    w0, ms0 = m.arena.data.clone(), m.optimizer.ms.clone()
+    err0 = int(p.b.dense_err[0].item())
+    m.impl._train_step(x, y)  # (the polling entry point would not issue the step)
+    torch.cuda.synchronize()
+    assert int(p.b.dense_err[0].item()) > err0, "the bounded waits did not give up"
+    assert ctypes.c_int.from_address(p.b.host_flag).value == 1
+    assert torch.equal(m.arena.data, w0) and torch.equal(m.optimizer.ms, ms0)
+    with pytest.raises(bld.PersistentLaunchError):
+        m.impl.train_step(x, y)
+
+
+def test_persistent_giveup_falls_back_to_per_layer_kernels(monkeypatch):
+    """Default policy: the programs are rebuilt without persistent launches and training goes on."""
+    m, x, y, bld = _giveup_model(monkeypatch, "fallback")
+    m.impl._train_step(x, y)
+    torch.cuda.synchronize()
+    w0 = m.arena.data.clone()
+    with pytest.warns(RuntimeWarning, match="persistent dense-stage launches disabled"):
+        loss, _ = m.impl.train_step(x, y)
+    torch.cuda.synchronize()
+    assert torch.isfinite(loss).item() and not torch.equal(m.arena.data, w0)
+    assert bld.persistent_disabled()
+    p = m.impl.progs[(32, True, torch.uint8)]
+    assert not any(p.plan.kind(i) in (bld.nat.OP_DENSE_STAGE, bld.nat.OP_DENSE_STAGE_BWD)
+                   for i in range(p.plan.size()))

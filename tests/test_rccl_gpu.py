@@ -38,6 +38,7 @@ def test_rccl_world_of_one(tmp_path):
     cases = {json.loads(l.split("RCCLCASE ", 1)[1])["case"]: json.loads(l.split("RCCLCASE ", 1)[1])
              for l in text.splitlines() if "RCCLCASE " in l}
     assert r.returncode == 0, text[-4000:]
-    assert set(cases) == {"native", "dp_det", "dp_tuned", "central", "masked", "fedavg"}, text[-4000:]
+    assert set(cases) == {"native", "nonblocking", "dp_det", "dp_tuned", "central", "masked",
+                          "fedavg"}, text[-4000:]
     for c in cases.values():
         assert c["ok"], c

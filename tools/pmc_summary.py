@@ -37,6 +37,8 @@ def main():
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--marker", default="input_stage")
     ap.add_argument("--md", default=None)
+    ap.add_argument("--bytes", action="store_true",
+                    help="traffic table from FETCH_SIZE / WRITE_SIZE passes (KB per dispatch)")
     a = ap.parse_args()
     merged = None
     for prefix in a.prefix:
@@ -72,6 +74,8 @@ def main():
         for key, v in e.items():
             if key != "name":
                 s[key] += v
+    if a.bytes:
+        return bytes_table(agg, a)
     rows = []
     tot_t = sum(s["t"] for s in agg.values())
     tot_mfma = sum(s["SQ_VALU_MFMA_BUSY_CYCLES"] for s in agg.values())
@@ -93,6 +97,34 @@ def main():
              "|---|---:|---:|---:|---:|---:|---:|"]
     for _, k, n, us, util, lds, wait, ldsw in rows[:40]:
         lines.append(f"| `{k}` | {n:.0f} | {us:.1f} | {util:.1%} | {lds:.3f} | {wait:.2f} | {ldsw:.3f} |")
+    out = "\n".join(lines) + "\n"
+    print(out)
+    if a.md:
+        with open(a.md, "w") as f:
+            f.write(out)
+
+
+def bytes_table(agg, a):
+    """Per kernel class: MB read / written per step (FETCH_SIZE / WRITE_SIZE are in KB) and the
+    implied HBM-side bandwidth over the serialised kernel time."""
+    rows = []
+    tot_t = sum(s["t"] for s in agg.values())
+    tot_r = sum(s["FETCH_SIZE"] for s in agg.values()) / 1e3 / a.steps
+    tot_w = sum(s["WRITE_SIZE"] for s in agg.values()) / 1e3 / a.steps
+    for k, s in agg.items():
+        us = s["t"] / 1e3 / a.steps
+        rd, wr = s["FETCH_SIZE"] / 1e3 / a.steps, s["WRITE_SIZE"] / 1e3 / a.steps
+        bw = (rd + wr) / 1e3 / (us * 1e-6) if us else 0.0  # GB/s
+        rows.append((s["t"], k, s["n"] / a.steps, us, rd, wr, bw))
+    rows.sort(reverse=True)
+    lines = [f"# PMC traffic per kernel ({a.steps} steps, rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE, "
+             "serialised dispatches)", "",
+             f"- kernel time per step under PMC: {tot_t / 1e6 / a.steps:.3f} ms",
+             f"- read {tot_r:.1f} MB + written {tot_w:.1f} MB per step", "",
+             "| kernel | calls/step | us/step | MB read/step | MB written/step | GB/s |",
+             "|---|---:|---:|---:|---:|---:|"]
+    for _, k, n, us, rd, wr, bw in rows[:40]:
+        lines.append(f"| `{k}` | {n:.0f} | {us:.1f} | {rd:.1f} | {wr:.1f} | {bw:.0f} |")
     out = "\n".join(lines) + "\n"
     print(out)
     if a.md:
