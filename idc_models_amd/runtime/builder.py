@@ -142,6 +142,21 @@ def persistent_disabled() -> bool:
     return bool(_PERSISTENT_OFF)
 
 
+_HOST_FLAGS = {"base": 0, "next": 0}
+_HOST_FLAG_SLOTS = 4096
+
+
+def _host_flag_slot() -> int:
+    """Address of a fresh zeroed int in ONE process-lifetime slab of mapped pinned host memory
+    (allocated once, never freed while kernels that hold slots may still be captured in graphs;
+    a program whose slots run out shares the last one: the flag is only a trigger)."""
+    if not _HOST_FLAGS["base"]:
+        _HOST_FLAGS["base"] = int(nat.load().host_alloc(4 * _HOST_FLAG_SLOTS))
+    i = min(_HOST_FLAGS["next"], _HOST_FLAG_SLOTS - 1)
+    _HOST_FLAGS["next"] += 1
+    return _HOST_FLAGS["base"] + 4 * i
+
+
 class PersistentLaunchError(RuntimeError):
     """A persistent dense-stage launch gave up on a wait (IDC_DS_ON_FAIL=raise); the step it
     belonged to skipped its weight update."""
@@ -740,10 +755,7 @@ class Builder:
         if getattr(self, "grouped", False):
             return  # a grouped program's pointers all lie in its region (the trainer reads dense_err)
         if not self.host_flag and torch.cuda.is_available():  # (CPU-only lowering tests: none)
-            import weakref
-            ext = nat.load()
-            self.host_flag = int(ext.host_alloc(64))
-            weakref.finalize(self, ext.host_free, self.host_flag)
+            self.host_flag = _host_flag_slot()
         a.hostflag = self.host_flag
 
     def dense_stage_ok(self, sbuf: Optional[Stats], layers, H: int, W: int) -> bool:
