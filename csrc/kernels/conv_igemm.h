@@ -81,6 +81,11 @@ constexpr int TILE_BIG128 = 101;
 constexpr int TILE_BIG256 = 102;
 constexpr int TILE_BIG64 = 103;
 constexpr int TILE_BIG128D = 104;  // 256 x 128 with three LDS buffers
+// tile TILE_IMG selects the image-resident 3x3 kernel (conv_img.hip): DenseNet's 128 -> 32
+// forward and 32 -> 128 data-gradient convolutions on maps up to 13 x 13
+constexpr int TILE_IMG = 105;
+bool conv_img_ok(const ConvArgs& a, bool a_f32);
+hipError_t conv_img(const ConvArgs& a, bool a_f32, hipStream_t st);
 bool conv_big_ok(const ConvArgs& a, bool a_f32);
 hipError_t conv_big(const ConvArgs& a, int bn, bool a_f32, hipStream_t st);
 hipError_t conv_igemm(const ConvArgs& a, int tile, bool a_f32, hipStream_t st);

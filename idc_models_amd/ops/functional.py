@@ -91,7 +91,7 @@ def conv2d(x: torch.Tensor, kernel_hwio: torch.Tensor, stride=(1, 1), pads=(0, 0
            bias: Optional[torch.Tensor] = None, act: int = 0, out_f32: bool = False,
            stats: Optional[torch.Tensor] = None, tile: int = -1,
            w_layout: Optional[torch.Tensor] = None, ksplit: int = 1,
-           stats_shift: Optional[torch.Tensor] = None) -> torch.Tensor:
+           stats_shift: Optional[torch.Tensor] = None, tickets: Optional[torch.Tensor] = None) -> torch.Tensor:
     """y = act(conv(pro(x)) + bias); x NHWC (bf16 or fp32), Cin % 8 == 0.  Optional output
     statistics [sum|sumsq] accumulated into ``stats`` (sums of y - ``stats_shift`` when given)."""
     N, H, W, Cin = x.shape
@@ -120,6 +120,8 @@ def conv2d(x: torch.Tensor, kernel_hwio: torch.Tensor, stride=(1, 1), pads=(0, 0
         a.stats_shift = nat.ptr(stats_shift)
     a.mbn = _ident()
     keep = _splitk_args(a, N * Ho * Wo, cout, ksplit, tile)
+    if tickets is not None:  # a plan op's zeroed ticket array (the image kernel keeps its slots there)
+        a.tickets, a.tickets_n = tickets.data_ptr(), tickets.numel()
     nat.require().conv(nat.raw(a), tile, 1 if x.dtype == torch.float32 else 0, nat.stream_handle())
     del keep
     return y
@@ -150,7 +152,8 @@ def conv2d_dgrad(dy: torch.Tensor, kernel_hwio: torch.Tensor, in_hw: Tuple[int, 
                  gsum: Optional[torch.Tensor] = None, gsumx: Optional[torch.Tensor] = None,
                  out_f32: bool = False, tile: int = -1, ksplit: int = 1,
                  bpro: Optional[nat.BwdAff] = None, bepi: Optional[nat.BwdAff] = None,
-                 acc: Optional[torch.Tensor] = None, aout: Optional[torch.Tensor] = None) -> torch.Tensor:
+                 acc: Optional[torch.Tensor] = None, aout: Optional[torch.Tensor] = None,
+                 tickets: Optional[torch.Tensor] = None) -> torch.Tensor:
     """Stride-1 data gradient.  With ``mx``/``mbn``: returns dZ = dX * act'(bn(mx)) and
     accumulates sum(dZ) into gsum, sum(dZ*xhat) into gsumx.  ``bpro``: dy staged through a
     pending BatchNorm backward.  ``bepi`` + ``acc`` (fp32): epilogue mode 2, acc += gamma*rstd*dZ
@@ -188,6 +191,8 @@ def conv2d_dgrad(dy: torch.Tensor, kernel_hwio: torch.Tensor, in_hw: Tuple[int, 
     else:
         a.out_mode = nat.OUT_F32 if out_f32 else nat.OUT_BF16
     keep = _splitk_args(a, N * H * W, cin, ksplit, tile)
+    if tickets is not None:
+        a.tickets, a.tickets_n = tickets.data_ptr(), tickets.numel()
     nat.require().conv(nat.raw(a), tile, 1 if dy.dtype == torch.float32 else 0, nat.stream_handle())
     del keep
     return dx

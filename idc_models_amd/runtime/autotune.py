@@ -87,6 +87,11 @@ def _conv_candidates(ext, M: int, cout: int, payload: bytes = None, a_f32: int =
         if bm > 64 and M <= 2 * 64:
             continue
         out.append(t)
+    # the image-resident 3x3 kernel (conv_img.hip: DenseNet's 128 -> 32 / 32 -> 128 convs on small
+    # maps), one workgroup per image
+    if payload is not None and os.environ.get("IDC_CONV_IMG", "1") != "0" and hasattr(ext, "img_ok") \
+            and ext.img_ok(payload, a_f32):
+        out.append(ext.TILE_IMG)
     # 256 x {128, 256} global_load_lds tiles for plain wide layers (conv_big.hip), when they
     # still make >= 128 workgroups
     if payload is not None and os.environ.get("IDC_CONV_BIG", "1") != "0" and ext.big_ok(payload, a_f32):

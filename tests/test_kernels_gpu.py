@@ -1034,3 +1034,86 @@ def test_dense_stage_inference_mode_matches_reference(fn, N, H, c0, L, grid):
     errs["buf"] = relerr(buf.float(), rbuf)
     assert all(v < 2e-2 for v in errs.values()), errs
     assert all(float(d["tstats"].abs().sum()) == 0.0 for d in lays)  # no statistics produced
+
+
+@pytest.mark.parametrize("N,H", [(5, 13), (7, 6), (9, 3), (3, 8), (64, 6)])
+def test_conv_img_forward_matches_reference(fn, N, H):
+    """Image-resident 3x3 kernel (conv_img.hip, tile TILE_IMG), DenseNet growth conv 128 -> 32:
+    pending BN + ReLU staged once per element, shifted output statistics; vs fp32 reference and
+    vs the implicit-GEMM tiles."""
+    ext = fn.nat.require()
+    Cin, Cout = 128, 32
+    x = bf(torch.randn(N, H, H, Cin, device=DEV) * 1.5 + 0.4)
+    st = torch.cat([x.sum((0, 1, 2)), (x * x).sum((0, 1, 2))])
+    gamma = torch.rand(Cin, device=DEV) + 0.5
+    beta = torch.randn(Cin, device=DEV) * 0.1
+    w = bf(torch.randn(3, 3, Cin, Cout, device=DEV) * 0.05)
+    cnt = N * H * H
+    shift = torch.randn(Cout, device=DEV) * 0.1
+    bn = fn.BN(stats=st, gamma=gamma, beta=beta, count=cnt, eps=1.001e-5, act=1)
+    outs = {}
+    tk = torch.zeros(17 + 16 * 2 * Cout, dtype=torch.int32, device=DEV)  # slot copies + arrival counter
+    for tile, tickets in ((ext.TILE_IMG, None), ("slots", tk), (-1, None)):
+        so = torch.zeros(2 * Cout, device=DEV)
+        y = fn.conv2d(x.to(torch.bfloat16), w, pads=(1, 1), pro=bn, stats=so, stats_shift=shift,
+                      tile=ext.TILE_IMG if tile == "slots" else tile, tickets=tickets)
+        outs[tile] = (y.float(), so)
+    torch.cuda.synchronize()
+    assert int(tk.abs().sum()) == 0  # the last arrival re-zeroed the slots and the counter
+    assert torch.equal(outs["slots"][0], outs[ext.TILE_IMG][0])
+    assert relerr(outs["slots"][1], outs[ext.TILE_IMG][1]) < 1e-5
+    a = bn_ref(x, st, gamma, beta, cnt, 1.001e-5, 1)
+    ref = ref_conv(bf(a), w, 1, (1, 1, 1, 1))
+    y, so = outs[ext.TILE_IMG]
+    assert relerr(y, ref) < 1e-2
+    assert relerr(y, outs[-1][0]) < 5e-3
+    d = y - shift
+    assert relerr(so[:Cout], d.sum((0, 1, 2))) < 1e-3
+    assert relerr(so[Cout:], (d * d).sum((0, 1, 2))) < 1e-3
+
+
+@pytest.mark.parametrize("N,H", [(5, 13), (7, 6), (9, 3), (48, 6)])
+def test_conv_img_dgrad_matches_reference(fn, N, H):
+    """Image-resident 3x3 data gradient 32 -> 128 as DenseNet's dgrad cv2 issues it: fp32 concat-
+    gradient operand holding A*dZ with the pending B*x + C added while staging (plus the fold and
+    the bf16 staged copy), epilogue dZ2 = dA * relu'(bn2(t)) reduced into gsum / gsumx."""
+    ext = fn.nat.require()
+    C, cin = 32, 128
+    k = _bn_case(N, H, C, seed=3)
+    v = (k["dZ"] * k["A"]).contiguous()
+    w = bf(torch.randn(3, 3, cin, C, device=DEV) * 0.1)
+    x16 = k["x"].to(torch.bfloat16)
+    t = bf(torch.randn(N, H, H, cin, device=DEV) * 1.2 + 0.2)
+    st2 = torch.cat([t.sum((0, 1, 2)), (t * t).sum((0, 1, 2))])
+    g2 = torch.rand(cin, device=DEV) + 0.5
+    b2 = torch.randn(cin, device=DEV) * 0.1
+    cnt = N * H * H
+    res = {}
+    tk = torch.zeros(17 + 16 * 2 * cin, dtype=torch.int32, device=DEV)
+    for tile in (ext.TILE_IMG, "slots", -1):
+        db, dg = torch.zeros(C, device=DEV), torch.zeros(C, device=DEV)
+        aff = fn.bwd_aff(x16, k["bn"], k["gsum"], k["gsumx"], unit_alpha=True, fold=(db, dg))
+        staged = torch.zeros(N, H, H, C, dtype=torch.bfloat16, device=DEV)
+        gsum, gsumx = torch.zeros(cin, device=DEV), torch.zeros(cin, device=DEV)
+        dz = fn.conv2d_dgrad(v, w, (H, H), pads=(1, 1), bpro=aff, aout=staged, mx=t.to(torch.bfloat16),
+                             mbn=fn.BN(stats=st2, gamma=g2, beta=b2, count=cnt, eps=1e-3, act=1),
+                             gsum=gsum, gsumx=gsumx, tile=ext.TILE_IMG if tile == "slots" else tile,
+                             tickets=tk if tile == "slots" else None)
+        torch.cuda.synchronize()
+        res[tile] = (dz.float(), staged.float(), gsum, gsumx, db, dg)
+    assert int(tk.abs().sum()) == 0
+    assert torch.equal(res["slots"][0], res[ext.TILE_IMG][0])
+    assert relerr(res["slots"][2], res[ext.TILE_IMG][2]) < 1e-5 and relerr(res["slots"][3], res[ext.TILE_IMG][3]) < 1e-5
+    dA = torch.nn.grad.conv2d_input((N, cin, H, H), w.permute(3, 2, 0, 1), bf(k["dX"]).permute(0, 3, 1, 2),
+                                    padding=1).permute(0, 2, 3, 1)
+    mean = st2[:cin] / cnt
+    var = st2[cin:] / cnt - mean ** 2
+    xhat = (t - mean) * torch.rsqrt(var + 1e-3)
+    dZ2 = dA * ((xhat * g2 + b2) > 0).float()
+    dz, staged, gsum, gsumx, db, dg = res[ext.TILE_IMG]
+    assert relerr(dz, dZ2) < 2e-2
+    assert relerr(dz, res[-1][0]) < 5e-3
+    assert relerr(staged, k["dX"]) < 1e-2 and torch.equal(staged, res[-1][1])
+    assert relerr(gsum, dZ2.sum((0, 1, 2))) < 2e-2
+    assert relerr(gsumx, (dZ2 * xhat).sum((0, 1, 2))) < 2e-2
+    assert torch.equal(db, k["gsum"]) and torch.equal(dg, k["gsumx"])
