@@ -399,7 +399,9 @@ __global__ __launch_bounds__(256) void conv3x3_img_kernel(ConvArgs a, GroupArg g
   // the last of those 16 is the last workgroup.  Words: [0, 17) counters, then S x 2*COUT slots.
   constexpr int NCW = 17;
   const int S = (a.tickets != nullptr && a.tickets_n > NCW) ? min(16, (a.tickets_n - NCW) / (2 * COUT)) : 0;
-  if (S < 2 || gridDim.x < 32) {
+  // (an output whose statistics already have slot copies -- the lowering allocated them for this
+  // producer -- takes the direct adds: <= 256 / slots per address, nothing to fold)
+  if (S < 2 || gridDim.x < 32 || stat_slots(EPI == 0 ? a.stats_slots : a.gsum_slots) > 1) {
     if (qq == 0) final_add(kind, col, acc1);
     return;
   }

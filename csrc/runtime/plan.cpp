@@ -1007,6 +1007,14 @@ PYBIND11_MODULE(_idc_native, m) {
   m.attr("TILE_BIG64") = TILE_BIG64;
   m.attr("TILE_BIG128D") = TILE_BIG128D;
   m.attr("TILE_IMG") = TILE_IMG;
+  m.attr("TILE_ROWS") = TILE_ROWS;
+  m.def("rows_ok", [](py::bytes payload, int a_f32) {
+    std::string s = payload;
+    if (s.size() != sizeof(ConvArgs)) throw std::runtime_error("ConvArgs size mismatch");
+    ConvArgs a;
+    std::memcpy(&a, s.data(), sizeof(a));
+    return conv_rows_ok(a, a_f32 != 0);
+  });
   m.def("img_ok", [](py::bytes payload, int a_f32) {
     std::string s = payload;
     if (s.size() != sizeof(ConvArgs)) throw std::runtime_error("ConvArgs size mismatch");

@@ -603,7 +603,7 @@ class Builder:
     def dgrad(self, dy: Tensor4, layer, dx: Tensor4, *, pads=(0, 0), mx: Optional[Tensor4] = None,
               mbn: Optional[nat.BnArgs] = None, gsum=None, gsumx=None, gbn: Optional["BNRef"] = None,
               out_mode=nat.OUT_BF16, bpro: Optional[nat.BwdAff] = None,
-              bepi: Optional[nat.BwdAff] = None, aout: Optional[Tensor4] = None):
+              bepi: Optional[nat.BwdAff] = None, aout: Optional[Tensor4] = None, slotted: bool = False):
         """Stride-1 data gradient: conv of dy with the flipped kernel; optional BN-backward
         epilogue through the BN+act that produced the forward input ``mx`` whose reductions go
         to ``gbn``'s gradient sums (or to explicit ``gsum``/``gsumx`` arrays).
@@ -651,7 +651,8 @@ class Builder:
                     raise RuntimeError("fp32 epilogue-1 dgrad needs OUT_F32 / OUT_F32_ACC without activation")
                 a.out_mode = out_mode
             if gbn is not None:
-                a.gsum, a.gsumx, a.gsum_slots, a.gsum_ld = self.grad_sums(gbn, dx.M, self._conv_row_tiles(dx.M))
+                a.gsum, a.gsumx, a.gsum_slots, a.gsum_ld = self.grad_sums(gbn, dx.M, self._conv_row_tiles(dx.M),
+                                                                          slotted=slotted)
             elif self.det and (gsum is not None or gsumx is not None):
                 a.gsum, a.gsumx, a.gsum_slots, a.gsum_ld = self._det_gsum_slots(
                     dx.C, self._conv_row_tiles(dx.M), nat.ptr(gsum) if gsum is not None else nat.ptr(gsumx),

@@ -51,22 +51,33 @@ def lower_densenet(b: Builder, net, U: int, input_dtype):
     b.add_moving(bn_stem)
     Hs, Ws = (H1 + 2 - 3) // 2 + 1, (W1 + 2 - 3) // 2 + 1
 
-    stages = []
-    c0 = 64
-    nblocks = base.blocks
-    ctot = c0 + 32 * nblocks[0]
-    buf = b.nhwc(B, Hs, Ws, ctot)
-    sbuf = b.stats(ctot, B * Hs * Ws) if training else None
-    argmax = b.alloc((B * Hs * Ws * 64,), torch.uint8)
-    b.pool(ys, buf.slice(0, 64), k=3, s=2, pt=1, pl=1, pro=bn_stem.args(), is_max=True,
-           argmax=argmax, stats=sbuf, stats_off=0)
-
     # Late stages (M <= IDC_DENSE_STAGE_MAXM pixels; default 2304: stages 3-4 at bs 256, stages 3-4
     # of a bs-32 federated client) run all their dense layers as ONE persistent work-queue launch
     # each (builder.dense_stage, dense_stage.hip) instead of 2 launch-latency-bound convs per layer.
     # DenseNet-121 bs 256 on 1x MI355X (bench.py, repeated A/B): stages 3+4 in-kernel 4.27-4.29
     # ms/step, stage 4 only 4.31, per-layer 4.35-4.41; stage 2 (9,216 rows) measured slower
     stage_maxm = int(os.environ.get("IDC_DENSE_STAGE_MAXM", "2304"))
+    # IDC_IMG_SLOTS=1: stages whose dense layers run per-layer convs on >= 8192 rows keep their batch
+    # statistics in slot copies, so the image-resident 3x3 kernels (conv_img.hip), whose workgroups
+    # all finish together, add <= 16 times per address instead of folding in-kernel; measured
+    # neutral (3.69-3.73 vs 3.66-3.69 ms/step, bench.py A/B round 5), so off by default.
+    img_slots = os.environ.get("IDC_IMG_SLOTS", "0") == "1"
+
+    bwd_maxm_env = int(os.environ.get("IDC_DENSE_STAGE_BWD_MAXM", "256"))
+
+    def slotted_stage(rows):  # (never a stage a persistent launch takes: those need single copies)
+        return img_slots and rows > max(stage_maxm, bwd_maxm_env) and rows >= 8192
+
+    stages = []
+    c0 = 64
+    nblocks = base.blocks
+    ctot = c0 + 32 * nblocks[0]
+    buf = b.nhwc(B, Hs, Ws, ctot)
+    sbuf = b.stats(ctot, B * Hs * Ws, slotted=slotted_stage(B * Hs * Ws)) if training else None
+    argmax = b.alloc((B * Hs * Ws * 64,), torch.uint8)
+    b.pool(ys, buf.slice(0, 64), k=3, s=2, pt=1, pl=1, pro=bn_stem.args(), is_max=True,
+           argmax=argmax, stats=sbuf, stats_off=0)
+
     for si, nb in enumerate(nblocks):
         st = {"buf": buf, "stats": sbuf, "c0": c0, "ctot": ctot, "H": Hs, "W": Ws, "layers": []}
         M = B * Hs * Ws
@@ -99,7 +110,7 @@ def lower_densenet(b: Builder, net, U: int, input_dtype):
             c0n = ctot // 2
             ctotn = c0n + 32 * nblocks[si + 1]
             bufn = b.nhwc(B, Hn, Wn, ctotn)
-            sbufn = b.stats(ctotn, B * Hn * Wn) if training else None
+            sbufn = b.stats(ctotn, B * Hn * Wn, slotted=slotted_stage(B * Hn * Wn)) if training else None
             b.conv(p, cvt, bufn.slice(0, c0n), stats=sbufn, stats_off=0)
             b.add_moving(bnt)
             st["trans"] = {"bn": bnt, "conv": cvt, "p": p}
@@ -202,7 +213,8 @@ def lower_densenet(b: Builder, net, U: int, input_dtype):
                 return
             dO16 = b.nhwc(N, Hs, Ws, 32)
             b.dgrad(dO, cv2, z2, pads=(1, 1), mx=t, mbn=bn2.args(), gbn=bn2,
-                    bpro=b.bwd_aff(pend, xO, c0=cin, unit_alpha=True, fold=True), aout=dO16)
+                    bpro=b.bwd_aff(pend, xO, c0=cin, unit_alpha=True, fold=True), aout=dO16,
+                    slotted=slotted_stage(N * Hs * Ws))
             if fz.trainable(cv2):
                 b.wgrad(t, cv2, dO16, b.arena.grad_of(cv2.kernel), pads=(1, 1), pro=bn2.args(), lane=1,
                         batch=wb)

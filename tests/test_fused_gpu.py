@@ -438,14 +438,17 @@ def test_direct_input_staging_one_hot_labels(monkeypatch):
 
 
 def test_persistent_timeout_is_reported(monkeypatch):
-    """A persistent dense-stage launch that gives up on a wait (poll bound forced to 1) is
-    reported by the backend and by fit() (a RuntimeWarning once per epoch), not silent."""
+    """A persistent dense-stage launch that gives up on a wait (poll bound forced to 1) is not
+    silent: fit() applies the fail-safe policy (default: fall back to per-layer kernels, with a
+    RuntimeWarning) at the latest at the end of the epoch."""
+    from idc_models_amd.runtime import builder as bld
     monkeypatch.setenv("IDC_DS_MAX_POLLS", "1")
+    monkeypatch.setattr(bld, "_PERSISTENT_OFF", [])  # restored after the test
     from idc_models_amd.data import prepare_for_training, synthetic_dataset
     m, ref, x, y = _setup("densenet121", 16)
     with pytest.warns(RuntimeWarning, match="persistent dense-stage"):
         m.fit(prepare_for_training(synthetic_dataset(32, seed=2), 16, drop_remainder=True), epochs=1, verbose=0)
-    assert m.impl.persistent_failures() > 0
+    assert bld.persistent_disabled()
 
 
 def _giveup_model(monkeypatch, policy):

@@ -34,6 +34,7 @@ SOURCES = [
     "kernels/conv_igemm_g5.hip",
     "kernels/conv_big.hip",
     "kernels/conv_img.hip",
+    "kernels/conv_rows.hip",
     "kernels/conv_wgrad.hip", "kernels/wgrad_big.hip",
     "kernels/nn_kernels.hip",
     "kernels/dwconv.hip",
