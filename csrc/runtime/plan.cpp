@@ -38,6 +38,7 @@
 #include "../kernels/conv_igemm.h"
 #include "../kernels/conv_wgrad.h"
 #include "../kernels/dense_stage.h"
+#include "../kernels/mb_chain.h"
 #include "../kernels/dwconv.h"
 #include "../kernels/mlp_head.h"
 #include "../kernels/nn_kernels.h"
@@ -86,6 +87,9 @@ enum OpKind : int {
   OP_DENSE_STAGE = 28,
   // persistent dense-stage backward (dense_stage_bwd.hip): payload DenseBwdArgs, i[0] = grid
   OP_DENSE_STAGE_BWD = 29,
+  // persistent MobileNetV2 block chain (mb_chain.hip): payload MbChainArgs, i[0] = grid,
+  // i[1] = dynamic LDS bytes
+  OP_MB_CHAIN = 30,
 };
 
 struct Op {
@@ -638,6 +642,7 @@ class Plan {
         break;
       case OP_DENSE_STAGE: check(dense_stage_fwd(as<DenseStageArgs>(op), op.i[0], st), "dense_stage_fwd"); break;
       case OP_DENSE_STAGE_BWD: check(dense_stage_bwd(as<DenseBwdArgs>(op), op.i[0], st), "dense_stage_bwd"); break;
+      case OP_MB_CHAIN: check(mb_chain(as<MbChainArgs>(op), op.i[0], op.i[1], st), "mb_chain"); break;
       case OP_STATS_SHIFT:
         check(stats_shift(reinterpret_cast<const ShiftDesc*>(op.p[0]), op.i[0], op.i[1], st), "stats_shift");
         break;
@@ -750,6 +755,9 @@ py::dict struct_sizes() {
   d["DenseBwdArgs"] = sizeof(DenseBwdArgs);
   d["DenseBwdLayerDesc"] = sizeof(DenseBwdLayerDesc);
   d["DenseBwdPhase"] = sizeof(DenseBwdPhase);
+  d["MbPhaseDesc"] = sizeof(MbPhaseDesc);
+  d["MbChainArgs"] = sizeof(MbChainArgs);
+  d["MbPhaseDesc.pre"] = offsetof(MbPhaseDesc, pre);
   d["BnArgs.shift"] = offsetof(BnArgs, shift);
   d["ConvArgs.stats_shift"] = offsetof(ConvArgs, stats_shift);
   d["PoolArgs.stats_shift"] = offsetof(PoolArgs, stats_shift);
@@ -1061,4 +1069,16 @@ PYBIND11_MODULE(_idc_native, m) {
   m.def("dense_stage_shape_ok", &dense_stage_shape_ok);
   m.attr("DS_SCRATCH_PER_LAYER") = DS_SCRATCH_PER_LAYER;
   m.attr("DS_MAX_CIN") = DS_MAX_CIN;
+  m.attr("OP_MB_CHAIN") = (int)OP_MB_CHAIN;
+  m.def("mb_phase_ok", [](py::bytes payload) {
+    std::string s = payload;
+    if (s.size() != sizeof(MbPhaseDesc)) throw std::runtime_error("mb_phase_ok: bad payload");
+    return mb_phase_ok(*reinterpret_cast<const MbPhaseDesc*>(s.data()));
+  });
+  m.def("mb_phase_smem", [](py::bytes payload) {
+    std::string s = payload;
+    if (s.size() != sizeof(MbPhaseDesc)) throw std::runtime_error("mb_phase_smem: bad payload");
+    return mb_phase_smem(*reinterpret_cast<const MbPhaseDesc*>(s.data()));
+  });
+  m.attr("MB_SMEM_LIMIT") = mb_smem_limit();
 }

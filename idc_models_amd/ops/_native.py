@@ -168,6 +168,23 @@ class DenseBwdArgs(C.Structure):
                [("inv_count", cf), ("max_polls", C.c_uint), ("stepflag", vp), ("hostflag", vp)]
 
 
+class MbPhaseDesc(C.Structure):
+    """One phase of a persistent MobileNetV2 block-chain launch (csrc/kernels/mb_chain.h)."""
+    _fields_ = [(n, ci) for n in ("kind", "first", "tiles", "dep", "pro", "act_in", "tab_in", "tab_out",
+                                  "N", "H", "W", "Ho", "Wo", "S", "PT", "PL", "Cin", "Cout", "tm", "tn",
+                                  "slots", "bn_mode", "ldx", "ldy")] + \
+               [(n, vp) for n in ("x", "res", "aout", "w16", "w32", "y", "stats", "shift", "slotbuf",
+                                  "gamma", "beta", "mmean", "mvar")] + \
+               [("eps", cf), ("inv_count", cf), ("pre", BnArgs)]
+
+
+class MbChainArgs(C.Structure):
+    _fields_ = [(n, vp) for n in ("phases", "sync", "tabs", "err", "stepflag", "hostflag", "stamps")] + \
+               [("nphases", ci), ("ntickets", ci), ("max_polls", C.c_uint), ("pad_", ci)]
+
+
+MB_TAB, MB_PW, MB_DW = 1, 2, 3
+
 _STRUCTS = {"BnArgs": BnArgs, "BwdAff": BwdAff, "ConvArgs": ConvArgs, "WgradArgs": WgradArgs,
             "WgBatchEntry": WgBatchEntry,
             "BnBwdApplyArgs": BnBwdApplyArgs, "BnBwdReduceArgs": BnBwdReduceArgs,
@@ -175,7 +192,8 @@ _STRUCTS = {"BnArgs": BnArgs, "BwdAff": BwdAff, "ConvArgs": ConvArgs, "WgradArgs
             "HeadArgs": HeadArgs, "HeadBwdArgs": HeadBwdArgs, "CastEntry": CastEntry,
             "DwArgs": DwArgs, "Mlp2Args": Mlp2Args, "ShiftDesc": ShiftDesc,
             "DenseStageArgs": DenseStageArgs, "DenseLayerDesc": DenseLayerDesc,
-            "DenseBwdArgs": DenseBwdArgs, "DenseBwdLayerDesc": DenseBwdLayerDesc, "DenseBwdPhase": DenseBwdPhase}
+            "DenseBwdArgs": DenseBwdArgs, "DenseBwdLayerDesc": DenseBwdLayerDesc, "DenseBwdPhase": DenseBwdPhase,
+            "MbPhaseDesc": MbPhaseDesc, "MbChainArgs": MbChainArgs}
 
 # op kinds (csrc/runtime/plan.cpp)
 OP_CONV, OP_WGRAD, OP_BN_BWD_APPLY, OP_BN_BWD_REDUCE, OP_MAXPOOL, OP_AVGPOOL, OP_POOL_BWD = range(7)
@@ -184,6 +202,7 @@ OP_BN_STATS, OP_BN_APPLY, OP_DW_FWD, OP_DW_BWD_DATA, OP_DW_WGRAD, OP_COPY, OP_FI
 OP_MLP_FWD, OP_MLP_BWD, OP_MLP_STEP, OP_COLLAPSE, OP_STATS_SHIFT, OP_ALLREDUCE, OP_WGRAD_BATCH = range(21, 28)
 OP_DENSE_STAGE = 28
 OP_DENSE_STAGE_BWD = 29
+OP_MB_CHAIN = 30
 
 ACT = {None: 0, "none": 0, "linear": 0, "relu": 1, "relu6": 2}
 OUT_BF16, OUT_F32, OUT_F32_ACC = 0, 1, 2
@@ -192,8 +211,8 @@ OUT_BF16, OUT_F32, OUT_F32_ACC = 0, 1, 2
 def _verify(ext):
     if ext.OP_ALLREDUCE != OP_ALLREDUCE:
         raise RuntimeError("native op-kind table drifted (OP_ALLREDUCE)")
-    if ext.OP_DENSE_STAGE != OP_DENSE_STAGE:
-        raise RuntimeError("native op-kind table drifted (OP_DENSE_STAGE)")
+    if ext.OP_DENSE_STAGE != OP_DENSE_STAGE or ext.OP_MB_CHAIN != OP_MB_CHAIN:
+        raise RuntimeError("native op-kind table drifted (OP_DENSE_STAGE / OP_MB_CHAIN)")
     sizes = ext.struct_sizes()
     for name, cls in _STRUCTS.items():
         if C.sizeof(cls) != sizes[name]:
@@ -212,7 +231,7 @@ def _verify(ext):
               "ConvArgs.stats_shift": ConvArgs.stats_shift.offset,
               "PoolArgs.stats_shift": PoolArgs.stats_shift.offset,
               "DwArgs.stats_shift": DwArgs.stats_shift.offset,
-              "BnMovingDesc.shift": BnMovingDesc.shift.offset}
+              "BnMovingDesc.shift": BnMovingDesc.shift.offset, "MbPhaseDesc.pre": MbPhaseDesc.pre.offset}
     for k, v in checks.items():
         if sizes[k] != v:
             raise RuntimeError(f"native struct field {k}: ctypes offset {v} != C++ {sizes[k]}")

@@ -38,12 +38,12 @@ _PAYLOAD = {
     nat.OP_POOL_BWD: nat.PoolBwdArgs, nat.OP_HEAD_FWD: nat.HeadArgs, nat.OP_HEAD_BWD: nat.HeadBwdArgs,
     nat.OP_BN_APPLY: nat.BnArgs, nat.OP_DW_FWD: nat.DwArgs, nat.OP_DW_BWD_DATA: nat.DwArgs,
     nat.OP_DW_WGRAD: nat.DwArgs, nat.OP_MLP_FWD: nat.Mlp2Args, nat.OP_MLP_BWD: nat.Mlp2Args,
-    nat.OP_DENSE_STAGE: nat.DenseStageArgs,
+    nat.OP_DENSE_STAGE: nat.DenseStageArgs, nat.OP_MB_CHAIN: nat.MbChainArgs,
 }
 # descriptor-table ops: (ptr slot of the table, int slot of its length, entry type)
 _TABLES = {nat.OP_BN_MOVING: (0, 0, nat.BnMovingDesc), nat.OP_STATS_SHIFT: (0, 0, nat.ShiftDesc),
            nat.OP_CAST: (0, 0, nat.CastEntry), nat.OP_WGRAD_BATCH: (0, 0, nat.WgBatchEntry),
-           nat.OP_DENSE_STAGE: (0, 1, nat.DenseLayerDesc)}
+           nat.OP_DENSE_STAGE: (0, 1, nat.DenseLayerDesc), nat.OP_MB_CHAIN: (0, 2, nat.MbPhaseDesc)}
 
 
 def _struct_ptrs(obj, path=""):

@@ -85,16 +85,33 @@ def lower_mobilenet(b: Builder, net, U: int, input_dtype):
             return
         p_, bnp_, res_ = pending_out
         b.conv(p_, layer, out, stats=stats, bpro=b.fwd_aff(bnp_, p_, res_), aout=h_in)
+
+    # the blocks from IDC_MB_CHAIN_FROM on run as ONE persistent launch (runtime/mb_chain.py,
+    # csrc/kernels/mb_chain.hip): same buffers and statistics, single-copy depthwise statistics
+    from .mb_chain import MbChain, chain_enabled
+    chain_from = int(os.environ.get("IDC_MB_CHAIN_FROM", "0"))
+    chain = MbChain(b) if (fold_out and chain_enabled(b)) else None
     for bid, (filters, stride, t) in enumerate(MBV2_BLOCKS):
         pre = f"block_{bid}_" if bid else "expanded_conv_"
         blk = {"bid": bid, "stride": stride, "h_in": h_in}
+        ch_on = chain is not None and bid >= chain_from
         if bid:
             ex, exbn = L[pre + "expand"], L[pre + "expand_BN"]
             e = b.nhwc(B, h, w, ex.filters)
             se = b.stats(ex.filters, B * h * w) if training else None
-            consume(ex, e, se)
-            pending_out = None
             bn_e = BNRef(exbn, b, se, RELU6)
+            if ch_on:
+                fb = (lambda ex=ex, e=e, se=se, po=pending_out, hi=h_in:
+                      b.conv(hi, ex, e, stats=se) if po is None else
+                      b.conv(po[0], ex, e, stats=se, bpro=b.fwd_aff(po[1], po[0], po[2]), aout=hi))
+                if pending_out is None:
+                    chain.pw(ex, h_in, e, se, bn_e, fallback=fb)
+                else:
+                    p_, bnp_, res_ = pending_out
+                    chain.pw(ex, p_, e, se, bn_e, pro_bn=bnp_, res=res_, aout=h_in, fallback=fb)
+            else:
+                consume(ex, e, se)
+            pending_out = None
             b.add_moving(bn_e)
             blk.update(ex=ex, e=e, bn_in=bn_e)
             dw_in, bn_in = e, bn_e
@@ -107,17 +124,27 @@ def lower_mobilenet(b: Builder, net, U: int, input_dtype):
         d = b.nhwc(B, ho, wo, ch)
         # the depthwise kernels run ~300-700 workgroups per channel chunk: one statistics copy took
         # that many float atomics per address (H=25 C=32: 28.6 us with, 14.5 us without the
-        # statistics epilogue; 16.9 us with slot copies, tools/bench_dw.py)
-        sd = b.stats(ch, B * ho * wo, slotted=dw_slots) if training else None
-        b.dwconv(dw_in, dwl, d, stride=stride, pads=pads, pro=bn_in.args(), stats=sd)
+        # statistics epilogue; 16.9 us with slot copies, tools/bench_dw.py); the chain reduces its
+        # slot copies in-launch and keeps ONE copy
+        sd = b.stats(ch, B * ho * wo, slotted=dw_slots and not ch_on) if training else None
         bn_d = BNRef(dwbn, b, sd, RELU6)
+        if ch_on:
+            chain.dw(dwl, dw_in, d, stride, pads, sd, bn_in, RELU6, bn_d,
+                     fallback=lambda dwl=dwl, dw_in=dw_in, d=d, stride=stride, pads=pads, bn_in=bn_in, sd=sd:
+                     b.dwconv(dw_in, dwl, d, stride=stride, pads=pads, pro=bn_in.args(), stats=sd))
+        else:
+            b.dwconv(dw_in, dwl, d, stride=stride, pads=pads, pro=bn_in.args(), stats=sd)
         b.add_moving(bn_d)
         prj, prjbn = L[pre + "project"], L[pre + "project_BN"]
         pw = prj.filters
         p = b.nhwc(B, ho, wo, pw)
         sp = b.stats(pw, B * ho * wo) if training else None
-        b.conv(d, prj, p, pro=bn_d.args(), stats=sp)
         bn_p = BNRef(prjbn, b, sp, 0)
+        if ch_on:
+            chain.pw(prj, d, p, sp, bn_p, pro_bn=bn_d, act=RELU6,
+                     fallback=lambda prj=prj, d=d, p=p, bn_d=bn_d, sp=sp: b.conv(d, prj, p, pro=bn_d.args(), stats=sp))
+        else:
+            b.conv(d, prj, p, pro=bn_d.args(), stats=sp)
         b.add_moving(bn_p)
         residual = (cin == pw and stride == 1)
         hout = b.nhwc(B, ho, wo, pw)
@@ -130,6 +157,8 @@ def lower_mobilenet(b: Builder, net, U: int, input_dtype):
         blocks.append(blk)
         h_in, cin, h, w = hout, pw, ho, wo
 
+    if chain is not None:
+        chain.emit()
     c1l, c1bnl = L["Conv_1"], L["Conv_1_bn"]
     c1 = b.nhwc(B, h, w, c1l.filters)
     sc1 = b.stats(c1l.filters, B * h * w) if training else None

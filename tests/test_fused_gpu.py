@@ -504,3 +504,43 @@ def test_persistent_giveup_falls_back_to_per_layer_kernels(monkeypatch):
     p = m.impl.progs[(32, True, torch.uint8)]
     assert not any(p.plan.kind(i) in (bld.nat.OP_DENSE_STAGE, bld.nat.OP_DENSE_STAGE_BWD)
                    for i in range(p.plan.size()))
+
+
+@pytest.mark.parametrize("B,frozen", [(8, False), (256, False), (64, True)])
+def test_mb_chain_matches_per_layer(monkeypatch, B, frozen):
+    """MobileNetV2: the blocks as ONE persistent work-queue launch (OP_MB_CHAIN, csrc/kernels/
+    mb_chain.hip; the default) against the per-layer convs (IDC_MB_CHAIN=0) on the same weights
+    and batch.  Every block's raw expand / depthwise / project output and every statistics array
+    agree to a bf16-level bound, the give-up counter stays zero, and the chain program's loss and
+    gradients pass the fp32 check (_check).  ``frozen``: inference-mode BatchNorms (phase 1)."""
+    from idc_models_amd.ops import _native as nat
+    outs = []
+    for on in ("0", "1"):
+        monkeypatch.setenv("IDC_MB_CHAIN", on)
+        m, ref, x, y = _setup("mobilenetv2", B, freeze_base=frozen)
+        p = m.impl._prog(B, True, torch.uint8)
+        n = sum(1 for i in range(p.plan.size()) if p.plan.kind(i) == nat.OP_MB_CHAIN)
+        assert n == (1 if on == "1" else 0), (on, n)
+        m.impl._stage_inputs(p, x, y)
+        p.run_segment("fwd")
+        torch.cuda.synchronize()
+        blocks = p.b.debug["blocks"]
+        acts = [blk[k].t.float().clone() for blk in blocks for k in ("e", "d", "p")]
+        stats = torch.cat([s.t.clone() for s in p.b.all_stats]) if p.b.all_stats else torch.zeros(1)
+        if on == "1":
+            assert int(p.b.dense_err[0]) == 0
+        outs.append((acts, stats, float(p.io.loss.item())))
+        if on == "1":
+            _check(m, ref, x, y)
+        m.impl.close()
+
+    def rel(a, b):
+        return float((a - b).norm() / (b.norm() + 1e-12))
+
+    (a0, s0, l0), (a1, s1, l1) = outs
+    worst = max(rel(u, v) for u, v in zip(a1, a0))
+    print("worst block-tensor rel", worst, "stats rel", rel(s1, s0), "loss", l0, l1)
+    assert worst <= 3e-2, worst
+    if not frozen:  # (a frozen base's per-layer convs still reduce statistics nobody reads)
+        assert rel(s1, s0) <= 3e-2
+    assert abs(l1 - l0) <= 0.05 * max(1.0, abs(l0))

@@ -43,7 +43,7 @@ STRUCTS = {nat.OP_CONV: nat.ConvArgs, nat.OP_WGRAD: nat.WgradArgs, nat.OP_BN_BWD
            nat.OP_HEAD_BWD: nat.HeadBwdArgs, nat.OP_DW_FWD: nat.DwArgs, nat.OP_DW_BWD_DATA: nat.DwArgs,
            nat.OP_DW_WGRAD: nat.DwArgs, nat.OP_BN_APPLY: nat.BnArgs, nat.OP_MLP_FWD: nat.Mlp2Args,
            nat.OP_MLP_BWD: nat.Mlp2Args, nat.OP_DENSE_STAGE: nat.DenseStageArgs,
-           nat.OP_DENSE_STAGE_BWD: nat.DenseBwdArgs}
+           nat.OP_DENSE_STAGE_BWD: nat.DenseBwdArgs, nat.OP_MB_CHAIN: nat.MbChainArgs}
 
 
 def _pointers(obj, out):
@@ -84,7 +84,18 @@ def test_plan_pointers_are_live(arch, ft):
                 e = nat.DenseLayerDesc.from_buffer_copy(raw_tab, j * C.sizeof(nat.DenseLayerDesc))
                 assert e.cin % 32 == 0 and e.cin <= 1024, (i, j, e.cin)
                 _pointers(e, vals)
+        if kind == nat.OP_MB_CHAIN:  # the phase table of a persistent MobileNetV2 block chain
+            tab = next(t for t in b.keep if t.data_ptr() == ptrs[0])
+            n = ints[2]
+            raw_tab = bytes(tab.cpu().numpy().tobytes())
+            assert len(raw_tab) == n * C.sizeof(nat.MbPhaseDesc), (i, n)
+            for j in range(n):
+                e = nat.MbPhaseDesc.from_buffer_copy(raw_tab, j * C.sizeof(nat.MbPhaseDesc))
+                assert nat.load().mb_phase_ok(nat.raw(e)), (i, j)
+                _pointers(e, vals)
         for name, v in vals:
+            if name == "hostflag":  # pinned host memory (persist.h FailSink)
+                continue
             if not any(lo <= v < hi for lo, hi in ranges):
                 bad.append((i, kind, name))
     assert not bad, bad[:10]
@@ -185,3 +196,48 @@ def test_dense_stage_bwd_lowering(monkeypatch):
     assert count(IDC_DETERMINISTIC="1")[0] == 0
     # stage 2 (6x6 maps) fits the launch too
     assert count(IDC_DENSE_STAGE_BWD_MAXM="9216")[0] == 3
+
+
+def test_mb_chain_lowering(monkeypatch):
+    """MobileNetV2's blocks lower to ONE OP_MB_CHAIN (expand / depthwise / project of every block
+    from IDC_MB_CHAIN_FROM on); IDC_MB_CHAIN=0 keeps the per-layer ops.
+    Tickets are contiguous per phase, every phase depends on an earlier one, and every conv phase's
+    output BatchNorm gets a table the next phase reads."""
+    def lower(**env):
+        for k, v in env.items():
+            monkeypatch.setenv(k, v)
+        _, _, b = _lower("mobilenetv2", None, True, B=256)
+        for k in env:
+            monkeypatch.delenv(k)
+        return b
+
+    def kinds(b):
+        return [k for (_, k, *_r) in b.ops]
+
+    on, off = lower(), lower(IDC_MB_CHAIN="0")
+    k_on, k_off = kinds(on), kinds(off)
+    assert k_on.count(nat.OP_MB_CHAIN) == 1 and k_off.count(nat.OP_MB_CHAIN) == 0
+    fwd_on = [op[1] for op in on.ops if op[0] == "fwd"]
+    fwd_off = [op[1] for op in off.ops if op[0] == "fwd"]
+    # 17 blocks: 16 expand + 17 depthwise + 17 project convs leave the forward
+    assert fwd_off.count(nat.OP_DW_FWD) - fwd_on.count(nat.OP_DW_FWD) == 17
+    assert fwd_off.count(nat.OP_CONV) - fwd_on.count(nat.OP_CONV) == 33
+    # the backward is unchanged
+    assert [op[1] for op in on.ops if op[0] == "bwd"] == [op[1] for op in off.ops if op[0] == "bwd"]
+    op = next(o for o in on.ops if o[1] == nat.OP_MB_CHAIN)
+    tab = next(t for t in on.keep if t.data_ptr() == op[6][0])
+    raw = bytes(tab.cpu().numpy().tobytes())
+    n = op[3][2]
+    descs = [nat.MbPhaseDesc.from_buffer_copy(raw, j * C.sizeof(nat.MbPhaseDesc)) for j in range(n)]
+    assert sum(d.kind == nat.MB_TAB for d in descs) == 1  # the stem BatchNorm
+    first = 0
+    for j, d in enumerate(descs):
+        assert d.first == first and d.dep < j
+        first += d.tiles
+        if d.kind != nat.MB_TAB:
+            assert d.bn_mode == 1 and d.slots >= 1 and d.tab_out >= 0
+    a = nat.MbChainArgs.from_buffer_copy(op[2])
+    assert a.ntickets == first and a.nphases == n
+    part = lower(IDC_MB_CHAIN_FROM="10")
+    d10 = [op for op in part.ops if op[1] == nat.OP_MB_CHAIN]
+    assert len(d10) == 1 and d10[0][3][2] == 1 + 3 * 7  # TAB of block 9's project BN + blocks 10-16

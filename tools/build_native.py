@@ -39,6 +39,7 @@ SOURCES = [
     "kernels/nn_kernels.hip",
     "kernels/dwconv.hip",
     "kernels/dense_stage.hip",
+    "kernels/mb_chain.hip",
     "kernels/dense_stage_bwd.hip",
     "kernels/mlp_head.hip",
     "kernels/secagg.hip",

@@ -55,6 +55,8 @@ def main():
     ap.add_argument("--batch", type=int, default=256)
     ap.add_argument("--reps", type=int, default=20)
     ap.add_argument("--seg", default="fwd,bwd,opt")
+    ap.add_argument("--alt", default="", help="comma list of extra conv tiles to time on every eligible op "
+                                             "(img, rows): printed beside the tuned choice")
     a = ap.parse_args()
     from idc_models_amd.engine import Model, RMSprop
     from idc_models_amd.models import build_model
@@ -80,7 +82,19 @@ def main():
             us = time_op(plan, i, st, a.reps)
             lane = plan.lane(i)
             d = describe(plan, i)
-            print(f"{i:4d} {seg} L{lane} {us:8.2f} us  {d}", flush=True)
+            alt = ""
+            if a.alt and plan.kind(i) == nat.OP_CONV:
+                ext = nat.load()
+                t0, f32 = plan.get_int(i, 0), plan.get_int(i, 1)
+                for name in a.alt.split(","):
+                    tile, ok = {"img": (ext.TILE_IMG, ext.img_ok), "rows": (ext.TILE_ROWS, ext.rows_ok)}[name]
+                    if ok(plan.payload(i), f32) and t0 != tile:
+                        plan.set_int(i, 0, tile)
+                        p.b.reset_tickets()
+                        alt += f"  [{name} {time_op(plan, i, st, a.reps):.2f} us]"
+                        plan.set_int(i, 0, t0)
+                p.b.reset_tickets()
+            print(f"{i:4d} {seg} L{lane} {us:8.2f} us  {d}{alt}", flush=True)
             key = (seg, lane, d.split(" ")[0] + (" " + " ".join(w for w in d.split(" ") if w.startswith(("pro=", "epi=", "gpro="))) if d.startswith(("conv", "wgrad")) else ""))
             tot[key] += us
             cnt[key] += 1
