@@ -6,6 +6,9 @@
 namespace idc {
 
 enum { MB_TAB = 1, MB_PW = 2, MB_DW = 3 };
+constexpr int MB_MAX_PHASES = 64;     // phases of one launch (their table is copied into LDS)
+constexpr int MB_MAX_SLOTS = 8;       // statistics slot copies per phase
+constexpr int MB_SYNC_PER_PHASE = 10; // 8 arrival shards, shards complete, READY
 
 // One phase of the chain (a conv, or the table of a BatchNorm whose statistics predate the launch).
 // Work items ("tiles") of phase p hold tickets [first, first + tiles).
@@ -43,9 +46,11 @@ struct MbPhaseDesc {
   BnArgs pre;        // MB_TAB: the BatchNorm (+ act) whose table is built
 };
 
+constexpr int MB_TABLE_BYTES = (MB_MAX_PHASES * (int)sizeof(MbPhaseDesc) + 15) / 16 * 16;
+
 struct MbChainArgs {
   const MbPhaseDesc* phases;
-  unsigned* sync;             // [2 + 2 * nphases]: ticket, fail, per phase (arrivals, ready);
+  unsigned* sync;             // [2 + MB_SYNC_PER_PHASE * nphases]: ticket, fail, per phase words;
                               // zeroed before every launch (the stats-arena memset)
   float* tabs;                // BatchNorm tables
   int* err;                   // persistent count of launches that gave up on a wait (nullable)
@@ -59,7 +64,7 @@ struct MbChainArgs {
 
 // dynamic LDS bytes a phase needs (the launch takes the maximum)
 int mb_phase_smem(const MbPhaseDesc& d);
-// the largest dynamic LDS a launch may use
+// the largest tile LDS a phase may use (the launch adds the phase table)
 int mb_smem_limit();
 // host-side shape rules of one phase descriptor (checked by the lowering before it emits a launch)
 bool mb_phase_ok(const MbPhaseDesc& d);

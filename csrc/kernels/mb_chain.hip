@@ -48,8 +48,9 @@ struct Ctl {
   int task, bad, last;
 };
 
-__device__ __forceinline__ unsigned* arrive_w(unsigned* sync, int p) { return sync + 2 + 2 * p; }
-__device__ __forceinline__ unsigned* ready_w(unsigned* sync, int p) { return sync + 3 + 2 * p; }
+// per phase MB_SYNC_PER_PHASE words: 8 arrival shards (tile % 8), the shards-complete count, READY
+__device__ __forceinline__ unsigned* arrive_w(unsigned* sync, int p) { return sync + 2 + MB_SYNC_PER_PHASE * p; }
+__device__ __forceinline__ unsigned* ready_w(unsigned* sync, int p) { return sync + 2 + MB_SYNC_PER_PHASE * p + 9; }
 
 // ------------------------------------------------------------------------------------------------
 // 1x1 conv tile: rows [m0, m0 + TM) x columns [nb0, nb1) in 64-column chunks
@@ -57,6 +58,7 @@ template <int TM>
 __device__ void pw_tile(const MbPhaseDesc& d, int t, long long go, char* smem, const float* tabs) {
   constexpr int RF = TM / 16;               // row fragments per wave
   constexpr int MAXQ = TM * KC / 8 / NT;    // staged 16-B operand chunks per thread
+  constexpr int MAXT = 2 * MAXK / NT;       // table floats per thread
   const int tid = threadIdx.x, lane = tid & 63;
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int M = d.N * d.H * d.W, K = d.Cin, Cout = d.Cout;
@@ -68,7 +70,7 @@ __device__ void pw_tile(const MbPhaseDesc& d, int t, long long go, char* smem, c
   const int ldx = d.ldx, ldy = d.ldy;
   float* sT = reinterpret_cast<float*>(smem);  // [scale | shift] over K
   bf16_t* sA = reinterpret_cast<bf16_t*>(smem + ((2 * K + 3) / 4) * 16);
-  bf16_t* sY = sA + 64 * APITCH;
+  bf16_t* sY = K > KC ? sA : sA + 64 * APITCH;  // (K > KC: one column chunk, see mb_phase_smem)
   const bf16_t* __restrict__ X = gsh(d.x, go);
   const bf16_t* __restrict__ R = gsh(d.res, go);
   bf16_t* __restrict__ AO = gsh(d.aout, go);
@@ -76,46 +78,80 @@ __device__ void pw_tile(const MbPhaseDesc& d, int t, long long go, char* smem, c
   bf16_t* __restrict__ Y = gsh(d.y, go);
   const float* __restrict__ KS = gsh(d.shift, go);
   float* __restrict__ SB = gsh(d.slotbuf, go);
+  const float* __restrict__ tin = tabs + (pro ? d.tab_in : 0);
   const float lo = act_lo(pro == 1 ? d.act_in : 0), hi = act_hi(pro == 1 ? d.act_in : 0);
-  if (pro) {
-    const float* tin = tabs + d.tab_in;
-    for (int i = tid; i < 2 * K; i += NT) sT[i] = ld_coh(tin + i);
-  }
   const bool store_a = pro == 2 && AO != nullptr && ct == 0;
+  const bool use_r = pro == 2 && R != nullptr;
 
-  auto stage = [&](int kc) {
-    const int k0 = kc * KC, kw = min(KC, K - k0), kwp = (kw + 31) & ~31, c8n = kwp >> 3;
+  uint4 va[MAXQ], vr[MAXQ];
+  v8bf bq[KC / 32];
+  // operand chunk kc of this tile into registers (issue only)
+  auto load_a = [&](int kc) {
+    const int k0 = kc * KC, kw = min(KC, K - k0), c8n = ((kw + 31) & ~31) >> 3;
     const int items = TM * c8n;
-    uint4 va[MAXQ], vr[MAXQ];
 #pragma unroll
     for (int i = 0; i < MAXQ; ++i) {
       const int q = tid + i * NT;
       const int r = q / c8n, c8 = q - r * c8n;
-      const int m = m0 + r, k = k0 + c8 * 8;
-      const bool ok = q < items && m < M && k < K;
-      va[i] = ok ? ld_coh16(X + (size_t)m * ldx + k) : make_uint4(0u, 0u, 0u, 0u);
-      vr[i] = (ok && pro == 2 && R) ? ld_coh16(R + (size_t)m * K + k) : make_uint4(0u, 0u, 0u, 0u);
+      const int m = min(m0 + r, M - 1), k = min(k0 + c8 * 8, K - 8);  // clamped: loads unconditional
+      va[i] = q < items ? ld_coh16(X + (size_t)m * ldx + k) : make_uint4(0u, 0u, 0u, 0u);
+      vr[i] = (q < items && use_r) ? ld_coh16(R + (size_t)m * K + k) : make_uint4(0u, 0u, 0u, 0u);
     }
+  };
+  auto load_b = [&](int cb, int kc) {
+    const int k0 = kc * KC, kw = min(KC, K - k0), ks = (kw + 31) >> 5;
+    const int col = min(cb + wid * 16 + (lane & 15), Cout - 1);
+#pragma unroll
+    for (int s = 0; s < KC / 32; ++s) {
+      const int k = min(k0 + 32 * s + 8 * (lane >> 4), K - 8);
+      bq[s] = s < ks ? *reinterpret_cast<const v8bf*>(Wt + (size_t)col * K + k) : v8bf{};
+    }
+  };
+  // registers -> transformed bf16 operand in LDS (zero past M / K)
+  auto store_a_lds = [&](int kc) {
+    const int k0 = kc * KC, kw = min(KC, K - k0), c8n = ((kw + 31) & ~31) >> 3;
+    const int items = TM * c8n;
 #pragma unroll
     for (int i = 0; i < MAXQ; ++i) {
       const int q = tid + i * NT;
       if (q >= items) break;
       const int r = q / c8n, c8 = q - r * c8n;
       const int m = m0 + r, k = k0 + c8 * 8;
-      const bool ok = m < M && k < K;
-      uint4 v = va[i];
-      if (pro && ok) {
-        float f[8], g[8];
-        unpack8(v, f);
-        unpack8(vr[i], g);
+      uint4 v = make_uint4(0u, 0u, 0u, 0u);
+      if (m < M && k < K) {
+        v = va[i];
+        if (pro) {
+          float f[8], g[8];
+          unpack8(v, f);
+          unpack8(vr[i], g);
 #pragma unroll
-        for (int j = 0; j < 8; ++j) f[j] = clampf(fmaf(f[j], sT[k + j], sT[K + k + j]), lo, hi) + g[j];
-        v = pack8(f);
-        if (store_a) st_coh16(AO + (size_t)m * K + k, v);
+          for (int j = 0; j < 8; ++j) f[j] = clampf(fmaf(f[j], sT[k + j], sT[K + k + j]), lo, hi) + g[j];
+          v = pack8(f);
+          if (store_a) st_coh16(AO + (size_t)m * K + k, v);
+        }
       }
       *reinterpret_cast<uint4*>(sA + r * APITCH + c8 * 8) = v;
     }
   };
+
+  // ---- tile inputs: the table, the first operand chunk and the first B fragments in flight at once
+  float tv[MAXT];
+#pragma unroll
+  for (int i = 0; i < MAXT; ++i) {
+    const int j = tid + i * NT;
+    tv[i] = (pro && j < 2 * K) ? ld_coh(tin + j) : 0.f;
+  }
+  load_a(0);
+  load_b(nb0, 0);
+  __syncthreads();  // (the previous tile's LDS reads are done)
+#pragma unroll
+  for (int i = 0; i < MAXT; ++i) {
+    const int j = tid + i * NT;
+    if (j < 2 * K) sT[j] = tv[i];
+  }
+  __syncthreads();
+  store_a_lds(0);
+  __syncthreads();
 
   for (int cb = nb0; cb < nb1; cb += 64) {
     v4f acc[RF];
@@ -123,19 +159,16 @@ __device__ void pw_tile(const MbPhaseDesc& d, int t, long long go, char* smem, c
     for (int i = 0; i < RF; ++i) acc[i] = (v4f){0.f, 0.f, 0.f, 0.f};
     const int col = cb + wid * 16 + (lane & 15);
     for (int kc = 0; kc < nkc; ++kc) {
-      if (nkc > 1 || cb == nb0) {
-        __syncthreads();  // (the previous chunk's fragment reads are done)
-        stage(kc);
+      if (kc > 0) {  // (K > KC: one column chunk per tile)
+        load_a(kc);
+        load_b(cb, kc);
         __syncthreads();
+        store_a_lds(kc);
+        __syncthreads();
+      } else if (cb != nb0) {
+        load_b(cb, 0);
       }
-      const int k0 = kc * KC, kw = min(KC, K - k0), ks = (kw + 31) >> 5;
-      v8bf bq[KC / 32];
-#pragma unroll
-      for (int s = 0; s < KC / 32; ++s) {
-        const int k = k0 + 32 * s + 8 * (lane >> 4);
-        bq[s] = (s < ks && col < Cout && k < K) ? *reinterpret_cast<const v8bf*>(Wt + (size_t)col * K + k)
-                                                : v8bf{};
-      }
+      const int ks = (min(KC, K - kc * KC) + 31) >> 5;
 #pragma unroll
       for (int s = 0; s < KC / 32; ++s) {
         if (s >= ks) break;
@@ -203,39 +236,21 @@ __device__ void dw_tile(const MbPhaseDesc& d, int t, long long go, char* smem, c
   const float* __restrict__ KS = gsh(d.shift, go);
   float* __restrict__ SB = gsh(d.slotbuf, go);
   const int pro = d.pro;
-  if (tid < 2 * CW) {
-    const int c = c0 + (tid % CW) + (tid >= CW ? C : 0);
-    sT[tid] = pro ? ld_coh(tabs + d.tab_in + c) : (tid < CW ? 1.f : 0.f);
-    sS[tid] = 0.f;
-  }
-  __syncthreads();
   const float lo = act_lo(pro ? d.act_in : 0), hi = act_hi(pro ? d.act_in : 0);
   const int tx = tid % CG, ty = tid / CG;
-  {
-    const int items = nimg * HWi * CG;
-    const size_t base = (size_t)n0 * HWi;
-    for (int q0 = tid; q0 < items; q0 += 4 * NT) {
-      uint4 v[4];
+  // ---- tile inputs, all in flight at once: the input maps, the table, the kernel, the shift
+  constexpr int MAXI = 8;  // 16-B input chunks per thread (sX <= 64 KB)
+  const int items = nimg * HWi * CG;
+  const size_t base = (size_t)n0 * HWi;
+  uint4 xv[MAXI];
 #pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        const int q = q0 + u * NT;
-        const int pix = q / CG, g = q - pix * CG;
-        v[u] = q < items ? ld_coh16(X + (base + pix) * d.ldx + c0 + g * 8) : make_uint4(0u, 0u, 0u, 0u);
-      }
-#pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        const int q = q0 + u * NT;
-        if (q >= items) break;
-        const int pix = q / CG, g = q - pix * CG;
-        float f[8];
-        unpack8(v[u], f);
-        affine_act8(f, sT + g * 8, sT + CW + g * 8, lo, hi);
-        float* dst = sX + (size_t)pix * CW + g * 8;
-        *reinterpret_cast<float4*>(dst) = make_float4(f[0], f[1], f[2], f[3]);
-        *reinterpret_cast<float4*>(dst + 4) = make_float4(f[4], f[5], f[6], f[7]);
-      }
-    }
+  for (int i = 0; i < MAXI; ++i) {
+    const int q = tid + i * NT;
+    const int pix = q / CG, g = q - pix * CG;
+    xv[i] = q < items ? ld_coh16(X + (base + pix) * d.ldx + c0 + g * 8) : make_uint4(0u, 0u, 0u, 0u);
   }
+  float tval = tid < CW ? 1.f : 0.f;
+  if (pro && tid < 2 * CW) tval = ld_coh(tabs + d.tab_in + c0 + (tid % CW) + (tid >= CW ? C : 0));
   float wk[9][8], kk[8], ps[8], pq[8];
 #pragma unroll
   for (int r = 0; r < 9; ++r) {
@@ -249,6 +264,24 @@ __device__ void dw_tile(const MbPhaseDesc& d, int t, long long go, char* smem, c
     kk[j] = KS ? KS[c0 + tx * 8 + j] : 0.f;
     ps[j] = 0.f;
     pq[j] = 0.f;
+  }
+  __syncthreads();  // (the previous tile's LDS reads are done)
+  if (tid < 2 * CW) {
+    sT[tid] = tval;
+    sS[tid] = 0.f;
+  }
+  __syncthreads();
+#pragma unroll
+  for (int i = 0; i < MAXI; ++i) {
+    const int q = tid + i * NT;
+    if (q >= items) break;
+    const int pix = q / CG, g = q - pix * CG;
+    float f[8];
+    unpack8(xv[i], f);
+    affine_act8(f, sT + g * 8, sT + CW + g * 8, lo, hi);
+    float* dst = sX + (size_t)pix * CW + g * 8;
+    *reinterpret_cast<float4*>(dst) = make_float4(f[0], f[1], f[2], f[3]);
+    *reinterpret_cast<float4*>(dst + 4) = make_float4(f[4], f[5], f[6], f[7]);
   }
   __syncthreads();
   const int outs = nimg * HWo;
@@ -307,8 +340,10 @@ __device__ void dw_tile(const MbPhaseDesc& d, int t, long long go, char* smem, c
   }
 }
 
-// the phase's last tile: single-copy statistics and the consumer's table
+// the phase's last tile: single-copy statistics and the consumer's table.  Every load of a thread's
+// (up to MAXK / NT) channels is issued before any arithmetic: one memory round trip.
 __device__ void finalize(const MbPhaseDesc& d, long long go, float* tabs) {
+  constexpr int CPT = MAXK / NT;
   const int C = d.Cout;
   const float* __restrict__ SB = gsh(d.slotbuf, go);
   float* __restrict__ ST = gsh(d.stats, go);
@@ -318,41 +353,72 @@ __device__ void finalize(const MbPhaseDesc& d, long long go, float* tabs) {
   const float* __restrict__ MM = gsh(d.mmean, go);
   const float* __restrict__ MV = gsh(d.mvar, go);
   const int S = d.slots;
-  for (int c = threadIdx.x; c < C; c += NT) {
-    float mean, var;
-    if (d.bn_mode == 1) {
-      float a0[16], a1[16];
+  const bool batch = d.bn_mode == 1;
+  float a0[CPT][MB_MAX_SLOTS], a1[CPT][MB_MAX_SLOTS], g[CPT], bt[CPT], k0[CPT], k1[CPT];
 #pragma unroll
-      for (int s = 0; s < 16; ++s) {
-        a0[s] = s < S ? ld_coh(SB + (size_t)s * 2 * C + c) : 0.f;
-        a1[s] = s < S ? ld_coh(SB + (size_t)s * 2 * C + C + c) : 0.f;
-      }
+  for (int u = 0; u < CPT; ++u) {
+    const int c = min((int)threadIdx.x + u * NT, C - 1);
+#pragma unroll
+    for (int s = 0; s < MB_MAX_SLOTS; ++s) {
+      const size_t o = (size_t)(s < S ? s : S - 1) * 2 * C + c;
+      a0[u][s] = batch ? ld_coh(SB + o) : 0.f;
+      a1[u][s] = batch ? ld_coh(SB + o + C) : 0.f;
+    }
+    g[u] = G ? G[c] : 1.f;
+    bt[u] = Bt ? Bt[c] : 0.f;
+    k0[u] = batch ? (KS ? KS[c] : 0.f) : MM[c];
+    k1[u] = batch ? 0.f : MV[c];
+  }
+#pragma unroll
+  for (int u = 0; u < CPT; ++u) {
+    const int c = threadIdx.x + u * NT;
+    if (c >= C) break;
+    float mean = k0[u], var = k1[u];
+    if (batch) {
       float s0 = 0.f, s1 = 0.f;
 #pragma unroll
-      for (int s = 0; s < 16; ++s) {
-        s0 += a0[s];
-        s1 += a1[s];
+      for (int s = 0; s < MB_MAX_SLOTS; ++s) {
+        s0 += s < S ? a0[u][s] : 0.f;
+        s1 += s < S ? a1[u][s] : 0.f;
       }
       if (ST) {
         ST[c] = s0;
         ST[C + c] = s1;
       }
-      shifted_mean_var(KS ? KS[c] : 0.f, s0, s1, d.inv_count, mean, var);
-    } else {
-      mean = MM[c];
-      var = MV[c];
+      shifted_mean_var(k0[u], s0, s1, d.inv_count, mean, var);
     }
-    const float sc = (G ? G[c] : 1.f) * rsqrtf(var + d.eps);
+    const float sc = g[u] * rsqrtf(var + d.eps);
     st_coh(tabs + d.tab_out + c, sc);
-    st_coh(tabs + d.tab_out + C + c, (Bt ? Bt[c] : 0.f) - mean * sc);
+    st_coh(tabs + d.tab_out + C + c, bt[u] - mean * sc);
   }
+}
+
+// every thread's stores / atomics of the tile performed, then ONE lane counts the tile in its shard
+// of the phase's arrivals; the tile that completes a shard counts the shard, and the tile that
+// completes the last shard is the phase's last (it saw every other tile's count through the values
+// its two adds returned).  Returns (to every thread, via LDS) whether this tile is the last.
+__device__ __forceinline__ bool arrive(unsigned* arr, int t, int tiles, Ctl& s) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const int sh = t & 7;
+    const unsigned old = __hip_atomic_fetch_add(arr + sh, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    bool last = false;
+    if ((int)old + 1 == (tiles - sh + 7) / 8) {
+      const unsigned o2 = __hip_atomic_fetch_add(arr + 8, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      last = (int)o2 + 1 == min(tiles, 8);
+    }
+    s.last = last;
+  }
+  __syncthreads();
+  return __builtin_amdgcn_readfirstlane(s.last) != 0;
 }
 
 __global__ __launch_bounds__(NT) void mb_chain_kernel(MbChainArgs a, GroupArg ga) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   __shared__ Ctl s;
   const long long go = goff(ga);
-  const MbPhaseDesc* __restrict__ P = gsh(a.phases, go);
   unsigned* sync = gsh(a.sync, go);
   unsigned* fail = sync + 1;
   float* tabs = gsh(a.tabs, go);
@@ -360,10 +426,21 @@ __global__ __launch_bounds__(NT) void mb_chain_kernel(MbChainArgs a, GroupArg ga
   unsigned long long* stamps = gsh(a.stamps, go);
   const unsigned max_polls = a.max_polls ? a.max_polls : DEFAULT_POLLS;
   const int tid = threadIdx.x;
+  // the phase table, copied once into LDS: every descriptor field a tile reads is an LDS read (read
+  // from global memory, each field was a dependent vector load on the tile's critical path)
+  MbPhaseDesc* P = reinterpret_cast<MbPhaseDesc*>(smem);
+  char* tsm = smem + MB_TABLE_BYTES;
+  {
+    const unsigned* src = reinterpret_cast<const unsigned*>(gsh(a.phases, go));
+    unsigned* dst = reinterpret_cast<unsigned*>(smem);
+    const int words = a.nphases * (int)sizeof(MbPhaseDesc) / 4;
+    for (int i = tid; i < words; i += NT) dst[i] = src[i];
+  }
   int cp = 0;
   for (;;) {
     // ticket: a thread-0 region between barriers, broadcast through LDS + readfirstlane so every
-    // branch of the loop is workgroup-uniform (dense_stage.hip)
+    // branch of the loop is workgroup-uniform (dense_stage.hip); the first barrier also publishes
+    // the phase table
     __syncthreads();
     if (tid == 0) s.task = (int)__hip_atomic_fetch_add(sync, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     __syncthreads();
@@ -382,13 +459,13 @@ __global__ __launch_bounds__(NT) void mb_chain_kernel(MbChainArgs a, GroupArg ga
     stamp(stamps, task, 1);
     const int kind = d.kind;
     if (kind == MB_PW) {
-      if (d.tm == 64) pw_tile<64>(d, t, go, smem, tabs);
-      else pw_tile<32>(d, t, go, smem, tabs);
+      if (d.tm == 64) pw_tile<64>(d, t, go, tsm, tabs);
+      else pw_tile<32>(d, t, go, tsm, tabs);
     } else if (kind == MB_DW) {
       const int cw = d.tn;
-      if (cw == 64) dw_tile<8>(d, t, go, smem, tabs);
-      else if (cw == 32) dw_tile<4>(d, t, go, smem, tabs);
-      else dw_tile<2>(d, t, go, smem, tabs);
+      if (cw == 64) dw_tile<8>(d, t, go, tsm, tabs);
+      else if (cw == 32) dw_tile<4>(d, t, go, tsm, tabs);
+      else dw_tile<2>(d, t, go, tsm, tabs);
     } else {  // MB_TAB
       BnArgs b = d.pre;
       gshift(b, go);
@@ -400,10 +477,7 @@ __global__ __launch_bounds__(NT) void mb_chain_kernel(MbChainArgs a, GroupArg ga
       }
     }
     stamp(stamps, task, 2);
-    const unsigned old = publish(arrive_w(sync, cp));
-    if (tid == 0) s.last = old == (unsigned)(d.tiles - 1);
-    __syncthreads();
-    if (__builtin_amdgcn_readfirstlane(s.last)) {
+    if (arrive(arrive_w(sync, cp), t, d.tiles, s)) {
       if (kind != MB_TAB && d.tab_out >= 0) finalize(d, go, tabs);
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __syncthreads();
@@ -415,10 +489,12 @@ __global__ __launch_bounds__(NT) void mb_chain_kernel(MbChainArgs a, GroupArg ga
 
 }  // namespace
 
-int mb_smem_limit() { return SMEM_LIMIT; }
+int mb_smem_limit() { return SMEM_LIMIT - MB_TABLE_BYTES; }
 
+// tile LDS: PW = table + operand chunk (+ the output staging tile, which aliases the operand when
+// K > KC: one column chunk, operand dead after its last MFMA); DW = tables + input maps
 int mb_phase_smem(const MbPhaseDesc& d) {
-  if (d.kind == MB_PW) return ((2 * d.Cin + 3) / 4) * 16 + 64 * APITCH * 2 + 64 * YP * 2;
+  if (d.kind == MB_PW) return ((2 * d.Cin + 3) / 4) * 16 + 64 * APITCH * 2 + (d.Cin > KC ? 0 : 64 * YP * 2);
   if (d.kind == MB_DW) return (4 * d.tn + d.tm * d.H * d.W * d.tn) * 4;
   return 0;
 }
@@ -429,7 +505,8 @@ bool mb_phase_ok(const MbPhaseDesc& d) {
   if (d.tiles < 1 || d.first < 0 || d.N < 1 || d.Cout < 1) return false;
   if (d.kind == MB_TAB) return d.tiles == 1 && d.tab_out >= 0 && d.Cout <= 4096;
   if (d.pro && d.tab_in < 0) return false;
-  if (d.bn_mode == 1 && (d.slots < 1 || d.slots > 16 || d.slotbuf == nullptr)) return false;
+  if (d.bn_mode == 1 && (d.slots < 1 || d.slots > MB_MAX_SLOTS || d.slotbuf == nullptr)) return false;
+  if (d.Cout > MAXK) return false;
   if (d.bn_mode && d.tab_out < 0) return false;
   if (d.kind == MB_PW) {
     const int M = d.N * d.H * d.W;
@@ -439,7 +516,7 @@ bool mb_phase_ok(const MbPhaseDesc& d) {
     if (d.pro == 2 && d.act_in != 0) return false;
     if (d.pro == 0 && (d.res || d.aout)) return false;
     const int tiles = ((M + d.tm - 1) / d.tm) * ((d.Cout + d.tn - 1) / d.tn);
-    return d.tiles == tiles && d.H == d.Ho && d.W == d.Wo && mb_phase_smem(d) <= SMEM_LIMIT;
+    return d.tiles == tiles && d.H == d.Ho && d.W == d.Wo && mb_phase_smem(d) <= mb_smem_limit();
   }
   if (d.kind == MB_DW) {
     if (d.tn != 16 && d.tn != 32 && d.tn != 64) return false;
@@ -448,15 +525,17 @@ bool mb_phase_ok(const MbPhaseDesc& d) {
       return false;
     if ((d.Ho - 1) * d.S - d.PT + 2 < 0 || d.Ho < 1 || d.Wo < 1) return false;
     const int tiles = ((d.N + d.tm - 1) / d.tm) * (d.Cin / d.tn);
-    return d.tiles == tiles && mb_phase_smem(d) <= SMEM_LIMIT;
+    return d.tiles == tiles && mb_phase_smem(d) <= mb_smem_limit() &&
+           d.tm * d.H * d.W * (d.tn / 8) <= 8 * NT;  // (dw_tile MAXI)
   }
   return false;
 }
 
 hipError_t mb_chain(const MbChainArgs& a, int grid, int smem, hipStream_t st) {
-  if (a.phases == nullptr || a.sync == nullptr || a.tabs == nullptr || a.nphases < 1 || a.ntickets < 1 ||
-      smem < 0 || smem > SMEM_LIMIT)
+  if (a.phases == nullptr || a.sync == nullptr || a.tabs == nullptr || a.nphases < 1 ||
+      a.nphases > MB_MAX_PHASES || a.ntickets < 1 || smem < 0 || smem > mb_smem_limit())
     return hipErrorInvalidValue;
+  smem += MB_TABLE_BYTES;
   if (grid <= 0) grid = 512;
   const int k = launch_groups().k;
   if (k > 1) grid = grid / k > 8 ? grid / k : 8;

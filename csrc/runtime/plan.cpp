@@ -1081,4 +1081,5 @@ PYBIND11_MODULE(_idc_native, m) {
     return mb_phase_smem(*reinterpret_cast<const MbPhaseDesc*>(s.data()));
   });
   m.attr("MB_SMEM_LIMIT") = mb_smem_limit();
+  m.attr("MB_MAX_PHASES") = MB_MAX_PHASES;
 }

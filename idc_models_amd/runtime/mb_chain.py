@@ -9,6 +9,14 @@ by the phase's last tile).  When any phase fails the kernel's shape rules (``mb_
 launch is switched off (``IDC_MB_CHAIN=0``, deterministic mode, persistent launches disabled after
 a give-up), ``emit`` replays the recorded per-layer emissions instead, in the same order.
 
+Off by default (IDC_MB_CHAIN=1 turns it on).  Measured on one MI355X, MobileNetV2 bs 256
+(tools/mb_stamps.py, profiles/mobilenetv2_chain_stamps.md): the 51-phase launch spans 1.64 ms
+against ~0.76 ms for the per-layer forward (3.67 vs 2.36 ms/step with the first version).  Phase
+hand-offs cost ~0.5 us, but a tile is a chain of dependent memory round trips (agent-coherent
+operand loads, B fragments, output stores and the arrival count) of 2-3 us each under load, with
+one or two workgroups per CU to overlap them, and every phase's last tile finalises its statistics
+(5-14 us) on the critical path; the per-layer kernels keep thousands of tiles in flight instead.
+
 Reference: the MobileNetV2 base of /root/reference/dist_model_tf_mobile.py:119-121,135-138.
 """
 from __future__ import annotations
@@ -29,7 +37,7 @@ _TILES = 512
 
 def chain_enabled(b) -> bool:
     from .builder import persistent_disabled
-    return os.environ.get("IDC_MB_CHAIN", "1") != "0" and not b.det and not persistent_disabled()
+    return os.environ.get("IDC_MB_CHAIN", "0") == "1" and not b.det and not persistent_disabled()
 
 
 class MbChain:
@@ -79,7 +87,7 @@ class MbChain:
             else:
                 d.stats, d.shift = stats.ptr, stats.shift_ptr()
                 d.inv_count = 1.0 / float(stats.count)
-                d.slots = max(1, min(16, -(-tiles // 64)))
+                d.slots = max(1, min(8, -(-tiles // 64)))
                 d.slotbuf = self.b._stats_floats(2 * y.C * d.slots).data_ptr()
         self.descs.append(d)
         if bn is not None:
@@ -157,7 +165,8 @@ class MbChain:
         ops (False)."""
         b = self.b
         ext = nat.load()
-        ok = self.ok and chain_enabled(b) and any(d.kind != nat.MB_TAB for d in self.descs)
+        ok = self.ok and chain_enabled(b) and any(d.kind != nat.MB_TAB for d in self.descs) and \
+            len(self.descs) <= int(ext.MB_MAX_PHASES)
         first = 0
         smem = 0
         if ok:
@@ -179,7 +188,7 @@ class MbChain:
         b.keep.append(tab)
         if getattr(b, "dense_err", None) is None:
             b.dense_err = b.alloc((4,), torch.int32)
-        sync = b._stats_floats(2 + 2 * n)
+        sync = b._stats_floats(2 + 10 * n)  # mb_chain.h MB_SYNC_PER_PHASE
         if not b.training:
             b.memset(sync)
         tabs = b.alloc((max(self.tab_size, 4),), F32)
@@ -192,7 +201,7 @@ class MbChain:
             stamps = b.alloc((8 * first,), torch.int64)
             a.stamps = stamps.data_ptr()
             b.mb_stamps = getattr(b, "mb_stamps", []) + [(stamps, [(d.kind, d.first, d.tiles) for d in self.descs])]
-        grid = int(os.environ.get("IDC_MB_GRID", "512"))
+        grid = int(os.environ.get("IDC_MB_GRID", "256"))
         b.emit(nat.OP_MB_CHAIN, a, ints=(grid, smem, n), ptrs=(tab.data_ptr(),))
         b.mb_chains = getattr(b, "mb_chains", 0) + 1
         return True

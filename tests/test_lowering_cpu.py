@@ -199,8 +199,8 @@ def test_dense_stage_bwd_lowering(monkeypatch):
 
 
 def test_mb_chain_lowering(monkeypatch):
-    """MobileNetV2's blocks lower to ONE OP_MB_CHAIN (expand / depthwise / project of every block
-    from IDC_MB_CHAIN_FROM on); IDC_MB_CHAIN=0 keeps the per-layer ops.
+    """MobileNetV2's blocks lower to ONE OP_MB_CHAIN with IDC_MB_CHAIN=1 (expand / depthwise /
+    project of every block from IDC_MB_CHAIN_FROM on); the default keeps the per-layer ops.
     Tickets are contiguous per phase, every phase depends on an earlier one, and every conv phase's
     output BatchNorm gets a table the next phase reads."""
     def lower(**env):
@@ -214,7 +214,8 @@ def test_mb_chain_lowering(monkeypatch):
     def kinds(b):
         return [k for (_, k, *_r) in b.ops]
 
-    on, off = lower(), lower(IDC_MB_CHAIN="0")
+    on, off = lower(IDC_MB_CHAIN="1"), lower(IDC_MB_CHAIN="0")
+    assert kinds(lower()).count(nat.OP_MB_CHAIN) == 0  # off by default (runtime/mb_chain.py)
     k_on, k_off = kinds(on), kinds(off)
     assert k_on.count(nat.OP_MB_CHAIN) == 1 and k_off.count(nat.OP_MB_CHAIN) == 0
     fwd_on = [op[1] for op in on.ops if op[0] == "fwd"]
@@ -238,6 +239,6 @@ def test_mb_chain_lowering(monkeypatch):
             assert d.bn_mode == 1 and d.slots >= 1 and d.tab_out >= 0
     a = nat.MbChainArgs.from_buffer_copy(op[2])
     assert a.ntickets == first and a.nphases == n
-    part = lower(IDC_MB_CHAIN_FROM="10")
+    part = lower(IDC_MB_CHAIN="1", IDC_MB_CHAIN_FROM="10")
     d10 = [op for op in part.ops if op[1] == nat.OP_MB_CHAIN]
     assert len(d10) == 1 and d10[0][3][2] == 1 + 3 * 7  # TAB of block 9's project BN + blocks 10-16
