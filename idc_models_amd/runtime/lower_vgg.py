@@ -105,6 +105,8 @@ def _pool_bwd_relu(b: Builder, dy, dx, argmax, x, gbias):
     a.gsumx = 0
     if b.det and gbias is not None:  # one private slot per workgroup + fixed-order collapse
         a.gsum, _, a.gsum_slots, a.gsum_ld = b._det_gsum_slots(dx.C, b._rows_grid(dx.M, dx.C, 4), gbias.data_ptr())
+    elif gbias is not None and b._rows_slotted(b._rows_grid(dx.M, dx.C, 4)):
+        a.gsum, _, a.gsum_slots, a.gsum_ld = b.slotted_sums(dx.C, b._rows_grid(dx.M, dx.C, 4), gbias.data_ptr())
     a.dx, a.lddx = dx.ptr, dx.ld
     a.is_avg = 0
     b.emit(nat.OP_POOL_BWD, a)

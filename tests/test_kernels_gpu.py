@@ -779,7 +779,8 @@ def test_wgrad_batch_matches_single_launches(fn, kind, N, H):
 
 
 @pytest.mark.parametrize("N,H,c0,L,grid", [(4, 3, 64, 3, 256), (6, 1, 96, 4, 7), (3, 5, 32, 2, 1),
-                                          (8, 6, 64, 3, 64), (2, 1, 1120, 3, 256), (5, 2, 256, 4, 256)])
+                                          (8, 6, 64, 3, 64), (2, 1, 1120, 3, 256), (5, 2, 256, 4, 256),
+                                          (256, 3, 256, 24, 256)])
 def test_dense_stage_persistent_matches_reference(fn, N, H, c0, L, grid):
     """The persistent dense-stage launch (work queue + per-phase completion counters, 1x1 partial
     sums over the finished channels accumulated before the newest slice is waited for, slotted
@@ -788,7 +789,8 @@ def test_dense_stage_persistent_matches_reference(fn, N, H, c0, L, grid):
     BN2->ReLU->3x3(32) (centre tap on 1x1 maps) into the stage buffer slice with its statistics.
     grid 7 / 1: far fewer workgroups than tiles (the queue must still drain: every wait depends only
     on earlier tickets).  c0 1120: DenseNet-201-wide inputs (cin > 1024, several 256-channel
-    staging chunks); 2x2 maps: DenseNet-201 @ 32x32's stage 3."""
+    staging chunks); 2x2 maps: DenseNet-201 @ 32x32's stage 3; (256, 3, 256, 24): DenseNet-121's
+    stage 3 at the bench batch exactly (M = 2,304, 24 layers, cin 256 -> 992, lookahead order)."""
     W = H
     ld = c0 + 32 * L
     g = torch.Generator(device="cpu").manual_seed(N * 100 + H)
@@ -891,7 +893,8 @@ def _bn_train(x, g, b, eps):
 
 
 @pytest.mark.parametrize("N,H,c0,L,grid", [(16, 3, 64, 3, 256), (64, 1, 96, 4, 256), (8, 3, 128, 2, 5),
-                                          (6, 2, 256, 3, 64), (4, 1, 1120, 2, 256), (64, 3, 256, 4, 256)])
+                                          (6, 2, 256, 3, 64), (4, 1, 1120, 2, 256), (64, 3, 256, 4, 256),
+                                          (256, 3, 256, 24, 256), (256, 1, 512, 16, 256)])
 def test_dense_stage_bwd_matches_autograd(fn, N, H, c0, L, grid):
     """The persistent dense-stage BACKWARD launch (dense_stage_bwd.hip: 3x3 dgrad, dT, newest-slice
     and older-channel 1x1 dgrads, every BatchNorm backward through the summed pending affines,
@@ -899,7 +902,8 @@ def test_dense_stage_bwd_matches_autograd(fn, N, H, c0, L, grid):
     where the kernels store them (straight-through).  Upstream: a consumer BatchNorm + ReLU over the
     whole stage buffer with a random output gradient (the transition / final BatchNorm of
     lower_densenet).  grid 5: far fewer workgroups than tickets (queue order must still drain);
-    c0 1120: DenseNet-201-wide inputs; 1x1 maps: centre-tap 3x3."""
+    c0 1120: DenseNet-201-wide inputs; 1x1 maps: centre-tap 3x3; (256, 3, 256, 24) and
+    (256, 1, 512, 16): DenseNet-121's stages 3 and 4 at the bench batch exactly."""
     torch.manual_seed(N * 1000 + c0 + L)
     W = H
     ld = c0 + 32 * L

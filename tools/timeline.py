@@ -21,6 +21,8 @@ def main():
     ap.add_argument("db")
     ap.add_argument("--marker", default="input_stage")
     ap.add_argument("--top", type=int, default=12)
+    ap.add_argument("--gaps", type=int, default=0, help="list the N largest backward main-lane gaps "
+                    "with the kernels around them and what the side lane ran meanwhile")
     a = ap.parse_args()
     c = sqlite3.connect(a.db)
     rows = list(c.execute("select name, start, end, queue_id from kernels order by start"))
@@ -53,6 +55,15 @@ def main():
     if side_q:
         busy = sum(r[2] - r[1] for r in side_q) / 1e3
         print(f"  side lane busy {busy:8.1f} us over {(side_q[-1][2] - side_q[0][1]) / 1e3:.1f} us")
+    if a.gaps:
+        bw = phases["backward"]
+        gl = sorted(((bw[i + 1][1] - bw[i][2]) / 1e3, i) for i in range(len(bw) - 1))[::-1][:a.gaps]
+        print(f"-- largest backward gaps (of {len(bw) - 1})")
+        for g, i in gl:
+            t0, t1 = bw[i][2], bw[i + 1][1]
+            side = [short(r[0]) for r in side_q if r[1] < t1 and r[2] > t0]
+            print(f"   {g:7.2f} us after {short(bw[i][0])[:44]} -> {short(bw[i + 1][0])[:44]}"
+                  f"  side: {', '.join(side)[:90] or '-'}")
     for name, rs in list(phases.items()) + [("side", side_q)]:
         agg, cnt = collections.Counter(), collections.Counter()
         for r in rs:
