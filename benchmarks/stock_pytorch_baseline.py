@@ -10,7 +10,8 @@ hot path; it exists only to produce that number.
 
 ``--phase``: ``full`` (every layer trains), ``frozen`` (reference phase 1, ``base_model.trainable =
 False``: only the head trains, frozen BatchNorms in inference mode) or ``finetune`` (reference
-phase 2, ``fine_tune_at`` = 150 for DenseNet / 100 for MobileNetV2 Keras layers frozen: the same
+phase 2, ``fine_tune_at`` = 150 for DenseNet / 100 for MobileNetV2 / 15 for VGG16 Keras layers
+frozen (recipes/transfer.py fine_tune_at_for): the same
 number of leading weighted layers -- Keras order = this module order -- is frozen here).
 """
 from __future__ import annotations
@@ -126,10 +127,11 @@ def _keras_frozen_weighted(model_name: str, phase: str, size: int, classes: int)
     import sys
     sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
     from idc_models_amd.models import build_model
+    from idc_models_amd.recipes.transfer import fine_tune_at_for
     net = build_model(model_name, (size, size, 3), classes, seed=0)
     layers = net.base.layers
-    if phase == "finetune":
-        layers = layers[:150 if model_name.startswith("densenet") else 100]
+    if phase == "finetune":  # the reference's cut: VGG16 15, MobileNetV2 100, DenseNets 150
+        layers = layers[:fine_tune_at_for(model_name)]
     return sum(1 for l in layers if l.keras_class in ("Conv2D", "BatchNormalization", "DepthwiseConv2D"))
 
 
