@@ -463,7 +463,24 @@ class Plan {
     check(hipDeviceGetStreamPriorityRange(&least, &greatest), "hipDeviceGetStreamPriorityRange");
     const char* sp = std::getenv("IDC_SIDE_PRIO");
     const int prio = (sp && std::strcmp(sp, "low") == 0) ? least : 0;
-    check(hipStreamCreateWithPriority(&side_, hipStreamNonBlocking, prio), "hipStreamCreate(side)");
+    // IDC_SIDE_CUS=N: the side lane runs on N of the device's CUs only (a CU-masked queue, bits
+    // spread evenly over the CU index space), so weight-gradient workgroups never occupy the
+    // CUs the data-gradient chain needs next (measured: runtime/program.py)
+    const char* scu = std::getenv("IDC_SIDE_CUS");
+    const int ncu_side = scu ? std::atoi(scu) : 0;
+    int dev = 0, ncu = 0;
+    check(hipGetDevice(&dev), "hipGetDevice");
+    check(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev), "hipDeviceGetAttribute");
+    if (ncu_side > 0 && ncu_side < ncu) {
+      std::vector<uint32_t> mask((ncu + 31) / 32, 0u);
+      for (int i = 0; i < ncu_side; ++i) {
+        const int cu = (int)((long long)i * ncu / ncu_side);
+        mask[cu / 32] |= 1u << (cu % 32);
+      }
+      check(hipExtStreamCreateWithCUMask(&side_, (uint32_t)mask.size(), mask.data()), "hipExtStreamCreateWithCUMask(side)");
+    } else {
+      check(hipStreamCreateWithPriority(&side_, hipStreamNonBlocking, prio), "hipStreamCreate(side)");
+    }
     check(hipEventCreateWithFlags(&fork_, hipEventDisableTiming), "hipEventCreate(fork)");
     check(hipEventCreateWithFlags(&join_, hipEventDisableTiming), "hipEventCreate(join)");
     check(hipEventCreateWithFlags(&mark_, hipEventDisableTiming), "hipEventCreate(mark)");

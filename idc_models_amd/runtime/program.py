@@ -161,6 +161,10 @@ class FusedProgram:
         n_bwd_main = sum(1 for op in b.ops if op[0] == "bwd" and op[7] == 0)
         # grouped (client-batched) DenseNet: secure FedAvg 0.410-0.414 s/round at 0 vs 0.416 at 2,
         # 0.418 at 4; grouped MobileNetV2 FedAvg keeps 4 (0.220-0.222 vs 0.223 at 0)
+        # IDC_SIDE_CUS=N (plan.cpp ensure_side: the side lane on a CU-masked queue of N CUs) is
+        # opt-in: round 5, 64 / 128 / 192 CUs against the unmasked default, ms/step: MobileNetV2
+        # 2.609 / 2.739 / 2.722 vs 2.311, VGG16 2.467 / 2.448 / 2.461 vs 2.388, DenseNet-121
+        # 3.942 / 3.931 / 3.865 vs 3.702
         big = n_bwd_main >= 90
         default_flush = "0" if b.grouped and big else "2" if big else "4" if n_bwd_main >= 64 else "0"
         self.plan.set_side_flush(int(os.environ.get("IDC_SIDE_FLUSH", default_flush)))
