@@ -91,6 +91,11 @@ hipError_t conv_img(const ConvArgs& a, bool a_f32, hipStream_t st);
 constexpr int TILE_ROWS = 106;
 bool conv_rows_ok(const ConvArgs& a, bool a_f32);
 hipError_t conv_rows(const ConvArgs& a, bool a_f32, hipStream_t st);
+// tile TILE_STEM selects the image-resident stem convolution (conv_stem.hip): 8-channel staged
+// images, KxK stride 1/2, up to 64 output channels
+constexpr int TILE_STEM = 107;
+bool conv_stem_ok(const ConvArgs& a, bool a_f32);
+hipError_t conv_stem(const ConvArgs& a, bool a_f32, hipStream_t st);
 bool conv_big_ok(const ConvArgs& a, bool a_f32);
 hipError_t conv_big(const ConvArgs& a, int bn, bool a_f32, hipStream_t st);
 hipError_t conv_igemm(const ConvArgs& a, int tile, bool a_f32, hipStream_t st);

@@ -42,6 +42,11 @@ int wgrad_variant_bp(int variant);
 // dw[i] += sum_{z < splits} part[z * n + i], in slice order
 hipError_t wgrad_reduce(const float* part, float* dw, long long n, int splits, hipStream_t st);
 int wgrad_effective_splits(const WgradArgs& a, int splits, int variant = 0);
+// the image-resident stem weight gradient (wgrad_stem.hip): 8-channel staged images, KxK stride
+// 1/2, <= 64 outputs; with IDC_WGRAD_STEM=1 conv_wgrad takes it whenever it applies (opt-in)
+bool wgrad_stem_ok(const WgradArgs& a, bool g_f32);
+hipError_t wgrad_stem(const WgradArgs& a, hipStream_t st);
+int wgrad_stem_slices(const WgradArgs& a);
 int wgrad_pick_splits(int M, int K, int Cout);
 
 // ---- batched weight gradients -----------------------------------------------------------------

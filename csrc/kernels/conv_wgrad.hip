@@ -545,6 +545,7 @@ static bool wgrad_big_tile(const WgradArgs& a) {
 }
 
 hipError_t conv_wgrad(WgradArgs a, int splits, bool g_f32, hipStream_t st, int variant) {
+  if (wgrad_stem_ok(a, g_f32)) return wgrad_stem(a, st);
   if (variant > 0 && wgrad_big_ok(a, g_f32, variant)) return wgrad_big(a, splits, g_f32, variant, st);
   if (wgrad_halo_ok(a, g_f32)) {
     const int groups = wgrad_halo_groups(a, splits);
@@ -575,6 +576,7 @@ hipError_t conv_wgrad(WgradArgs a, int splits, bool g_f32, hipStream_t st, int v
 }
 
 int wgrad_effective_splits(const WgradArgs& a, int splits, int variant) {
+  if (wgrad_stem_ok(a, false)) return wgrad_stem_slices(a);
   const bool big = variant > 0 && wgrad_big_ok(a, false, variant);
   if (!big && wgrad_halo_ok(a, false)) return wgrad_halo_groups(a, splits);
   const int M = a.N * a.Ho * a.Wo;

@@ -415,6 +415,9 @@ __device__ __forceinline__ bool arrive(unsigned* arr, int t, int tiles, Ctl& s) 
   return __builtin_amdgcn_readfirstlane(s.last) != 0;
 }
 
+}  // namespace
+
+// (outside the anonymous namespace so profiles name it)
 __global__ __launch_bounds__(NT) void mb_chain_kernel(MbChainArgs a, GroupArg ga) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   __shared__ Ctl s;
@@ -486,6 +489,8 @@ __global__ __launch_bounds__(NT) void mb_chain_kernel(MbChainArgs a, GroupArg ga
     stamp(stamps, task, 3);
   }
 }
+
+namespace {
 
 }  // namespace
 

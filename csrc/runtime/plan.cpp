@@ -1021,6 +1021,13 @@ PYBIND11_MODULE(_idc_native, m) {
   m.def("wgrad", &py_wgrad, py::arg("payload"), py::arg("splits"), py::arg("g_f32"), py::arg("stream"),
         py::arg("variant") = 0);
   m.def("wgrad_big_ok", &py_wgrad_big_ok);
+  m.def("wgrad_stem_ok", [](py::bytes payload, int g_f32) {
+    std::string s = payload;
+    if (s.size() != sizeof(WgradArgs)) throw std::runtime_error("WgradArgs size mismatch");
+    WgradArgs a;
+    std::memcpy(&a, s.data(), sizeof(a));
+    return wgrad_stem_ok(a, g_f32 != 0);
+  });
   m.def("wgrad_big_pick_splits", &wgrad_big_pick_splits);
   m.def("wgrad_num_variants", &wgrad_num_variants);
   m.def("struct_sizes", &struct_sizes);
@@ -1033,6 +1040,7 @@ PYBIND11_MODULE(_idc_native, m) {
   m.attr("TILE_BIG128D") = TILE_BIG128D;
   m.attr("TILE_IMG") = TILE_IMG;
   m.attr("TILE_ROWS") = TILE_ROWS;
+  m.attr("TILE_STEM") = TILE_STEM;
   m.def("rows_ok", [](py::bytes payload, int a_f32) {
     std::string s = payload;
     if (s.size() != sizeof(ConvArgs)) throw std::runtime_error("ConvArgs size mismatch");
@@ -1046,6 +1054,13 @@ PYBIND11_MODULE(_idc_native, m) {
     ConvArgs a;
     std::memcpy(&a, s.data(), sizeof(a));
     return conv_img_ok(a, a_f32 != 0);
+  });
+  m.def("stem_ok", [](py::bytes payload, int a_f32) {
+    std::string s = payload;
+    if (s.size() != sizeof(ConvArgs)) throw std::runtime_error("ConvArgs size mismatch");
+    ConvArgs a;
+    std::memcpy(&a, s.data(), sizeof(a));
+    return conv_stem_ok(a, a_f32 != 0);
   });
   m.def("pick_splits", &py_pick_splits);
   m.def("effective_splits", &py_effective_splits);

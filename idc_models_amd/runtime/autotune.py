@@ -92,6 +92,10 @@ def _conv_candidates(ext, M: int, cout: int, payload: bytes = None, a_f32: int =
     if payload is not None and os.environ.get("IDC_CONV_IMG", "1") != "0" and hasattr(ext, "img_ok") \
             and ext.img_ok(payload, a_f32):
         out.append(ext.TILE_IMG)
+    # the image-resident stem conv (conv_stem.hip: 8-channel staged images)
+    if payload is not None and os.environ.get("IDC_CONV_STEM", "1") != "0" and hasattr(ext, "stem_ok") \
+            and ext.stem_ok(payload, a_f32):
+        out.append(ext.TILE_STEM)
     # the row-block 1x1 data gradient with the concat-gradient epilogue (conv_rows.hip)
     if payload is not None and os.environ.get("IDC_CONV_ROWS", "1") != "0" and hasattr(ext, "rows_ok") \
             and ext.rows_ok(payload, a_f32):

@@ -734,6 +734,13 @@ class Builder:
                 slab = self.alloc((max(need, 2 * (slab.numel() if slab is not None else 0)),), F32)
                 self._wslab[ln] = slab
             a.part, a.part_floats = slab.data_ptr(), slab.numel()
+        elif nat.load().wgrad_stem_ok(nat.raw(a), 1 if g.is_f32 else 0):
+            # the image-resident stem weight gradient (wgrad_stem.hip) stores one partial dW per
+            # workgroup into its own slab, summed in order right after (plan.cpp OP_WGRAD): float
+            # atomics from its ~500-1000 workgroups onto the same few thousand addresses serialise
+            need = int(nat.load().effective_splits(nat.raw(a), splits)) * dw.numel()
+            slab = self.alloc((need,), F32)
+            a.part, a.part_floats = slab.data_ptr(), slab.numel()
         self.emit(nat.OP_WGRAD, a, ints=(splits, 1 if g.is_f32 else 0), lane=lane)
 
     def has_wgrad_batch(self) -> bool:

@@ -45,7 +45,8 @@ def lower_densenet(b: Builder, net, U: int, input_dtype):
     conv1, bn1l = L["conv1/conv"], L["conv1/bn"]
     H1, W1 = (H + 6 - 7) // 2 + 1, (W + 6 - 7) // 2 + 1
     ys = b.nhwc(B, H1, W1, 64)
-    ss = b.stats(64, B * H1 * W1) if training else None
+    # (slot copies: the stem conv runs ~1k workgroups, each adding every channel's sums)
+    ss = b.stats(64, B * H1 * W1, slotted=True) if training else None
     b.conv(x8, conv1, ys, stride=(2, 2), pads=(3, 3), stats=ss)
     bn_stem = BNRef(bn1l, b, ss, RELU)
     b.add_moving(bn_stem)

@@ -63,7 +63,7 @@ def lower_mobilenet(b: Builder, net, U: int, input_dtype):
     W1 = (W + pad[1][0] + pad[1][1] - 3) // 2 + 1
     stem_pads = (pad[0][0], pad[1][0])
     y0 = b.nhwc(B, H1, W1, conv1.filters)
-    s0 = b.stats(conv1.filters, B * H1 * W1) if training else None
+    s0 = b.stats(conv1.filters, B * H1 * W1, slotted=True) if training else None  # (stem: ~1k workgroups)
     b.conv(x8, conv1, y0, stride=(2, 2), pads=stem_pads, stats=s0)
     bn0 = BNRef(bnl0, b, s0, RELU6)
     b.add_moving(bn0)

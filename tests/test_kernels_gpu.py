@@ -87,6 +87,37 @@ def test_conv_every_tile_large_m_odd_ktiles(fn, tile):
     assert relerr(st[:Cout], ref.sum((0, 1, 2))) < 1e-2
 
 
+@pytest.mark.parametrize("N,H,k,s,pads,cout,bias", [
+    (64, 50, 7, 2, (3, 3, 3, 3), 64, False),   # DenseNet-121 conv1/conv (ZeroPadding2D(3))
+    (37, 50, 3, 2, (0, 1, 0, 1), 32, False),   # MobileNetV2 Conv1 (correct_pad), odd batch
+    (8, 50, 3, 1, (1, 1, 1, 1), 64, True),     # VGG16 block1_conv1 (bias + ReLU)
+    (3, 32, 3, 1, (1, 1, 1, 1), 16, True),     # one column fragment, CIFAR-sized maps
+])
+def test_conv_stem_matches_reference(fn, N, H, k, s, pads, cout, bias):
+    """Image-resident stem conv (conv_stem.hip, tile TILE_STEM): 8-channel staged images (RGB +
+    zero channels, as the input op stores them), the band's input rows in LDS, bf16 output with
+    bias + activation and shifted output statistics, vs fp32 PyTorch on the same bf16 operands."""
+    ext = fn.nat.require()
+    g = torch.Generator(device="cpu").manual_seed(N + k)
+    x = torch.zeros(N, H, H, 8)
+    x[..., :3] = torch.rand(N, H, H, 3, generator=g)
+    x = bf(x.to(DEV))
+    w = torch.zeros(k, k, 8, cout)
+    w[:, :, :3] = torch.randn(k, k, 3, cout, generator=g) * (2.0 / (k * k * 3)) ** 0.5
+    w = bf(w.to(DEV))
+    b = (torch.randn(cout, generator=g) * 0.1).to(DEV) if bias else None
+    ho = (H + pads[0] + pads[1] - k) // s + 1
+    K = (torch.randn(cout, generator=g) * 0.1).to(DEV)
+    st = torch.zeros(2 * cout, device=DEV)
+    y = fn.conv2d(x.to(torch.bfloat16), w, stride=(s, s), pads=(pads[0], pads[2]), out_hw=(ho, ho), bias=b,
+                  act=1 if bias else 0, tile=ext.TILE_STEM, stats=st, stats_shift=K)
+    ref = ref_conv(x, w, s, pads, b, act=1 if bias else 0)
+    assert y.shape == ref.shape
+    assert relerr(y.float(), ref) < 1e-2
+    yk = y.float().reshape(-1, cout) - K
+    assert relerr(st[:cout], yk.sum(0)) < 1e-3 and relerr(st[cout:], (yk * yk).sum(0)) < 1e-3
+
+
 @pytest.mark.parametrize("tile,ks", [(4, 2), (9, 4), (12, 2), (17, 2), (18, 4), (8, 8), (7, 3), (19, 4), (22, 2)])
 def test_conv_split_k_matches_reference(fn, tile, ks):
     """Split-K (in-launch last-arriver reduction) on a small-M deep-K layer with the BN prologue
@@ -225,6 +256,37 @@ def test_conv_wgrad_prologue_and_cin_real(fn):
                                       stride=2, padding=3).permute(2, 3, 1, 0)
     assert dw.shape == (7, 7, 3, 64)
     assert relerr(dw, ref) < 1e-2
+
+
+@pytest.mark.parametrize("N,H,k,s,pads,ho,cout,aff", [
+    (64, 50, 7, 2, (3, 3), 25, 64, True),    # DenseNet-121 stem, G through the stem BN's backward
+    (37, 50, 3, 2, (0, 0), 25, 32, False),   # MobileNetV2 Conv1 (correct_pad: bottom/right implicit)
+    (8, 50, 3, 1, (1, 1), 50, 64, False),    # VGG16 block1_conv1
+    (3, 32, 3, 1, (1, 1), 32, 16, True),
+])
+def test_wgrad_stem_matches_reference(fn, N, H, k, s, pads, ho, cout, aff):
+    """Image-resident stem weight gradient (wgrad_stem.hip, taken by conv_wgrad whenever it
+    applies): 8-channel staged images with 3 real channels, dW over the real channels only; with
+    ``aff`` the gradient is the stem BatchNorm's pending backward A*g + B*x + C."""
+    g = torch.Generator(device="cpu").manual_seed(N * 3 + k)
+    x = torch.zeros(N, H, H, 8)
+    x[..., :3] = torch.rand(N, H, H, 3, generator=g)
+    x = bf(x.to(DEV))
+    if aff:
+        kc = _bn_case(N, ho, cout, seed=N + 1)
+        gin = kc["dZ"].to(torch.bfloat16)
+        gp = fn.bwd_aff(kc["x"].to(torch.bfloat16), kc["bn"], kc["gsum"], kc["gsumx"])
+        dy = bf(kc["dX"])
+    else:
+        dy = bf(torch.randn(N, ho, ho, cout, generator=g).to(DEV))
+        gin, gp = dy.to(torch.bfloat16), None
+    dw = fn.conv2d_wgrad(x.to(torch.bfloat16), gin, (k, k), stride=(s, s), pads=pads, cin_real=3, gpro=gp)
+    L = (ho - 1) * s + k  # the padded extent the output reads (top/left pad, implicit bottom/right)
+    xr = F.pad(x[..., :3].permute(0, 3, 1, 2), (pads[1], L, pads[0], L))[:, :, :L, :L]
+    ref = torch.nn.grad.conv2d_weight(xr, (cout, 3, k, k), dy.permute(0, 3, 1, 2), stride=s)
+    ref = ref.permute(2, 3, 1, 0)
+    assert dw.shape == (k, k, 3, cout)
+    assert relerr(dw, ref) < 2e-2
 
 
 def test_wgrad_with_bn_prologue(fn):

@@ -35,6 +35,8 @@ SOURCES = [
     "kernels/conv_big.hip",
     "kernels/conv_img.hip",
     "kernels/conv_rows.hip",
+    "kernels/conv_stem.hip",
+    "kernels/wgrad_stem.hip",
     "kernels/conv_wgrad.hip", "kernels/wgrad_big.hip",
     "kernels/nn_kernels.hip",
     "kernels/dwconv.hip",
