@@ -24,6 +24,16 @@ def timeit(f, reps=20):
 
 def main():
     ext = fn.nat.require()
+    only = len(sys.argv) > 1 and sys.argv[1] == "--stem-only"
+    if only:  # (PMC runs: the DenseNet stem shape, the stem kernel only, a few launches)
+        x = torch.zeros(256, 50, 50, 8, device=DEV)
+        x[..., :3] = torch.rand(256, 50, 50, 3, device=DEV)
+        x = x.to(torch.bfloat16)
+        w = torch.randn(7, 7, 8, 64, device=DEV) * 0.05
+        for _ in range(3):
+            fn.conv2d(x, w, stride=(2, 2), pads=(3, 3), out_hw=(25, 25), tile=ext.TILE_STEM)
+        torch.cuda.synchronize()
+        return
     for (N, H, k, s, p, ho, C) in ((256, 50, 7, 2, 3, 25, 64), (256, 50, 3, 1, 1, 50, 64), (256, 50, 3, 2, 0, 25, 32)):
         x = torch.zeros(N, H, H, 8, device=DEV)
         x[..., :3] = torch.rand(N, H, H, 3, device=DEV)
