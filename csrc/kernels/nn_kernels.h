@@ -188,5 +188,6 @@ hipError_t slot_collapse(const float* src, float* dst, const float* src2, float*
 // workgroups of the row-streaming kernels (pool / BN-reduce / BN-apply) for M rows of C channels,
 // `per_thread_rows` rows per thread: one statistics slot per workgroup in the deterministic mode
 int rows_grid(int M, int C, int per_thread_rows);
+int pool_rows_grid(int M, int C, int per_thread_rows);  // the pool kernels' grid (IDC_POOL_GRID_DIV)
 
 }  // namespace idc

@@ -86,7 +86,7 @@ __device__ __forceinline__ void store8(void* base, int f32, size_t off, const fl
   }
 }
 
-inline int grid_rows(int M, int C, int per_thread_rows = 4) {
+inline int grid_rows(int M, int C, int per_thread_rows = 4, int div = 8) {
   int C8 = C / 8;
   int R = 256 / C8;
   if (R < 1) R = 1;
@@ -95,7 +95,7 @@ inline int grid_rows(int M, int C, int per_thread_rows = 4) {
   // round trips of a few us) and then grid-strides over rows: a grid sized for one pass of
   // per_thread_rows rows ran the prologue per ~64 rows (the stem max-pool backward: 2500
   // workgroups, 151 us).  Keep at most max(512, full/8) workgroups (>= 2 per CU).
-  long long blocks = full < 512 ? full : (full + 7) / 8 > 512 ? (full + 7) / 8 : 512;
+  long long blocks = full < 512 ? full : (full + div - 1) / div > 512 ? (full + div - 1) / div : 512;
   if (blocks > 4096) blocks = 4096;
   if (blocks < 1) blocks = 1;
   return (int)blocks;
@@ -425,10 +425,20 @@ __global__ __launch_bounds__(256) void pool_fwd_kernel(PoolArgs a, GroupArg ga) 
                slot_ptr(a.stats, a.stats_slots, 2 * (size_t)a.stats_ld) + a.stats_ld + a.stats_off);
 }
 
+// grid divisor of the pool kernels (grid_rows): IDC_POOL_GRID_DIV, default 8
+static int pool_grid_div() {
+  static const int d = [] {
+    const char* e = std::getenv("IDC_POOL_GRID_DIV");
+    const int v = e ? std::atoi(e) : 8;
+    return v >= 1 ? v : 8;
+  }();
+  return d;
+}
+
 template <bool IS_MAX>
 static hipError_t pool_fwd(const PoolArgs& a, hipStream_t st) {
   // one output row per thread per pass: the k*k taps already give k*k loads in flight
-  const dim3 grid(grid_rows(a.N * a.Ho * a.Wo, a.C, 1)), block(256);
+  const dim3 grid(grid_rows(a.N * a.Ho * a.Wo, a.C, 1, pool_grid_div())), block(256);
   const size_t shm = (4 * a.C + 2 * 256 * 8) * 4;
   if (a.k == 3) hipLaunchKernelGGL((pool_fwd_kernel<IS_MAX, 3>), ggrid(grid), block, shm, st, a, garg());
   else if (a.k == 2) hipLaunchKernelGGL((pool_fwd_kernel<IS_MAX, 2>), ggrid(grid), block, shm, st, a, garg());
@@ -595,7 +605,7 @@ __global__ __launch_bounds__(256) void pool_bwd_kernel(PoolBwdArgs a, GroupArg g
 // input pixel (dZ = g * act'(bn(x)), sums of dZ and dZ*xhat, fp32 gamma*rstd*dZ or bf16 dZ),
 // exactly as the gather form.  Used for the VGG16 max pools (no epilogue) and the DenseNet
 // transition average pools (BN epilogue, fp32 concat-gradient output).
-template <bool AVG, bool EPI>
+template <bool AVG, bool EPI, int K>
 __global__ __launch_bounds__(256) void pool_bwd_scatter_kernel(PoolBwdArgs a, GroupArg ga) {
   prefetch_kernargs<sizeof(PoolBwdArgs) + sizeof(GroupArg)>();
   gshift(a, goff(ga));
@@ -613,11 +623,16 @@ __global__ __launch_bounds__(256) void pool_bwd_scatter_kernel(PoolBwdArgs a, Gr
   }
   const bool sums = EPI && (a.gsum || a.gsumx);
   ChunkMap cm(a.C);
-  const int k = a.k;
+  const int k = K > 0 ? K : a.k;
   const float inv = 1.f / (float)(k * k);
   const float lo = act_lo(a.bn.act), hi = act_hi(a.bn.act);
   const long long Np = (long long)a.N * a.Ho * a.Wo;
   float ps[8] = {0, 0, 0, 0, 0, 0, 0, 0}, px[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  // K > 0: the window is unrolled and every load of it (dy, argmax, the k*k x chunks) is issued
+  // before any arithmetic -- one memory round trip per window instead of k*k dependent ones (the
+  // runtime-bounded loop waited for each x load in turn: the DenseNet transition pools ran at
+  // ~1.5 TB/s, 30 us each)
+  constexpr int KK = K > 0 ? K * K : 1;
   if (cm.active()) {
     const int c = cm.tx * 8;
     for (long long pp = (long long)blockIdx.x * cm.R + cm.ty; pp < Np; pp += (long long)gridDim.x * cm.R) {
@@ -625,31 +640,37 @@ __global__ __launch_bounds__(256) void pool_bwd_scatter_kernel(PoolBwdArgs a, Gr
       const long long t = pp / a.Wo;
       const int ho = (int)(t % a.Ho);
       const int n = (int)(t / a.Ho);
+      const int h0 = ho * k, w0 = wo * k;
       float d[8];
       load8(a.dy, a.dy_f32, (size_t)pp * a.lddy + c, d);
       uint2 am = make_uint2(0, 0);
       if constexpr (!AVG) am = *reinterpret_cast<const uint2*>(a.argmax + (size_t)pp * a.C + c);
-      const int h0 = ho * k, w0 = wo * k;
-      const int h1 = ho == a.Ho - 1 ? a.H : h0 + k;  // the last window row also clears dropped rows
-      const int w1 = wo == a.Wo - 1 ? a.W : w0 + k;
-      for (int h = h0; h < h1; ++h)
-        for (int w = w0; w < w1; ++w) {
-          const size_t pix = (size_t)(n * a.H + h) * a.W + w;
-          const bool in = h < h0 + k && w < w0 + k;
+      uint4 xr[KK];
+      if constexpr (EPI && K > 0) {
+#pragma unroll
+        for (int q = 0; q < KK; ++q)
+          xr[q] = *reinterpret_cast<const uint4*>(a.x + ((size_t)(n * a.H + h0 + q / K) * a.W + w0 + q % K) * a.ldx + c);
+      }
+      // the window's k x k pixels
+#pragma unroll
+      for (int q = 0; q < (K > 0 ? KK : 1); ++q)
+        for (int qq = (K > 0 ? q : 0); qq < (K > 0 ? q + 1 : k * k); ++qq) {
+          const int dh = qq / k, dw = qq - dh * k;
+          const size_t pix = (size_t)(n * a.H + h0 + dh) * a.W + w0 + dw;
           float g[8];
-          const uint8_t pos = (uint8_t)((h - h0) * k + (w - w0));
 #pragma unroll
           for (int j = 0; j < 8; ++j) {
             if constexpr (AVG) {
-              g[j] = in ? d[j] * inv : 0.f;
+              g[j] = d[j] * inv;
             } else {
               const uint32_t word = j < 4 ? am.x : am.y;
-              g[j] = (in && (uint8_t)(word >> (8 * (j & 3))) == pos) ? d[j] : 0.f;
+              g[j] = (uint8_t)(word >> (8 * (j & 3))) == (uint8_t)qq ? d[j] : 0.f;
             }
           }
           if constexpr (EPI) {
             float x[8];
-            unpack8(*reinterpret_cast<const uint4*>(a.x + pix * a.ldx + c), x);
+            if constexpr (K > 0) unpack8(xr[q], x);
+            else unpack8(*reinterpret_cast<const uint4*>(a.x + pix * a.ldx + c), x);
 #pragma unroll
             for (int j = 0; j < 8; ++j) {
               const float z = x[j] * s_sc[c + j] + s_sh[c + j];
@@ -663,9 +684,9 @@ __global__ __launch_bounds__(256) void pool_bwd_scatter_kernel(PoolBwdArgs a, Gr
                 ps[j] += g[j];
                 px[j] += g[j] * (x[j] - s_mu[c + j]) * s_rs[c + j];
               }
-              float* q = reinterpret_cast<float*>(a.dx) + pix * a.lddx + c;
-              *reinterpret_cast<float4*>(q) = make_float4(o[0], o[1], o[2], o[3]);
-              *reinterpret_cast<float4*>(q + 4) = make_float4(o[4], o[5], o[6], o[7]);
+              float* o4 = reinterpret_cast<float*>(a.dx) + pix * a.lddx + c;
+              *reinterpret_cast<float4*>(o4) = make_float4(o[0], o[1], o[2], o[3]);
+              *reinterpret_cast<float4*>(o4 + 4) = make_float4(o[4], o[5], o[6], o[7]);
             } else {
               const uint4 pk = pack8(g);
               *reinterpret_cast<uint4*>(a.dx + pix * a.lddx + c) = pk;
@@ -680,6 +701,25 @@ __global__ __launch_bounds__(256) void pool_bwd_scatter_kernel(PoolBwdArgs a, Gr
             *reinterpret_cast<uint4*>(a.dx + pix * a.lddx + c) = pack8(g);
           }
         }
+      // input rows / columns past the last window (floor pooling, 13 -> 6) get zero gradients
+      // from the threads of the last window row / column: no loads (a zero gradient adds nothing
+      // to the BatchNorm sums, and gamma*rstd*0 = 0 in the fp32 form)
+      if (ho == a.Ho - 1 || wo == a.Wo - 1) {
+        const int h1 = ho == a.Ho - 1 ? a.H : h0 + k;
+        const int w1 = wo == a.Wo - 1 ? a.W : w0 + k;
+        for (int h = h0; h < h1; ++h)
+          for (int w = w0; w < w1; ++w) {
+            if (h < h0 + k && w < w0 + k) continue;
+            const size_t pix = (size_t)(n * a.H + h) * a.W + w;
+            if (EPI && a.dx_f32) {
+              float* o4 = reinterpret_cast<float*>(a.dx) + pix * a.lddx + c;
+              *reinterpret_cast<float4*>(o4) = make_float4(0.f, 0.f, 0.f, 0.f);
+              *reinterpret_cast<float4*>(o4 + 4) = make_float4(0.f, 0.f, 0.f, 0.f);
+            } else {
+              *reinterpret_cast<uint4*>(a.dx + pix * a.lddx + c) = make_uint4(0u, 0u, 0u, 0u);
+            }
+          }
+      }
     }
   }
   if (sums) {
@@ -715,22 +755,26 @@ hipError_t pool_bwd(const PoolBwdArgs& a, hipStream_t st) {
     if (blocks < 1) return hipSuccess;
     const bool epi = a.bn.mode != 0 || a.bn.act != ACT_NONE;
     const size_t shm_s = epi ? (9 * (size_t)a.C + 2 * 256 * 8) * 4 : 0;
+#define IDC_PS(AV, EP)                                                                                      \
+  if (a.k == 2)                                                                                             \
+    hipLaunchKernelGGL((pool_bwd_scatter_kernel<AV, EP, 2>), ggrid((int)blocks), dim3(256), shm_s, st, a, garg()); \
+  else                                                                                                      \
+    hipLaunchKernelGGL((pool_bwd_scatter_kernel<AV, EP, 0>), ggrid((int)blocks), dim3(256), shm_s, st, a, garg());
     if (a.is_avg) {
-      if (epi) hipLaunchKernelGGL((pool_bwd_scatter_kernel<true, true>), ggrid((int)blocks), dim3(256), shm_s, st, a, garg());
-      else hipLaunchKernelGGL((pool_bwd_scatter_kernel<true, false>), ggrid((int)blocks), dim3(256), shm_s, st, a, garg());
+      if (epi) { IDC_PS(true, true) } else { IDC_PS(true, false) }
     } else {
-      if (epi) hipLaunchKernelGGL((pool_bwd_scatter_kernel<false, true>), ggrid((int)blocks), dim3(256), shm_s, st, a, garg());
-      else hipLaunchKernelGGL((pool_bwd_scatter_kernel<false, false>), ggrid((int)blocks), dim3(256), shm_s, st, a, garg());
+      if (epi) { IDC_PS(false, true) } else { IDC_PS(false, false) }
     }
+#undef IDC_PS
     return hipGetLastError();
   }
   if (a.dyaff.mode != 0 && (a.dyaff.x == nullptr || (a.dyaff.ldx % 8))) return hipErrorInvalidValue;
   const size_t shm = (9 * a.C + 2 * 256 * 8) * 4;
   const int M = a.N * a.H * a.W;
   if (a.k <= a.s) {
-    hipLaunchKernelGGL((pool_bwd_kernel<1, 4>), ggrid(dim3(grid_rows(M, a.C, 4))), dim3(256), shm, st, a, garg());
+    hipLaunchKernelGGL((pool_bwd_kernel<1, 4>), ggrid(dim3(grid_rows(M, a.C, 4, pool_grid_div()))), dim3(256), shm, st, a, garg());
   } else if (a.k <= 2 * a.s) {
-    hipLaunchKernelGGL((pool_bwd_kernel<2, 2>), ggrid(dim3(grid_rows(M, a.C, 2))), dim3(256), shm, st, a, garg());
+    hipLaunchKernelGGL((pool_bwd_kernel<2, 2>), ggrid(dim3(grid_rows(M, a.C, 2, pool_grid_div()))), dim3(256), shm, st, a, garg());
   } else {
     return hipErrorInvalidValue;  // windows overlapping more than 2 per dim: not used by any model
   }
@@ -1356,5 +1400,6 @@ hipError_t slot_collapse(const float* src, float* dst, const float* src2, float*
 }
 
 int rows_grid(int M, int C, int per_thread_rows) { return grid_rows(M, C, per_thread_rows); }
+int pool_rows_grid(int M, int C, int per_thread_rows) { return grid_rows(M, C, per_thread_rows, pool_grid_div()); }
 
 }  // namespace idc

@@ -1068,6 +1068,7 @@ PYBIND11_MODULE(_idc_native, m) {
   m.def("wgrad_batch_pack", &py_wgrad_batch_pack);
   m.attr("WG_BATCH_MAX") = WG_BATCH_MAX;
   m.def("rows_grid", &rows_grid);
+  m.def("pool_rows_grid", &pool_rows_grid);
   m.def("num_tiles", &conv_num_tiles);
   m.def("tile_bm", &conv_tile_bm);
   m.def("tile_bn", &conv_tile_bn);

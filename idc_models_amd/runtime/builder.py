@@ -387,6 +387,12 @@ class Builder:
     def _rows_grid(self, M: int, C: int, per: int) -> int:
         return int(nat.load().rows_grid(int(M), int(C), int(per)))
 
+    def _pool_grid(self, M: int, C: int, per: int) -> int:
+        """Grid of the pool kernels (nn_kernels.hip pool_grid_div, IDC_POOL_GRID_DIV)."""
+        ext = nat.load()
+        f = getattr(ext, "pool_rows_grid", None)
+        return int(f(int(M), int(C), int(per)) if f is not None else ext.rows_grid(int(M), int(C), int(per)))
+
     def mark_grads_ready(self, params):
         """Backward has finished producing the grads of ``params`` (for DP bucket overlap).
         While batched weight gradients are pending, the mark waits for their launch."""
@@ -1016,7 +1022,7 @@ class Builder:
             a.stats_shift = stats.shift_ptr(stats_off)
             if self.det:
                 a.stats, a.stats_ld, a.stats_off, a.stats_slots = self._det_stats_slots(
-                    x.C, self._rows_grid(x.N * y.H * y.W, x.C, 1), stats, stats_off)
+                    x.C, self._pool_grid(x.N * y.H * y.W, x.C, 1), stats, stats_off)
         self.emit(nat.OP_MAXPOOL if is_max else nat.OP_AVGPOOL, a)
 
     def pool_bwd(self, dy: Tensor4, dx: Tensor4, *, k, s, pt=0, pl=0, is_max=True, argmax=None,
@@ -1038,7 +1044,7 @@ class Builder:
             a.x, a.ldx = x.ptr, x.ld
             a.bn = bn.args() if bn is not None else act_only(act)
             if bn is not None:
-                grid = self._rows_grid(dx.M, dx.C, 4 if k <= s else 2) if self.det else 0
+                grid = self._pool_grid(dx.M, dx.C, 4 if k <= s else 2) if self.det else 0
                 a.gsum, a.gsumx, a.gsum_slots, a.gsum_ld = self.grad_sums(bn, dx.M, grid)
         else:
             a.bn = act_only(0)

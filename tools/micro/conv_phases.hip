@@ -5,6 +5,7 @@
 #include <hip/hip_runtime.h>
 #include <algorithm>
 #include <cstdio>
+#include <cstdlib>
 #include <vector>
 
 __device__ unsigned long long g_stamps[4096][16];
@@ -13,6 +14,7 @@ __device__ unsigned long long g_stamps[4096][16];
     if (threadIdx.x == 0 && blockIdx.x < 4096) g_stamps[blockIdx.x][i] = __builtin_amdgcn_s_memtime(); \
   } while (0)
 #include "conv_igemm_impl.h"
+#include "conv_rows.hip"
 
 using namespace idc;
 namespace idc {
@@ -93,6 +95,46 @@ static void run_case(const Case& c) {
         if (h[b][i] >= h[b][0] && h[b][i] - h[b][0] < 1000000) ph[i].push_back((long long)(h[b][i] - h[b][0]));
     }
   }
+  // kernel span and per-workgroup lifetime (entry -> end stamp) of the last launch
+  {
+    static unsigned long long h[4096][16];
+    hipMemcpyFromSymbol(h, HIP_SYMBOL(g_stamps), sizeof(h));
+    const int tiles = std::min(4096, ((M + BM - 1) / BM) * ((c.Cout + BN - 1) / BN));
+    unsigned long long t0 = ~0ull, t1 = 0;
+    std::vector<long long> life;
+    for (int b = 0; b < tiles; ++b) {
+      if (!h[b][0] || !h[b][10]) continue;
+      t0 = std::min(t0, h[b][0]);
+      t1 = std::max(t1, h[b][10]);
+      life.push_back((long long)(h[b][10] - h[b][0]));
+    }
+    if (!life.empty()) {
+      long long sum = 0;
+      for (long long v : life) sum += v;
+      std::nth_element(life.begin(), life.begin() + life.size() / 2, life.end());
+      printf("%-34s span=%llu cycles (at 2.4 GHz: %.1f us)  WG life median=%lld  mean concurrency=%.1f WGs\n", c.name,
+             t1 - t0, (t1 - t0) / 2400.0, life[life.size() / 2], (double)sum / (double)(t1 - t0));
+    }
+  }
+  hipEvent_t e0, e1;
+  hipEventCreate(&e0);
+  hipEventCreate(&e1);
+  hipEventRecord(e0, st);
+  for (int r = 0; r < 20; ++r) launch_cfg<BM, BN, BK, WM, WN>(a, true, c.a_f32, c.pro, c.epi, st);
+  hipEventRecord(e1, st);
+  hipEventSynchronize(e1);
+  float ms = 0.f;
+  hipEventElapsedTime(&ms, e0, e1);
+  printf("%-34s back-to-back %.2f us/launch\n", c.name, ms * 1000.f / 20);
+  if (c.pro == 2 && c.epi == 2 && conv_rows_ok(a, false)) {  // the row-block kernel on the same op
+    conv_rows(a, false, st);
+    hipEventRecord(e0, st);
+    for (int r = 0; r < 20; ++r) conv_rows(a, false, st);
+    hipEventRecord(e1, st);
+    hipEventSynchronize(e1);
+    hipEventElapsedTime(&ms, e0, e1);
+    printf("%-34s conv_rows back-to-back %.2f us/launch\n", c.name, ms * 1000.f / 20);
+  }
   printf("%-34s tiles=%d  cycles since entry (median over WGs x launches):", c.name,
          ((M + BM - 1) / BM) * ((c.Cout + BN - 1) / BN));
   const char* lbl[] = {"", "tiles_issued", "pro_tab", "epi2_tab", "epi_tab", "ep_prefetch", "loop_start", "loop_end",
@@ -108,6 +150,13 @@ static void run_case(const Case& c) {
 }
 
 int main() {
+  // DenseNet-121 bs256 concat-gradient dgrads (cv1, PRO 2 + EPI 2) of stages 1 / 2
+  run_case<64, 64, 32, 2, 2>({"bwd s1 dg1 pro2 epi2 K128 N224 t3", 43264, 128, 224, 2, 2, 0, 0});
+  run_case<64, 64, 32, 2, 2>({"bwd s1 dg1 pro2 epi2 K128 N64 t3", 43264, 128, 64, 2, 2, 0, 0});
+  run_case<128, 32, 64, 4, 1>({"bwd s1 dg1 pro2 epi2 K128 N64 t7", 43264, 128, 64, 2, 2, 0, 0});
+  run_case<64, 64, 32, 2, 2>({"bwd s2 dg1 pro2 epi2 K128 N480 t3", 9216, 128, 480, 2, 2, 0, 0});
+  run_case<64, 64, 64, 2, 2>({"bwd s2 dg1 pro2 epi2 K128 N480 t8", 9216, 128, 480, 2, 2, 0, 0});
+  if (getenv("IDC_PHASES_DG_ONLY")) return 0;
   // DenseNet-121 bs256 stage-1/2 1x1 shapes (M = 43264 / 9216)
   run_case<256, 32, 32, 4, 1>({"fwd s1 1x1 pro1 epi0 K64 t2", 43264, 64, 128, 1, 0, 0, 0});
   run_case<64, 32, 64, 2, 2>({"fwd s1 1x1 pro1 epi0 K64 t9", 43264, 64, 128, 1, 0, 0, 0});
