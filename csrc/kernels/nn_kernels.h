@@ -160,6 +160,11 @@ __device__ __forceinline__ void gshift(CastEntry& a, long long o) {
 hipError_t bn_bwd_apply(const BnBwdApplyArgs& a, hipStream_t st);
 hipError_t bn_bwd_reduce(const BnBwdReduceArgs& a, hipStream_t st);
 hipError_t maxpool_fwd(const PoolArgs& a, hipStream_t st);
+// image-resident overlapping max pool (pool_img.hip): one workgroup per image x 16 channels
+bool maxpool_img_fwd_ok(const PoolArgs& a);
+bool maxpool_img_bwd_ok(const PoolBwdArgs& a);
+hipError_t maxpool_img_fwd(const PoolArgs& a, hipStream_t st);
+hipError_t maxpool_img_bwd(const PoolBwdArgs& a, hipStream_t st);
 hipError_t avgpool_fwd(const PoolArgs& a, hipStream_t st);
 hipError_t pool_bwd(const PoolBwdArgs& a, hipStream_t st);
 hipError_t bn_update_moving(const BnMovingDesc* d_descs, int n, int maxC, hipStream_t st);

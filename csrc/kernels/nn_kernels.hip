@@ -446,7 +446,10 @@ static hipError_t pool_fwd(const PoolArgs& a, hipStream_t st) {
   return hipGetLastError();
 }
 
-hipError_t maxpool_fwd(const PoolArgs& a, hipStream_t st) { return pool_fwd<true>(a, st); }
+hipError_t maxpool_fwd(const PoolArgs& a, hipStream_t st) {
+  if (maxpool_img_fwd_ok(a)) return maxpool_img_fwd(a, st);
+  return pool_fwd<true>(a, st);
+}
 
 hipError_t avgpool_fwd(const PoolArgs& a, hipStream_t st) { return pool_fwd<false>(a, st); }
 
@@ -769,6 +772,7 @@ hipError_t pool_bwd(const PoolBwdArgs& a, hipStream_t st) {
     return hipGetLastError();
   }
   if (a.dyaff.mode != 0 && (a.dyaff.x == nullptr || (a.dyaff.ldx % 8))) return hipErrorInvalidValue;
+  if (maxpool_img_bwd_ok(a)) return maxpool_img_bwd(a, st);
   const size_t shm = (9 * a.C + 2 * 256 * 8) * 4;
   const int M = a.N * a.H * a.W;
   if (a.k <= a.s) {

@@ -59,10 +59,11 @@ def stat_slots_for(rows: int) -> int:
     """Statistics slot copies for a reduction over ``rows`` rows (csrc/kernels/common.h,
     "Statistics slots"): global float atomics serialise per address at ~24 ns each, so producers
     with many row blocks spread their per-channel adds over copies that consumers sum.  About
-    one copy per 4096 rows keeps every address under ~70 adds (block-1 DenseNet convs: 676 row
-    tiles -> 16 copies, ~42 adds each) while a consumer's table read stays <= 32 x C floats."""
+    one copy per 4096 rows, at most IDC_STAT_SLOTS_CAP (default 4) copies: the consumers' batched
+    table loads take <= 4 copies (common.h "Batched table inputs")."""
+    cap = max(1, min(16, int(os.environ.get("IDC_STAT_SLOTS_CAP", "4"))))
     s = 1
-    while s < 16 and s * 4096 < rows:
+    while s < cap and s * 4096 < rows:
         s *= 2
     return s
 
@@ -181,12 +182,15 @@ class Builder:
         self.segment = "fwd"
         self.side_lane = os.environ.get("IDC_SIDE_LANE", "1") != "0"
         self.guard = os.environ.get("IDC_GUARD") == "1"
-        # statistics slots (stat_slots_for): opt-in (IDC_STAT_SLOTS=1).  Spreading the per-channel
-        # adds over copies paid while the statistics were plain sums; with the shifted statistics,
-        # the batched table loads and the consumer-applied BN backward, single-copy reductions
-        # measured faster on DenseNet-121 (4.31 vs 4.36-4.43 ms/step, repeated A/B) and neutral on
-        # MobileNetV2
-        self.stat_slots_on = os.environ.get("IDC_STAT_SLOTS", "0") == "1"
+        # statistics slots (stat_slots_for, default on; IDC_STAT_SLOTS=0: one copy everywhere).
+        # Every workgroup of a large-map producer adds its per-channel sums into the same few
+        # addresses, and float atomics on one address serialise at the memory side (a 676-tile
+        # stage-1 concat-gradient dgrad: 28.3 us with one copy, 17.0 us with 4, conv phase micro,
+        # round 5).  At most 4 copies (IDC_STAT_SLOTS_CAP): consumers then keep the one-round-trip
+        # batched table loads (common.h "Batched table inputs").  bench.py A/B on one box, round 5:
+        # DenseNet-121 3.53-3.55 ms/step with 4 copies vs 3.64-3.67 with one (2 copies 3.64-3.66,
+        # 8 copies 3.65); MobileNetV2 2.26 vs 2.32; VGG16 2.40 either way.
+        self.stat_slots_on = os.environ.get("IDC_STAT_SLOTS", "1") == "1"
         self.pending_sums: List["BNRef"] = []  # BatchNorms whose gradient slot copies await a fold
         # IDC_DETERMINISTIC=1: every float reduction has a fixed order (see _det_* below); the
         # same program on the same inputs then produces the same bits run after run

@@ -51,6 +51,9 @@ def lower_mobilenet(b: Builder, net, U: int, input_dtype):
     L = {l.name: l for l in base.layers}
     H, W, Cimg = base.input_shape
     io = HeadIO(b, U)
+    from .mb_chain import chain_enabled as _chain_on
+    if _chain_on(b):
+        b.stat_slots_on = False  # the chain keeps its own slot copies over single-copy statistics
 
     # ------------------------------------------------------------------ forward
     b.segment = "fwd"

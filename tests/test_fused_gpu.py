@@ -236,8 +236,8 @@ def test_tinycnn_fused_dropout_trains_and_eval_is_deterministic():
                                         ("mobilenetv2", "0"), ("mobilenetv2", "1")])
 def test_fused_matches_eager_at_bench_batch(monkeypatch, arch, slots):
     """The benchmarked configuration, bs=256: the autotuner's tile and split-K choices, the
-    full-size workspaces and both statistics layouts (single copy, the default; IDC_STAT_SLOTS=1:
-    16 slot copies on the large maps) — not only the small test batches."""
+    full-size workspaces and both statistics layouts (slot copies on the large maps, the default;
+    IDC_STAT_SLOTS=0: one copy) — not only the small test batches."""
     monkeypatch.setenv("IDC_STAT_SLOTS", slots)
     m, ref, x, y = _setup(arch, 256)
     _check(m, ref, x, y)

@@ -39,6 +39,7 @@ SOURCES = [
     "kernels/wgrad_stem.hip",
     "kernels/conv_wgrad.hip", "kernels/wgrad_big.hip",
     "kernels/nn_kernels.hip",
+    "kernels/pool_img.hip",
     "kernels/dwconv.hip",
     "kernels/dense_stage.hip",
     "kernels/mb_chain.hip",

@@ -50,6 +50,7 @@ static void run_case(const Case& c) {
   float* gam = (float*)dalloc(1 << 16);
   a.ksplit = 1;
   a.stats_slots = a.gsum_slots = 1;
+  if (const char* e = getenv("IDC_MICRO_GSUM_SLOTS")) a.gsum_slots = atoi(e);  // epilogue sum copies
   a.gsum_ld = c.Cout;
   if (c.pro == 1) {
     a.pro = BnArgs{stats, gam, gam, nullptr, nullptr, 1.f / M, 1e-3f, 1, 1, c.Cin, 1};
