@@ -330,6 +330,8 @@ def test_dense_stage_matches_per_layer(monkeypatch, B, maxm):
     from idc_models_amd.models import build_model
     from idc_models_amd.ops import _native as nat
     from idc_models_amd.utils.fidelity import grad_failures
+    if maxm == "9216":  # the launch takes single-copy statistics; stage 2's default to 4 copies
+        monkeypatch.setenv("IDC_STAT_SLOTS", "0")
     g = torch.Generator().manual_seed(5)
     x = torch.randint(0, 256, (B, 50, 50, 3), generator=g, dtype=torch.uint8)
     y = torch.randint(0, 2, (B,), generator=g)
