@@ -79,6 +79,13 @@ def _compile(src: str, extra) -> str:
     cmd = [HIPCC, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-c", s, "-o", o,
            f"-I{pybind11.get_include()}", f"-I{sysconfig.get_paths()['include']}",
            "-Wno-unused-result", "-Wno-unused-variable"]
+    # MFMA accumulators in the VGPR form: without it the register allocator keeps them in AGPRs ON
+    # TOP of the kernel's VGPRs (unified register file), one occupancy step below what the kernel
+    # needs -- e.g. the DenseNet concat-gradient dgrad tile 126 VGPRs + 16 AGPRs = 3 waves/SIMD,
+    # 4 with this flag; 46 of the 552 conv tiles and the image-resident 3x3 data gradients (1 -> 2,
+    # 2 -> 4 waves) gain, none spills (tools/kernel_resources.py, round 5)
+    if not src.endswith(".cpp"):
+        cmd += ["-mllvm", "-amdgpu-mfma-vgpr-form"]
     if src.endswith(".cpp"):
         cmd += ["-x", "hip"]
     r = subprocess.run(cmd, capture_output=True, text=True)

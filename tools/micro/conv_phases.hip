@@ -9,9 +9,14 @@
 #include <vector>
 
 __device__ unsigned long long g_stamps[4096][16];
+__device__ unsigned long long g_rt[4096][2];  // s_memrealtime (100 MHz, chip-wide) at entry / end
 #define IDC_PHASE_STAMP(i)                                                                  \
   do {                                                                                      \
-    if (threadIdx.x == 0 && blockIdx.x < 4096) g_stamps[blockIdx.x][i] = __builtin_amdgcn_s_memtime(); \
+    if (threadIdx.x == 0 && blockIdx.x < 4096) {                                            \
+      g_stamps[blockIdx.x][i] = __builtin_amdgcn_s_memtime();                               \
+      if ((i) == 0) g_rt[blockIdx.x][0] = __builtin_amdgcn_s_memrealtime();                 \
+      if ((i) == 10) g_rt[blockIdx.x][1] = __builtin_amdgcn_s_memrealtime();                \
+    }                                                                                       \
   } while (0)
 #include "conv_igemm_impl.h"
 #include "conv_rows.hip"
@@ -96,25 +101,32 @@ static void run_case(const Case& c) {
         if (h[b][i] >= h[b][0] && h[b][i] - h[b][0] < 1000000) ph[i].push_back((long long)(h[b][i] - h[b][0]));
     }
   }
-  // kernel span and per-workgroup lifetime (entry -> end stamp) of the last launch
+  // kernel span and per-workgroup lifetime (entry -> end, s_memrealtime: 100 MHz, chip-wide) of
+  // the last launch; start-time deciles show how fast workgroups get a slot
   {
-    static unsigned long long h[4096][16];
-    hipMemcpyFromSymbol(h, HIP_SYMBOL(g_stamps), sizeof(h));
+    static unsigned long long h[4096][2];
+    hipMemcpyFromSymbol(h, HIP_SYMBOL(g_rt), sizeof(h));
     const int tiles = std::min(4096, ((M + BM - 1) / BM) * ((c.Cout + BN - 1) / BN));
     unsigned long long t0 = ~0ull, t1 = 0;
-    std::vector<long long> life;
+    std::vector<long long> life, starts;
     for (int b = 0; b < tiles; ++b) {
-      if (!h[b][0] || !h[b][10]) continue;
+      if (!h[b][0] || !h[b][1] || h[b][1] < h[b][0]) continue;
       t0 = std::min(t0, h[b][0]);
-      t1 = std::max(t1, h[b][10]);
-      life.push_back((long long)(h[b][10] - h[b][0]));
+      t1 = std::max(t1, h[b][1]);
+      life.push_back((long long)(h[b][1] - h[b][0]));
+      starts.push_back((long long)h[b][0]);
     }
     if (!life.empty()) {
       long long sum = 0;
       for (long long v : life) sum += v;
-      std::nth_element(life.begin(), life.begin() + life.size() / 2, life.end());
-      printf("%-34s span=%llu cycles (at 2.4 GHz: %.1f us)  WG life median=%lld  mean concurrency=%.1f WGs\n", c.name,
-             t1 - t0, (t1 - t0) / 2400.0, life[life.size() / 2], (double)sum / (double)(t1 - t0));
+      std::sort(life.begin(), life.end());
+      std::sort(starts.begin(), starts.end());
+      const size_t n = life.size();
+      printf("%-34s span=%.1f us  WG life p10/p50/p90/max=%.1f/%.1f/%.1f/%.1f us  mean concurrency=%.0f WGs  start "
+             "deciles(us):", c.name, (t1 - t0) / 100.0, life[n / 10] / 100.0, life[n / 2] / 100.0,
+             life[n * 9 / 10] / 100.0, life[n - 1] / 100.0, (double)sum / (double)(t1 - t0));
+      for (int d = 1; d <= 9; ++d) printf(" %.1f", (starts[n * d / 10] - t0) / 100.0);
+      printf("\n");
     }
   }
   hipEvent_t e0, e1;
