@@ -139,6 +139,8 @@ static void run_case(const Case& c) {
   float ms = 0.f;
   hipEventElapsedTime(&ms, e0, e1);
   printf("%-34s back-to-back %.2f us/launch\n", c.name, ms * 1000.f / 20);
+  a.epi_mode = c.epi;
+  if (c.pro == 2 && c.epi == 2 && !conv_rows_ok(a, false)) printf("%-34s conv_rows not eligible\n", c.name);
   if (c.pro == 2 && c.epi == 2 && conv_rows_ok(a, false)) {  // the row-block kernel on the same op
     conv_rows(a, false, st);
     hipEventRecord(e0, st);
