@@ -244,3 +244,26 @@ def test_mb_chain_lowering(monkeypatch):
     part = lower(IDC_MB_CHAIN="1", IDC_MB_CHAIN_FROM="10")
     d10 = [op for op in part.ops if op[1] == nat.OP_MB_CHAIN]
     assert len(d10) == 1 and d10[0][3][2] == 1 + 3 * 7  # TAB of block 9's project BN + blocks 10-16
+
+
+def test_stat_slot_copies_default_and_cap(monkeypatch):
+    """Large-map reductions keep statistics slot copies by default, at most 4 (the consumers'
+    batched table loads take <= 4: builder.stat_slots_for); IDC_STAT_SLOTS_CAP moves the cap and
+    IDC_STAT_SLOTS=0 keeps one copy everywhere."""
+    from idc_models_amd.runtime.builder import stat_slots_for
+    monkeypatch.delenv("IDC_STAT_SLOTS_CAP", raising=False)
+    assert [stat_slots_for(r) for r in (256, 2304, 4096, 9216, 43264, 160000)] == [1, 1, 1, 4, 4, 4]
+    monkeypatch.setenv("IDC_STAT_SLOTS_CAP", "16")
+    assert stat_slots_for(43264) == 16 and stat_slots_for(9216) == 4
+    monkeypatch.delenv("IDC_STAT_SLOTS_CAP")
+
+    def slots(**env):
+        for k, v in env.items():
+            monkeypatch.setenv(k, v)
+        _, _, b = _lower("densenet121", None, True, B=256)
+        for k in env:
+            monkeypatch.delenv(k)
+        return sorted({s.slots for s in b.all_stats}), sum(1 for s in b.all_stats if s.slots > 1)
+    (kinds, n_on), (kinds_off, n_off) = slots(), slots(IDC_STAT_SLOTS="0")
+    assert kinds == [1, 4]  # stages 3-4 one copy; stages 1-2, the stem and the transitions 4
+    assert n_off == 1 and n_on > 1  # off: only the stem conv's reduction (always slotted) keeps copies
