@@ -539,12 +539,18 @@ __device__ __forceinline__ void bwd_aff_table(const BwdAff& b, int c0, int n, in
 // round trips before its K loop (tools/micro/conv_phases.hip: ~6k shader cycles for the prologue
 // table alone).  Here every load of every table a thread builds is issued first (4 clamped slot
 // loads per array, unconditional), then everything is combined: one round trip.
+#ifndef IDC_BATCH_SLOTS
+#define IDC_BATCH_SLOTS 4
+#endif
+// slot copies the batched loads take: 8 (-DIDC_BATCH_SLOTS=8) costs 20-40 registers in the
+// backward conv tiles and one occupancy step on 32 of them (tools/kernel_resources.py, round 5)
+constexpr int BATCH_SLOTS = IDC_BATCH_SLOTS;
 struct Raw4 {
-  float a0[4], a1[4];
+  float a0[BATCH_SLOTS], a1[BATCH_SLOTS];
 };
 __device__ __forceinline__ void load4(const float* p0, const float* p1, int S, size_t stride, int c, Raw4& r) {
 #pragma unroll
-  for (int s = 0; s < 4; ++s) {
+  for (int s = 0; s < BATCH_SLOTS; ++s) {
     const size_t o = (size_t)(s < S ? s : S - 1) * stride + c;
     r.a0[s] = p0[o];
     r.a1[s] = p1[o];
@@ -554,14 +560,15 @@ __device__ __forceinline__ void sum4(const Raw4& r, int S, float& v0, float& v1)
   v0 = r.a0[0];
   v1 = r.a1[0];
 #pragma unroll
-  for (int s = 1; s < 4; ++s) {
+  for (int s = 1; s < BATCH_SLOTS; ++s) {
     v0 += s < S ? r.a0[s] : 0.f;
     v1 += s < S ? r.a1[s] : 0.f;
   }
 }
-__device__ __forceinline__ bool bn_slots4(const BnArgs& b) { return b.mode != 1 || stat_slots(b.slots) <= 4; }
+__device__ __forceinline__ bool bn_slots4(const BnArgs& b) { return b.mode != 1 || stat_slots(b.slots) <= BATCH_SLOTS; }
 __device__ __forceinline__ bool bwd_aff_slots4(const BwdAff& b) {
-  return b.mode == 0 || b.bn.mode != 1 || (stat_slots(b.bn.slots) <= 4 && stat_slots(b.gsum_slots) <= 4);
+  return b.mode == 0 || b.bn.mode != 1 ||
+         (stat_slots(b.bn.slots) <= BATCH_SLOTS && stat_slots(b.gsum_slots) <= BATCH_SLOTS);
 }
 
 // raw inputs of one channel of a BwdAff table (training-mode BatchNorm, <= 4 slots)
