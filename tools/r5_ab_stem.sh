@@ -1,0 +1,14 @@
+#!/bin/bash
+# stem weight-gradient A/B (interleaved, 2 rounds)
+cd "$GRAFT_REPO_ROOT" || exit 1
+mkdir -p gpurun_out/r5
+run() {
+  local tag=$1; shift
+  env "$@" timeout -k 10 200 python bench.py --steps 30 --warmup 10 > gpurun_out/r5/b_stem_$tag.txt 2>&1 || { tail -5 gpurun_out/r5/b_stem_$tag.txt; exit 1; }
+  echo "$tag $(tail -1 gpurun_out/r5/b_stem_$tag.txt | python -c 'import json,sys; d=json.loads(sys.stdin.read()); print(d["ms_per_step"], d["value"])')"
+}
+for r in 1 2; do
+  run base$r IDC_X=0
+  run ws$r IDC_WGRAD_STEM=1
+  run side$r IDC_STEM_SIDE=1
+done
