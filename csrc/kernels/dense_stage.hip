@@ -228,12 +228,15 @@ __global__ __launch_bounds__(NT) void dense_stage_kernel(DenseStageArgs a, Group
         if (__builtin_amdgcn_readfirstlane(s.bad)) return;
       }
       stamp(stamps, task, 1);
-      const int srow = m0 + (tid >> 3), sseg = (tid & 7) * 32;  // staging: a row, 32 channels
+      // staging: 8 threads per row, thread piece u at channels ((tid & 7) + 8u) * 8 -- each
+      // wave-level access covers 128 contiguous bytes of a row (a 32-channel run per thread wrote
+      // 16-B pieces at a 64-B stride: 2-way LDS bank conflicts, half-line global loads)
+      const int srow = m0 + (tid >> 3), sseg = (tid & 7) * 8;
       uint4 ar[4];
       auto load_a = [&](int ch) {
 #pragma unroll
         for (int u = 0; u < 4; ++u) {
-          const int c = ch * ACH + sseg + u * 8;
+          const int c = ch * ACH + sseg + u * 64;
           ar[u] = (srow < M && c < cold) ? ld_coh16(buf + (size_t)srow * a.ld + c) : make_uint4(0, 0, 0, 0);
         }
       };
@@ -248,10 +251,10 @@ __global__ __launch_bounds__(NT) void dense_stage_kernel(DenseStageArgs a, Group
         bf16_t* ab = s.u.a[ch & 1] + (tid >> 3) * APITCH + sseg;
 #pragma unroll
         for (int u = 0; u < 4; ++u) {
-          const int c = ch * ACH + sseg + u * 8;
+          const int c = ch * ACH + sseg + u * 64;
           const bool keep = srow < M && c < cold;
           const int cc = keep ? c : 0;
-          *reinterpret_cast<v8bf*>(ab + u * 8) = bn_act8(ar[u], s.sc + cc, s.sh + cc, lo1, hi1, keep);
+          *reinterpret_cast<v8bf*>(ab + u * 64) = bn_act8(ar[u], s.sc + cc, s.sh + cc, lo1, hi1, keep);
         }
       };
       auto mfma_chunk = [&](int ch, const v8bf (&bq)[8]) {
