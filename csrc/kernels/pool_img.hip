@@ -1,5 +1,6 @@
 // Image-resident overlapping max pool, gfx950: DenseNet's stem pool (3x3 / 2, pad 1, 25x25 -> 13x13
-// on 50x50 patches), forward and backward.
+// on 50x50 patches; Keras DenseNet121's pool1 after ZeroPadding2D, which the reference builds through
+// keras.applications in /root/reference/dist_model_tf_dense.py), forward and backward.
 //
 // The row kernels (nn_kernels.hip pool_fwd_kernel / pool_bwd_kernel) give every thread one
 // 8-channel chunk of a few pixels and grid-stride over the map: the forward re-reads each input
