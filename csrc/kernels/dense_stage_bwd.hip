@@ -43,6 +43,10 @@ namespace {
 using namespace persist;
 
 constexpr int NT = 256;
+// a lane's 16 channels of a 128-channel row are two 8-channel pieces 64 apart: each wave-level
+// access then covers 128 contiguous bytes of the 8-lane row group (16 consecutive channels per
+// lane put the pieces at a 32-B stride: half-line accesses, 2-way LDS bank conflicts)
+constexpr int ESEG2 = 64;
 constexpr int S = DS_SLOTS;
 constexpr int DPITCH = 32 + 8;  // staged dY rows (bf16)
 constexpr int TP = 128 + 8;     // staged dT rows (bf16)
@@ -216,11 +220,11 @@ __global__ __launch_bounds__(NT) void dense_stage_bwd_kernel(DenseBwdArgs a, Gro
         s.tab[2][tid] = mean;
         s.tab[3][tid] = rstd;
       }
-      const int er = tid >> 3, eseg = (tid & 7) * 16, em = m0 + er;
+      const int er = tid >> 3, eseg = (tid & 7) * 8, em = m0 + er;  // pieces eseg, eseg + 64 (ESEG2)
       uint4 tv0 = make_uint4(0, 0, 0, 0), tv1 = tv0;
       if (em < M) {
         tv0 = *reinterpret_cast<const uint4*>(tb + (size_t)em * 128 + eseg);
-        tv1 = *reinterpret_cast<const uint4*>(tb + (size_t)em * 128 + eseg + 8);
+        tv1 = *reinterpret_cast<const uint4*>(tb + (size_t)em * 128 + eseg + ESEG2);
       }
       const int mend = min(m0 + 32, M);
       const int img_lo = m0 / HW, img_hi = (mend - 1) / HW;
@@ -347,7 +351,7 @@ __global__ __launch_bounds__(NT) void dense_stage_bwd_kernel(DenseBwdArgs a, Gro
         const bool okm = em < M;
 #pragma unroll
         for (int q = 0; q < 16; ++q) {
-          const int c = eseg + q;
+          const int c = eseg + q + (q >= 8 ? ESEG2 - 8 : 0);
           const float dA = s.u.p.r0[er * RP + c];
           const float z = s.tab[0][c] * tvf[q] + s.tab[1][c];
           dz[q] = (okm && z > lo && z < hi) ? dA : 0.f;
@@ -357,7 +361,7 @@ __global__ __launch_bounds__(NT) void dense_stage_bwd_kernel(DenseBwdArgs a, Gro
         }
         if (okm) {
           st_coh16(z2 + (size_t)em * 128 + eseg, pack8(dz));
-          st_coh16(z2 + (size_t)em * 128 + eseg + 8, pack8(dz + 8));
+          st_coh16(z2 + (size_t)em * 128 + eseg + ESEG2, pack8(dz + 8));
         }
       }
       __syncthreads();
@@ -398,11 +402,11 @@ __global__ __launch_bounds__(NT) void dense_stage_bwd_kernel(DenseBwdArgs a, Gro
         s.tab[2][i] = mean;
         s.tab[3][i] = rstd;
       }
-      const int er = tid >> 3, eseg = (tid & 7) * 16, em = m0 + er;
+      const int er = tid >> 3, eseg = (tid & 7) * 8, em = m0 + er;  // pieces eseg, eseg + 64 (ESEG2)
       uint4 tv0 = make_uint4(0, 0, 0, 0), tv1 = tv0;
       if (em < M) {
         tv0 = *reinterpret_cast<const uint4*>(tb + (size_t)em * 128 + eseg);
-        tv1 = *reinterpret_cast<const uint4*>(tb + (size_t)em * 128 + eseg + 8);
+        tv1 = *reinterpret_cast<const uint4*>(tb + (size_t)em * 128 + eseg + ESEG2);
       }
       // epilogue rows of this lane: 2 rows per wave instruction, 32 channels each
       const int ech = lane & 31;
@@ -417,7 +421,7 @@ __global__ __launch_bounds__(NT) void dense_stage_bwd_kernel(DenseBwdArgs a, Gro
       uint4 zv0 = make_uint4(0, 0, 0, 0), zv1 = zv0;
       if (em < M) {
         zv0 = ld_coh16(z2 + (size_t)em * 128 + eseg);
-        zv1 = ld_coh16(z2 + (size_t)em * 128 + eseg + 8);
+        zv1 = ld_coh16(z2 + (size_t)em * 128 + eseg + ESEG2);
       }
       if (tid < 128) {
         float q0, q1, B2, C2;
@@ -438,16 +442,16 @@ __global__ __launch_bounds__(NT) void dense_stage_bwd_kernel(DenseBwdArgs a, Gro
         unpack16(tv0, tv1, tf);
 #pragma unroll
         for (int q = 0; q < 16; ++q) {
-          const int c = eseg + q;
+          const int c = eseg + q + (q >= 8 ? ESEG2 - 8 : 0);
           v[q] = s.u.q.r0[c] * zf[q] + s.u.q.r0[128 + c] * tf[q] + s.u.q.r0[256 + c];
         }
         const uint4 p0 = pack8(v), p1 = pack8(v + 8);
         *reinterpret_cast<uint4*>(s.u.q.dt + er * TP + eseg) = p0;
-        *reinterpret_cast<uint4*>(s.u.q.dt + er * TP + eseg + 8) = p1;
+        *reinterpret_cast<uint4*>(s.u.q.dt + er * TP + eseg + ESEG2) = p1;
         if (em < M) {
           bf16_t* dtg = gsh(d.dt, go) + (size_t)em * 128 + eseg;
           st_coh16(dtg, p0);
-          st_coh16(dtg + 8, p1);
+          st_coh16(dtg + ESEG2, p1);
         }
       }
       __syncthreads();
