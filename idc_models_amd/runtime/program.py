@@ -666,6 +666,8 @@ class FusedStep:
         return n
 
     def eval_step(self, x, y):
+        """One inference step.  Returns (loss, logits) as VIEWS of the program's output buffers,
+        like train_step: the next step of the same program overwrites them (clone() to keep)."""
         if self.progs:
             self.check_persistent()
         dtype = torch.uint8 if x.dtype == torch.uint8 else torch.float32
