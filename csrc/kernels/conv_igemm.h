@@ -86,11 +86,6 @@ constexpr int TILE_BIG128D = 104;  // 256 x 128 with three LDS buffers
 constexpr int TILE_IMG = 105;
 bool conv_img_ok(const ConvArgs& a, bool a_f32);
 hipError_t conv_img(const ConvArgs& a, bool a_f32, hipStream_t st);
-// tile TILE_ROWS selects the row-block 1x1 data gradient with the concat-gradient epilogue
-// (conv_rows.hip): DenseNet's dgrad cv1 (PRO 2 + EPI 2, 128-deep)
-constexpr int TILE_ROWS = 106;
-bool conv_rows_ok(const ConvArgs& a, bool a_f32);
-hipError_t conv_rows(const ConvArgs& a, bool a_f32, hipStream_t st);
 // tile TILE_STEM selects the image-resident stem convolution (conv_stem.hip): 8-channel staged
 // images, KxK stride 1/2, up to 64 output channels
 constexpr int TILE_STEM = 107;

@@ -34,7 +34,6 @@ int conv_tile_bk(int t) { return kTiles[t].bk; }
 
 hipError_t conv_igemm(const ConvArgs& a, int tile, bool a_f32, hipStream_t st) {
   if (tile == TILE_IMG) return conv_img(a, a_f32, st);
-  if (tile == TILE_ROWS) return conv_rows(a, a_f32, st);
   if (tile == TILE_STEM) return conv_stem(a, a_f32, st);
   if (tile < 0 || (tile >= conv_num_tiles() && tile != TILE_BIG128 && tile != TILE_BIG256 && tile != TILE_BIG64 &&
                    tile != TILE_BIG128D))

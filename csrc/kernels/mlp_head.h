@@ -28,6 +28,7 @@ struct Mlp2Args {
   // backward
   float* dw1; float* db1; float* dw2; float* db2;
   float* dx;              // [N][D0] fp32 gradient of the flattened input (may be null)
+  float dl_scale;         // dlogits factor (loss_scale x the rank's uneven-batch weight)
 };
 
 __device__ __forceinline__ void gshift(Mlp2Args& a, long long o) {

@@ -76,7 +76,7 @@ __global__ __launch_bounds__(256) void mlp2_fwd_kernel(Mlp2Args a, GroupArg ga) 
     float y = a.labels[n], x = z[0];
     float l = fmaxf(x, 0.f) - x * y + log1pf(expf(-fabsf(x)));
     lsum = l;
-    if (a.dlogits) a.dlogits[n] = (1.f / (1.f + expf(-x)) - y) * a.loss_scale;
+    if (a.dlogits) a.dlogits[n] = (1.f / (1.f + expf(-x)) - y) * a.dl_scale;
   } else {
     float se = 0.f;
     for (int u = 0; u < a.U; ++u) se += expf(z[u] - zmax);
@@ -84,7 +84,7 @@ __global__ __launch_bounds__(256) void mlp2_fwd_kernel(Mlp2Args a, GroupArg ga) 
     for (int u = 0; u < a.U; ++u) {
       float y = a.labels[(size_t)n * a.U + u];
       lsum += y * (lse - z[u]);
-      if (a.dlogits) a.dlogits[(size_t)n * a.U + u] = (expf(z[u] - lse) - y) * a.loss_scale;
+      if (a.dlogits) a.dlogits[(size_t)n * a.U + u] = (expf(z[u] - lse) - y) * a.dl_scale;
     }
   }
   atomicAdd(a.loss, lsum * a.loss_scale);

@@ -93,6 +93,8 @@ struct HeadArgs {
   float* loss_vec;  // [N] per-sample losses: the last block sums them in sample order and WRITES
                     // loss (run-to-run identical, no zero-fill before the head)
   unsigned* ticket; // arrival counter of loss_vec (counts modulo N, never reset)
+  float dl_scale;   // dlogits factor: loss_scale x this rank's share weight of an uneven global
+                    // batch (applied BEFORE the gradient all-reduce; the optimizer's scale is 1/N)
 };
 
 struct HeadBwdArgs {
@@ -172,7 +174,7 @@ hipError_t head_fwd(const HeadArgs& a, hipStream_t st);
 hipError_t head_bwd(const HeadBwdArgs& a, hipStream_t st);
 hipError_t zero_fill(void* p, long long nbytes, hipStream_t st);
 hipError_t rmsprop(float* w, const float* g, float* ms, long long n, float lr, float rho,
-                   float eps, float grad_scale, const int* skip, hipStream_t st);
+                   float eps, float grad_scale, const int* skip, int* hostflag, hipStream_t st);
 hipError_t finite_check(const float* g, long long n, int* flag, hipStream_t st);
 // status[0] = flag (last step skipped?), status[1] += flag (skipped steps), flag = 0
 hipError_t finite_flag_reset(int* flag, int* status, hipStream_t st);

@@ -877,7 +877,7 @@ __global__ __launch_bounds__(256) void head_fwd_kernel(HeadArgs a, GroupArg ga) 
         float x = lg[0], z = a.labels[n];
         loss = fmaxf(x, 0.f) - x * z + log1pf(expf(-fabsf(x)));
         float sig = 1.f / (1.f + expf(-x));
-        if (a.dlogits) a.dlogits[n] = (sig - z) * a.loss_scale;
+        if (a.dlogits) a.dlogits[n] = (sig - z) * a.dl_scale;
       } else {
         float mx = lg[0];
         for (int u = 1; u < a.U; ++u) mx = fmaxf(mx, lg[u]);
@@ -889,7 +889,7 @@ __global__ __launch_bounds__(256) void head_fwd_kernel(HeadArgs a, GroupArg ga) 
         for (int u = 0; u < a.U; ++u) {
           float y = a.labels[n * a.U + u];
           loss += -y * (lg[u] - lse);
-          if (a.dlogits) a.dlogits[n * a.U + u] = (expf(lg[u] - lse) * tsum - y) * a.loss_scale;
+          if (a.dlogits) a.dlogits[n * a.U + u] = (expf(lg[u] - lse) * tsum - y) * a.dl_scale;
         }
       }
       if (a.loss && a.loss_vec) {
@@ -1004,12 +1004,20 @@ hipError_t head_bwd(const HeadBwdArgs& a, hipStream_t st) {
 __global__ __launch_bounds__(256) void rmsprop_kernel(float* __restrict__ w, const float* __restrict__ g,
                                                       float* __restrict__ ms, long long n4, float lr,
                                                       float rho, float eps, float gs,
-                                                      const int* __restrict__ skip, GroupArg ga) {
+                                                      const int* __restrict__ skip, int* hostflag,
+                                                      GroupArg ga) {
   {
     const long long go = goff(ga);
     w = gsh(w, go); g = gsh(g, go); ms = gsh(ms, go); skip = gsh(skip, go);
   }
-  if (skip && *skip) return;  // non-finite gradients this step: keep weights and slots unchanged
+  if (skip && *skip) {  // non-finite gradients / a persistent give-up: weights and slots unchanged
+    // a give-up on ANY rank (bits above bit 0 of the all-reduced guard word) also raises this
+    // rank's pinned host flag, so every replica's runtime applies the same IDC_DS_ON_FAIL policy
+    // at the same step (program.py check_persistent), not only the rank whose launch gave up
+    if (hostflag && (*skip & ~1) && blockIdx.x == 0 && threadIdx.x == 0)
+      __hip_atomic_store(hostflag, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    return;
+  }
   for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n4;
        i += (long long)gridDim.x * blockDim.x) {
     float4 gv = reinterpret_cast<const float4*>(g)[i];
@@ -1091,13 +1099,13 @@ hipError_t finite_flag_reset(int* flag, int* status, hipStream_t st) {
 }
 
 hipError_t rmsprop(float* w, const float* g, float* ms, long long n, float lr, float rho, float eps,
-                   float grad_scale, const int* skip, hipStream_t st) {
+                   float grad_scale, const int* skip, int* hostflag, hipStream_t st) {
   long long n4 = n / 4;  // arena sizes are multiples of 64 elements
   long long blocks = (n4 + 255) / 256;
   if (blocks > 8192) blocks = 8192;
   if (blocks < 1) blocks = 1;
   hipLaunchKernelGGL(rmsprop_kernel, ggrid((int)blocks), dim3(256), 0, st, w, g, ms, n4, lr, rho, eps,
-                     grad_scale, skip, garg());
+                     grad_scale, skip, hostflag, garg());
   return hipGetLastError();
 }
 

@@ -602,7 +602,7 @@ class Plan {
       case OP_RMSPROP:
         check(rmsprop(reinterpret_cast<float*>(op.p[0]), reinterpret_cast<const float*>(op.p[1]),
                       reinterpret_cast<float*>(op.p[2]), op.l[0], op.f[0], op.f[1], op.f[2], op.f[3],
-                      reinterpret_cast<const int*>(op.p[3]), st),
+                      reinterpret_cast<const int*>(op.p[3]), reinterpret_cast<int*>(op.p[4]), st),
               "rmsprop");
         break;
       case OP_CAST:
@@ -897,7 +897,7 @@ void py_secagg_unmask(uintptr_t sum, uintptr_t out, long long n, uintptr_t seg_s
 void py_rmsprop(uintptr_t w, uintptr_t g, uintptr_t ms, long long n, float lr, float rho, float eps, float gs,
                 uintptr_t stream) {
   check(rmsprop(reinterpret_cast<float*>(w), reinterpret_cast<const float*>(g), reinterpret_cast<float*>(ms), n,
-                lr, rho, eps, gs, nullptr, reinterpret_cast<hipStream_t>(stream)),
+                lr, rho, eps, gs, nullptr, nullptr, reinterpret_cast<hipStream_t>(stream)),
         "rmsprop");
 }
 
@@ -1039,15 +1039,7 @@ PYBIND11_MODULE(_idc_native, m) {
   m.attr("TILE_BIG64") = TILE_BIG64;
   m.attr("TILE_BIG128D") = TILE_BIG128D;
   m.attr("TILE_IMG") = TILE_IMG;
-  m.attr("TILE_ROWS") = TILE_ROWS;
   m.attr("TILE_STEM") = TILE_STEM;
-  m.def("rows_ok", [](py::bytes payload, int a_f32) {
-    std::string s = payload;
-    if (s.size() != sizeof(ConvArgs)) throw std::runtime_error("ConvArgs size mismatch");
-    ConvArgs a;
-    std::memcpy(&a, s.data(), sizeof(a));
-    return conv_rows_ok(a, a_f32 != 0);
-  });
   m.def("img_ok", [](py::bytes payload, int a_f32) {
     std::string s = payload;
     if (s.size() != sizeof(ConvArgs)) throw std::runtime_error("ConvArgs size mismatch");

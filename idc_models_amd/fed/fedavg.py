@@ -371,14 +371,10 @@ class FedAvgProcess:
             clear = [n_sum, met]
         else:
             clear = [delta_sum, n_sum, met] + ([ntr_sum] if ntr_sum is not None else [])
-        # one packed all-reduce of [delta sums | bn sums | n | metrics] (clear parts)
+        # packed all-reduces of [delta sums | bn sums] and [n | metrics] (clear parts), one per
+        # dtype: the float64 example counts and metric sums stay exact across ranks
         if world > 1:
-            flatp = torch.cat([p.reshape(-1).float() for p in clear])
-            comm.all_reduce_(flatp)
-            off = 0
-            for p in clear:  # copy back IN PLACE (n_sum/met are float64 accumulators)
-                p.copy_(flatp[off:off + p.numel()].view(p.shape).to(p.dtype))
-                off += p.numel()
+            comm.all_reduce_packed_(clear)
         total = float(n_sum.item())
         if total > 0:
             mean_delta = delta_sum / total

@@ -99,7 +99,7 @@ class HeadArgs(C.Structure):
     _fields_ = [("x", vp), ("ldx", ci), ("N", ci), ("HW", ci), ("C", ci), ("U", ci),
                 ("pro", BnArgs), ("w", vp), ("b", vp), ("labels", vp), ("logits", vp),
                 ("feats", vp), ("dlogits", vp), ("loss", vp), ("loss_scale", cf), ("training", ci),
-                ("loss_vec", vp), ("ticket", vp)]
+                ("loss_vec", vp), ("ticket", vp), ("dl_scale", cf)]
 
 
 class HeadBwdArgs(C.Structure):
@@ -126,7 +126,7 @@ class Mlp2Args(C.Structure):
                 ("w2", vp), ("b2", vp), ("p0", cf), ("p1", cf), ("seed", C.c_uint64), ("step", vp),
                 ("labels", vp), ("logits", vp), ("h1", vp), ("loss", vp), ("dlogits", vp),
                 ("loss_scale", cf), ("training", ci), ("dw1", vp), ("db1", vp), ("dw2", vp),
-                ("db2", vp), ("dx", vp)]
+                ("db2", vp), ("dx", vp), ("dl_scale", cf)]
 
 
 class WgBatchEntry(C.Structure):

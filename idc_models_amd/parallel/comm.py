@@ -99,35 +99,42 @@ def all_reduce_max(value: float, device) -> float:
     return float(t.item())
 
 
-_NATIVE_RING = None  # (group identity, NativeCommunicator) for ring sums on RCCL
-
-
 def _native_ring(device):
-    """A native RCCL communicator over the default group (created on first use), or None when the
-    group is not RCCL or native collectives are off (IDC_NATIVE_COMM=0)."""
-    global _NATIVE_RING
+    """The rank's native RCCL communicator (``native_comm.shared_communicator``: the one the
+    strategy's gradient buckets use, with its init timeout and watchdog), or None when the group is
+    not RCCL or native collectives are off (IDC_NATIVE_COMM=0)."""
     if backend() != "nccl" or os.environ.get("IDC_NATIVE_COMM", "1") == "0":
         return None
-    key = id(dist.group.WORLD)
-    if _NATIVE_RING is None or _NATIVE_RING[0] != key:
-        from .native_comm import NativeCommunicator
-        _NATIVE_RING = (key, NativeCommunicator(dist.get_rank(), dist.get_world_size(), device, watchdog=False))
-    return _NATIVE_RING[1]
+    from .native_comm import shared_communicator
+    return shared_communicator(dist.get_rank(), dist.get_world_size(), device)
 
 
 def ring_sum_u32_(t: torch.Tensor) -> torch.Tensor:
     """In-place SUM over the ranks modulo 2^32 of an int32 tensor that holds uint32 bit patterns
     (the masked fixed-point vectors of secure aggregation, fed/secagg.py).  On RCCL: ONE native
-    ``ncclUint32`` all-reduce (unsigned wrap is defined; a signed int32 sum that wraps is not); on
-    gloo (or with native collectives off): an exact int64 sum of the unsigned values, reduced mod
-    2^32."""
+    ``ncclUint32`` all-reduce (unsigned wrap is defined; a signed int32 sum that wraps is not) on
+    the communicator's own stream behind a watchdog progress mark, and the caller's stream is
+    released only when it completed -- a dead peer raises ``CommFailure`` after the watchdog
+    timeout instead of hanging the secure round; on gloo (or with native collectives off): an
+    exact int64 sum of the unsigned values, reduced mod 2^32."""
     if not is_dist():
         return t
     if t.dtype != torch.int32:
         raise TypeError("ring_sum_u32_: int32 bit patterns expected")
     nc = _native_ring(t.device) if t.is_cuda else None
     if nc is not None:
-        nc.all_reduce_u32_(t, stream=torch.cuda.current_stream(t.device))
+        nc.check()
+        cur = torch.cuda.current_stream(t.device)
+        cs = torch.cuda.ExternalStream(nc.stream_handle, device=t.device)
+        cs.wait_stream(cur)
+        nc.all_reduce_u32_(t, stream=cs)
+        nc.step_issued()
+        done = torch.cuda.Event()
+        done.record(cs)
+        if nc.watchdog is not None:
+            from .watchdog import wait_with_watchdog
+            wait_with_watchdog(nc.watchdog, done.query)
+        cur.wait_event(done)
         return t
     wide = t.to(torch.int64) & 0xFFFFFFFF
     dist.all_reduce(wide)  # < world * 2^32: exact in int64
@@ -137,10 +144,28 @@ def ring_sum_u32_(t: torch.Tensor) -> torch.Tensor:
 
 
 def destroy_native_ring():
-    global _NATIVE_RING
-    if _NATIVE_RING is not None:
-        _NATIVE_RING[1].close()
-        _NATIVE_RING = None
+    """Close the rank's shared native communicator (end of the process group)."""
+    from .native_comm import _SHARED, release_shared
+    for nc in list(_SHARED.values()):
+        release_shared(nc)
+
+
+def all_reduce_packed_(tensors: List[torch.Tensor], op=dist.ReduceOp.SUM) -> List[torch.Tensor]:
+    """In-place SUM over the ranks of many tensors: ONE packed all-reduce per dtype, each in its
+    own dtype (float64 accumulators are never rounded through float32)."""
+    if not is_dist() or not tensors:
+        return tensors
+    groups = {}
+    for t in tensors:
+        groups.setdefault(t.dtype, []).append(t)
+    for dt, ts in groups.items():
+        flat = torch.cat([t.reshape(-1) for t in ts])
+        all_reduce_(flat, op)
+        off = 0
+        for t in ts:
+            t.copy_(flat[off:off + t.numel()].view(t.shape))
+            off += t.numel()
+    return tensors
 
 
 def pack_all_reduce(tensors: List[torch.Tensor], op=dist.ReduceOp.SUM) -> List[torch.Tensor]:

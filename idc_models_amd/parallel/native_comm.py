@@ -161,3 +161,38 @@ class NativeCommunicator:
         if self.c is not None:
             self.c.close()
             self.c = None
+
+
+# ---- one communicator per rank ------------------------------------------------------------------
+# The strategy's gradient buckets, the federated sums and the secure-aggregation ring all use the
+# SAME communicator of a rank (one RCCL context, one comm stream, one watchdog), created on first
+# use and keyed by the default group and device.
+_SHARED: dict = {}
+
+
+def _group_key(world: int, device: torch.device):
+    import torch.distributed as dist
+    g = id(dist.group.WORLD) if dist.is_available() and dist.is_initialized() else None
+    return (g, int(world), device.index or 0)
+
+
+def shared_communicator(rank: int, world: int, device, **kw) -> NativeCommunicator:
+    """The rank's native communicator over the default group (created on first use; a closed or
+    aborted one is replaced).  ``kw`` go to the constructor when it is created."""
+    dev = torch.device(device)
+    key = _group_key(world, dev)
+    nc = _SHARED.get(key)
+    if nc is None or nc.c is None:
+        nc = NativeCommunicator(rank, world, dev, **kw)
+        _SHARED[key] = nc
+    return nc
+
+
+def release_shared(nc: Optional[NativeCommunicator]):
+    """Close ``nc`` and forget it (every holder of the rank's communicator sees it closed)."""
+    if nc is None:
+        return
+    for k, v in list(_SHARED.items()):
+        if v is nc:
+            del _SHARED[k]
+    nc.close()

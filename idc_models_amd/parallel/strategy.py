@@ -126,8 +126,8 @@ class MirroredStrategy(Strategy):
         if native_comm is None:
             native_comm = os.environ.get("IDC_NATIVE_COMM", "1") != "0"
         if native_comm and self.active and dev.type == "cuda" and comm.backend() == "nccl":
-            from .native_comm import NativeCommunicator
-            self.native_comm = NativeCommunicator(rank, world, dev)
+            from .native_comm import shared_communicator
+            self.native_comm = shared_communicator(rank, world, dev)
 
     @property
     def active(self) -> bool:
@@ -136,7 +136,8 @@ class MirroredStrategy(Strategy):
     def close(self):
         """Release the native communicator and the process group (end of a run)."""
         if self.native_comm is not None:
-            self.native_comm.close()
+            from .native_comm import release_shared
+            release_shared(self.native_comm)
             self.native_comm = None
         comm.destroy()
 

@@ -12,13 +12,15 @@ device synchronisation.  The watchdog turns that into an error:
   (``check_async``) and the age of the outstanding mark (``mark_age``);
 * on an asynchronous error, or a mark older than ``timeout_s``, it aborts the communicator
   (``ncclCommAbort``: the stuck collective kernels exit, so a blocked synchronisation returns) and
-  records the failure; ``raise_if_failed()`` -- called by the runtime before every step -- raises
-  ``CommFailure`` on the training thread.
+  records the failure; ``raise_if_failed()`` raises ``CommFailure`` on the training thread.  The
+  fused runtime calls it at the top of every data-parallel step (``NativeCommunicator.check`` in
+  ``FusedStep._train_step``) and again after issuing the step's collectives (``step_issued``).
 
 The reference's equivalent is implicit: TF's collective executor timeouts around the NCCL
 all-reduce of ``MirroredStrategy`` (``/root/reference/dist_model_tf_vgg.py:115-117,135-138``).
 The policy is written against a duck-typed communicator (``check_async``, ``mark_age``,
-``abort``) so it is unit-tested on the CPU with a fake (``tests/test_watchdog.py``).
+``abort``) so it is unit-tested on the CPU with a fake (``tests/test_watchdog.py``), and a real
+gloo world of 2 on the CPU checks the abort-on-hang path end to end (same file).
 """
 from __future__ import annotations
 
@@ -86,8 +88,10 @@ class CommWatchdog:
 
     # ------------------------------------------------------------------ training-thread side
     def mark(self):
-        if self.error is None and self.comm is not None:
-            with self._lock:
+        # checked under the lock: poll_once may abort the communicator between a check made
+        # outside it and the mark (marking an aborted communicator raises a generic error)
+        with self._lock:
+            if self.error is None and self.comm is not None:
                 self.comm.mark()
 
     def raise_if_failed(self):

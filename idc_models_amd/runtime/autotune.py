@@ -96,10 +96,6 @@ def _conv_candidates(ext, M: int, cout: int, payload: bytes = None, a_f32: int =
     if payload is not None and os.environ.get("IDC_CONV_STEM", "1") != "0" and hasattr(ext, "stem_ok") \
             and ext.stem_ok(payload, a_f32):
         out.append(ext.TILE_STEM)
-    # the row-block 1x1 data gradient with the concat-gradient epilogue (conv_rows.hip)
-    if payload is not None and os.environ.get("IDC_CONV_ROWS", "1") != "0" and hasattr(ext, "rows_ok") \
-            and ext.rows_ok(payload, a_f32):
-        out.append(ext.TILE_ROWS)
     # 256 x {128, 256} global_load_lds tiles for plain wide layers (conv_big.hip), when they
     # still make >= 128 workgroups
     if payload is not None and os.environ.get("IDC_CONV_BIG", "1") != "0" and ext.big_ok(payload, a_f32):

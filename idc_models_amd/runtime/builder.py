@@ -224,6 +224,14 @@ class Builder:
         # forward launch's lookahead queue order, which needs more than one phase of its own
         # workgroups resident, is not used
         self.shared_device = False
+        # this rank's weight in an uneven split of a global batch (n_local * world / global): the
+        # loss head's gradient seed carries it, so each rank's local gradient is weighted BEFORE
+        # the all-reduce sum (lower_common.emit_head dl_scale)
+        self.grad_weight = 1.0
+        # persistent (work-queue) launches allowed: FusedProgram clears it for training programs
+        # whose update cannot honour the step guard word (a host optimizer) or whose replicas would
+        # not agree on it (data parallelism without the native communicator's guard all-reduce)
+        self.persist_ok = True
 
     # ------------------------------------------------------------------ allocation
     def alloc(self, shape, dtype=BF16) -> torch.Tensor:
@@ -801,7 +809,8 @@ class Builder:
         1x1 inputs of <= DS_MAX_CIN (2,048) channels in multiples of 32 (DenseNet-121/169/201),
         128-channel bottlenecks, 32 new channels per layer, maps whose 3x3 windows fit the
         launch's staging rows, and no fixed-order (deterministic) reductions."""
-        if os.environ.get("IDC_DENSE_STAGE", "1") == "0" or self.det or persistent_disabled():
+        if os.environ.get("IDC_DENSE_STAGE", "1") == "0" or self.det or persistent_disabled() \
+                or not self.persist_ok:
             return False
         infer = all(lay["bn1"].mode == 2 and lay["bn2"].mode == 2 for lay in layers)
         if infer:
@@ -894,7 +903,7 @@ class Builder:
         # under load (761 + 234 us against ~720 us per-layer: 4.12 ms/step, round 4, see
         # tools/dense_stamps.py).  Not in grouped (client-batched) programs.
         if os.environ.get("IDC_DENSE_STAGE_BWD", "1") != "1" or not self.training or self.det or \
-                persistent_disabled():
+                persistent_disabled() or not self.persist_ok:
             return False
         if getattr(self, "grouped", False):
             return False

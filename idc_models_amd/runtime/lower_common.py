@@ -77,6 +77,9 @@ def emit_head(b: Builder, feat: Tensor4, pro: Optional[nat.BnArgs], dense, U: in
     a.dlogits = io.dlogits.data_ptr() if training else 0
     a.loss = io.loss.data_ptr()
     a.loss_scale = 1.0 / float(feat.N)
+    # this rank's share of an uneven global batch enters the gradient at its seed, before the
+    # all-reduce (the optimizer then scales the reduced sum by a uniform 1/N)
+    a.dl_scale = a.loss_scale * b.grad_weight
     a.training = 1 if training else 0
     # per-sample losses summed in sample order by the last block (deterministic, no zero-fill op)
     a.loss_vec = b.alloc((feat.N,), F32).data_ptr()

@@ -64,6 +64,7 @@ def lower_tiny(b: Builder, net, U: int, input_dtype):
     a.loss = io.loss.data_ptr()
     a.dlogits = io.dlogits.data_ptr() if training else 0
     a.loss_scale = 1.0 / float(B)
+    a.dl_scale = a.loss_scale * b.grad_weight
     a.training = 1 if training else 0
     b.memset(io.loss)
     b.emit(nat.OP_MLP_FWD, a)

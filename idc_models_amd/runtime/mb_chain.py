@@ -37,7 +37,8 @@ _TILES = 512
 
 def chain_enabled(b) -> bool:
     from .builder import persistent_disabled
-    return os.environ.get("IDC_MB_CHAIN", "0") == "1" and not b.det and not persistent_disabled()
+    return os.environ.get("IDC_MB_CHAIN", "0") == "1" and not b.det and not persistent_disabled() \
+        and b.persist_ok
 
 
 class MbChain:

@@ -59,11 +59,64 @@ def fused_supported(net, loss) -> bool:
     return nat.available()
 
 
+def persistent_allowed(model, training: bool) -> bool:
+    """Whether a program may build persistent (work-queue) launches.  A persistent launch that
+    gives up leaves stale stage outputs and relies on the step's update being skipped through the
+    step guard word: only the fused RMSprop reads that word (a host optimizer would apply the stale
+    update), and only the native communicator's guard all-reduce makes every replica skip
+    together (the torch bucketer path and central storage would let the other replicas apply
+    gradients that include the stale contribution).  Evaluation programs are unaffected."""
+    if not training or not model.arena.params:
+        return True
+    opt = model.optimizer
+    host_opt = not isinstance(opt, RMSprop) or bool(opt.momentum) or bool(opt.centered)
+    st = model.strategy
+    unguarded_dp = st.active and (getattr(st, "native_comm", None) is None
+                                  or getattr(st, "central_storage", False))
+    return not (host_opt or unguarded_dp)
+
+
+def place_buckets(ops, bwd_marks, buckets) -> Dict[int, List[Tuple[int, int]]]:
+    """Where each gradient bucket's all-reduce goes in a lowered op list: ``{i: [(start, end)]}``
+    = the buckets issued right before ``ops[i]`` (``i`` may be the first op after the backward
+    segment, or ``len(ops)``, for buckets no mark released).
+
+    ``bwd_marks``: ``(op index, lowest arena parameter index whose gradient is final before that
+    op)`` from the lowering (``Builder.mark_grads_ready``); ``buckets``: ``(param ids, start, end)``
+    of ``GradBucketer``.  A bucket is released at the first mark whose lowest-ready index is at or
+    below its lowest parameter (gradients become final in reverse parameter order).  Every bucket
+    is placed exactly once, at or before the end of the backward segment."""
+    mark_at: Dict[int, int] = {}
+    for pos, lo in bwd_marks:
+        mark_at[pos] = min(lo, mark_at.get(pos, lo))
+    pending = sorted(((min(ids), s0, s1) for ids, s0, s1 in buckets), reverse=True)
+    out: Dict[int, List[Tuple[int, int]]] = {}
+    cur = None
+    for i, op in enumerate(ops):
+        seg = op[0]
+        if seg != cur:
+            if cur == "bwd" and pending:
+                out.setdefault(i, []).extend((s0, s1) for _, s0, s1 in pending)
+                pending = []
+            cur = seg
+        if cur == "bwd" and i in mark_at:
+            while pending and pending[0][0] >= mark_at[i]:
+                _, s0, s1 = pending.pop(0)
+                out.setdefault(i, []).append((s0, s1))
+    if pending:
+        out.setdefault(len(ops), []).extend((s0, s1) for _, s0, s1 in pending)
+    return out
+
+
 class FusedProgram:
     def __init__(self, model, batch: int, training: bool, input_dtype, grad_scale: float = 1.0,
-                 use_graphs: bool = True, skip_nonfinite: bool = False, group=None):
+                 use_graphs: bool = True, skip_nonfinite: bool = False, group=None,
+                 grad_weight: float = 1.0):
         """``group``: a ``runtime.grouped.GroupRegion`` — the program is built inside copy 0 of the
-        region and every launch runs its K copies (client-batched federated training)."""
+        region and every launch runs its K copies (client-batched federated training).
+        ``grad_weight``: this rank's weight in an uneven split of a global batch; it scales the
+        loss head's gradient seed, i.e. the LOCAL gradient before any all-reduce, while
+        ``grad_scale`` (the optimizer's factor on the reduced sum) is the same on every rank."""
         nat.require()
         self.group = group
         self.model = model
@@ -74,6 +127,8 @@ class FusedProgram:
         b = Builder(net, model.arena, model.device, batch, training)
         b.grouped = group is not None
         b.shared_device = bool(getattr(getattr(model, "impl", None), "shared_device", False))
+        b.grad_weight = float(grad_weight)
+        b.persist_ok = persistent_allowed(model, training)
         _lowering_for(net)(b, net, self.U, input_dtype)
         if b.has_wgrad_batch():  # a lowering that returned early (frozen layers) mid-batch
             b.segment = "bwd"
@@ -138,9 +193,17 @@ class FusedProgram:
                        ptrs=(model.arena.grad.data_ptr(), flag))
             if not self.host_optimizer:
                 ms = opt.ms
+                hflag = 0
+                if flag and flag == guard and not b.grouped and torch.cuda.is_available():
+                    # a skip caused by a give-up on any rank raises this rank's host flag too
+                    if not b.host_flag:
+                        from .builder import _host_flag_slot
+                        b.host_flag = _host_flag_slot()
+                    hflag = b.host_flag
                 b.emit(nat.OP_RMSPROP, floats=(opt.learning_rate, opt.rho, opt.epsilon, grad_scale),
                        longs=(model.arena.numel,),
-                       ptrs=(model.arena.data.data_ptr(), model.arena.grad.data_ptr(), ms.data_ptr(), flag))
+                       ptrs=(model.arena.data.data_ptr(), model.arena.grad.data_ptr(), ms.data_ptr(), flag,
+                             hflag))
             if b.cast_tr_n:
                 b.emit(nat.OP_CAST, ints=(b.cast_tr_n,), longs=(b.cast_tr_total,),
                        ptrs=(b.cast_tr_dev.data_ptr(), b.cast_tr_map.data_ptr()))
@@ -170,7 +233,6 @@ class FusedProgram:
         self.plan.set_side_flush(int(os.environ.get("IDC_SIDE_FLUSH", default_flush)))
         self.seg: Dict[str, Tuple[int, int]] = {}
         self.rms_index = None
-        cur, start = None, 0
         op_index = 0
         self.bwd_marks = []
         mark_at = {}
@@ -178,23 +240,21 @@ class FusedProgram:
             mark_at.setdefault(pos, []).append(lo)
         # Data parallelism over the strategy's native RCCL communicator: every gradient bucket's
         # all-reduce becomes a plan op (OP_ALLREDUCE, comm lane) placed at the first backward mark
-        # after which all of its parameters' gradients are final, so the C++ executor issues the
-        # whole backward + collectives in one call.
-        strategy = model.strategy
+        # after which all of its parameters' gradients are final (place_buckets), so the C++
+        # executor issues the whole backward + collectives in one call.
         self.native_comm = None
-        pending_buckets: List[Tuple[int, int, int]] = []  # (lowest param index, start, end)
+        placed: Dict[int, List[Tuple[int, int]]] = {}
         if training and model.arena.params and getattr(strategy, "native_comm", None) is not None \
                 and strategy.active and not getattr(strategy, "central_storage", False):
             from ..parallel.buckets import GradBucketer
             self.native_comm = strategy.native_comm
             gb = GradBucketer(model.arena, strategy.bucket_bytes)
-            pending_buckets = sorted(((min(bk.param_ids), bk.start, bk.end) for bk in gb.buckets), reverse=True)
+            placed = place_buckets(b.ops, b.bwd_marks, [(bk.param_ids, bk.start, bk.end) for bk in gb.buckets])
         self.n_comm_ops = 0
 
-        def add_ready_buckets(lo_ready: int):
+        def add_buckets(i: int):
             nonlocal op_index
-            while pending_buckets and pending_buckets[0][0] >= lo_ready:
-                _, s0, s1 = pending_buckets.pop(0)
+            for s0, s1 in placed.get(i, ()):
                 self.plan.add(nat.OP_ALLREDUCE, b"", [0, 0], [], [s1 - s0],
                               [model.arena.grad.data_ptr() + 4 * s0], 0)
                 op_index += 1
@@ -213,19 +273,19 @@ class FusedProgram:
                 self.n_comm_ops += 1
                 guard_ar = False
 
+        cur, start = None, 0
         for i, (seg, kind, raw, ints, floats, longs, ptrs, lane) in enumerate(b.ops):
             if seg != cur:
-                if cur == "bwd" and pending_buckets:
-                    add_ready_buckets(-1)  # buckets no mark released (params without gradient)
                 if cur == "bwd":
+                    add_buckets(i)  # buckets no mark released (params without gradient)
                     add_guard_allreduce()
                 if cur is not None:
                     self.seg[cur] = (start, op_index)
                 cur, start = seg, op_index
             if i in mark_at:
                 self.bwd_marks.append((op_index, min(mark_at[i])))
-                if pending_buckets:
-                    add_ready_buckets(min(mark_at[i]))
+                if cur == "bwd":
+                    add_buckets(i)
             if kind == "MOVING":
                 if b.moving_dev is None:
                     continue
@@ -236,9 +296,8 @@ class FusedProgram:
                 self.rms_index = op_index
             self.plan.add(kind, raw, ints, floats, longs, ptrs, lane)
             op_index += 1
-        if cur == "bwd" and pending_buckets:
-            add_ready_buckets(-1)
         if cur == "bwd":
+            add_buckets(len(b.ops))
             add_guard_allreduce()
         if cur is not None:
             self.seg[cur] = (start, op_index)
@@ -472,9 +531,11 @@ class FusedStep:
         key = (batch, training, dtype) if w == 1.0 else (batch, training, dtype, w)
         p = self.progs.get(key)
         if p is None:
-            gs = w / self.m.strategy.num_replicas_in_sync
+            # the share weight w scales this rank's gradient seed (before the all-reduce); the
+            # reduced sum is scaled by the same 1/N on every rank, so replicas stay identical
+            gs = 1.0 / self.m.strategy.num_replicas_in_sync
             p = FusedProgram(self.m, batch, training, dtype, grad_scale=gs, use_graphs=self.use_graphs,
-                             skip_nonfinite=self.skip_nonfinite, group=self.group)
+                             skip_nonfinite=self.skip_nonfinite, group=self.group, grad_weight=w)
             self.progs[key] = p
         return p
 
@@ -559,6 +620,10 @@ class FusedStep:
         m = self.m
         dtype = torch.uint8 if x.dtype == torch.uint8 else torch.float32
         p = self._prog(x.shape[0], True, dtype)
+        if p.native_comm is not None:
+            # a failure the watchdog acted on since the last step surfaces as CommFailure here,
+            # before anything is enqueued on the aborted communicator
+            p.native_comm.check()
         self._stage_inputs(p, x, y)
         validate = os.environ.get("IDC_VALIDATE") == "1"
         if validate:

@@ -10,12 +10,13 @@ if ROOT not in sys.path:
 
 
 def pytest_configure(config):
-    # Eager-PyTorch REFERENCE runs use PyTorch's native convolutions, not MIOpen: since round 5 a
-    # MIOpen kernel faults the GPU inside an eager MobileNetV2 backward when earlier eager runs are in
-    # the same process (the round-4 tree faults the same way on the same boxes).  Our fused path never
-    # calls MIOpen; the variable reaches the worker subprocesses too (idc_models_amd/__init__.py).
-    os.environ.setdefault("IDC_EAGER_MIOPEN", "0")
-    if os.environ["IDC_EAGER_MIOPEN"] == "0":
+    # Eager-PyTorch reference runs use MIOpen (PyTorch's default).  Round 5 switched them to
+    # PyTorch's native convolutions after an illegal memory access surfaced in MIOpen's first call
+    # after fused FedAvg clients; round 6 replayed that exact sequence at HEAD with MIOpen on --
+    # eager-only, fused-then-eager under AMD_SERIALIZE_KERNEL=3, and the failing pytest sequence
+    # itself -- and none faulted (profiles/fault_attribution_r6.md), so the default is MIOpen
+    # again.  IDC_EAGER_MIOPEN=0 still selects the native convolutions.
+    if os.environ.get("IDC_EAGER_MIOPEN", "1") == "0":
         torch.backends.cudnn.enabled = False
     config.addinivalue_line("markers", "gpu: needs an MI355X (runs on the GPU box)")
     config.addinivalue_line("markers", "slow: long-running")

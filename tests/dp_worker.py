@@ -33,6 +33,7 @@ def run_case(arch, kind, per=None):
     from idc_models_amd.engine import Model, RMSprop
     from idc_models_amd.models import build_model
     from idc_models_amd.parallel import CentralStorageStrategy, MirroredStrategy, OneDeviceStrategy
+    from idc_models_amd.parallel.strategy import current_replica_weight
     cls = CentralStorageStrategy if kind == "central" else MirroredStrategy
     st = cls(backend="gloo", device="cuda:0", bucket_bytes=2 << 20)
     rank, world = st.rank, st.world
@@ -41,14 +42,24 @@ def run_case(arch, kind, per=None):
     m.compile(RMSprop(1e-4), "binary_crossentropy", [], backend="fused")
     g = torch.Generator().manual_seed(3)
     H, W, C = net.input_shape
-    x = torch.randint(0, 256, (per * world, H, W, C), generator=g, dtype=torch.uint8)
-    y = torch.randint(0, 2, (per * world,), generator=g)
-    xs, ys = x[rank * per:(rank + 1) * per], y[rank * per:(rank + 1) * per]
-    m.impl.train_step(xs, ys)
-    torch.cuda.synchronize()
-    red = m.arena.grad.detach().clone()  # the SUM the optimizer consumed (rank 0 for central)
-    m.impl.train_step(xs, ys)
-    torch.cuda.synchronize()
+    # "uneven": a global batch of world * per + 1 rows, rank 0 holding the extra one (the split
+    # strategy._ShardedBatches makes); each rank's local gradient is weighted n_r * world / b
+    sizes = [per + (1 if (kind == "uneven" and r == 0) else 0) for r in range(world)]
+    offs = [sum(sizes[:r]) for r in range(world + 1)]
+    gb = offs[-1]
+    wts = [n * world / gb for n in sizes]
+    x = torch.randint(0, 256, (gb, H, W, C), generator=g, dtype=torch.uint8)
+    y = torch.randint(0, 2, (gb,), generator=g)
+    xs, ys = x[offs[rank]:offs[rank + 1]], y[offs[rank]:offs[rank + 1]]
+    current_replica_weight[0] = wts[rank]
+    try:
+        m.impl.train_step(xs, ys)
+        torch.cuda.synchronize()
+        red = m.arena.grad.detach().clone()  # the SUM the optimizer consumed (rank 0 for central)
+        m.impl.train_step(xs, ys)
+        torch.cuda.synchronize()
+    finally:
+        current_replica_weight[0] = 1.0
     w = flat(m.net.trainable_weights)
     gathered = [torch.empty_like(w) for _ in range(world)]
     dist.all_gather(gathered, w)
@@ -58,20 +69,25 @@ def run_case(arch, kind, per=None):
     if rank == 0:
         ref = Model(build_model(arch, None, 1, seed=7), OneDeviceStrategy("cuda:0"))
         ref.compile(RMSprop(1e-4), "binary_crossentropy", [], backend="fused")
-        p = ref.impl._prog(per, True, torch.uint8)
-        tot = torch.zeros_like(red)
+        tot = torch.zeros_like(red, dtype=torch.float64)
         for r in range(world):
+            p = ref.impl._prog(sizes[r], True, torch.uint8)
             p.reset_stats_shift()  # each rank's shard as a first step (statistics shift K = 0)
-            ref.impl._stage_inputs(p, x[r * per:(r + 1) * per], y[r * per:(r + 1) * per])
+            ref.impl._stage_inputs(p, x[offs[r]:offs[r + 1]], y[offs[r]:offs[r + 1]])
             p.run_segment("fwd")
             p.run_segment("bwd")
             torch.cuda.current_stream().wait_stream(p.stream)
             torch.cuda.synchronize()
-            tot += ref.arena.grad
-        d, e = red.double(), tot.double()
+            tot += ref.arena.grad.double() * wts[r]
+        d, e = red.double(), tot
         out["grad_cos"] = float(d @ e / (d.norm() * e.norm() + 1e-30))
         out["grad_rel_err"] = float((d - e).norm() / (e.norm() + 1e-30))
-        if os.environ.get("IDC_DETERMINISTIC") == "1":
+        if kind == "uneven":
+            # weights applied at the gradient seed: equal to the weighted shard sum up to fp32
+            # rounding of the seed products, and the replicas stay bit-identical
+            out["weights"] = wts
+            out["ok"] = bool(same == 0.0 and out["grad_rel_err"] < 1e-5)
+        elif os.environ.get("IDC_DETERMINISTIC") == "1":
             # fixed-order reductions: each rank's shard gradient is the single-process one to the
             # bit, and a two-rank sum is exactly g0 + g1
             out["ok"] = bool(same == 0.0 and out["grad_rel_err"] == 0.0)

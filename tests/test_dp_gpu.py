@@ -29,7 +29,7 @@ def test_fused_data_parallel_two_ranks_on_one_gpu(tmp_path):
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
            "--master-addr", "127.0.0.1", "--master-port", str(_free_port()),
            os.path.join(ROOT, "tests", "dp_worker.py"),
-           "vgg16:mirrored,densenet121:mirrored,densenet121:central,vgg16:central"]
+           "vgg16:mirrored,densenet121:mirrored,densenet121:central,vgg16:central,vgg16:uneven"]
     # progress goes to a file as it happens (a GPU box treats minutes of silence as a hang)
     out_dir = os.path.join(ROOT, "gpurun_out") if os.path.isdir(os.path.join(ROOT, "gpurun_out")) else str(tmp_path)
     log = os.path.join(out_dir, "dp_worker.log")
@@ -37,6 +37,6 @@ def test_fused_data_parallel_two_ranks_on_one_gpu(tmp_path):
         r = subprocess.run(cmd, cwd=ROOT, env=env, stdout=f, stderr=subprocess.STDOUT, timeout=540)
     text = open(log).read()
     lines = [json.loads(l.split("DPCASE ", 1)[1]) for l in text.splitlines() if "DPCASE " in l]
-    assert r.returncode == 0 and len(lines) == 4, (r.returncode, text[-4000:])
+    assert r.returncode == 0 and len(lines) == 5, (r.returncode, text[-4000:])
     for c in lines:
         assert c["ok"], c

@@ -1185,45 +1185,3 @@ def test_conv_img_dgrad_matches_reference(fn, N, H):
     assert relerr(gsum, dZ2.sum((0, 1, 2))) < 2e-2
     assert relerr(gsumx, (dZ2 * xhat).sum((0, 1, 2))) < 2e-2
     assert torch.equal(db, k["gsum"]) and torch.equal(dg, k["gsumx"])
-
-
-@pytest.mark.parametrize("N,H,cin", [(4, 6, 160), (40, 13, 224), (9, 3, 992), (3, 13, 64)])
-def test_conv_rows_concat_gradient_matches_reference(fn, N, H, cin):
-    """Row-block 1x1 data gradient (conv_rows.hip, tile TILE_ROWS) as DenseNet's dgrad cv1 issues
-    it: dt staged once (and stored for the wgrad), epilogue mode 2 accumulating into the fp32
-    concat gradient with bn1's reductions; vs fp32 reference and vs the implicit-GEMM tiles."""
-    ext = fn.nat.require()
-    C = 128
-    x = bf(torch.randn(N, H, H, cin, device=DEV) * 1.5 + 0.3)
-    kb = _bn_case(N, H, cin, x=x, seed=3, act=1)
-    kp = _bn_case(N, H, cin, x=x, seed=4)
-    k2 = _bn_case(N, H, C, seed=7)
-    t16, z16 = k2["x"].to(torch.bfloat16), k2["dZ"].to(torch.bfloat16)
-    w = bf(torch.randn(1, 1, cin, C, device=DEV) * 0.1)
-    acc0 = torch.randn(N, H, H, cin, device=DEV)
-    x16 = x.to(torch.bfloat16)
-    res = {}
-    for tile in (ext.TILE_ROWS, -1):
-        acc = acc0.clone()
-        gsum, gsumx = torch.zeros(cin, device=DEV), torch.zeros(cin, device=DEV)
-        db, dg = torch.zeros(C, device=DEV), torch.zeros(C, device=DEV)
-        bpro = fn.bwd_aff(t16, k2["bn"], k2["gsum"], k2["gsumx"], fold=(db, dg))
-        bepi = fn.bwd_aff(x16, kp["bn"], kp["gsum"], kp["gsumx"], unit_alpha=True)
-        dt = torch.zeros(N, H, H, C, dtype=torch.bfloat16, device=DEV)
-        fn.conv2d_dgrad(z16, w, (H, H), mx=x16, mbn=kb["bn"], gsum=gsum, gsumx=gsumx, bpro=bpro, bepi=bepi,
-                        acc=acc, aout=dt, tile=tile)
-        torch.cuda.synchronize()
-        res[tile] = (acc, gsum, gsumx, dt.float(), db, dg)
-    dy = bf(k2["dX"])
-    dA = torch.nn.grad.conv2d_input((N, cin, H, H), w.permute(3, 2, 0, 1), dy.permute(0, 3, 1, 2)).permute(0, 2, 3, 1)
-    z = kb["xhat"] * kb["bn"].gamma + kb["bn"].beta
-    dZ1 = dA * (z > 0).float()
-    pend = kp["dX"] - kp["A"] * kp["dZ"]
-    ref = acc0 + kb["A"] * dZ1 + pend
-    acc, gsum, gsumx, dt, db, dg = res[ext.TILE_ROWS]
-    assert relerr(acc - acc0, ref - acc0) < 2e-2
-    assert relerr(acc - acc0, res[-1][0] - acc0) < 5e-3
-    assert relerr(gsum, dZ1.sum((0, 1, 2))) < 2e-2
-    assert relerr(gsumx, (dZ1 * kb["xhat"]).sum((0, 1, 2))) < 2e-2
-    assert torch.equal(dt, res[-1][3]) and relerr(dt, k2["dX"]) < 1e-2
-    assert torch.equal(db, k2["gsum"]) and torch.equal(dg, k2["gsumx"])

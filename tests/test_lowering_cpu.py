@@ -267,3 +267,101 @@ def test_stat_slot_copies_default_and_cap(monkeypatch):
     (kinds, n_on), (kinds_off, n_off) = slots(), slots(IDC_STAT_SLOTS="0")
     assert kinds == [1, 4]  # stages 3-4 one copy; stages 1-2, the stem and the transitions 4
     assert n_off == 1 and n_on > 1  # off: only the stem conv's reduction (always slotted) keeps copies
+
+
+def _grad_writes(b, arena):
+    """{op index: arena offsets (floats) of the gradient tensors the op's operands point at}."""
+    lo, hi = arena.grad.data_ptr(), arena.grad.data_ptr() + 4 * arena.numel
+    out = {}
+    for i, (seg, kind, raw, ints, floats, longs, ptrs, lane) in enumerate(b.ops):
+        if seg != "bwd" or kind == nat.OP_MEMSET:
+            continue
+        vals = [("ptr", p) for p in ptrs if p]
+        if kind in STRUCTS:
+            _pointers(STRUCTS[kind].from_buffer_copy(raw), vals)
+        tabs = {nat.OP_WGRAD_BATCH: (0, 0, nat.WgBatchEntry), nat.OP_DENSE_STAGE_BWD: (0, 1, nat.DenseBwdLayerDesc)}
+        if kind in tabs:
+            ps, ns, typ = tabs[kind]
+            tab = next(t for t in b.keep if t.data_ptr() == ptrs[ps])
+            raw_tab = bytes(tab.cpu().numpy().tobytes())
+            for j in range(ints[ns]):
+                e = typ.from_buffer_copy(raw_tab, j * C.sizeof(typ))
+                _pointers(e.a if kind == nat.OP_WGRAD_BATCH else e, vals)
+        offs = [(v - lo) // 4 for _, v in vals if lo <= v < hi]
+        if offs:
+            out[i] = offs
+    return out
+
+
+@pytest.mark.parametrize("arch,ft", [("vgg16", 15), ("vgg16", None), ("densenet121", 150),
+                                     ("densenet121", None), ("mobilenetv2", 100)])
+def test_allreduce_placement_world4(arch, ft):
+    """Data parallelism at world 4 (``dist_model_tf_vgg.py:115-117,141-151``): every gradient bucket's
+    all-reduce is placed after every backward op that writes into the bucket, exactly once, inside
+    the backward; with the phase-2 cuts (VGG16 15, DenseNet 150) the buckets start mid-network."""
+    from idc_models_amd.parallel.buckets import DEFAULT_BUCKET_BYTES, GradBucketer
+    from idc_models_amd.runtime.program import place_buckets
+    m, net, b = _lower(arch, ft, True, B=64)
+    gb = GradBucketer(m.arena, DEFAULT_BUCKET_BYTES // 4)  # several buckets per model
+    buckets = [(bk.param_ids, bk.start, bk.end) for bk in gb.buckets]
+    assert len(buckets) >= 2
+    placed = place_buckets(b.ops, b.bwd_marks, buckets)
+    where = {}
+    for i, lst in placed.items():
+        for s0, s1 in lst:
+            assert (s0, s1) not in where, "bucket placed twice"
+            where[(s0, s1)] = i
+    assert sorted(where) == sorted((s0, s1) for _, s0, s1 in buckets)
+    bwd = [i for i, op in enumerate(b.ops) if op[0] == "bwd"]
+    writes = _grad_writes(b, m.arena)
+    assert writes  # the backward writes gradients through pointers we can see
+    covered = set()
+    for (s0, s1), at in where.items():
+        assert bwd[0] < at <= bwd[-1] + 1, (s0, s1, at)
+        for i, offs in writes.items():
+            if any(s0 <= o < s1 for o in offs):
+                assert i < at, f"op {i} writes into bucket [{s0},{s1}) all-reduced before op {at}"
+                covered.add((s0, s1))
+    assert covered == set(where)  # every bucket has a producer before its all-reduce
+    # overlap: at least one bucket is released before the backward ends (mid-network start)
+    assert min(where.values()) <= bwd[-1], where
+
+
+def test_uneven_share_weight_scales_the_gradient_seed():
+    """a rank's weight in an unevenly split global batch scales its loss head's
+    gradient seed (before the all-reduce), not the optimizer's factor after it."""
+    from idc_models_amd.engine import Model, RMSprop
+    from idc_models_amd.models import build_model
+    from idc_models_amd.parallel import OneDeviceStrategy
+    from idc_models_amd.runtime.builder import Builder
+    from idc_models_amd.runtime.program import _lowering_for
+    for arch, kind, typ in (("vgg16", nat.OP_HEAD_FWD, nat.HeadArgs), ("tinycnn", nat.OP_MLP_FWD, nat.Mlp2Args)):
+        net = build_model(arch, None, 1, seed=0)
+        m = Model(net, OneDeviceStrategy("cpu"))
+        m.compile(RMSprop(1e-4), "binary_crossentropy", [], backend="eager")
+        b = Builder(net, m.arena, torch.device("cpu"), 6, True)
+        b.grad_weight = 1.5
+        _lowering_for(net)(b, net, 1, torch.uint8)
+        a = typ.from_buffer_copy(next(op[2] for op in b.ops if op[1] == kind))
+        assert a.loss_scale == pytest.approx(1 / 6)
+        assert a.dl_scale == pytest.approx(1.5 / 6)
+
+
+def test_persistent_launches_need_a_guarded_update():
+    """persistent launches only where a give-up can skip the update on every
+    replica: the fused RMSprop (not a host optimizer) and, under data parallelism, the native
+    communicator's guard all-reduce (not the torch bucketer or central storage)."""
+    from types import SimpleNamespace as NS
+    from idc_models_amd.engine import SGD, RMSprop
+    from idc_models_amd.runtime.program import persistent_allowed
+
+    def model(opt, active=False, native=None, central=False):
+        st = NS(active=active, native_comm=native, central_storage=central)
+        return NS(optimizer=opt, strategy=st, arena=NS(params=[1]))
+    assert persistent_allowed(model(RMSprop(1e-3)), True)
+    assert persistent_allowed(model(RMSprop(1e-3), active=True, native=object()), True)
+    assert not persistent_allowed(model(SGD(0.1)), True)
+    assert not persistent_allowed(model(RMSprop(1e-3, momentum=0.9)), True)
+    assert not persistent_allowed(model(RMSprop(1e-3), active=True, native=None), True)
+    assert not persistent_allowed(model(RMSprop(1e-3), active=True, native=object(), central=True), True)
+    assert persistent_allowed(model(SGD(0.1)), False)  # evaluation programs

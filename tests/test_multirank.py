@@ -6,14 +6,12 @@
   on that batch; FedAvg with 8 clients over 4 ranks equals 1 rank; the masked secure sum of 8
   clients over 4 ranks is bitwise the plain fixed-point sum, through the mod-2^32 ring sum whose
   operands cross 2^31;
-* the communicator watchdog's policy (``parallel/watchdog.py``) with a fake communicator.
+* (the communicator watchdog: ``tests/test_watchdog.py``).
 
 Reference configurations these rehearse: 4 GPUs (``/root/reference/dist_model_tf_dense.py:16-22``),
 8 train clients (``/root/reference/fed_model.py:47-49,207-229``), the secure aggregation round
 (``/root/reference/secure_fed_model.py:156-168``).
 """
-import time
-
 import numpy as np
 import pytest
 import torch
@@ -59,82 +57,6 @@ def test_native_bootstrap_world4_shares_one_unique_id():
     for r, (_, rank, world, device, tmo) in enumerate(res):
         assert (rank, world, device) == (r, 4, r)
         assert tmo > 0  # a world > 1 is created non-blocking, with an init timeout
-
-
-# ---------------------------------------------------------------------------------------------
-# watchdog policy
-
-
-class _WdComm:
-    def __init__(self):
-        self.age = 0.0
-        self.async_err = None
-        self.aborted = 0
-        self.marks = 0
-
-    def check_async(self):
-        if self.async_err:
-            raise RuntimeError(self.async_err)
-
-    def mark_age(self):
-        return self.age
-
-    def mark(self):
-        self.marks += 1
-
-    def abort(self):
-        self.aborted += 1
-
-
-def test_watchdog_aborts_on_stalled_collectives():
-    from idc_models_amd.parallel.watchdog import CommFailure, CommWatchdog
-    c = _WdComm()
-    wd = CommWatchdog(c, timeout_s=5.0)
-    wd.mark()
-    assert c.marks == 1
-    c.age = 4.0
-    assert wd.poll_once() is None and c.aborted == 0
-    wd.raise_if_failed()
-    c.age = 6.0
-    reason = wd.poll_once()
-    assert reason is not None and "no progress" in reason and c.aborted == 1
-    with pytest.raises(CommFailure):
-        wd.raise_if_failed()
-    wd.poll_once()  # sticky: no second abort
-    assert c.aborted == 1
-    wd.mark()
-    assert c.marks == 1  # no marks on an aborted communicator
-
-
-def test_watchdog_aborts_on_async_error_from_its_thread():
-    from idc_models_amd.parallel.watchdog import CommFailure, CommWatchdog
-    c = _WdComm()
-    wd = CommWatchdog(c, timeout_s=100.0, poll_s=0.01).start()
-    try:
-        time.sleep(0.05)
-        assert c.aborted == 0
-        c.async_err = "remote process exited"
-        t0 = time.time()
-        while wd.error is None and time.time() - t0 < 5:
-            time.sleep(0.01)
-        assert c.aborted == 1 and "remote process exited" in wd.error
-        with pytest.raises(CommFailure):
-            wd.raise_if_failed()
-    finally:
-        wd.stop()
-
-
-def test_wait_with_watchdog_raises_when_aborted():
-    from idc_models_amd.parallel.watchdog import CommFailure, CommWatchdog, wait_with_watchdog
-    c = _WdComm()
-    wd = CommWatchdog(c, timeout_s=0.5, poll_s=0.01).start()
-    try:
-        wd.mark()
-        c.age = 1.0  # the mark never completes
-        with pytest.raises(CommFailure):
-            wait_with_watchdog(wd, lambda: False, poll_s=0.01, timeout_s=10)
-    finally:
-        wd.stop()
 
 
 # ---------------------------------------------------------------------------------------------

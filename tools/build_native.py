@@ -34,7 +34,6 @@ SOURCES = [
     "kernels/conv_igemm_g5.hip",
     "kernels/conv_big.hip",
     "kernels/conv_img.hip",
-    "kernels/conv_rows.hip",
     "kernels/conv_stem.hip",
     "kernels/wgrad_stem.hip",
     "kernels/conv_wgrad.hip", "kernels/wgrad_big.hip",

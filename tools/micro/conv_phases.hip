@@ -19,7 +19,6 @@ __device__ unsigned long long g_rt[4096][2];  // s_memrealtime (100 MHz, chip-wi
     }                                                                                       \
   } while (0)
 #include "conv_igemm_impl.h"
-#include "conv_rows.hip"
 
 using namespace idc;
 namespace idc {
@@ -140,16 +139,6 @@ static void run_case(const Case& c) {
   hipEventElapsedTime(&ms, e0, e1);
   printf("%-34s back-to-back %.2f us/launch\n", c.name, ms * 1000.f / 20);
   a.epi_mode = c.epi;
-  if (c.pro == 2 && c.epi == 2 && !conv_rows_ok(a, false)) printf("%-34s conv_rows not eligible\n", c.name);
-  if (c.pro == 2 && c.epi == 2 && conv_rows_ok(a, false)) {  // the row-block kernel on the same op
-    conv_rows(a, false, st);
-    hipEventRecord(e0, st);
-    for (int r = 0; r < 20; ++r) conv_rows(a, false, st);
-    hipEventRecord(e1, st);
-    hipEventSynchronize(e1);
-    hipEventElapsedTime(&ms, e0, e1);
-    printf("%-34s conv_rows back-to-back %.2f us/launch\n", c.name, ms * 1000.f / 20);
-  }
   printf("%-34s tiles=%d  cycles since entry (median over WGs x launches):", c.name,
          ((M + BM - 1) / BM) * ((c.Cout + BN - 1) / BN));
   const char* lbl[] = {"", "tiles_issued", "pro_tab", "epi2_tab", "epi_tab", "ep_prefetch", "loop_start", "loop_end",

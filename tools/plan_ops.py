@@ -87,7 +87,7 @@ def main():
                 ext = nat.load()
                 t0, f32 = plan.get_int(i, 0), plan.get_int(i, 1)
                 for name in a.alt.split(","):
-                    tile, ok = {"img": (ext.TILE_IMG, ext.img_ok), "rows": (ext.TILE_ROWS, ext.rows_ok)}[name]
+                    tile, ok = {"img": (ext.TILE_IMG, ext.img_ok)}[name]
                     if ok(plan.payload(i), f32) and t0 != tile:
                         plan.set_int(i, 0, tile)
                         p.b.reset_tickets()
