@@ -41,8 +41,9 @@ struct DenseStageArgs {
   float* sstats;                // [2][ld] shifted statistics of the stage buffer (single copy)
   const float* sshift;          // [ld] (nullable)
   const DenseLayerDesc* layers; // device table [nlayers]
-  unsigned* sync;               // [2 + 2 * nlayers] ticket, per-phase completion counters, fail flag
-                                // (zeroed before every launch: the program's stats-arena memset)
+  unsigned* sync;               // [dense_stage_sync_words] ticket, per-phase completion counters,
+                                // fail flag, per-tile helper counters (zeroed before every launch:
+                                // the program's stats-arena memset)
   int* err;                     // persistent count of launches that gave up on a wait (nullable)
   float* scratch;               // [nlayers * DS_SCRATCH_PER_LAYER] zeroed per launch (stats arena)
   unsigned long long* stamps;   // nullable: 4 s_memrealtime stamps per work item (diagnostics)
@@ -61,15 +62,34 @@ struct DenseStageArgs {
                                 // up ORs 2 into it (the optimizer then skips the step's update)
   int* hostflag;                // nullable: pinned host word set to 1 on a give-up (never shifted
                                 // per group copy; the runtime polls it without a device sync)
+  float* partials;              // split-K slab [2][A tiles][ksplit-1][256][8] fp32 (ksplit > 1)
+  int ksplit;                   // work items per 1x1 tile (older-channel K split; 0/1: none)
+  int rows;                     // 1: row-resident launch (dense_rows.hip) where its geometry fits
+  int rows_ipg;                 // (set by the launcher) images per row-resident workgroup
 };
 
+// most K splits of an A tile (the helpers' partials: one slab slot each)
+constexpr int DS_MAX_KSPLIT = 8;
 // number of work items of one launch (the grid never needs more workgroups than this)
 int dense_stage_tasks(const DenseStageArgs& a);
-// work items of each phase of one layer: 1x1 tiles (32 rows x 64 channels), 3x3 tiles (32 rows)
-void dense_stage_phase_tiles(int M, int& nA, int& nB);
+// work items of each phase of one layer: 1x1 items (32 rows x 64 channels x 1/ksplit of the
+// older channels), 3x3 tiles (32 rows)
+void dense_stage_phase_tiles(int M, int ksplit, int& nA, int& nB);
+// sync words of a launch: ticket, sharded phase counters, last-slice count, fail flag, and one
+// helper-arrival counter per A tile and layer
+int dense_stage_sync_words(int M, int nlayers);
+// floats of the split-K partial slab (0 for ksplit <= 1)
+long long dense_stage_partial_floats(int M, int ksplit);
+// the K split for a stage of M rows on a grid of `grid` workgroups: 1 (off) unless IDC_DS_KSPLIT
+// forces a value or IDC_DS_KSPLIT_TARGET names the A items aimed at (measured slower, see .hip)
+int dense_stage_default_ksplit(int M, int grid);
 // whether a stage shape fits the launch (cin, staged rows)
 bool dense_stage_shape_ok(int N, int H, int W, int max_cin);
 hipError_t dense_stage_fwd(const DenseStageArgs& a, int grid, hipStream_t st);
+// row-resident form (dense_rows.hip): each workgroup owns whole images for the whole stage and
+// only the BatchNorm statistics cross workgroups (two barriers per layer; none in inference mode)
+bool dense_rows_geometry(int N, int H, int W, int ld, int max_cin, int& rb, int& ipg, int& grid);
+hipError_t dense_rows_fwd(const DenseStageArgs& a, hipStream_t st);
 
 // ---------------------------------------------------------------------------------------------
 // Persistent dense-stage BACKWARD (dense_stage_bwd.hip): the data gradients of every dense layer

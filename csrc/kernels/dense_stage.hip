@@ -96,9 +96,10 @@ __device__ __forceinline__ v8bf bn_act8(const uint4& x, const float* sc, const f
 // (row length ld), read agent-coherently (some of them were written in this launch); each thread's
 // loads of a batch of 4 channels are all issued before the arithmetic
 __device__ __forceinline__ void bn_table(const float* st, int ld, const float* shift, const float* g,
-                                         const float* b, float inv_n, float eps, int C, float* sc, float* sh) {
+                                         const float* b, float inv_n, float eps, int C0, int C, float* sc,
+                                         float* sh) {
   const int tid = threadIdx.x;
-  for (int base = 0; base < C; base += 4 * NT) {
+  for (int base = C0; base < C; base += 4 * NT) {
     float s0[4], s1[4], k[4], gg[4], bb[4];
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
@@ -141,6 +142,8 @@ __global__ __launch_bounds__(NT) void dense_stage_kernel(DenseStageArgs a, Group
   auto cntB = [&](int l) { return sync + 9 + 16 * l; };
   unsigned* lastfin = sync + 1 + 16 * a.nlayers;
   unsigned* fail = lastfin + 1;  // this launch gave up (zeroed with the counters)
+  unsigned* tilecnt = fail + 1;  // [nlayers][nT] helper partials arrived per A tile
+  float* partials = gsh(a.partials, go);
   int* err = gsh(a.err, go);
   const persist::FailSink fsink{err, gsh(a.stepflag, go), a.hostflag};
   float* scratch = gsh(a.scratch, go);
@@ -153,7 +156,12 @@ __global__ __launch_bounds__(NT) void dense_stage_kernel(DenseStageArgs a, Group
   const int fr = lane & 15, fk = (lane >> 4) * 8;
   const int HW = a.H * a.W, M = a.N * HW;
   const int nmt = (M + 31) / 32;
-  const int nA = 2 * nmt, nB = nmt;
+  // split K: an A tile's older channels are spread over KS work items -- KS-1 helpers (queued
+  // first) hand fp32 partial tiles to the tile's finalizer, which adds them, runs the newest-slice
+  // step and the epilogue
+  const int KS = a.ksplit > 1 ? a.ksplit : 1;
+  const int nT = 2 * nmt, nH = nT * (KS - 1);
+  const int nA = nT * KS, nB = nmt;
   const int per = nA + nB, total = per * a.nlayers;
   const int taps = a.k2 * a.k2, pad = a.k2 >> 1;
   const float lo1 = act_lo(a.act1), hi1 = act_hi(a.act1);
@@ -205,9 +213,15 @@ __global__ __launch_bounds__(NT) void dense_stage_kernel(DenseStageArgs a, Group
       const float* __restrict__ tsh = gsh(d.tshift, go);
       const float* __restrict__ g1 = gsh(d.g1, go);
       const float* __restrict__ b1 = gsh(d.b1, go);
-      const int mt = r >> 1, n0 = (r & 1) * 64, m0 = mt * 32;
+      const bool helper = r < nH;
+      const int tile = helper ? r / (KS - 1) : r - nH;
+      const int ks = helper ? 1 + r % (KS - 1) : 0;
+      const int mt = tile >> 1, n0 = (tile & 1) * 64, m0 = mt * 32;
       const int cin = d.cin;
       const int cold = l == 0 ? cin : cin - 32;  // channels final before B_{l-1}
+      // this item's share of the older channels, in 32-channel k-steps
+      const int nst = cold >> 5;
+      const int k_lo = (ks * nst / KS) * 32, k_hi = ((ks + 1) * nst / KS) * 32;
       const bf16_t* wrow = w1 + (size_t)(n0 + wid * 16 + fr) * cin;  // this lane's B column
       const v8bf bnew = l > 0 ? *reinterpret_cast<const v8bf*>(wrow + cold + fk) : v8bf{};
       const int erow = tid >> 3, ecol = (tid & 7) * 8;
@@ -236,23 +250,23 @@ __global__ __launch_bounds__(NT) void dense_stage_kernel(DenseStageArgs a, Group
       auto load_a = [&](int ch) {
 #pragma unroll
         for (int u = 0; u < 4; ++u) {
-          const int c = ch * ACH + sseg + u * 64;
-          ar[u] = (srow < M && c < cold) ? ld_coh16(buf + (size_t)srow * a.ld + c) : make_uint4(0, 0, 0, 0);
+          const int c = k_lo + ch * ACH + sseg + u * 64;
+          ar[u] = (srow < M && c < k_hi) ? ld_coh16(buf + (size_t)srow * a.ld + c) : make_uint4(0, 0, 0, 0);
         }
       };
       auto load_b = [&](int ch, v8bf (&bq)[8]) {
 #pragma unroll
         for (int i = 0; i < 8; ++i) {
-          const int k = ch * ACH + i * 32;
-          bq[i] = k < cold ? *reinterpret_cast<const v8bf*>(wrow + k + fk) : v8bf{};
+          const int k = k_lo + ch * ACH + i * 32;
+          bq[i] = k < k_hi ? *reinterpret_cast<const v8bf*>(wrow + k + fk) : v8bf{};
         }
       };
       auto stage = [&](int ch) {
         bf16_t* ab = s.u.a[ch & 1] + (tid >> 3) * APITCH + sseg;
 #pragma unroll
         for (int u = 0; u < 4; ++u) {
-          const int c = ch * ACH + sseg + u * 64;
-          const bool keep = srow < M && c < cold;
+          const int c = k_lo + ch * ACH + sseg + u * 64;
+          const bool keep = srow < M && c < k_hi;
           const int cc = keep ? c : 0;
           *reinterpret_cast<v8bf*>(ab + u * 64) = bn_act8(ar[u], s.sc + cc, s.sh + cc, lo1, hi1, keep);
         }
@@ -261,7 +275,7 @@ __global__ __launch_bounds__(NT) void dense_stage_kernel(DenseStageArgs a, Group
         const bf16_t* ab = s.u.a[ch & 1];
 #pragma unroll
         for (int i = 0; i < 8; ++i) {
-          if (ch * ACH + i * 32 < cold) {
+          if (k_lo + ch * ACH + i * 32 < k_hi) {
 #pragma unroll
             for (int h = 0; h < 2; ++h) {
               const v8bf af = *reinterpret_cast<const v8bf*>(ab + (h * 16 + fr) * APITCH + i * 32 + fk);
@@ -270,7 +284,7 @@ __global__ __launch_bounds__(NT) void dense_stage_kernel(DenseStageArgs a, Group
           }
         }
       };
-      const int nch = (cold + ACH - 1) / ACH;
+      const int nch = (k_hi - k_lo + ACH - 1) / ACH;
       v8bf bq0[8], bq1[8];
       load_a(0);
       load_b(0, bq0);
@@ -279,18 +293,20 @@ __global__ __launch_bounds__(NT) void dense_stage_kernel(DenseStageArgs a, Group
       // layer's own moving statistics; the statistics of the stage buffer are still produced
       // for the trainable layers after it (unless the whole launch is inference mode)
       const bool inf1 = a.infer || (d.pad_ & 1);
-      if (inf1) {  // inference mode: the layer's own moving statistics, every channel at once
+      if (inf1) {  // inference mode: the layer's own moving statistics (the finalizer's newest slice too)
         const float* __restrict__ mm = gsh(d.mm1, go);
         const float* __restrict__ mv = gsh(d.mv1, go);
-        for (int c = tid; c < cin; c += NT) {
+        const int c_end = helper ? k_hi : cin;
+        for (int c = k_lo + tid; c < c_end; c += NT) {
+          if (c >= k_hi && c < cold) continue;
           const float rr = g1[c] * rsqrtf(mv[c] + d.eps1);
           s.sc[c] = rr;
           s.sh[c] = b1[c] - mm[c] * rr;
         }
       } else {
-        bn_table(sstats, a.ld, sshift, g1, b1, a.inv_count, d.eps1, ccanon, s.sc, s.sh);
+        bn_table(sstats, a.ld, sshift, g1, b1, a.inv_count, d.eps1, k_lo, min(ccanon, k_hi), s.sc, s.sh);
       }
-      if (!inf1 && l >= 2 && tid < 32) {
+      if (!inf1 && l >= 2 && ccanon >= k_lo && ccanon < k_hi && tid < 32) {
         float s0, s1, mean, var;
         slot_sum<S>(lslots - 2 * DS_SCRATCH_PER_LAYER, 32, tid, s0, s1);
         const int c = ccanon + tid;
@@ -322,14 +338,43 @@ __global__ __launch_bounds__(NT) void dense_stage_kernel(DenseStageArgs a, Group
       }
 
       stamp(stamps, task, 2);
-      // ---- the newest slice [cold, cin): wait for B_{l-1}
-      if (l > 0) {
+      float* pslab = partials + (size_t)(l & 1) * nH * (NT * 8);  // layers l and l+2 alternate
+      if (helper) {
+        // ---- a helper's partial tile (MFMA register layout, 32 B per thread) to the finalizer.
+        // The slab slot is free again: the previous layer of this parity finished its finalizers
+        // before B of that layer ran, which this item's B_{l-2} wait (l >= 2) ordered before it
+        float* dst = pslab + ((size_t)tile * (KS - 1) + (ks - 1)) * (NT * 8) + tid * 8;
+        st_coh16(dst, __builtin_bit_cast(uint4, acc[0]));
+        st_coh16(dst + 4, __builtin_bit_cast(uint4, acc[1]));
+        publish(tilecnt + (size_t)l * nT + tile);
+        continue;
+      }
+      // ---- the newest slice [cold, cin): wait for B_{l-1}; and this tile's helpers
+      if (l > 0 || KS > 1) {
         if (wid == 0) {
-          const bool ok = wait_sum8(cntB(l - 1), (unsigned)nB, fail, fsink, max_polls);
+          bool ok = l == 0 || wait_sum8(cntB(l - 1), (unsigned)nB, fail, fsink, max_polls);
+          if (ok && KS > 1 && lane == 0)
+            ok = wait_count(tilecnt + (size_t)l * nT + tile, (unsigned)(KS - 1), fail, fsink, max_polls);
           if (lane == 0) s.bad = !ok;
         }
         __syncthreads();
         if (__builtin_amdgcn_readfirstlane(s.bad)) return;
+      }
+      if (KS > 1) {  // the helpers' partials, all loads in flight together
+        uint4 pv[2 * (DS_MAX_KSPLIT - 1)];
+        const float* src = pslab + (size_t)tile * (KS - 1) * (NT * 8) + tid * 8;
+#pragma unroll
+        for (int h = 0; h < DS_MAX_KSPLIT - 1; ++h)
+          if (h < KS - 1) {
+            pv[2 * h] = ld_coh16(src + (size_t)h * (NT * 8));
+            pv[2 * h + 1] = ld_coh16(src + (size_t)h * (NT * 8) + 4);
+          }
+#pragma unroll
+        for (int h = 0; h < DS_MAX_KSPLIT - 1; ++h)
+          if (h < KS - 1) {
+            acc[0] += __builtin_bit_cast(v4f, pv[2 * h]);
+            acc[1] += __builtin_bit_cast(v4f, pv[2 * h + 1]);
+          }
       }
       stamp(stamps, task, 3);
       if (l > 0) {
@@ -347,7 +392,7 @@ __global__ __launch_bounds__(NT) void dense_stage_kernel(DenseStageArgs a, Group
             s.sc[c] = rr;
             s.sh[c] = b1[c] - mean * rr;
           }
-          if (r == 0) {  // the slice's single-copy statistics (read by later layers' tables)
+          if (tile == 0) {  // the slice's single-copy statistics (read by later layers' tables)
             st_coh(sstats + c, s0);
             st_coh(sstats + a.ld + c, s1);
           }
@@ -398,7 +443,7 @@ __global__ __launch_bounds__(NT) void dense_stage_kernel(DenseStageArgs a, Group
       }
       stamp(stamps, task, 6);
       {
-        const unsigned o = publish_shard(cntA(l), r);
+        const unsigned o = publish_shard(cntA(l), tile);
         if (stamps && tid == 0) stamps[(size_t)task * NSTAMP + 7] = __builtin_amdgcn_s_memrealtime() + (o & 0u);
       }
     } else {
@@ -457,7 +502,7 @@ __global__ __launch_bounds__(NT) void dense_stage_kernel(DenseStageArgs a, Group
       }
       stamp(stamps, task, 1);
       if (wid == 0) {
-        const bool ok = wait_sum8(cntA(l), (unsigned)nA, fail, fsink, max_polls);
+        const bool ok = wait_sum8(cntA(l), (unsigned)nT, fail, fsink, max_polls);
         if (lane == 0) s.bad = !ok;
       }
       __syncthreads();
@@ -583,16 +628,43 @@ __global__ __launch_bounds__(NT) void dense_stage_kernel(DenseStageArgs a, Group
   }
 }
 
-void dense_stage_phase_tiles(int M, int& nA, int& nB) {
+void dense_stage_phase_tiles(int M, int ksplit, int& nA, int& nB) {
   const int nmt = (M + 31) / 32;
-  nA = 2 * nmt;
+  nA = 2 * nmt * (ksplit > 1 ? ksplit : 1);
   nB = nmt;
 }
 
 int dense_stage_tasks(const DenseStageArgs& a) {
   int nA, nB;
-  dense_stage_phase_tiles(a.N * a.H * a.W, nA, nB);
+  dense_stage_phase_tiles(a.N * a.H * a.W, a.ksplit, nA, nB);
   return a.nlayers * (nA + nB);
+}
+
+int dense_stage_sync_words(int M, int nlayers) {
+  const int nmt = (M + 31) / 32;
+  return 3 + 16 * nlayers + 2 * nmt * nlayers;
+}
+
+long long dense_stage_partial_floats(int M, int ksplit) {
+  if (ksplit <= 1) return 0;
+  const long long nmt = (M + 31) / 32;
+  return 2LL * (2 * nmt) * (ksplit - 1) * NT * 8;
+}
+
+int dense_stage_default_ksplit(int M, int grid) {
+  // Opt-in (round 6, bench.py A/B on one box, DenseNet-121 bs 256): stage 4 split 8 ways took its
+  // older-channel accumulation from 12.9 to 2.6 us, but the finalizers then waited ~12 us for the
+  // previous 3x3 phase instead -- the per-layer chain is the two hand-offs, not the accumulation
+  // -- and the step went 3.46-3.48 -> 3.52-3.56 ms (stage 3 split 3 as well: 3.69-3.72 ms).
+  const char* e = std::getenv("IDC_DS_KSPLIT");
+  int ks = 1;
+  if (e && e[0]) {
+    ks = std::atoi(e);
+  } else if (const char* t = std::getenv("IDC_DS_KSPLIT_TARGET")) {
+    const int target = t[0] ? std::atoi(t) : (grid > 0 ? grid : 256);
+    ks = target / (2 * ((M + 31) / 32));
+  }
+  return ks < 1 ? 1 : ks > DS_MAX_KSPLIT ? DS_MAX_KSPLIT : ks;
 }
 
 bool dense_stage_shape_ok(int N, int H, int W, int max_cin) {
@@ -608,8 +680,10 @@ bool dense_stage_shape_ok(int N, int H, int W, int max_cin) {
 hipError_t dense_stage_fwd(const DenseStageArgs& a, int grid, hipStream_t st) {
   if (a.nlayers < 1 || (a.k2 != 1 && a.k2 != 3) || a.ld % 8 != 0 || a.N < 1 || a.H < 1 || a.W < 1 ||
       a.buf == nullptr || a.layers == nullptr || a.sync == nullptr ||
-      (!a.infer && (a.sstats == nullptr || a.scratch == nullptr)) || !dense_stage_shape_ok(a.N, a.H, a.W, 0))
+      (!a.infer && (a.sstats == nullptr || a.scratch == nullptr)) || !dense_stage_shape_ok(a.N, a.H, a.W, 0) ||
+      a.ksplit > DS_MAX_KSPLIT || (a.ksplit > 1 && a.partials == nullptr))
     return hipErrorInvalidValue;
+  if (a.rows && dense_rows_fwd(a, st) == hipSuccess) return hipSuccess;
   const int tasks = dense_stage_tasks(a);
   if (grid <= 0) grid = 256;
   // a grouped launch (K copies, each with its own queue) shares the CUs
@@ -617,16 +691,16 @@ hipError_t dense_stage_fwd(const DenseStageArgs& a, int grid, hipStream_t st) {
   if (k > 1) grid = grid / k > 8 ? grid / k : 8;
   if (grid > tasks) grid = tasks;
   // the lookahead queue order lets an A phase wait on the B phase queued after it: it needs more
-  // than nA workgroups of this queue resident at once, so it is used for one ungrouped launch
-  // whose grid (one workgroup per CU, 2 fit) exceeds nA with margin (IDC_DS_LOOKAHEAD=0: off)
+  // than nT (A tiles) workgroups of this queue resident at once, so it is used for one ungrouped
+  // launch whose grid (one workgroup per CU, 2 fit) exceeds nT with margin (IDC_DS_LOOKAHEAD=0: off)
   static const bool la_on = [] {
     const char* e = std::getenv("IDC_DS_LOOKAHEAD");
     return !(e && e[0] == '0');
   }();
-  int nA, nB;
-  dense_stage_phase_tiles(a.N * a.H * a.W, nA, nB);
+  // (split K: only the finalizers, one per A tile, wait on a later ticket -- their B phase)
+  const int nT = 2 * ((a.N * a.H * a.W + 31) / 32);
   DenseStageArgs b = a;
-  b.lookahead = (a.lookahead >= 0 && la_on && k == 1 && a.nlayers > 1 && grid >= nA + 16) ? 1 : 0;
+  b.lookahead = (a.lookahead >= 0 && la_on && k == 1 && a.nlayers > 1 && grid >= nT + 16) ? 1 : 0;
   hipLaunchKernelGGL(dense_stage_kernel, ggrid(grid), dim3(NT), 0, st, b, garg());
   return hipGetLastError();
 }

@@ -1086,11 +1086,20 @@ PYBIND11_MODULE(_idc_native, m) {
     if (s.size() != sizeof(DenseStageArgs)) throw std::runtime_error("dense_stage_tasks: bad payload");
     return dense_stage_tasks(*reinterpret_cast<const DenseStageArgs*>(s.data()));
   });
-  m.def("dense_stage_phase_tiles", [](int M) {
+  m.def("dense_stage_phase_tiles", [](int M, int ksplit) {
     int nA, nB;
-    dense_stage_phase_tiles(M, nA, nB);
+    dense_stage_phase_tiles(M, ksplit, nA, nB);
     return py::make_tuple(nA, nB);
+  }, py::arg("M"), py::arg("ksplit") = 1);
+  m.def("dense_stage_sync_words", &dense_stage_sync_words);
+  m.def("dense_rows_geometry", [](int N, int H, int W, int ld, int max_cin) {
+    int rb = 0, ipg = 0, grid = 0;
+    const bool ok = dense_rows_geometry(N, H, W, ld, max_cin, rb, ipg, grid);
+    return py::make_tuple(ok, rb, ipg, grid);
   });
+  m.def("dense_stage_partial_floats", &dense_stage_partial_floats);
+  m.def("dense_stage_default_ksplit", &dense_stage_default_ksplit);
+  m.attr("DS_MAX_KSPLIT") = DS_MAX_KSPLIT;
   m.def("dense_stage_shape_ok", &dense_stage_shape_ok);
   m.attr("DS_SCRATCH_PER_LAYER") = DS_SCRATCH_PER_LAYER;
   m.attr("DS_MAX_CIN") = DS_MAX_CIN;

@@ -146,7 +146,8 @@ class DenseStageArgs(C.Structure):
                 ("scratch", vp), ("stamps", vp),
                 ("N", ci), ("H", ci), ("W", ci), ("ld", ci), ("nlayers", ci), ("k2", ci),
                 ("act1", ci), ("act2", ci), ("inv_count", cf), ("max_polls", C.c_uint), ("lookahead", ci),
-                ("infer", ci), ("stepflag", vp), ("hostflag", vp)]
+                ("infer", ci), ("stepflag", vp), ("hostflag", vp), ("partials", vp), ("ksplit", ci),
+                ("rows", ci), ("rows_ipg", ci)]
 
 
 class DenseBwdLayerDesc(C.Structure):

@@ -434,7 +434,7 @@ def bn_moments(stats: torch.Tensor, count: int, shift: Optional[torch.Tensor] = 
 
 def dense_stage(buf: torch.Tensor, sstats: torch.Tensor, layers, sshift: Optional[torch.Tensor] = None,
                 act: int = RELU, grid: int = 256, k2: int = 3, max_polls: int = 0, stamps: bool = False,
-                infer: bool = False):
+                infer: bool = False, ksplit: int = 1, rows: int = 0):
     """All dense layers of a DenseNet stage in one persistent launch (csrc/kernels/dense_stage.hip).
 
     ``buf``: NHWC bf16 stage buffer [N, H, W, ld] whose channels [0, c0) are filled and whose
@@ -444,7 +444,10 @@ def dense_stage(buf: torch.Tensor, sstats: torch.Tensor, layers, sshift: Optiona
     ``max_polls``: bound on each wait (0: the kernel's default; tests force timeouts with 1).
     ``infer``: inference-mode BatchNorms from each layer's mm1 / mv1 ([cin]) and mm2 / mv2 ([128])
     moving statistics; no statistics are produced (``sstats`` may be None).
-    Returns (sync counters, err counter, stamps or None) for inspection."""
+    ``ksplit``: work items per 1x1 tile (split K of the older channels, <= DS_MAX_KSPLIT).
+    ``rows``: 1 runs the row-resident launch (dense_rows.hip) where its geometry fits.
+    Returns (sync counters [ticket, 16 per layer, last-slice count, fail], err counter, stamps or
+    None) for inspection."""
     N, H, W, ld = buf.shape
     ext = nat.require()
     if max(L["cin"] for L in layers) > int(ext.DS_MAX_CIN) or not ext.dense_stage_shape_ok(N, H, W, 0):
@@ -460,7 +463,10 @@ def dense_stage(buf: torch.Tensor, sstats: torch.Tensor, layers, sshift: Optiona
     import ctypes
     tab = torch.frombuffer(bytearray(ctypes.string_at(ctypes.addressof(arr), ctypes.sizeof(arr))),
                            dtype=torch.uint8).to(buf.device)
-    sync = torch.zeros(3 + 16 * len(layers), dtype=torch.int32, device=buf.device)
+    M = N * H * W
+    sync = torch.zeros(int(ext.dense_stage_sync_words(M, len(layers))), dtype=torch.int32, device=buf.device)
+    pfl = int(ext.dense_stage_partial_floats(M, ksplit))
+    partials = torch.zeros(max(pfl, 1), dtype=torch.float32, device=buf.device)
     err = torch.zeros(1, dtype=torch.int32, device=buf.device)
     scratch = torch.zeros(int(ext.DS_SCRATCH_PER_LAYER) * len(layers), dtype=torch.float32, device=buf.device)
     a = nat.DenseStageArgs()
@@ -472,13 +478,16 @@ def dense_stage(buf: torch.Tensor, sstats: torch.Tensor, layers, sshift: Optiona
     a.act1 = a.act2 = act
     a.inv_count = 1.0 / float(N * H * W)
     a.max_polls = max_polls
+    a.ksplit = ksplit
+    a.partials = partials.data_ptr() if pfl else 0
+    a.rows = rows
     st = None
     if stamps:
         st = torch.zeros(8 * int(ext.dense_stage_tasks(nat.raw(a))), dtype=torch.int64, device=buf.device)
         a.stamps = st.data_ptr()
     _plan1(nat.OP_DENSE_STAGE, a, ints=(grid, len(layers)), ptrs=(tab.data_ptr(),))
     torch.cuda.current_stream().synchronize()
-    return sync, err, st
+    return sync[:3 + 16 * len(layers)], err, st
 
 
 def dense_bwd_queue(L: int, nmt: int, c0: int, kg: int):

@@ -867,9 +867,18 @@ class Builder:
         ext = nat.load()
         # counters and the in-launch statistics slots live in the stats arena: zeroed every step
         # (a program without a stats-arena reset -- evaluation -- zeroes its counters itself)
-        sync = self._stats_floats(3 + 16 * len(layers))  # ticket, sharded phase counters, fail
+        M = buf.N * H * W
+        # ticket, sharded phase counters, fail flag, per-tile split-K helper counters
+        sync = self._stats_floats(int(ext.dense_stage_sync_words(M, len(layers))))
         if not self.training:
             self.memset(sync)
+        # split K of the 1x1 phases' older-channel accumulation (dense_stage.hip): enough items
+        # per phase to occupy the launch's grid (stage 4 at bs 256: 16 tiles x 8); not in grouped
+        # programs (their K copies share the grid)
+        grid = int(os.environ.get("IDC_DS_GRID", "256"))
+        ksplit = 1 if getattr(self, "grouped", False) else int(ext.dense_stage_default_ksplit(M, grid))
+        pfl = int(ext.dense_stage_partial_floats(M, ksplit))
+        partials = self.alloc((pfl,), F32) if pfl else None
         scratch = self._stats_floats(int(ext.DS_SCRATCH_PER_LAYER) * len(layers)) if not infer else None
         a = nat.DenseStageArgs()
         a.buf = buf.ptr
@@ -883,13 +892,19 @@ class Builder:
         a.inv_count = 1.0 / float(buf.N * H * W)
         a.max_polls = int(os.environ.get("IDC_DS_MAX_POLLS", "0"))
         a.lookahead = -1 if self.shared_device else 0
+        a.ksplit = ksplit
+        a.partials = partials.data_ptr() if partials is not None else 0
+        # row-resident form (dense_rows.hip: whole images per workgroup, only BatchNorm statistics
+        # cross workgroups) where its geometry fits; not beside other launches of its kind
+        # (grouped programs, concurrent federated clients: its workgroups must be co-resident)
+        a.rows = 1 if (os.environ.get("IDC_DS_ROWS", "0") == "1" and not getattr(self, "grouped", False)
+                       and not self.shared_device) else 0
         self._fail_words(a)
         if os.environ.get("IDC_DS_STAMPS", "0") == "1":
             # per-work-item s_memrealtime stamps (tools/dense_stamps.py reads them after a step)
             stamps = self.alloc((8 * int(ext.dense_stage_tasks(nat.raw(a))),), torch.int64)
             a.stamps = stamps.data_ptr()
-            self.dense_stamps = getattr(self, "dense_stamps", []) + [(stamps, len(layers), buf.N * H * W)]
-        grid = int(os.environ.get("IDC_DS_GRID", "256"))
+            self.dense_stamps = getattr(self, "dense_stamps", []) + [(stamps, len(layers), M, ksplit)]
         self.emit(nat.OP_DENSE_STAGE, a, ints=(grid, len(layers)), ptrs=(tab.data_ptr(),))
 
     def dense_stage_bwd_ok(self, buf: Tensor4, layers, pend: "BNRef") -> bool:

@@ -842,10 +842,21 @@ def test_wgrad_batch_matches_single_launches(fn, kind, N, H):
         assert relerr(o, r) < 1.5e-2
 
 
-@pytest.mark.parametrize("N,H,c0,L,grid", [(4, 3, 64, 3, 256), (6, 1, 96, 4, 7), (3, 5, 32, 2, 1),
-                                          (8, 6, 64, 3, 64), (2, 1, 1120, 3, 256), (5, 2, 256, 4, 256),
-                                          (256, 3, 256, 24, 256)])
-def test_dense_stage_persistent_matches_reference(fn, N, H, c0, L, grid):
+@pytest.mark.parametrize("N,H,c0,L,grid,ks", [(4, 3, 64, 3, 256, 1), (6, 1, 96, 4, 7, 1), (3, 5, 32, 2, 1, 1),
+                                             (8, 6, 64, 3, 64, 1), (2, 1, 1120, 3, 256, 1), (5, 2, 256, 4, 256, 1),
+                                             (256, 3, 256, 24, 256, 1),
+                                             # split K of the older channels (helpers + finalizer)
+                                             (2, 1, 1120, 3, 256, 8), (4, 3, 64, 3, 256, 3), (6, 1, 96, 4, 7, 4),
+                                             (3, 5, 32, 2, 1, 2), (256, 1, 512, 16, 256, 8),
+                                             (256, 3, 256, 24, 256, 2),
+                                             # row-resident launch (ks = -1 / -2: dense_rows.hip
+                                             # with 1 / 2 row blocks per workgroup)
+                                             (4, 3, 64, 3, 256, -2), (6, 1, 96, 4, 7, -1),
+                                             (3, 5, 32, 2, 1, -2), (5, 2, 256, 4, 256, -2),
+                                             (2, 1, 1120, 3, 256, -1), (256, 3, 256, 24, 256, -2),
+                                             (256, 3, 256, 24, 256, -1), (256, 1, 512, 16, 256, -2),
+                                             (256, 1, 512, 16, 256, -1)])
+def test_dense_stage_persistent_matches_reference(fn, N, H, c0, L, grid, ks, monkeypatch):
     """The persistent dense-stage launch (work queue + per-phase completion counters, 1x1 partial
     sums over the finished channels accumulated before the newest slice is waited for, slotted
     in-launch statistics) vs a PyTorch fp32 reference of the same dense layers:
@@ -854,7 +865,16 @@ def test_dense_stage_persistent_matches_reference(fn, N, H, c0, L, grid):
     grid 7 / 1: far fewer workgroups than tiles (the queue must still drain: every wait depends only
     on earlier tickets).  c0 1120: DenseNet-201-wide inputs (cin > 1024, several 256-channel
     staging chunks); 2x2 maps: DenseNet-201 @ 32x32's stage 3; (256, 3, 256, 24): DenseNet-121's
-    stage 3 at the bench batch exactly (M = 2,304, 24 layers, cin 256 -> 992, lookahead order)."""
+    stage 3 at the bench batch exactly (M = 2,304, 24 layers, cin 256 -> 992, lookahead order);
+    (256, 1, 512, 16): its stage 4.  ks > 1: each 1x1 tile's older channels split over ks work
+    items whose fp32 partials the tile's finalizer adds (grid 1 / 7: helpers queued before their
+    finalizer, so the queue drains with any number of workgroups).  ks < 0: the row-resident
+    launch with -ks row blocks (16 rows each) of whole images per workgroup."""
+    if ks < 0:
+        monkeypatch.setenv("IDC_DS_ROWS_RB", str(-ks))
+        ext = fn.nat.require()
+        ok, rb, ipg, g = ext.dense_rows_geometry(N, H, H, c0 + 32 * L, c0 + 32 * (L - 1))
+        assert ok and rb == -ks, (ok, rb, ipg, g)
     W = H
     ld = c0 + 32 * L
     g = torch.Generator(device="cpu").manual_seed(N * 100 + H)
@@ -905,12 +925,16 @@ def test_dense_stage_persistent_matches_reference(fn, N, H, c0, L, grid):
         rst[ld + cin:ld + cin + 32] = (yk * yk).sum(0)
         rts.append(t)
         rtst.append(tst)
-    sync, err, _ = fn.dense_stage(buf, sst, lays, sshift=K, grid=grid, k2=k2)
+    sync, err, _ = fn.dense_stage(buf, sst, lays, sshift=K, grid=grid, k2=k2, ksplit=max(ks, 1), rows=int(ks < 0))
     M = N * H * W
     nA, nB = -(-M // 32) * 2, -(-M // 32)
     assert int(err[0].item()) == 0 and int(sync[-1].item()) == 0
     cnt = sync[1:1 + 16 * L].reshape(L, 2, 8).sum(-1)  # per layer: A_l, B_l sharded counters
-    assert cnt[:, 0].tolist() == [nA] * L and cnt[:, 1].tolist() == [nB] * L, sync.tolist()
+    if ks < 0:  # barrier arrivals: every workgroup at both barriers of every layer but the last
+        G = -(-N // ipg)
+        assert cnt[:-1, 0].tolist() == [G] * (L - 1) and cnt[:-1, 1].tolist() == [G] * (L - 1), sync.tolist()
+    else:
+        assert cnt[:, 0].tolist() == [nA] * L and cnt[:, 1].tolist() == [nB] * L, sync.tolist()
     errs = {}
     for i, d in enumerate(lays):
         errs[f"t{i}"] = relerr(d["t"].float(), rts[i])
@@ -920,7 +944,8 @@ def test_dense_stage_persistent_matches_reference(fn, N, H, c0, L, grid):
     assert all(v < 2e-2 for v in errs.values()), errs
 
 
-def test_dense_stage_timeout_is_counted(fn):
+@pytest.mark.parametrize("ks", [1, 4])
+def test_dense_stage_timeout_is_counted(fn, ks):
     """A wait that gives up (poll bound forced to 1) fails the launch: every workgroup leaves and
     the persistent error counter records it (dense_stage.hip wait_count)."""
     N, H, c0, L = 64, 3, 64, 4
@@ -939,14 +964,14 @@ def test_dense_stage_timeout_is_counted(fn):
                          g2=torch.ones(128, device=DEV), b2=torch.zeros(128, device=DEV),
                          t=torch.zeros(N, H, H, 128, dtype=torch.bfloat16, device=DEV),
                          tstats=torch.zeros(256, device=DEV), tshift=None, eps1=1e-5, eps2=1e-5, cin=cin))
-    sync, err, _ = fn.dense_stage(buf, sst, lays, grid=256, k2=3, max_polls=1)
+    sync, err, _ = fn.dense_stage(buf, sst, lays, grid=256, k2=3, max_polls=1, ksplit=ks)
     assert int(sync[-1].item()) == 1 and int(err[0].item()) == 1, (sync.tolist(), err.tolist())
     # the same launch with the default bound completes
     sst2 = torch.zeros(2 * ld, device=DEV)
     sst2[:c0], sst2[ld:ld + c0] = x0.sum(0), (x0 * x0).sum(0)
     for d in lays:
         d["tstats"].zero_()
-    sync, err, _ = fn.dense_stage(buf, sst2, lays, grid=256, k2=3)
+    sync, err, _ = fn.dense_stage(buf, sst2, lays, grid=256, k2=3, ksplit=ks)
     assert int(sync[-1].item()) == 0 and int(err[0].item()) == 0
 
 
@@ -1060,8 +1085,11 @@ def test_secagg_segment_absmax_matches_torch():
     assert torch.equal(got, ref), (got, ref)
 
 
-@pytest.mark.parametrize("N,H,c0,L,grid", [(4, 3, 64, 3, 256), (6, 1, 96, 4, 7), (2, 1, 1120, 3, 256)])
-def test_dense_stage_inference_mode_matches_reference(fn, N, H, c0, L, grid):
+@pytest.mark.parametrize("N,H,c0,L,grid,ks", [(4, 3, 64, 3, 256, 1), (6, 1, 96, 4, 7, 1), (2, 1, 1120, 3, 256, 1),
+                                             (6, 1, 96, 4, 7, 3), (2, 1, 1120, 3, 256, 8),
+                                             (4, 3, 64, 3, 256, -2), (6, 1, 96, 4, 7, -1),
+                                             (2, 1, 1120, 3, 256, -1)])
+def test_dense_stage_inference_mode_matches_reference(fn, N, H, c0, L, grid, ks, monkeypatch):
     """Inference-mode dense stage (frozen base / evaluation): BN1 and BN2 from each layer's own
     moving statistics, nothing produced but t and the stage-buffer slices, vs a PyTorch reference."""
     W = H
@@ -1096,7 +1124,10 @@ def test_dense_stage_inference_mode_matches_reference(fn, N, H, c0, L, grid):
         a2 = bf(torch.relu((t - d["mm2"]) * torch.rsqrt(d["mv2"] + d["eps2"]) * d["g2"] + d["b2"]))
         rbuf[..., cin:cin + 32] = bf(ref_conv(a2, w2, 1, (1, 1, 1, 1)))
         rts.append(t)
-    sync, err, _ = fn.dense_stage(buf, None, lays, grid=grid, k2=k2, infer=True)
+    if ks < 0:
+        monkeypatch.setenv("IDC_DS_ROWS_RB", str(-ks))
+    sync, err, _ = fn.dense_stage(buf, None, lays, grid=grid, k2=k2, infer=True, ksplit=max(ks, 1),
+                                  rows=int(ks < 0))
     assert int(err[0].item()) == 0 and int(sync[-1].item()) == 0
     errs = {f"t{i}": relerr(d["t"].float(), rts[i]) for i, d in enumerate(lays)}
     errs["buf"] = relerr(buf.float(), rbuf)

@@ -41,6 +41,7 @@ SOURCES = [
     "kernels/pool_img.hip",
     "kernels/dwconv.hip",
     "kernels/dense_stage.hip",
+    "kernels/dense_rows.hip",
     "kernels/mb_chain.hip",
     "kernels/dense_stage_bwd.hip",
     "kernels/mlp_head.hip",

@@ -70,16 +70,16 @@ def _table(rows, title):
     return out
 
 
-def analyse_fwd(st, nlayers: int, M: int):
+def analyse_fwd(st, nlayers: int, M: int, ksplit: int = 1):
     import numpy as np
     nmt = (M + 31) // 32
-    nA, nB = 2 * nmt, nmt
+    nA, nB = 2 * nmt * max(1, ksplit), nmt  # split K: helpers (no stamps past 2) + finalizers
     per = nA + nB
     a = st.reshape(nlayers * per, NSTAMP).astype(np.float64)
     a[a == 0] = np.nan  # stamp points a tile never reaches stay 0
     a = (a - np.nanmin(a[:, 0])) * 0.01  # 10 ns ticks -> us
     spans = []
-    lookahead = os.environ.get("IDC_DS_LOOKAHEAD", "1") != "0" and nlayers > 1 and 256 >= nA + 16
+    lookahead = os.environ.get("IDC_DS_LOOKAHEAD", "1") != "0" and nlayers > 1 and 256 >= 2 * nmt + 16
     if not lookahead:
         for l in range(nlayers):
             spans.append((f"A{l}", l * per, l * per + nA))
@@ -130,9 +130,9 @@ def main():
     torch.cuda.synchronize()
     p = m.impl._prog(args.batch, True, torch.uint8)
     out = []
-    for si, (stamps, nl, M) in enumerate(getattr(p.b, "dense_stamps", [])):
-        rows = analyse_fwd(stamps.cpu().numpy(), nl, M)
-        out += _table(rows, f"## forward launch {si}: {nl} layers, M = {M} rows, span {rows[-1]['end']:.1f} us "
+    for si, (stamps, nl, M, ks) in enumerate(getattr(p.b, "dense_stamps", [])):
+        rows = analyse_fwd(stamps.cpu().numpy(), nl, M, ks)
+        out += _table(rows, f"## forward launch {si}: {nl} layers, M = {M} rows, K split {ks}, span {rows[-1]['end']:.1f} us "
                             f"(err counter {int(p.b.dense_err[0])})")
     for si, (stamps, phases, M) in enumerate(getattr(p.b, "dense_bwd_stamps", [])):
         rows = analyse_bwd(stamps.cpu().numpy(), phases)
