@@ -37,13 +37,13 @@ constexpr int NTR = 512;      // 8 waves
 constexpr int TPR = 128 + 8;  // t / act2 row pitch (bf16)
 constexpr int YP = 33;        // fp32 slice tile pitch
 constexpr int S = DS_SLOTS;
-constexpr int KC = 8;         // 1x1 weight chunk (k-steps of 32)
+constexpr int KC = 8;         // 1x1 weight chunk (k-steps of 32): two chunks = cin 512
 
 struct RowsLayout {
-  int xs, act1, tb, act2, red, ybuf, mean, var, sc, sh, total;
+  int xs, act1, tb, act2, red, ybuf, mean, var, sc, sh, lay, total;
 };
 
-__host__ __device__ inline RowsLayout rows_layout(int RB, int ld) {
+__host__ __device__ inline RowsLayout rows_layout(int RB, int ld, int nlayers) {
   RowsLayout L{};
   const int R = 16 * RB, ldp = ld + 8;
   const int nblk = 2 * RB, wpb = 8 / nblk;
@@ -58,14 +58,18 @@ __host__ __device__ inline RowsLayout rows_layout(int RB, int ld) {
   L.ybuf = L.red + nblk * (wpb - 1) * 256 * 4;
   const int alias_end = L.ybuf + R * YP * 4;
   o += (R * ldp * 2 > alias_end - L.act1) ? R * ldp * 2 : alias_end - L.act1;
+  // per-channel tables: the stage's channels, and bn2's 128 (a narrow test stage has ld < 128)
+  const int tl = ld > 128 ? ld : 128;
   L.mean = o;
-  o += ld * 4;
+  o += tl * 4;
   L.var = o;
-  o += ld * 4;
+  o += tl * 4;
   L.sc = o;
-  o += ld * 4;
+  o += tl * 4;
   L.sh = o;
-  o += ld * 4;
+  o += tl * 4;
+  L.lay = o;  // the layer table (LDS copy)
+  o += nlayers * (int)sizeof(DenseLayerDesc);
   L.total = o;
   return L;
 }
@@ -106,9 +110,10 @@ __global__ __launch_bounds__(NTR) void dense_rows_kernel(DenseStageArgs a, Group
   const persist::FailSink fsink{err, gsh(a.stepflag, go), a.hostflag};
   float* scratch = gsh(a.scratch, go);
   const unsigned max_polls = a.max_polls ? a.max_polls : DEFAULT_POLLS;
+  unsigned long long* stamps = gsh(a.stamps, go);  // [layer][group][NSTAMP] (diagnostics)
 
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  const RowsLayout LY = rows_layout(RB, a.ld);
+  const RowsLayout LY = rows_layout(RB, a.ld, a.nlayers);
   const int ld = a.ld, ldp = ld + 8;
   bf16_t* xs = reinterpret_cast<bf16_t*>(smem + LY.xs);
   bf16_t* act1 = reinterpret_cast<bf16_t*>(smem + LY.act1);
@@ -120,6 +125,7 @@ __global__ __launch_bounds__(NTR) void dense_rows_kernel(DenseStageArgs a, Group
   float* s_var = reinterpret_cast<float*>(smem + LY.var);
   float* s_sc = reinterpret_cast<float*>(smem + LY.sc);
   float* s_sh = reinterpret_cast<float*>(smem + LY.sh);
+  DenseLayerDesc* s_lay = reinterpret_cast<DenseLayerDesc*>(smem + LY.lay);
   __shared__ int s_bad;
 
   const int tid = threadIdx.x, lane = tid & 63;
@@ -137,6 +143,10 @@ __global__ __launch_bounds__(NTR) void dense_rows_kernel(DenseStageArgs a, Group
   const float lo2 = act_lo(a.act2), hi2 = act_hi(a.act2);
   const int taps = a.k2 * a.k2, pad = a.k2 >> 1, Kc = taps * 128, nks2 = taps * 4;
 
+  {
+    const int nw = a.nlayers * (int)sizeof(DenseLayerDesc) / 4;
+    for (int i = tid; i < nw; i += NTR) reinterpret_cast<unsigned*>(s_lay)[i] = reinterpret_cast<const unsigned*>(layers)[i];
+  }
   // ---- the group's rows of the stage input (channels [0, c0); the rest zero) and their moments
   for (int idx = tid; idx < R * (ld / 8); idx += NTR) {
     const int r = idx / (ld / 8), c = (idx - r * (ld / 8)) * 8;
@@ -165,7 +175,7 @@ __global__ __launch_bounds__(NTR) void dense_rows_kernel(DenseStageArgs a, Group
     pw = rem - ph * a.W;
   }
 
-  v8bf wq[2][KC];  // 1x1 weight chunks (double buffer)
+  v8bf wq[2][KC];  // 1x1 weight chunks (double buffer; the first two are issued a layer ahead)
   auto load_w1 = [&](const bf16_t* w1, int cin, int ch, v8bf (&q)[KC]) {
     const bf16_t* wrow = w1 + (size_t)(16 * wid + fr) * cin + fk;
 #pragma unroll
@@ -174,51 +184,84 @@ __global__ __launch_bounds__(NTR) void dense_rows_kernel(DenseStageArgs a, Group
       q[i] = k < cin ? *reinterpret_cast<const v8bf*>(wrow + k) : v8bf{};
     }
   };
-  {
-    const DenseLayerDesc d0 = layers[0];
-    load_w1(gsh(d0.w1, go), d0.cin, 0, wq[0]);
-  }
+  // a layer's BN1 affine parameters of this thread's channels (tid + 512 j), issued a layer ahead
+  constexpr int GJ = (DS_MAX_CIN + NTR - 1) / NTR;
+  float g1r[GJ], b1r[GJ];
+  auto prefetch_layer = [&](const DenseLayerDesc& dn) {
+    load_w1(gsh(dn.w1, go), dn.cin, 0, wq[0]);
+    load_w1(gsh(dn.w1, go), dn.cin, 1, wq[1]);
+    const float* g = gsh(dn.g1, go);
+    const float* b = gsh(dn.b1, go);
+#pragma unroll
+    for (int j = 0; j < GJ; ++j) {
+      const int c = tid + NTR * j;
+      g1r[j] = c < dn.cin ? g[c] : 0.f;
+      b1r[j] = c < dn.cin ? b[c] : 0.f;
+    }
+  };
+  prefetch_layer(layers[0]);
 
   for (int l = 0; l < a.nlayers; ++l) {
     __syncthreads();  // the previous layer's moments, slice rows and tile reads are complete
-    const DenseLayerDesc d = layers[l];
+    const int sti = l * G + gi;  // stamp row
+    stamp(stamps, sti, 0);
+    const DenseLayerDesc d = s_lay[l];
     const int cin = d.cin, nks1 = cin >> 5, nch = (nks1 + KC - 1) / KC;
     const bf16_t* __restrict__ w1 = gsh(d.w1, go);
     const bf16_t* __restrict__ w2 = gsh(d.w2, go);
-    const float* __restrict__ g1 = gsh(d.g1, go);
-    const float* __restrict__ b1 = gsh(d.b1, go);
     const float* __restrict__ tsh = gsh(d.tshift, go);
     float* lslots = scratch + (size_t)l * DS_SCRATCH_PER_LAYER;  // [S][2][32] slice statistics
     float* tslots = lslots + S * 64;                              // [S][2][128] t statistics
-    // 3x3 weight fragments of this wave's block and k share: in flight during the 1x1
+    // 3x3 weight fragments of this wave's block and k share (issued once the t statistics are
+    // published: in flight during the barrier)
     v8bf bw[MAXK2];
+    auto load_w2 = [&]() {
 #pragma unroll
-    for (int i = 0; i < MAXK2; ++i) {
-      const int ks = kp + WPB * i;
-      bw[i] = ks < nks2 ? *reinterpret_cast<const v8bf*>(w2 + (size_t)(16 * cb + fr) * Kc + (ks >> 2) * 128 +
-                                                         (ks & 3) * 32 + fk)
-                        : v8bf{};
-    }
+      for (int i = 0; i < MAXK2; ++i) {
+        const int ks = kp + WPB * i;
+        bw[i] = ks < nks2 ? *reinterpret_cast<const v8bf*>(w2 + (size_t)(16 * cb + fr) * Kc + (ks >> 2) * 128 +
+                                                           (ks & 3) * 32 + fk)
+                          : v8bf{};
+      }
+    };
 
     // ---- BN1 table [0, cin) (batch moments, or the layer's moving statistics) and act1
     const bool inf1 = infer || (d.pad_ & 1);
     {
       const float* __restrict__ mm = inf1 ? gsh(d.mm1, go) : nullptr;
       const float* __restrict__ mv = inf1 ? gsh(d.mv1, go) : nullptr;
-      for (int c = tid; c < cin; c += NTR) {
-        const float mean = inf1 ? mm[c] : s_mean[c], var = inf1 ? mv[c] : s_var[c];
-        const float r = g1[c] * rsqrtf(var + d.eps1);
-        s_sc[c] = r;
-        s_sh[c] = b1[c] - mean * r;
+#pragma unroll
+      for (int j = 0; j < GJ; ++j) {
+        const int c = tid + NTR * j;
+        if (c < cin) {
+          const float mean = inf1 ? mm[c] : s_mean[c], var = inf1 ? mv[c] : s_var[c];
+          const float r = g1r[j] * rsqrtf(var + d.eps1);
+          s_sc[c] = r;
+          s_sh[c] = b1r[j] - mean * r;
+        }
       }
     }
+    stamp(stamps, sti, 1);
     __syncthreads();  // tables; the previous layer's reads of the act1 region are done
-    for (int idx = tid; idx < R * (cin / 8); idx += NTR) {
-      const int r = idx / (cin / 8), c = (idx - r * (cin / 8)) * 8;
-      const uint4 x = *reinterpret_cast<const uint4*>(xs + r * ldp + c);
-      *reinterpret_cast<v8bf*>(act1 + r * ldp + c) = bnr8(x, s_sc + c, s_sh + c, lo1, hi1, r < Rg);
+    // act1: thread -> one 8-channel chunk (its scale / shift held in registers) x every 4th row
+    for (int c8 = tid & 127; c8 < cin / 8; c8 += 128) {
+      const int c = c8 * 8;
+      const float4 a0 = *reinterpret_cast<const float4*>(s_sc + c), a1 = *reinterpret_cast<const float4*>(s_sc + c + 4);
+      const float4 h0 = *reinterpret_cast<const float4*>(s_sh + c), h1 = *reinterpret_cast<const float4*>(s_sh + c + 4);
+      const float av[8] = {a0.x, a0.y, a0.z, a0.w, a1.x, a1.y, a1.z, a1.w};
+      const float hv[8] = {h0.x, h0.y, h0.z, h0.w, h1.x, h1.y, h1.z, h1.w};
+#pragma unroll
+      for (int rr = 0; rr < R / 4; ++rr) {
+        const int r = (tid >> 7) + 4 * rr;
+        float f[8];
+        unpack8(*reinterpret_cast<const uint4*>(xs + r * ldp + c), f);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) f[j] = r < Rg ? clampf(f[j] * av[j] + hv[j], lo1, hi1) : 0.f;
+        *reinterpret_cast<uint4*>(act1 + r * ldp + c) = pack8(f);
+      }
     }
     __syncthreads();
+    stamp(stamps, sti, 2);
 
     // ---- 1x1: t[:, 16 wid .. +16) over all RB row blocks, weight chunks double-buffered
     v4f acc[RB];
@@ -237,17 +280,18 @@ __global__ __launch_bounds__(NTR) void dense_rows_kernel(DenseStageArgs a, Group
         }
       }
     };
+    // chunks 0 and 1 were issued a layer ahead; later chunks (cin > 1024) stream behind them
     for (int ch = 0; ch < nch; ch += 2) {
-      if (ch + 1 < nch) load_w1(w1, cin, ch + 1, wq[1]);
       mfma1(ch, wq[0]);
+      if (ch + 2 < nch) load_w1(w1, cin, ch + 2, wq[0]);
       if (ch + 1 < nch) {
-        if (ch + 2 < nch) load_w1(w1, cin, ch + 2, wq[0]);
         mfma1(ch + 1, wq[1]);
+        if (ch + 3 < nch) load_w1(w1, cin, ch + 3, wq[1]);
       }
     }
     __syncthreads();  // every wave done reading act1: t may overwrite it
+    stamp(stamps, sti, 3);
     {
-      bf16_t* tg = gsh(d.t, go);
 #pragma unroll
       for (int h = 0; h < RB; ++h)
 #pragma unroll
@@ -256,12 +300,16 @@ __global__ __launch_bounds__(NTR) void dense_rows_kernel(DenseStageArgs a, Group
           tb[r * TPR + 16 * wid + fr] = (bf16_t)(pack2bf(acc[h][q], 0.f) & 0xffffu);
         }
       __syncthreads();
-      // t to global (16-B stores), rows of the group only
+    }
+    // t to global (16-B stores, rows of the group): after the barrier's publish, which need not
+    // wait for them
+    auto store_t = [&]() {
+      bf16_t* tg = gsh(d.t, go);
       for (int idx = tid; idx < Rg * 16; idx += NTR) {
         const int r = idx >> 4, c = (idx & 15) * 8;
         *reinterpret_cast<uint4*>(tg + (size_t)(row0 + r) * 128 + c) = *reinterpret_cast<const uint4*>(tb + r * TPR + c);
       }
-    }
+    };
 
     // ---- t statistics -> slots, barrier 1, BN2 table
     const bool inf2 = infer || (d.pad_ & 2);
@@ -277,13 +325,19 @@ __global__ __launch_bounds__(NTR) void dense_rows_kernel(DenseStageArgs a, Group
         atomicAdd(&tslots[(gi % S) * 256 + which * 128 + c], sum);
       }
       publish_shard(cnt1(l), gi);
+      load_w2();
+      store_t();
       if (wid == 0) {
         const bool ok = wait_sum8(cnt1(l), (unsigned)G, fail, fsink, max_polls);
         if (lane == 0) s_bad = !ok;
       }
       __syncthreads();
       if (__builtin_amdgcn_readfirstlane(s_bad)) return;
+    } else {
+      load_w2();
+      store_t();
     }
+    stamp(stamps, sti, 4);
     if (tid < 128) {
       const int c = tid;
       const float g2 = gsh(d.g2, go)[c], b2 = gsh(d.b2, go)[c];
@@ -314,6 +368,7 @@ __global__ __launch_bounds__(NTR) void dense_rows_kernel(DenseStageArgs a, Group
       *reinterpret_cast<v8bf*>(act2 + r * TPR + c) = bnr8(x, s_sc + c, s_sh + c, lo2, hi2, r < Rg);
     }
     __syncthreads();
+    stamp(stamps, sti, 5);
 
     // ---- 3x3 (or centre tap): block (rb, cb) = rows 16 rb.., slice channels 16 cb..; k share kp
     {
@@ -345,16 +400,23 @@ __global__ __launch_bounds__(NTR) void dense_rows_kernel(DenseStageArgs a, Group
       }
       __syncthreads();
     }
-    // ---- the slice: LDS rows (later layers), global stage buffer, statistics
+    stamp(stamps, sti, 6);
+    // ---- the slice: LDS rows (later layers), global stage buffer (after the barrier's publish),
+    // statistics
     for (int idx = tid; idx < Rg * 4; idx += NTR) {
       const int r = idx >> 2, c = (idx & 3) * 8;
       float f[8];
 #pragma unroll
       for (int j = 0; j < 8; ++j) f[j] = ybuf[r * YP + c + j];
-      const uint4 pk = pack8(f);
-      *reinterpret_cast<uint4*>(xs + r * ldp + cin + c) = pk;
-      *reinterpret_cast<uint4*>(buf + (size_t)(row0 + r) * ld + cin + c) = pk;
+      *reinterpret_cast<uint4*>(xs + r * ldp + cin + c) = pack8(f);
     }
+    auto store_slice = [&]() {
+      for (int idx = tid; idx < Rg * 4; idx += NTR) {
+        const int r = idx >> 2, c = (idx & 3) * 8;
+        *reinterpret_cast<uint4*>(buf + (size_t)(row0 + r) * ld + cin + c) =
+            *reinterpret_cast<const uint4*>(xs + r * ldp + cin + c);
+      }
+    };
     if (!infer) {
       if (tid < 64) {
         const int c = tid & 31, which = tid >> 5;
@@ -367,16 +429,18 @@ __global__ __launch_bounds__(NTR) void dense_rows_kernel(DenseStageArgs a, Group
         atomicAdd(&lslots[(gi % S) * 64 + which * 32 + c], sum);
       }
       if (l + 1 < a.nlayers) {
+        __syncthreads();  // the slice rows in LDS (store_slice reads them)
         publish_shard(cnt2(l), gi);
-        // the next layer's first weight chunk, in flight while this barrier waits
-        const DenseLayerDesc dn = layers[l + 1];
-        load_w1(gsh(dn.w1, go), dn.cin, 0, wq[0]);
+        // the next layer's first weight chunks and BN1 parameters, in flight while this barrier waits
+        prefetch_layer(s_lay[l + 1]);
+        store_slice();
         if (wid == 0) {
           const bool ok = wait_sum8(cnt2(l), (unsigned)G, fail, fsink, max_polls);
           if (lane == 0) s_bad = !ok;
         }
         __syncthreads();
         if (__builtin_amdgcn_readfirstlane(s_bad)) return;
+        stamp(stamps, sti, 7);
         if (tid < 32) {
           float s0, s1, mean, var;
           slot_sum<S>(lslots, 32, tid, s0, s1);
@@ -390,6 +454,8 @@ __global__ __launch_bounds__(NTR) void dense_rows_kernel(DenseStageArgs a, Group
         }
       } else {
         // the last slice has no in-launch consumer: the last arrival writes its statistics
+        __syncthreads();
+        store_slice();
         const unsigned old = publish(lastfin);
         if (tid == 0) s_bad = old == (unsigned)(G - 1);
         __syncthreads();
@@ -400,9 +466,10 @@ __global__ __launch_bounds__(NTR) void dense_rows_kernel(DenseStageArgs a, Group
           sstats[ld + cin + tid] = s1;
         }
       }
-    } else if (l + 1 < a.nlayers) {
-      const DenseLayerDesc dn = layers[l + 1];
-      load_w1(gsh(dn.w1, go), dn.cin, 0, wq[0]);
+    } else {
+      __syncthreads();
+      store_slice();
+      if (l + 1 < a.nlayers) prefetch_layer(s_lay[l + 1]);
     }
   }
 }
@@ -419,7 +486,7 @@ bool dense_rows_geometry(int N, int H, int W, int ld, int max_cin, int& rb, int&
     if (force && r != force) continue;
     const int ip = 16 * r / HW;
     if (ip < 1) continue;
-    if (rows_layout(r, ld).total > LDS_MAX) continue;
+    if (rows_layout(r, ld, 64).total > LDS_MAX) continue;
     const int g = (N + ip - 1) / ip;
     if (g > 256) continue;
     rb = r;
@@ -438,7 +505,8 @@ hipError_t dense_rows_fwd(const DenseStageArgs& a, hipStream_t st) {
     return hipErrorInvalidValue;
   DenseStageArgs b = a;
   b.rows_ipg = ipg;
-  const int shm = rows_layout(rb, a.ld).total;
+  if (a.nlayers > 64) return hipErrorInvalidValue;
+  const int shm = rows_layout(rb, a.ld, a.nlayers).total;
   if (rb == 2)
     hipLaunchKernelGGL(dense_rows_kernel<2>, ggrid(grid), dim3(NTR), shm, st, b, garg());
   else

@@ -901,10 +901,15 @@ class Builder:
                        and not self.shared_device) else 0
         self._fail_words(a)
         if os.environ.get("IDC_DS_STAMPS", "0") == "1":
-            # per-work-item s_memrealtime stamps (tools/dense_stamps.py reads them after a step)
-            stamps = self.alloc((8 * int(ext.dense_stage_tasks(nat.raw(a))),), torch.int64)
+            # per-work-item s_memrealtime stamps (tools/dense_stamps.py reads them after a step);
+            # row-resident launches: one row per (layer, workgroup)
+            rows_geo = tuple(ext.dense_rows_geometry(buf.N, H, W, buf.ld, max(lay["cin"] for lay in layers))) \
+                if a.rows else (False, 0, 0, 0)
+            n_items = len(layers) * rows_geo[3] if rows_geo[0] else int(ext.dense_stage_tasks(nat.raw(a)))
+            stamps = self.alloc((8 * n_items,), torch.int64)
             a.stamps = stamps.data_ptr()
-            self.dense_stamps = getattr(self, "dense_stamps", []) + [(stamps, len(layers), M, ksplit)]
+            self.dense_stamps = getattr(self, "dense_stamps", []) + [
+                (stamps, len(layers), M, ksplit, rows_geo[3] if rows_geo[0] else 0)]
         self.emit(nat.OP_DENSE_STAGE, a, ints=(grid, len(layers)), ptrs=(tab.data_ptr(),))
 
     def dense_stage_bwd_ok(self, buf: Tensor4, layers, pend: "BNRef") -> bool:

@@ -94,6 +94,26 @@ def analyse_fwd(st, nlayers: int, M: int, ksplit: int = 1):
     return _phase_rows(a, spans, {"A": 3, "B": 2}, {"A": 7, "B": 7})
 
 
+def analyse_rows(st, nlayers: int, G: int, M: int):
+    """Row-resident launch (dense_rows.hip): per layer, the median over workgroups of each
+    interval [start, BN1 table, act1 staged, 1x1 done, barrier 1 passed, act2 staged, 3x3 done,
+    barrier 2 passed] and the layer's span (first start to the next layer's last start)."""
+    import numpy as np
+    a = st.reshape(nlayers, G, NSTAMP).astype(np.float64)
+    a[a == 0] = np.nan
+    a = (a - np.nanmin(a[:, :, 0])) * 0.01
+    names = ["bn1tab", "act1", "1x1", "bar1", "act2", "3x3", "bar2"]
+    out = [f"## row-resident launch: {nlayers} layers, M = {M} rows, {G} workgroups, span "
+           f"{np.nanmax(a[-1]) :.1f} us", "",
+           "| layer | start | " + " | ".join(names) + " | next start |", "|---|---:|" + "---:|" * (len(names) + 1)]
+    for l in range(nlayers):
+        iv = [np.nanmedian(a[l, :, k + 1] - a[l, :, k]) for k in range(len(names))]
+        nxt = np.nanmax(a[l + 1, :, 0]) if l + 1 < nlayers else np.nanmax(a[l])
+        out.append(f"| {l} | {np.nanmin(a[l, :, 0]):.1f} | " + " | ".join(f"{v:.2f}" for v in iv) + f" | {nxt:.1f} |")
+    out.append("")
+    return out
+
+
 def analyse_bwd(st, phases):
     import numpy as np
     n = phases[-1][0] + phases[-1][3]
@@ -130,7 +150,10 @@ def main():
     torch.cuda.synchronize()
     p = m.impl._prog(args.batch, True, torch.uint8)
     out = []
-    for si, (stamps, nl, M, ks) in enumerate(getattr(p.b, "dense_stamps", [])):
+    for si, (stamps, nl, M, ks, G) in enumerate(getattr(p.b, "dense_stamps", [])):
+        if G:
+            out += analyse_rows(stamps.cpu().numpy(), nl, G, M)
+            continue
         rows = analyse_fwd(stamps.cpu().numpy(), nl, M, ks)
         out += _table(rows, f"## forward launch {si}: {nl} layers, M = {M} rows, K split {ks}, span {rows[-1]['end']:.1f} us "
                             f"(err counter {int(p.b.dense_err[0])})")
