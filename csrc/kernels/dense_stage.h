@@ -130,7 +130,7 @@ constexpr int DSB_MAX_CG = 64;     // 32-channel groups of the stage input (c0 <
 // sync words: [0] ticket; layer l at 1 + 32 l: P (8 shards), QN (8 shards), G arrivals, G done;
 // then GIN (8 shards), FIN1 arrivals per input channel group, FIN1 done, FIN2, fail
 constexpr int DSB_SYNC_PER_LAYER = 32;
-inline int dsb_sync_words(int L) { return 1 + DSB_SYNC_PER_LAYER * L + 8 + DSB_MAX_CG + 3; }
+__host__ __device__ inline int dsb_sync_words(int L) { return 1 + DSB_SYNC_PER_LAYER * L + 8 + DSB_MAX_CG + 3; }
 
 struct DenseBwdArgs {
   const bf16_t* buf;              // stage buffer [M][ld] (forward, raw)
@@ -154,8 +154,17 @@ struct DenseBwdArgs {
   unsigned max_polls;
   int* stepflag;                  // nullable: per-step guard word (as DenseStageArgs::stepflag)
   int* hostflag;                  // nullable: pinned host give-up flag (as DenseStageArgs::hostflag)
+  int rows;                       // 1: row-resident launch (dense_rows_bwd.hip) where its geometry fits
+  int rows_ipg;                   // (set by the launcher) images per row-resident workgroup
+  float* rpart;                   // row-resident: per-workgroup bn1 sums [layer][group][2][cin]
+  long long rpart_floats;         // its size (dense_rows_bwd_part_floats)
 };
 
 hipError_t dense_stage_bwd(const DenseBwdArgs& a, int grid, hipStream_t st);
+// row-resident form (dense_rows_bwd.hip): whole images per workgroup, the concat gradient in LDS,
+// only the BatchNorm reductions cross workgroups (two barriers per layer)
+bool dense_rows_bwd_geometry(int N, int H, int W, int ld, int nlayers, int& ipg, int& grid);
+hipError_t dense_rows_bwd(const DenseBwdArgs& a, hipStream_t st);
+long long dense_rows_bwd_part_floats(int c0, int nlayers, int grid);
 
 }  // namespace idc

@@ -709,6 +709,7 @@ hipError_t dense_stage_bwd(const DenseBwdArgs& a, int grid, hipStream_t st) {
       a.layers == nullptr || a.phases == nullptr || a.sync == nullptr || a.btot == nullptr || a.nphases < 1 ||
       a.ntickets < 1 || !dense_stage_shape_ok(a.N, a.H, a.W, 0))
     return hipErrorInvalidValue;
+  if (a.rows && dense_rows_bwd(a, st) == hipSuccess) return hipSuccess;
   if (grid <= 0) grid = 256;
   const int k = launch_groups().k;
   if (k > 1) grid = grid / k > 8 ? grid / k : 8;

@@ -1092,6 +1092,12 @@ PYBIND11_MODULE(_idc_native, m) {
     return py::make_tuple(nA, nB);
   }, py::arg("M"), py::arg("ksplit") = 1);
   m.def("dense_stage_sync_words", &dense_stage_sync_words);
+  m.def("dense_rows_bwd_part_floats", &dense_rows_bwd_part_floats);
+  m.def("dense_rows_bwd_geometry", [](int N, int H, int W, int ld, int nlayers) {
+    int ipg = 0, grid = 0;
+    const bool ok = dense_rows_bwd_geometry(N, H, W, ld, nlayers, ipg, grid);
+    return py::make_tuple(ok, ipg, grid);
+  });
   m.def("dense_rows_geometry", [](int N, int H, int W, int ld, int max_cin) {
     int rb = 0, ipg = 0, grid = 0;
     const bool ok = dense_rows_geometry(N, H, W, ld, max_cin, rb, ipg, grid);

@@ -166,7 +166,8 @@ class DenseBwdArgs(C.Structure):
                [("pend", BwdAff)] + \
                [(n, vp) for n in ("layers", "phases", "sync", "btot", "err", "stamps")] + \
                [(n, ci) for n in ("N", "H", "W", "ld", "c0", "nlayers", "k2", "act", "nphases", "ntickets")] + \
-               [("inv_count", cf), ("max_polls", C.c_uint), ("stepflag", vp), ("hostflag", vp)]
+               [("inv_count", cf), ("max_polls", C.c_uint), ("stepflag", vp), ("hostflag", vp),
+                ("rows", ci), ("rows_ipg", ci), ("rpart", vp), ("rpart_floats", C.c_longlong)]
 
 
 class MbPhaseDesc(C.Structure):

@@ -513,7 +513,7 @@ def dense_bwd_queue(L: int, nmt: int, c0: int, kg: int):
 
 def dense_stage_bwd(buf: torch.Tensor, sstats: torch.Tensor, layers, dbuf: torch.Tensor, pend: nat.BwdAff,
                     sshift: Optional[torch.Tensor] = None, act: int = RELU, grid: int = 256, k2: int = 3,
-                    max_polls: int = 0):
+                    max_polls: int = 0, rows: int = 0):
     """Data gradients of all dense layers of a DenseNet stage in one persistent launch
     (csrc/kernels/dense_stage_bwd.hip).
 
@@ -567,6 +567,14 @@ def dense_stage_bwd(buf: torch.Tensor, sstats: torch.Tensor, layers, dbuf: torch
     a.k2, a.act, a.nphases, a.ntickets = k2, act, len(ph), ph[-1][0] + ph[-1][3]
     a.inv_count = 1.0 / float(M)
     a.max_polls = max_polls
+    a.rows = rows  # 1: the row-resident launch (dense_rows_bwd.hip) where its geometry fits
+    if rows:
+        ok, _ipg, g = ext.dense_rows_bwd_geometry(N, H, W, ld, L)
+        if ok:
+            n = int(ext.dense_rows_bwd_part_floats(c0, L, g))
+            rpart = torch.zeros(n, device=dev)
+            keep.append(rpart)
+            a.rpart, a.rpart_floats = rpart.data_ptr(), n
     _plan1(nat.OP_DENSE_STAGE_BWD, a, ints=(grid, L), ptrs=(tab.data_ptr(),))
     torch.cuda.current_stream().synchronize()
     del keep

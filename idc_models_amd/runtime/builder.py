@@ -143,6 +143,11 @@ def persistent_disabled() -> bool:
     return bool(_PERSISTENT_OFF)
 
 
+def rows_bwd_enabled() -> bool:
+    """The row-resident dense-stage backward (dense_rows_bwd.hip; IDC_DS_ROWS_BWD)."""
+    return os.environ.get("IDC_DS_ROWS_BWD", "0") == "1"
+
+
 _HOST_FLAGS = {"base": 0, "next": 0}
 _HOST_FLAG_SLOTS = 4096
 
@@ -897,8 +902,12 @@ class Builder:
         # row-resident form (dense_rows.hip: whole images per workgroup, only BatchNorm statistics
         # cross workgroups) where its geometry fits; not beside other launches of its kind
         # (grouped programs, concurrent federated clients: its workgroups must be co-resident)
-        a.rows = 1 if (os.environ.get("IDC_DS_ROWS", "0") == "1" and not getattr(self, "grouped", False)
-                       and not self.shared_device) else 0
+        # Round 6, bench.py A/B (DenseNet-121 bs 256, 3 rounds on one box): stage 3 (M = 2,304) row-
+        # resident 3.449-3.465 vs 3.468-3.476 ms/step work-queue (stamps: 382 vs 410 us); stage 4 (M =
+        # 256, 16 workgroups) is faster on the work queue (181 vs 208 us), hence IDC_DS_ROWS_MINM
+        a.rows = 1 if (os.environ.get("IDC_DS_ROWS", "1") == "1" and not getattr(self, "grouped", False)
+                       and not self.shared_device
+                       and M >= int(os.environ.get("IDC_DS_ROWS_MINM", "1024"))) else 0
         self._fail_words(a)
         if os.environ.get("IDC_DS_STAMPS", "0") == "1":
             # per-work-item s_memrealtime stamps (tools/dense_stamps.py reads them after a step);
@@ -995,8 +1004,22 @@ class Builder:
         a.k2, a.act, a.nphases, a.ntickets = 1 if center else 3, act, len(ph), ntickets
         a.inv_count = 1.0 / float(M)
         a.max_polls = int(os.environ.get("IDC_DS_MAX_POLLS", "0"))
+        # row-resident form (dense_rows_bwd.hip) where its geometry fits (not beside other launches
+        # of its kind: its workgroups must be co-resident)
+        a.rows = 1 if (rows_bwd_enabled() and not getattr(self, "grouped", False) and not self.shared_device) else 0
+        if a.rows:
+            ok, _ipg, g = ext.dense_rows_bwd_geometry(N, H, W, buf.ld, L)
+            if ok:
+                n = int(ext.dense_rows_bwd_part_floats(c0, L, g))
+                a.rpart, a.rpart_floats = self.alloc((n,), F32).data_ptr(), n
         self._fail_words(a)
-        if os.environ.get("IDC_DS_STAMPS", "0") == "1":
+        if os.environ.get("IDC_DS_STAMPS", "0") == "1" and a.rows:
+            ok, ipg, g = ext.dense_rows_bwd_geometry(N, H, W, buf.ld, L)
+            if ok:
+                stamps = self.alloc((8 * L * g,), torch.int64)
+                a.stamps = stamps.data_ptr()
+                self.dense_bwd_stamps = getattr(self, "dense_bwd_stamps", []) + [(stamps, None, M, g, L)]
+        elif os.environ.get("IDC_DS_STAMPS", "0") == "1":
             stamps = self.alloc((8 * ntickets,), torch.int64)
             a.stamps = stamps.data_ptr()
             self.dense_bwd_stamps = getattr(self, "dense_bwd_stamps", []) + [(stamps, ph, M)]

@@ -173,7 +173,9 @@ def lower_densenet(b: Builder, net, U: int, input_dtype):
     # The smallest stages (M <= IDC_DENSE_STAGE_BWD_MAXM pixels, default 256: stage 4 at bs 256) run
     # the data gradients of all their dense layers as ONE persistent launch (builder.dense_stage_bwd,
     # dense_stage_bwd.hip); it hands the stage input's final gradient (bf16) to the transition
-    bwd_maxm = int(os.environ.get("IDC_DENSE_STAGE_BWD_MAXM", "256"))
+    # (the row-resident form, IDC_DS_ROWS_BWD=1, runs stage 3 as well: M = 2,304)
+    from .builder import rows_bwd_enabled
+    bwd_maxm = int(os.environ.get("IDC_DENSE_STAGE_BWD_MAXM", "2304" if rows_bwd_enabled() else "256"))
     for si in range(len(stages) - 1, -1, -1):
         st = stages[si]
         buf = st["buf"]

@@ -981,10 +981,16 @@ def _bn_train(x, g, b, eps):
     return (x - mean) * torch.rsqrt(var + eps) * g + b
 
 
-@pytest.mark.parametrize("N,H,c0,L,grid", [(16, 3, 64, 3, 256), (64, 1, 96, 4, 256), (8, 3, 128, 2, 5),
-                                          (6, 2, 256, 3, 64), (4, 1, 1120, 2, 256), (64, 3, 256, 4, 256),
-                                          (256, 3, 256, 24, 256), (256, 1, 512, 16, 256)])
-def test_dense_stage_bwd_matches_autograd(fn, N, H, c0, L, grid):
+@pytest.mark.parametrize("N,H,c0,L,grid,rows", [(16, 3, 64, 3, 256, 0), (64, 1, 96, 4, 256, 0), (8, 3, 128, 2, 5, 0),
+                                               (6, 2, 256, 3, 64, 0), (4, 1, 1120, 2, 256, 0),
+                                               (64, 3, 256, 4, 256, 0), (256, 3, 256, 24, 256, 0),
+                                               (256, 1, 512, 16, 256, 0),
+                                               # row-resident launch (dense_rows_bwd.hip)
+                                               (16, 3, 64, 3, 256, 1), (64, 1, 96, 4, 256, 1),
+                                               (8, 3, 128, 2, 5, 1), (6, 2, 256, 3, 64, 1),
+                                               (20, 3, 256, 4, 256, 1), (256, 3, 256, 24, 256, 1),
+                                               (256, 1, 512, 16, 256, 1)])
+def test_dense_stage_bwd_matches_autograd(fn, N, H, c0, L, grid, rows):
     """The persistent dense-stage BACKWARD launch (dense_stage_bwd.hip: 3x3 dgrad, dT, newest-slice
     and older-channel 1x1 dgrads, every BatchNorm backward through the summed pending affines,
     d gamma / d beta) vs fp32 autograd of the same dense layers, forward values rounded to bf16
@@ -992,7 +998,11 @@ def test_dense_stage_bwd_matches_autograd(fn, N, H, c0, L, grid):
     whole stage buffer with a random output gradient (the transition / final BatchNorm of
     lower_densenet).  grid 5: far fewer workgroups than tickets (queue order must still drain);
     c0 1120: DenseNet-201-wide inputs; 1x1 maps: centre-tap 3x3; (256, 3, 256, 24) and
-    (256, 1, 512, 16): DenseNet-121's stages 3 and 4 at the bench batch exactly."""
+    (256, 1, 512, 16): DenseNet-121's stages 3 and 4 at the bench batch exactly.  rows 1: the
+    row-resident launch (whole images per workgroup, the concat gradient held in LDS)."""
+    if rows:
+        ok, ipg, g = fn.nat.require().dense_rows_bwd_geometry(N, H, H, c0 + 32 * L, L)
+        assert ok, (N, H, c0, L)
     torch.manual_seed(N * 1000 + c0 + L)
     W = H
     ld = c0 + 32 * L
@@ -1059,7 +1069,7 @@ def test_dense_stage_bwd_matches_autograd(fn, N, H, c0, L, grid):
                          dt=torch.zeros(N, H, W, 128, dtype=torch.bfloat16, device=DEV),
                          dbeta1=torch.zeros(cin, device=DEV), dgamma1=torch.zeros(cin, device=DEV),
                          dbeta2=torch.zeros(128, device=DEV), dgamma2=torch.zeros(128, device=DEV)))
-    dx16, sync, err = fn.dense_stage_bwd(buf, sst, lays, dbuf, pend, sshift=K, grid=grid, k2=k2)
+    dx16, sync, err = fn.dense_stage_bwd(buf, sst, lays, dbuf, pend, sshift=K, grid=grid, k2=k2, rows=rows)
     assert int(err[0].item()) == 0 and int(sync[-1].item()) == 0, sync.tolist()
     errs = {"dx": relerr(dx16, x0.grad)}
     for i, (p, d) in enumerate(zip(params, lays)):

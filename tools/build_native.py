@@ -44,6 +44,7 @@ SOURCES = [
     "kernels/dense_rows.hip",
     "kernels/mb_chain.hip",
     "kernels/dense_stage_bwd.hip",
+    "kernels/dense_rows_bwd.hip",
     "kernels/mlp_head.hip",
     "kernels/secagg.hip",
     "comm/communicator.cpp",

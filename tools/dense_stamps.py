@@ -114,6 +114,25 @@ def analyse_rows(st, nlayers: int, G: int, M: int):
     return out
 
 
+def analyse_rows_bwd(st, nlayers: int, G: int, M: int):
+    """Row-resident backward (dense_rows_bwd.hip), layers in processing order (L-1 .. 0): median
+    over workgroups of [dy staged, 3x3 dgrad + bn2 sums, barrier A, dT, 1x1 dgrad + bn1 sums,
+    barrier B, pending-affine update]."""
+    import numpy as np
+    a = st.reshape(nlayers, G, NSTAMP).astype(np.float64)
+    a[a == 0] = np.nan
+    a = (a - np.nanmin(a[:, :, 0])) * 0.01
+    names = ["dy", "3x3", "barA", "dT", "1x1", "barB", "aff"]
+    out = [f"## row-resident backward: {nlayers} layers, M = {M} rows, {G} workgroups, span "
+           f"{np.nanmax(a) - np.nanmin(a):.1f} us", "",
+           "| layer | start | " + " | ".join(names) + " |", "|---|---:|" + "---:|" * len(names)]
+    for l in range(nlayers - 1, -1, -1):
+        iv = [np.nanmedian(a[l, :, k + 1] - a[l, :, k]) for k in range(len(names))]
+        out.append(f"| {l} | {np.nanmin(a[l, :, 0]):.1f} | " + " | ".join(f"{v:.2f}" for v in iv) + " |")
+    out.append("")
+    return out
+
+
 def analyse_bwd(st, phases):
     import numpy as np
     n = phases[-1][0] + phases[-1][3]
@@ -157,7 +176,11 @@ def main():
         rows = analyse_fwd(stamps.cpu().numpy(), nl, M, ks)
         out += _table(rows, f"## forward launch {si}: {nl} layers, M = {M} rows, K split {ks}, span {rows[-1]['end']:.1f} us "
                             f"(err counter {int(p.b.dense_err[0])})")
-    for si, (stamps, phases, M) in enumerate(getattr(p.b, "dense_bwd_stamps", [])):
+    for si, rec in enumerate(getattr(p.b, "dense_bwd_stamps", [])):
+        if rec[1] is None:  # row-resident backward: (stamps, None, M, workgroups, layers)
+            out += analyse_rows_bwd(rec[0].cpu().numpy(), rec[4], rec[3], rec[2])
+            continue
+        stamps, phases, M = rec
         rows = analyse_bwd(stamps.cpu().numpy(), phases)
         out += _table(rows, f"## backward launch {si}: M = {M} rows, span {max(r['end'] for r in rows):.1f} us")
     text = "\n".join(out)
