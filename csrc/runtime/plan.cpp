@@ -571,7 +571,32 @@ class Plan {
     comm_->all_reduce(reinterpret_cast<void*>(op.p[0]), op.l[0], op.i[0], op.i[1], cs);
   }
 
+  // IDC_SYNC_OPS=1 (fault attribution only): every directly issued op is followed by a stream
+  // synchronisation, so an asynchronous fault is reported by the op that caused it instead of by
+  // whatever API call happens to run next (torch, MIOpen)
+  static bool sync_ops() {
+    static const bool on = [] {
+      const char* e = std::getenv("IDC_SYNC_OPS");
+      return e && e[0] == '1';
+    }();
+    return on;
+  }
   void exec(const Op& op, hipStream_t st) {
+    exec_op(op, st);
+    if (sync_ops()) {
+      hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+      (void)hipStreamIsCapturing(st, &cs);
+      if (cs == hipStreamCaptureStatusNone) {
+        const hipError_t e = hipStreamSynchronize(st);
+        if (e != hipSuccess) {
+          const long idx = (long)(&op - ops_.data());
+          throw std::runtime_error("IDC_SYNC_OPS: op " + std::to_string(idx) + " (" + describe((int)idx) +
+                                   ") faulted: " + hipGetErrorString(e));
+        }
+      }
+    }
+  }
+  void exec_op(const Op& op, hipStream_t st) {
     switch (op.kind) {
       case OP_CONV: {
         ConvArgs a = as<ConvArgs>(op);
