@@ -49,6 +49,7 @@ SOURCES = [
     "kernels/secagg.hip",
     "comm/communicator.cpp",
     "runtime/plan.cpp",
+    "runtime/guard_alloc.cpp",
 ]
 
 # RCCL (= NCCL API on ROCm) for the native communicator.  Its soname is librccl.so.1, the same as
