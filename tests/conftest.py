@@ -10,11 +10,11 @@ if ROOT not in sys.path:
 
 
 def pytest_configure(config):
-    # Eager-PyTorch reference runs use PyTorch's native convolutions, not MIOpen.  A MIOpen kernel
-    # of the eager MobileNetV2 backward in tests/test_fed_gpu.py faults (hipErrorIllegalAddress)
-    # when the determinism, DP and eval tests ran before it in the same process; with every
-    # dispatch serialised and every fused-program op synchronised and checked, the failing launch
-    # is MIOpen's own (profiles/fault_attribution_r6.md).  IDC_EAGER_MIOPEN=1 selects MIOpen.
+    # Eager-PyTorch reference runs use PyTorch's native convolutions, not MIOpen: a MIOpen kernel
+    # of the eager MobileNetV2 batch-32 backward accesses memory past the end of a tensor.  It
+    # faults deterministically with no fused program in the process once every tensor ends at an
+    # unmapped page (tools/guard_pages.py), and in the suite whenever earlier tests leave a tensor
+    # at a segment end (profiles/fault_attribution_r6.md).  IDC_EAGER_MIOPEN=1 selects MIOpen.
     if os.environ.get("IDC_EAGER_MIOPEN", "0") != "1":
         torch.backends.cudnn.enabled = False
     config.addinivalue_line("markers", "gpu: needs an MI355X (runs on the GPU box)")
