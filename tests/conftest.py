@@ -19,6 +19,8 @@ def pytest_configure(config):
         torch.backends.cudnn.enabled = False
     config.addinivalue_line("markers", "gpu: needs an MI355X (runs on the GPU box)")
     config.addinivalue_line("markers", "slow: long-running")
+    config.addinivalue_line("markers", "miopen_ref: DenseNet/VGG-only eager reference, which runs on MIOpen "
+                                       "(guard-page clean, profiles/fault_attribution_r6.md)")
 
 
 def pytest_collection_modifyitems(config, items):
@@ -34,3 +36,20 @@ def pytest_collection_modifyitems(config, items):
 def _seed():
     torch.manual_seed(0)
     yield
+
+
+@pytest.fixture(autouse=True)
+def _miopen_reference(request):
+    """Tests marked ``miopen_ref`` build eager references of DenseNet/VGG only, whose MIOpen
+    convolutions ran clean under the guard-page allocator (tools/guard_pages.py): they use MIOpen,
+    which is several times faster than PyTorch's native fp32 convolutions at batch 256.  MobileNetV2
+    references stay on the native convolutions."""
+    if request.node.get_closest_marker("miopen_ref") is None or os.environ.get("IDC_EAGER_MIOPEN") == "0":
+        yield
+        return
+    prev = torch.backends.cudnn.enabled
+    torch.backends.cudnn.enabled = True
+    try:
+        yield
+    finally:
+        torch.backends.cudnn.enabled = prev

@@ -23,6 +23,7 @@ def _model(arch, seed=0):
     return m, ref
 
 
+@pytest.mark.miopen_ref
 @pytest.mark.parametrize("arch,B", [("densenet121", 64), ("vgg16", 32)])
 def test_deterministic_mode_is_bitwise_reproducible(monkeypatch, arch, B):
     monkeypatch.setenv("IDC_DETERMINISTIC", "1")
@@ -56,6 +57,7 @@ def test_deterministic_mode_is_bitwise_reproducible(monkeypatch, arch, B):
         assert torch.equal(a, b)
 
 
+@pytest.mark.miopen_ref
 @pytest.mark.parametrize("arch,B", [("densenet121", 64), ("vgg16", 32)])
 def test_dual_graph_backward_matches_direct_issue(monkeypatch, arch, B):
     """The backward replayed as two graphs (main lane + side lane joined by external events,

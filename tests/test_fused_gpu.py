@@ -73,6 +73,7 @@ def _check(m, ref, x, y, slack=0.03, loss_slack=None):
     assert not bad, bad[:8]
 
 
+@pytest.mark.miopen_ref
 def test_densenet121_fused_matches_eager():
     # batch 32: at batch 8 the 1x1 stage-4 maps normalise over 8 samples and one run in a few
     # drew a cluster of stage-4 gradients 1.6-1.8x further from fp32 than autocast (float-atomic
@@ -81,6 +82,7 @@ def test_densenet121_fused_matches_eager():
     _check(m, ref, x, y)
 
 
+@pytest.mark.miopen_ref
 def test_densenet121_moving_stats_and_step():
     m, ref, x, y = _setup("densenet121", 16)
     from idc_models_amd.engine import RMSprop
@@ -104,12 +106,14 @@ def test_densenet121_moving_stats_and_step():
     assert losses[-1] < losses[0], losses
 
 
+@pytest.mark.miopen_ref
 def test_densenet_phase1_frozen_base():
     m, ref, x, y = _setup("densenet121", 8, freeze_base=True)
     assert len(m.arena.params) == 2  # head kernel + bias only
     _check(m, ref, x, y)
 
 
+@pytest.mark.miopen_ref
 def test_densenet_fine_tune_at_150():
     # batch 32: at batch 8 the bf16 forward of this random-init net is chaotic (autocast's own
     # logit deviation from fp32 reaches 0.16), so the comparison would only measure noise
@@ -117,6 +121,7 @@ def test_densenet_fine_tune_at_150():
     _check(m, ref, x, y)
 
 
+@pytest.mark.miopen_ref
 def test_densenet201_cifar_shape():
     # batch 32: at batch 8 random-init DenseNet-201 is chaotic in bf16 (autocast's own gradient
     # cosine vs fp32 drops to ~0.4), which makes any comparison meaningless
@@ -128,6 +133,7 @@ def test_densenet201_cifar_shape():
     _check(m, ref, x, y, loss_slack=0.06)
 
 
+@pytest.mark.miopen_ref
 def test_vgg16_fused_matches_eager():
     m, ref, x, y = _setup("vgg16", 8)
     _check(m, ref, x, y)
@@ -232,7 +238,9 @@ def test_tinycnn_fused_dropout_trains_and_eval_is_deterministic():
     assert torch.equal(g1, g2)  # no dropout at inference
 
 
-@pytest.mark.parametrize("arch,slots", [("densenet121", "0"), ("densenet121", "1"), ("vgg16", "0"),
+@pytest.mark.parametrize("arch,slots", [pytest.param("densenet121", "0", marks=pytest.mark.miopen_ref),
+                                        pytest.param("densenet121", "1", marks=pytest.mark.miopen_ref),
+                                        pytest.param("vgg16", "0", marks=pytest.mark.miopen_ref),
                                         ("mobilenetv2", "0"), ("mobilenetv2", "1")])
 def test_fused_matches_eager_at_bench_batch(monkeypatch, arch, slots):
     """The benchmarked configuration, bs=256: the autotuner's tile and split-K choices, the
@@ -287,6 +295,7 @@ def _fp32_yardsticks(seed, x, y):
     return eager_grads(net, x, y, "fp32"), eager_grads(net, x, y, "autocast")
 
 
+@pytest.mark.miopen_ref
 @pytest.mark.parametrize("maxm", ["2304", "9216"])
 def test_batched_weight_gradients_match_per_layer(monkeypatch, maxm):
     """DenseNet-121 at the bench batch: the late stages' weight gradients launched as one batched
@@ -318,6 +327,7 @@ def test_batched_weight_gradients_match_per_layer(monkeypatch, maxm):
         m.impl.close()
 
 
+@pytest.mark.miopen_ref
 @pytest.mark.parametrize("B,maxm", [(8, "2304"), (256, "512"), (256, "9216"), (256, "2304")])
 def test_dense_stage_matches_per_layer(monkeypatch, B, maxm):
     """DenseNet-121: the late stages' dense layers as ONE persistent work-queue launch each
