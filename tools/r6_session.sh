@@ -1,4 +1,8 @@
-# round-6 GPU session (one call): same-box A/B of the row-resident stage-3 forward
+# round-6 GPU session (one call): HEAD bench + kernel-trace profiles of the three models
 set -o pipefail
 mkdir -p gpurun_out/r6
-tools/env_ab.sh 3 "base|-" "rows3|IDC_DS_ROWS=1 IDC_DS_ROWS_RB=1" "rows3rb2|IDC_DS_ROWS=1 IDC_DS_ROWS_RB=2" || exit 1
+timeout -k 10 300 python bench.py > gpurun_out/r6/bench_head.log 2>&1 || exit 1
+tail -1 gpurun_out/r6/bench_head.log
+tools/prof_session.sh dn121_head || exit 1
+tools/prof_session.sh vgg16_head --model vgg16 || exit 1
+tools/prof_session.sh mbv2_head --model mobilenetv2 || exit 1
