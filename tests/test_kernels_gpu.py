@@ -984,7 +984,7 @@ def _bn_train(x, g, b, eps):
 @pytest.mark.parametrize("N,H,c0,L,grid,rows", [(16, 3, 64, 3, 256, 0), (64, 1, 96, 4, 256, 0), (8, 3, 128, 2, 5, 0),
                                                (6, 2, 256, 3, 64, 0), (4, 1, 1120, 2, 256, 0),
                                                (64, 3, 256, 4, 256, 0), (256, 3, 256, 24, 256, 0),
-                                               (256, 1, 512, 16, 256, 0),
+                                               (256, 1, 512, 16, 256, 0), (256, 6, 128, 12, 256, 0),
                                                # row-resident launch (dense_rows_bwd.hip)
                                                (16, 3, 64, 3, 256, 1), (64, 1, 96, 4, 256, 1),
                                                (8, 3, 128, 2, 5, 1), (6, 2, 256, 3, 64, 1),
@@ -998,7 +998,8 @@ def test_dense_stage_bwd_matches_autograd(fn, N, H, c0, L, grid, rows):
     whole stage buffer with a random output gradient (the transition / final BatchNorm of
     lower_densenet).  grid 5: far fewer workgroups than tickets (queue order must still drain);
     c0 1120: DenseNet-201-wide inputs; 1x1 maps: centre-tap 3x3; (256, 3, 256, 24) and
-    (256, 1, 512, 16): DenseNet-121's stages 3 and 4 at the bench batch exactly.  rows 1: the
+    (256, 1, 512, 16): DenseNet-121's stages 3 and 4 at the bench batch exactly, (256, 6, 128, 12)
+    its stage 2.  rows 1: the
     row-resident launch (whole images per workgroup, the concat gradient held in LDS)."""
     if rows:
         ok, ipg, g = fn.nat.require().dense_rows_bwd_geometry(N, H, H, c0 + 32 * L, L)
