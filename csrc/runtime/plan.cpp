@@ -39,6 +39,7 @@
 #include "../kernels/conv_wgrad.h"
 #include "../kernels/dense_stage.h"
 #include "../kernels/mb_chain.h"
+#include "../kernels/mb_infer.h"
 #include "../kernels/dwconv.h"
 #include "../kernels/mlp_head.h"
 #include "../kernels/nn_kernels.h"
@@ -90,6 +91,8 @@ enum OpKind : int {
   // persistent MobileNetV2 block chain (mb_chain.hip): payload MbChainArgs, i[0] = grid,
   // i[1] = dynamic LDS bytes
   OP_MB_CHAIN = 30,
+  // one MobileNetV2 block in inference mode (mb_infer.hip): payload MbInferArgs
+  OP_MB_INFER = 31,
 };
 
 struct Op {
@@ -448,7 +451,7 @@ class Plan {
                                   "input", "memset", "bn_stats", "bn_apply", "dw_fwd", "dw_bwd_data",
                                   "dw_wgrad", "copy", "finite_check", "mlp_fwd", "mlp_bwd", "mlp_step",
                                   "collapse", "stats_shift", "allreduce", "wgrad_batch", "dense_stage",
-                                  "dense_stage_bwd"};
+                                  "dense_stage_bwd", "mb_chain", "mb_infer"};
     int k = ops_.at(idx).kind;
     return (k >= 0 && k < (int)(sizeof(names) / sizeof(names[0]))) ? names[k] : "?";
   }
@@ -685,6 +688,7 @@ class Plan {
       case OP_DENSE_STAGE: check(dense_stage_fwd(as<DenseStageArgs>(op), op.i[0], st), "dense_stage_fwd"); break;
       case OP_DENSE_STAGE_BWD: check(dense_stage_bwd(as<DenseBwdArgs>(op), op.i[0], st), "dense_stage_bwd"); break;
       case OP_MB_CHAIN: check(mb_chain(as<MbChainArgs>(op), op.i[0], op.i[1], st), "mb_chain"); break;
+      case OP_MB_INFER: check(mb_infer(as<MbInferArgs>(op), st), "mb_infer"); break;
       case OP_STATS_SHIFT:
         check(stats_shift(reinterpret_cast<const ShiftDesc*>(op.p[0]), op.i[0], op.i[1], st), "stats_shift");
         break;
@@ -798,6 +802,7 @@ py::dict struct_sizes() {
   d["DenseBwdLayerDesc"] = sizeof(DenseBwdLayerDesc);
   d["DenseBwdPhase"] = sizeof(DenseBwdPhase);
   d["MbPhaseDesc"] = sizeof(MbPhaseDesc);
+  d["MbInferArgs"] = sizeof(MbInferArgs);
   d["MbChainArgs"] = sizeof(MbChainArgs);
   d["MbPhaseDesc.pre"] = offsetof(MbPhaseDesc, pre);
   d["BnArgs.shift"] = offsetof(BnArgs, shift);
@@ -1135,6 +1140,13 @@ PYBIND11_MODULE(_idc_native, m) {
   m.attr("DS_SCRATCH_PER_LAYER") = DS_SCRATCH_PER_LAYER;
   m.attr("DS_MAX_CIN") = DS_MAX_CIN;
   m.attr("OP_MB_CHAIN") = (int)OP_MB_CHAIN;
+  m.attr("OP_MB_INFER") = (int)OP_MB_INFER;
+  m.def("mb_infer_smem", [](py::bytes payload) {
+    std::string s = payload;
+    if (s.size() != sizeof(MbInferArgs)) throw std::runtime_error("mb_infer_smem: bad payload");
+    return mb_infer_smem(*reinterpret_cast<const MbInferArgs*>(s.data()));
+  });
+  m.attr("MBI_MAX_ACC") = MBI_MAX_ACC;
   m.def("mb_phase_ok", [](py::bytes payload) {
     std::string s = payload;
     if (s.size() != sizeof(MbPhaseDesc)) throw std::runtime_error("mb_phase_ok: bad payload");

@@ -187,6 +187,14 @@ class MbChainArgs(C.Structure):
 
 MB_TAB, MB_PW, MB_DW = 1, 2, 3
 
+
+class MbInferArgs(C.Structure):
+    """One MobileNetV2 block in inference mode, one launch (csrc/kernels/mb_infer.h)."""
+    _fields_ = [("x", vp), ("ldx", ci), ("ldres", ci), ("xbn", BnArgs), ("res", vp), ("we", vp), ("ebn", BnArgs),
+                ("wd", vp), ("dbn", BnArgs), ("wp", vp), ("pbn", BnArgs), ("y", vp), ("ldy", ci)] + \
+               [(n, ci) for n in ("N", "H", "W", "Cin", "Cexp", "Cout", "Ho", "Wo", "S", "PT", "PL",
+                                  "residual", "ipg")]
+
 _STRUCTS = {"BnArgs": BnArgs, "BwdAff": BwdAff, "ConvArgs": ConvArgs, "WgradArgs": WgradArgs,
             "WgBatchEntry": WgBatchEntry,
             "BnBwdApplyArgs": BnBwdApplyArgs, "BnBwdReduceArgs": BnBwdReduceArgs,
@@ -195,7 +203,7 @@ _STRUCTS = {"BnArgs": BnArgs, "BwdAff": BwdAff, "ConvArgs": ConvArgs, "WgradArgs
             "DwArgs": DwArgs, "Mlp2Args": Mlp2Args, "ShiftDesc": ShiftDesc,
             "DenseStageArgs": DenseStageArgs, "DenseLayerDesc": DenseLayerDesc,
             "DenseBwdArgs": DenseBwdArgs, "DenseBwdLayerDesc": DenseBwdLayerDesc, "DenseBwdPhase": DenseBwdPhase,
-            "MbPhaseDesc": MbPhaseDesc, "MbChainArgs": MbChainArgs}
+            "MbPhaseDesc": MbPhaseDesc, "MbChainArgs": MbChainArgs, "MbInferArgs": MbInferArgs}
 
 # op kinds (csrc/runtime/plan.cpp)
 OP_CONV, OP_WGRAD, OP_BN_BWD_APPLY, OP_BN_BWD_REDUCE, OP_MAXPOOL, OP_AVGPOOL, OP_POOL_BWD = range(7)
@@ -205,6 +213,7 @@ OP_MLP_FWD, OP_MLP_BWD, OP_MLP_STEP, OP_COLLAPSE, OP_STATS_SHIFT, OP_ALLREDUCE, 
 OP_DENSE_STAGE = 28
 OP_DENSE_STAGE_BWD = 29
 OP_MB_CHAIN = 30
+OP_MB_INFER = 31
 
 ACT = {None: 0, "none": 0, "linear": 0, "relu": 1, "relu6": 2}
 OUT_BF16, OUT_F32, OUT_F32_ACC = 0, 1, 2
@@ -213,7 +222,7 @@ OUT_BF16, OUT_F32, OUT_F32_ACC = 0, 1, 2
 def _verify(ext):
     if ext.OP_ALLREDUCE != OP_ALLREDUCE:
         raise RuntimeError("native op-kind table drifted (OP_ALLREDUCE)")
-    if ext.OP_DENSE_STAGE != OP_DENSE_STAGE or ext.OP_MB_CHAIN != OP_MB_CHAIN:
+    if ext.OP_DENSE_STAGE != OP_DENSE_STAGE or ext.OP_MB_CHAIN != OP_MB_CHAIN or ext.OP_MB_INFER != OP_MB_INFER:
         raise RuntimeError("native op-kind table drifted (OP_DENSE_STAGE / OP_MB_CHAIN)")
     sizes = ext.struct_sizes()
     for name, cls in _STRUCTS.items():

@@ -384,6 +384,42 @@ def dwconv(x, kernel, stride=1, pads=(1, 1), out_hw=None, pro: Optional[BN] = No
     return y
 
 
+def mb_infer(x: torch.Tensor, we_hwio: Optional[torch.Tensor], ebn: Optional[BN], wd: torch.Tensor, dbn: BN,
+             wp_hwio: torch.Tensor, pbn: BN, stride=1, pads=(1, 1), out_hw=None, xbn: Optional[BN] = None,
+             res: Optional[torch.Tensor] = None, residual=False, ipg: int = 1) -> torch.Tensor:
+    """One MobileNetV2 block in inference mode as one launch (csrc/kernels/mb_infer.hip):
+    y = pbn(conv1x1_p(dbn(dw3x3(ebn(conv1x1_e(x_eff)))))) (+ x_eff), x_eff = xbn(x) (+ res);
+    ``we_hwio`` None: no expand (block 0).  BNs in mode 2 (moving statistics), ebn/dbn with ReLU6."""
+    N, H, W, Cin = x.shape
+    cexp = we_hwio.shape[3] if we_hwio is not None else Cin
+    cout = wp_hwio.shape[3]
+    if out_hw is None:
+        out_hw = ((H + 2 * pads[0] - 3) // stride + 1, (W + 2 * pads[1] - 3) // stride + 1)
+    Ho, Wo = out_hw
+    y = torch.empty((N, Ho, Wo, cout), dtype=torch.bfloat16, device=x.device)
+    we = weight_fwd_layout(we_hwio) if we_hwio is not None else None
+    wp = weight_fwd_layout(wp_hwio)
+    wdc = wd.contiguous()
+    a = nat.MbInferArgs()
+    a.x, a.ldx = x.data_ptr(), Cin
+    a.xbn = xbn.args() if xbn is not None else _ident()
+    if res is not None:
+        a.res, a.ldres = res.data_ptr(), res.shape[-1]
+    a.we = nat.ptr(we)
+    a.ebn = ebn.args() if ebn is not None else _ident()
+    a.wd = wdc.data_ptr()
+    a.dbn, a.wp, a.pbn = dbn.args(), wp.data_ptr(), pbn.args()
+    a.y, a.ldy = y.data_ptr(), cout
+    a.N, a.H, a.W, a.Cin, a.Cexp, a.Cout = N, H, W, Cin, cexp, cout
+    a.Ho, a.Wo, a.S, a.PT, a.PL = Ho, Wo, stride, pads[0], pads[1]
+    a.residual, a.ipg = 1 if residual else 0, ipg
+    if nat.require().mb_infer_smem(nat.raw(a)) < 0:
+        raise ValueError("mb_infer: shape outside the kernel's limits")
+    _plan1(nat.OP_MB_INFER, a)
+    torch.cuda.current_stream(x.device).synchronize()  # the bf16 weight copies die with this frame
+    return y
+
+
 def _dw_args(x, kernel, stride, pads, Ho, Wo, pro):
     N, H, W, C = x.shape
     a = nat.DwArgs()

@@ -1135,6 +1135,48 @@ class Builder:
         a.KH, a.KW, a.S, a.PT, a.PL, a.Ho, a.Wo = kh, kw, stride, pads[0], pads[1], Ho, Wo
         return a
 
+    def mb_infer(self, x: Tensor4, xbn: nat.BnArgs, res: Optional[Tensor4], ex, ebn: Optional["BNRef"], dwl,
+                 dbn: "BNRef", prj, pbn: "BNRef", y: Tensor4, *, stride: int, pads, residual: bool) -> bool:
+        """One MobileNetV2 block in inference mode as ONE launch (csrc/kernels/mb_infer.hip):
+        y = pbn(prj(ReLU6(dbn(dw(ReLU6(ebn(ex(x_eff)))))))) (+ x_eff), x_eff = xbn(x) (+ res).
+        ``ex`` None: no expand layer (block 0).  Every BatchNorm must be in inference mode.  Returns
+        False (nothing emitted) when the shape is outside the kernel's limits or the program is
+        grouped / deterministic; the caller then lowers the block layer by layer."""
+        if os.environ.get("IDC_MB_INFER", "1") != "1" or getattr(self, "grouped", False):
+            return False
+        if any(bn is not None and bn.mode != 2 for bn in (ebn, dbn, pbn)):
+            return False
+        ext = nat.load()
+        a = nat.MbInferArgs()
+        a.x, a.ldx = x.ptr, x.ld
+        a.xbn = xbn
+        if res is not None:
+            a.res, a.ldres = res.ptr, res.ld
+        cexp = ex.filters if ex is not None else x.C
+        if ex is not None:
+            a.we = self.conv_weight(ex, cin_pad=x.C)["fwd"].data_ptr()
+            a.ebn = ebn.args()
+        a.wd = dwl.depthwise_kernel.data_ptr()
+        a.dbn = dbn.args()
+        a.wp = self.conv_weight(prj, cin_pad=cexp)["fwd"].data_ptr()
+        a.pbn = pbn.args()
+        a.y, a.ldy = y.ptr, y.ld
+        a.N, a.H, a.W, a.Cin, a.Cexp, a.Cout = x.N, x.H, x.W, x.C, cexp, y.C
+        a.Ho, a.Wo, a.S, a.PT, a.PL = y.H, y.W, stride, pads[0], pads[1]
+        a.residual = 1 if residual else 0
+        # whole images per workgroup: enough output rows for the 16-row MFMA tiles (>= 64), as few
+        # images as that takes (every image a workgroup on the large maps)
+        hw = y.H * y.W
+        ipg = max(1, min(x.N, -(-64 // hw)))
+        if os.environ.get("IDC_MB_INFER_IPG"):
+            ipg = max(1, int(os.environ["IDC_MB_INFER_IPG"]))
+        for cand in (ipg, max(1, ipg // 2), max(1, ipg // 4), 1):
+            a.ipg = cand
+            if int(ext.mb_infer_smem(nat.raw(a))) >= 0:
+                self.emit(nat.OP_MB_INFER, a)
+                return True
+        return False
+
     def _no_det(self, what: str):
         if self.det:
             raise NotImplementedError(f"IDC_DETERMINISTIC: {what} has no fixed-order reduction yet "

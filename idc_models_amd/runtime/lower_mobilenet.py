@@ -30,7 +30,7 @@ import torch
 
 from ..models.layers import correct_pad
 from ..ops import _native as nat
-from .builder import F32, BNRef, Builder, Tensor4
+from .builder import F32, BNRef, Builder, Tensor4, act_only
 from .lower_common import RELU6, FreezeInfo, HeadIO, emit_head, emit_head_bwd, emit_input
 
 
@@ -98,6 +98,35 @@ def lower_mobilenet(b: Builder, net, U: int, input_dtype):
         pre = f"block_{bid}_" if bid else "expanded_conv_"
         blk = {"bid": bid, "stride": stride, "h_in": h_in}
         ch_on = chain is not None and bid >= chain_from
+        # a block no gradient reaches, whose BatchNorms all run on moving statistics (evaluate(),
+        # the frozen base of phase 1, the frozen prefix of the fine-tune phase): ONE launch for
+        # expand -> depthwise -> project (builder.mb_infer, csrc/kernels/mb_infer.hip)
+        prjbn_l = L[pre + "project_BN"]
+        if not ch_on and not fz.at_or_before(prjbn_l):
+            ex = L[pre + "expand"] if bid else None
+            bn_e = BNRef(L[pre + "expand_BN"], b, None, RELU6) if bid else None
+            dwl = L[pre + "depthwise"]
+            bn_d = BNRef(L[pre + "depthwise_BN"], b, None, RELU6)
+            prj = L[pre + "project"]
+            bn_p = BNRef(prjbn_l, b, None, 0)
+            pads, ho, wo = _dw_geometry(h, w, stride)
+            pw = prj.filters
+            residual = (cin == pw and stride == 1)
+            hout = b.nhwc(B, ho, wo, pw)
+            if bid == 0:
+                xsrc, xbn, xres = y0, bn0.args(), None
+            elif pending_out is not None:
+                xsrc, xbn, xres = pending_out[0], pending_out[1].args(), pending_out[2]
+            else:
+                xsrc, xbn, xres = h_in, act_only(0), None
+            if b.mb_infer(xsrc, xbn, xres, ex, bn_e, dwl, bn_d, prj, bn_p, hout, stride=stride, pads=pads,
+                          residual=residual):
+                blk.update(ex=ex, e=None, bn_in=bn_e if bid else bn0, dwl=dwl, pads=pads, d=None, bn_d=bn_d,
+                           prj=prj, p=None, bn_p=bn_p, residual=residual, h_out=hout, fused=True)
+                blocks.append(blk)
+                pending_out = None
+                h_in, cin, h, w = hout, pw, ho, wo
+                continue
         if bid:
             ex, exbn = L[pre + "expand"], L[pre + "expand_BN"]
             e = b.nhwc(B, h, w, ex.filters)

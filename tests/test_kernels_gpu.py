@@ -1227,3 +1227,63 @@ def test_conv_img_dgrad_matches_reference(fn, N, H):
     assert relerr(gsum, dZ2.sum((0, 1, 2))) < 2e-2
     assert relerr(gsumx, (dZ2 * xhat).sum((0, 1, 2))) < 2e-2
     assert torch.equal(db, k["gsum"]) and torch.equal(dg, k["gsumx"])
+
+
+@pytest.mark.parametrize("N,H,Cin,Cexp,Cout,S,residual,xin,ipg", [
+    (8, 25, 32, None, 16, 1, False, "bnrelu6", 1),   # block 0: no expand, stem BN + ReLU6 pending
+    (4, 25, 16, 96, 24, 2, False, "id", 1),          # block 1: stride 2 from the 25x25 map
+    (6, 13, 24, 144, 24, 1, True, "bnres", 1),       # block 2: pending project BN + shortcut input
+    (9, 7, 32, 192, 32, 1, True, "id", 2),           # 7x7 identity block, last group one image
+    (20, 4, 96, 576, 160, 2, False, "id", 16),       # block 13: stride 2 to 2x2, 16 images a group
+    (33, 2, 160, 960, 320, 1, False, "id", 16),      # block 16: 20 output tiles per group
+    (17, 2, 160, 960, 160, 1, True, "bnres", 16)])   # block 14
+def test_mb_infer_matches_reference(fn, N, H, Cin, Cexp, Cout, S, residual, xin, ipg):
+    """One MobileNetV2 block in inference mode as ONE launch (mb_infer.hip) vs an fp32 PyTorch
+    reference of the same block: x_eff = xbn(x) (+ res), expand 1x1 + BN + ReLU6, depthwise 3x3
+    (Keras correct_pad on stride 2) + BN + ReLU6, project 1x1 + BN (+ x_eff).  Intermediates are
+    rounded to bf16 where the kernel stores them (x_eff, the expanded and depthwise slices)."""
+    from idc_models_amd.models.layers import correct_pad
+    torch.manual_seed(N * 100 + Cin + H)
+    W = H
+    if S == 1:
+        pt, pb, pl, pr = 1, 1, 1, 1
+    else:
+        (pt, pb), (pl, pr) = correct_pad(H, W, 3)
+    Ho, Wo = (H + pt + pb - 3) // S + 1, (W + pl + pr - 3) // S + 1
+    ce = Cexp or Cin
+
+    def bnp(C, act):
+        return fn.BN(gamma=torch.rand(C, device=DEV) + 0.5, beta=torch.randn(C, device=DEV) * 0.1,
+                     mean=torch.randn(C, device=DEV) * 0.2, var=torch.rand(C, device=DEV) + 0.5, eps=1e-3,
+                     mode=2, act=act)
+
+    def bn_apply(v, bn):
+        z = (v - bn.mean) * torch.rsqrt(bn.var + bn.eps) * bn.gamma + bn.beta
+        return z.clamp(0, 6) if bn.act == 2 else z
+
+    x = bf(torch.randn(N, H, W, Cin, device=DEV))
+    res = bf(torch.randn(N, H, W, Cin, device=DEV)) if xin == "bnres" else None
+    xbn = bnp(Cin, 2 if xin == "bnrelu6" else 0) if xin != "id" else None
+    we = torch.randn(1, 1, Cin, ce, device=DEV) * (2.0 / Cin) ** 0.5 if Cexp else None
+    ebn = bnp(ce, 2) if Cexp else None
+    wd = torch.randn(3, 3, ce, 1, device=DEV) * (2.0 / 9) ** 0.5
+    dbn = bnp(ce, 2)
+    wp = torch.randn(1, 1, ce, Cout, device=DEV) * (1.0 / ce) ** 0.5
+    pbn = bnp(Cout, 0)
+    y = fn.mb_infer(x.to(torch.bfloat16), we, ebn, wd, dbn, wp, pbn, stride=S, pads=(pt, pl), out_hw=(Ho, Wo),
+                    xbn=xbn, res=res.to(torch.bfloat16) if res is not None else None, residual=residual, ipg=ipg)
+    # fp32 reference
+    xe = bn_apply(x, xbn) if xbn is not None else x
+    if res is not None:
+        xe = xe + res
+    xe = bf(xe)
+    e = bf(bn_apply(ref_conv(xe, bf(we), 1, (0, 0, 0, 0)), ebn)) if Cexp else xe
+    ec = F.pad(e.permute(0, 3, 1, 2), (pl, pr, pt, pb))
+    d = F.conv2d(ec, wd.permute(2, 3, 0, 1), stride=S, groups=ce).permute(0, 2, 3, 1)
+    d = bf(bn_apply(d, dbn))
+    ref = bn_apply(ref_conv(d, bf(wp), 1, (0, 0, 0, 0)), pbn)
+    if residual:
+        ref = ref + xe
+    assert y.shape == ref.shape
+    assert torch.isfinite(y.float()).all()
+    assert relerr(y, ref) < 1.5e-2, relerr(y, ref)

@@ -43,7 +43,8 @@ STRUCTS = {nat.OP_CONV: nat.ConvArgs, nat.OP_WGRAD: nat.WgradArgs, nat.OP_BN_BWD
            nat.OP_HEAD_BWD: nat.HeadBwdArgs, nat.OP_DW_FWD: nat.DwArgs, nat.OP_DW_BWD_DATA: nat.DwArgs,
            nat.OP_DW_WGRAD: nat.DwArgs, nat.OP_BN_APPLY: nat.BnArgs, nat.OP_MLP_FWD: nat.Mlp2Args,
            nat.OP_MLP_BWD: nat.Mlp2Args, nat.OP_DENSE_STAGE: nat.DenseStageArgs,
-           nat.OP_DENSE_STAGE_BWD: nat.DenseBwdArgs, nat.OP_MB_CHAIN: nat.MbChainArgs}
+           nat.OP_DENSE_STAGE_BWD: nat.DenseBwdArgs, nat.OP_MB_CHAIN: nat.MbChainArgs,
+           nat.OP_MB_INFER: nat.MbInferArgs}
 
 
 def _pointers(obj, out):
@@ -113,6 +114,34 @@ def test_frozen_base_backward_is_head_only():
     bwd = [op[1] for op in b.ops if op[0] == "bwd"]
     assert nat.OP_HEAD_BWD in bwd
     assert not any(k in (nat.OP_WGRAD, nat.OP_DW_WGRAD, nat.OP_CONV) for k in bwd)
+
+
+@pytest.mark.parametrize("ft,training,fused", [("frozen", True, 17), (None, False, 17), (100, True, None),
+                                               (None, True, 0)])
+def test_mb_infer_lowering(monkeypatch, ft, training, fused):
+    """Blocks no gradient reaches, with every BatchNorm on moving statistics, lower to ONE
+    OP_MB_INFER each (csrc/kernels/mb_infer.hip): all 17 in evaluation and in the frozen-base phase,
+    the frozen prefix only when fine-tuning from layer 100, none in full training;
+    IDC_MB_INFER=0 restores the three per-layer launches."""
+    from idc_models_amd.runtime.lower_common import FreezeInfo
+    _, net, b = _lower("mobilenetv2", ft, training)
+    kinds = [op[1] for op in b.ops if op[0] == "fwd"]
+    n = kinds.count(nat.OP_MB_INFER)
+    if fused is None:  # the blocks entirely inside the frozen prefix
+        fz = FreezeInfo(net.base, True)
+        names = ["expanded_conv_project_BN"] + [f"block_{i}_project_BN" for i in range(1, 17)]
+        L = {l.name: l for l in net.base.layers}
+        fused = sum(1 for nm in names if not fz.at_or_before(L[nm]))
+        assert 0 < fused < 17
+    assert n == fused
+    if fused == 17:
+        assert nat.OP_DW_FWD not in kinds
+    for op in b.ops:
+        if op[1] == nat.OP_MB_INFER:
+            assert nat.load().mb_infer_smem(op[2]) > 0
+    monkeypatch.setenv("IDC_MB_INFER", "0")
+    _, _, b0 = _lower("mobilenetv2", ft, training)
+    assert nat.OP_MB_INFER not in [op[1] for op in b0.ops]
 
 
 def test_fine_tune_backward_stops_at_first_trainable_layer():

@@ -43,6 +43,7 @@ SOURCES = [
     "kernels/dense_stage.hip",
     "kernels/dense_rows.hip",
     "kernels/mb_chain.hip",
+    "kernels/mb_infer.hip",
     "kernels/dense_stage_bwd.hip",
     "kernels/dense_rows_bwd.hip",
     "kernels/mlp_head.hip",
