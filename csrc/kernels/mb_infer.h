@@ -21,14 +21,21 @@ struct MbInferArgs {
   int N, H, W, Cin, Cexp, Cout, Ho, Wo, S, PT, PL;
   int residual;                 // 1: y += act(xbn(x)) + res (stride 1, Cin == Cout)
   int ipg;                      // whole images per workgroup
+  int cs;                       // expanded channels per workgroup (multiple of MBI_CC); the
+                                // ceil(Cexp / cs) workgroups of an image group reduce their
+                                // project partials through `slab` (last arriver: `tickets`)
+  float* slab;                  // >= mb_infer_slab_floats() fp32 (cs < Cexp only)
+  unsigned* tickets;            // one counter per image group, any start value (counts modulo)
 };
 
 constexpr int MBI_CC = 32;        // expanded channels per chunk (one MFMA K step of the project)
-constexpr int MBI_MAX_ACC = 20;   // project accumulator tiles per wave (16 x 16 fp32 each)
+constexpr int MBI_NT = 512;       // threads per workgroup (8 waves, 2 per SIMD)
+constexpr int MBI_MAX_ACC = 10;   // project accumulator tiles per wave (16 x 16 fp32 each)
 constexpr int MBI_MAX_KX = 192;   // padded input channels (expand K)
 
 // Dynamic LDS bytes of a launch, or -1 when the shape is outside the kernel's limits.
 long long mb_infer_smem(const MbInferArgs& a);
+long long mb_infer_slab_floats(const MbInferArgs& a);
 hipError_t mb_infer(const MbInferArgs& a, hipStream_t st);
 
 }  // namespace idc

@@ -1146,6 +1146,11 @@ PYBIND11_MODULE(_idc_native, m) {
     if (s.size() != sizeof(MbInferArgs)) throw std::runtime_error("mb_infer_smem: bad payload");
     return mb_infer_smem(*reinterpret_cast<const MbInferArgs*>(s.data()));
   });
+  m.def("mb_infer_slab_floats", [](py::bytes payload) {
+    std::string s = payload;
+    if (s.size() != sizeof(MbInferArgs)) throw std::runtime_error("mb_infer_slab_floats: bad payload");
+    return mb_infer_slab_floats(*reinterpret_cast<const MbInferArgs*>(s.data()));
+  });
   m.attr("MBI_MAX_ACC") = MBI_MAX_ACC;
   m.def("mb_phase_ok", [](py::bytes payload) {
     std::string s = payload;

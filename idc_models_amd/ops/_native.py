@@ -193,7 +193,18 @@ class MbInferArgs(C.Structure):
     _fields_ = [("x", vp), ("ldx", ci), ("ldres", ci), ("xbn", BnArgs), ("res", vp), ("we", vp), ("ebn", BnArgs),
                 ("wd", vp), ("dbn", BnArgs), ("wp", vp), ("pbn", BnArgs), ("y", vp), ("ldy", ci)] + \
                [(n, ci) for n in ("N", "H", "W", "Cin", "Cexp", "Cout", "Ho", "Wo", "S", "PT", "PL",
-                                  "residual", "ipg")]
+                                  "residual", "ipg", "cs")] + \
+               [("slab", vp), ("tickets", vp)]
+
+
+def mb_infer_default_cs(cexp: int, groups: int, expand: bool = True) -> int:
+    """Expanded channels per workgroup of an mb_infer launch (csrc/kernels/mb_infer.h): enough
+    slices per image group that the launch has >= 256 workgroups, in multiples of 32."""
+    full = -(-cexp // 32) * 32
+    if not expand:
+        return full
+    want = max(1, -(-256 // max(groups, 1)))
+    return min(full, max(32, -(-(-(-cexp // want)) // 32) * 32))
 
 _STRUCTS = {"BnArgs": BnArgs, "BwdAff": BwdAff, "ConvArgs": ConvArgs, "WgradArgs": WgradArgs,
             "WgBatchEntry": WgBatchEntry,

@@ -386,7 +386,8 @@ def dwconv(x, kernel, stride=1, pads=(1, 1), out_hw=None, pro: Optional[BN] = No
 
 def mb_infer(x: torch.Tensor, we_hwio: Optional[torch.Tensor], ebn: Optional[BN], wd: torch.Tensor, dbn: BN,
              wp_hwio: torch.Tensor, pbn: BN, stride=1, pads=(1, 1), out_hw=None, xbn: Optional[BN] = None,
-             res: Optional[torch.Tensor] = None, residual=False, ipg: int = 1) -> torch.Tensor:
+             res: Optional[torch.Tensor] = None, residual=False, ipg: int = 1,
+             cs: Optional[int] = None) -> torch.Tensor:
     """One MobileNetV2 block in inference mode as one launch (csrc/kernels/mb_infer.hip):
     y = pbn(conv1x1_p(dbn(dw3x3(ebn(conv1x1_e(x_eff)))))) (+ x_eff), x_eff = xbn(x) (+ res);
     ``we_hwio`` None: no expand (block 0).  BNs in mode 2 (moving statistics), ebn/dbn with ReLU6."""
@@ -413,10 +414,18 @@ def mb_infer(x: torch.Tensor, we_hwio: Optional[torch.Tensor], ebn: Optional[BN]
     a.N, a.H, a.W, a.Cin, a.Cexp, a.Cout = N, H, W, Cin, cexp, cout
     a.Ho, a.Wo, a.S, a.PT, a.PL = Ho, Wo, stride, pads[0], pads[1]
     a.residual, a.ipg = 1 if residual else 0, ipg
+    a.cs = cs or nat.mb_infer_default_cs(cexp, -(-N // ipg), we is not None)
+    slab = tickets = None
+    if -(-cexp // a.cs) > 1:  # several slices per image group: a partial slab + a ticket per group
+        tickets = torch.zeros(-(-N // ipg), dtype=torch.int32, device=x.device)
+        a.tickets = tickets.data_ptr()
+        slab = torch.empty(int(nat.require().mb_infer_slab_floats(nat.raw(a))), dtype=torch.float32,
+                           device=x.device)
+        a.slab = slab.data_ptr()
     if nat.require().mb_infer_smem(nat.raw(a)) < 0:
         raise ValueError("mb_infer: shape outside the kernel's limits")
     _plan1(nat.OP_MB_INFER, a)
-    torch.cuda.current_stream(x.device).synchronize()  # the bf16 weight copies die with this frame
+    torch.cuda.current_stream(x.device).synchronize()  # weights, slab and tickets die with this frame
     return y
 
 

@@ -1165,16 +1165,34 @@ class Builder:
         a.Ho, a.Wo, a.S, a.PT, a.PL = y.H, y.W, stride, pads[0], pads[1]
         a.residual = 1 if residual else 0
         # whole images per workgroup: enough output rows for the 16-row MFMA tiles (>= 64), as few
-        # images as that takes (every image a workgroup on the large maps)
+        # images as that takes (every image a workgroup on the large maps); expanded channels per
+        # workgroup: enough slices for >= 256 workgroups (nat.mb_infer_default_cs)
         hw = y.H * y.W
         ipg = max(1, min(x.N, -(-64 // hw)))
         if os.environ.get("IDC_MB_INFER_IPG"):
             ipg = max(1, int(os.environ["IDC_MB_INFER_IPG"]))
         for cand in (ipg, max(1, ipg // 2), max(1, ipg // 4), 1):
             a.ipg = cand
-            if int(ext.mb_infer_smem(nat.raw(a))) >= 0:
-                self.emit(nat.OP_MB_INFER, a)
-                return True
+            groups = -(-x.N // cand)
+            cs = nat.mb_infer_default_cs(cexp, groups, ex is not None)
+            if os.environ.get("IDC_MB_INFER_CS") and ex is not None:
+                cs = max(32, int(os.environ["IDC_MB_INFER_CS"]) // 32 * 32)
+            while cs >= 32:
+                a.cs = cs
+                if -(-cexp // cs) > 1:  # several slices: the shared split-K slab + a ticket per group
+                    if self.splitk_slab is None:
+                        self.splitk_slab = self.alloc((self.SLAB_FLOATS,), F32)
+                    a.slab = self.splitk_slab.data_ptr()
+                    a.tickets = self.alloc((groups,), torch.int32).data_ptr()
+                else:
+                    a.slab, a.tickets = 0, 0
+                if int(ext.mb_infer_smem(nat.raw(a))) >= 0 and \
+                        int(ext.mb_infer_slab_floats(nat.raw(a))) <= self.SLAB_FLOATS:
+                    self.emit(nat.OP_MB_INFER, a)
+                    return True
+                if ex is None:
+                    break
+                cs -= 32
         return False
 
     def _no_det(self, what: str):

@@ -1229,19 +1229,24 @@ def test_conv_img_dgrad_matches_reference(fn, N, H):
     assert torch.equal(db, k["gsum"]) and torch.equal(dg, k["gsumx"])
 
 
-@pytest.mark.parametrize("N,H,Cin,Cexp,Cout,S,residual,xin,ipg", [
-    (8, 25, 32, None, 16, 1, False, "bnrelu6", 1),   # block 0: no expand, stem BN + ReLU6 pending
-    (4, 25, 16, 96, 24, 2, False, "id", 1),          # block 1: stride 2 from the 25x25 map
-    (6, 13, 24, 144, 24, 1, True, "bnres", 1),       # block 2: pending project BN + shortcut input
-    (9, 7, 32, 192, 32, 1, True, "id", 2),           # 7x7 identity block, last group one image
-    (20, 4, 96, 576, 160, 2, False, "id", 16),       # block 13: stride 2 to 2x2, 16 images a group
-    (33, 2, 160, 960, 320, 1, False, "id", 16),      # block 16: 20 output tiles per group
-    (17, 2, 160, 960, 160, 1, True, "bnres", 16)])   # block 14
-def test_mb_infer_matches_reference(fn, N, H, Cin, Cexp, Cout, S, residual, xin, ipg):
+@pytest.mark.parametrize("N,H,Cin,Cexp,Cout,S,residual,xin,ipg,cs", [
+    (8, 25, 32, None, 16, 1, False, "bnrelu6", 1, None),   # block 0: no expand, stem BN + ReLU6 pending
+    (4, 25, 16, 96, 24, 2, False, "id", 1, None),          # block 1: stride 2 from the 25x25 map
+    (6, 13, 24, 144, 24, 1, True, "bnres", 1, None),       # block 2: pending project BN + shortcut input
+    (6, 13, 24, 144, 24, 1, True, "bnres", 1, 64),         # same, 3 slices (last one 16 channels)
+    (9, 7, 32, 192, 32, 1, True, "id", 2, None),           # 7x7 identity block, last group one image
+    (20, 4, 96, 576, 160, 2, False, "id", 16, None),       # block 13: stride 2 to 2x2, 16 images a group
+    (33, 2, 160, 960, 320, 1, False, "id", 16, None),      # block 16: 20 output tiles per group, 15 slices
+    (17, 2, 160, 960, 160, 1, True, "bnres", 16, 320),     # block 14, 3 slices
+    (17, 2, 160, 960, 160, 1, True, "bnres", 16, 960)])    # block 14, one slice (no partials)
+def test_mb_infer_matches_reference(fn, N, H, Cin, Cexp, Cout, S, residual, xin, ipg, cs):
     """One MobileNetV2 block in inference mode as ONE launch (mb_infer.hip) vs an fp32 PyTorch
     reference of the same block: x_eff = xbn(x) (+ res), expand 1x1 + BN + ReLU6, depthwise 3x3
     (Keras correct_pad on stride 2) + BN + ReLU6, project 1x1 + BN (+ x_eff).  Intermediates are
-    rounded to bf16 where the kernel stores them (x_eff, the expanded and depthwise slices)."""
+    rounded to bf16 where the kernel stores them (x_eff, the expanded and depthwise slices).  ``cs``:
+    expanded channels per workgroup (several slices: partials summed by the group's last arriver;
+    None: the launch default); the second launch of the same op must agree bit for bit (tickets
+    count modulo the slices, the partials sum in slice order)."""
     from idc_models_amd.models.layers import correct_pad
     torch.manual_seed(N * 100 + Cin + H)
     W = H
@@ -1271,7 +1276,8 @@ def test_mb_infer_matches_reference(fn, N, H, Cin, Cexp, Cout, S, residual, xin,
     wp = torch.randn(1, 1, ce, Cout, device=DEV) * (1.0 / ce) ** 0.5
     pbn = bnp(Cout, 0)
     y = fn.mb_infer(x.to(torch.bfloat16), we, ebn, wd, dbn, wp, pbn, stride=S, pads=(pt, pl), out_hw=(Ho, Wo),
-                    xbn=xbn, res=res.to(torch.bfloat16) if res is not None else None, residual=residual, ipg=ipg)
+                    xbn=xbn, res=res.to(torch.bfloat16) if res is not None else None, residual=residual, ipg=ipg,
+                    cs=cs)
     # fp32 reference
     xe = bn_apply(x, xbn) if xbn is not None else x
     if res is not None:
@@ -1287,3 +1293,7 @@ def test_mb_infer_matches_reference(fn, N, H, Cin, Cexp, Cout, S, residual, xin,
     assert y.shape == ref.shape
     assert torch.isfinite(y.float()).all()
     assert relerr(y, ref) < 1.5e-2, relerr(y, ref)
+    y2 = fn.mb_infer(x.to(torch.bfloat16), we, ebn, wd, dbn, wp, pbn, stride=S, pads=(pt, pl), out_hw=(Ho, Wo),
+                     xbn=xbn, res=res.to(torch.bfloat16) if res is not None else None, residual=residual,
+                     ipg=ipg, cs=cs)
+    assert torch.equal(y, y2)
