@@ -101,8 +101,14 @@ def lower_mobilenet(b: Builder, net, U: int, input_dtype):
         # a block no gradient reaches, whose BatchNorms all run on moving statistics (evaluate(),
         # the frozen base of phase 1, the frozen prefix of the fine-tune phase): ONE launch for
         # expand -> depthwise -> project (builder.mb_infer, csrc/kernels/mb_infer.hip)
+        # Only the blocks with <= IDC_MB_INFER_MAX_CEXP expanded channels (default 192: blocks 0-6,
+        # the 25x25 / 13x13 / 7x7 maps): there one launch beats the three per-layer ones (block 1,
+        # 25x25 -> 13x13, 96 channels: 33 vs 92 us); on the wide 4x4 / 2x2 blocks (384-960 channels)
+        # the per-layer launches are faster (block 16: 77 vs 37 us), see BASELINE.md round 6
         prjbn_l = L[pre + "project_BN"]
-        if not ch_on and not fz.at_or_before(prjbn_l):
+        cexp_b = L[pre + "expand"].filters if bid else cin
+        if not ch_on and not fz.at_or_before(prjbn_l) and \
+                cexp_b <= int(os.environ.get("IDC_MB_INFER_MAX_CEXP", "192")):
             ex = L[pre + "expand"] if bid else None
             bn_e = BNRef(L[pre + "expand_BN"], b, None, RELU6) if bid else None
             dwl = L[pre + "depthwise"]

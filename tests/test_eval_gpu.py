@@ -31,9 +31,14 @@ def _randomise_bn(net, seed):
     return n
 
 
-@pytest.mark.parametrize("arch,B,shape", [("densenet121", 256, None), ("vgg16", 256, None),
-                                          ("mobilenetv2", 256, None), ("densenet201", 256, (32, 32, 3))])
-def test_fused_eval_matches_eager_inference(arch, B, shape):
+@pytest.mark.parametrize("arch,B,shape,fuse_all", [("densenet121", 256, None, False), ("vgg16", 256, None, False),
+                                                   ("mobilenetv2", 256, None, False), ("mobilenetv2", 256, None, True),
+                                                   ("densenet201", 256, (32, 32, 3), False)])
+def test_fused_eval_matches_eager_inference(monkeypatch, arch, B, shape, fuse_all):
+    """``fuse_all``: every MobileNetV2 block as one mb_infer launch (IDC_MB_INFER_MAX_CEXP lifted;
+    the default fuses blocks 0-6 only)."""
+    if fuse_all:
+        monkeypatch.setenv("IDC_MB_INFER_MAX_CEXP", "4096")
     from idc_models_amd.engine import Model, RMSprop
     from idc_models_amd.models import build_model
     net = build_model(arch, shape, num_outputs=1, seed=21)

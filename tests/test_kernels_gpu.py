@@ -1237,8 +1237,8 @@ def test_conv_img_dgrad_matches_reference(fn, N, H):
     (9, 7, 32, 192, 32, 1, True, "id", 2, None),           # 7x7 identity block, last group one image
     (20, 4, 96, 576, 160, 2, False, "id", 16, None),       # block 13: stride 2 to 2x2, 16 images a group
     (33, 2, 160, 960, 320, 1, False, "id", 16, None),      # block 16: 20 output tiles per group, 15 slices
-    (17, 2, 160, 960, 160, 1, True, "bnres", 16, 320),     # block 14, 3 slices
-    (17, 2, 160, 960, 160, 1, True, "bnres", 16, 960)])    # block 14, one slice (no partials)
+    (17, 2, 160, 960, 160, 1, True, "bnres", 16, 128),     # block 14, 8 slices (last one 64 channels)
+    (17, 2, 160, 960, 160, 1, True, "bnres", 16, 96)])     # block 14, 10 slices
 def test_mb_infer_matches_reference(fn, N, H, Cin, Cexp, Cout, S, residual, xin, ipg, cs):
     """One MobileNetV2 block in inference mode as ONE launch (mb_infer.hip) vs an fp32 PyTorch
     reference of the same block: x_eff = xbn(x) (+ res), expand 1x1 + BN + ReLU6, depthwise 3x3
