@@ -22,6 +22,12 @@
 // L2/HBM twice (MobileNetV2 frozen-base step: 55 forward dispatches of ~13 us).
 // Reference: the MobileNetV2 backbone of dist_model_tf_mobile.py:119-122, 134-138 (inference passes).
 #include "mb_infer.h"
+#include "persist.h"
+
+// phase timestamps for tools/micro/mbi_phases.hip (compiled out everywhere else)
+#ifndef IDC_MBI_STAMP
+#define IDC_MBI_STAMP(i)
+#endif
 
 namespace idc {
 
@@ -97,47 +103,16 @@ __global__ __launch_bounds__(NT) void mb_infer_kernel(MbInferArgs a) {
   const int HWi = a.H * a.W, HWo = a.Ho * a.Wo;
   const int pin = nimg * HWi, pout = nimg * HWo;
   const int frow = lane & 15, fk = (lane >> 4) * 8;
+  IDC_MBI_STAMP(0);
 
-  // ---- 0a. affine tables and the slice's depthwise taps (one item per thread, one latency)
-  {
-    const int nx = g.KX, nes = g.CS, np = g.NTO * 16, nwd = 9 * g.CS;
-    for (int i = tid; i < nx + nes + np + nwd; i += NT) {
-      if (i < nx) {
-        float s = 0.f, f = 0.f;
-        if (i < a.Cin) bn_coeffs(a.xbn, i, s, f);
-        x_sc[i] = s;
-        x_sf[i] = f;
-      } else if (i < nx + nes) {
-        const int lc = i - nx, c = cs0 + lc;
-        float s = 0.f, f = 0.f, s2 = 0.f, f2 = 0.f;
-        if (lc < csn) {
-          if (expand) bn_coeffs(a.ebn, c, s, f);
-          bn_coeffs(a.dbn, c, s2, f2);
-        }
-        e_sc[lc] = s;
-        e_sf[lc] = f;
-        d_sc[lc] = s2;
-        d_sf[lc] = f2;
-      } else if (i < nx + nes + np) {
-        const int c = i - nx - nes;
-        float s = 0.f, f = 0.f;
-        if (c < a.Cout) bn_coeffs(a.pbn, c, s, f);
-        p_sc[c] = s;
-        p_sf[c] = f;
-      } else {
-        const int j = i - nx - nes - np, t = j / g.CS, lc = j - t * g.CS;
-        s_wd[j] = lc < csn ? a.wd[(size_t)t * a.Cexp + cs0 + lc] : 0.f;
-      }
-    }
-  }
-  __syncthreads();  // x_sc / x_sf feed the input transform below
-
-  // ---- 0b. weight slices and x_eff into LDS: one index space, 8 loads in flight per thread
+  // ---- 0. weight slices, x_eff, affine tables and depthwise taps into LDS, 8 loads in flight per
+  // thread.  The tables' loads are issued after the first round of weight / input loads, so both
+  // arrive in one memory latency (the input transform needs the x table: it runs after the barrier)
   {
     const int KX8 = g.KX / 8, CS8 = g.CS / 8;
     const int n_we = expand ? g.CS * KX8 : 0, n_wp = g.NTO * 16 * CS8, n_x = g.RIN * KX8;
     const int total = n_we + n_wp + n_x;
-    const float lo = act_lo(a.xbn.act), hi = act_hi(a.xbn.act);
+    const float xlo = act_lo(a.xbn.act), xhi = act_hi(a.xbn.act);
     constexpr int U = 8;
     for (int base = 0; base < total; base += U * NT) {
       uint4 v[U], r[U];
@@ -148,12 +123,10 @@ __global__ __launch_bounds__(NT) void mb_infer_kernel(MbInferArgs a) {
         r[u] = make_uint4(0, 0, 0, 0);
         if (i < n_we) {
           const int row = i / KX8, k = (i - row * KX8) * 8;
-          if (row < csn && k < a.Cin)
-            v[u] = *reinterpret_cast<const uint4*>(a.we + (size_t)(cs0 + row) * a.Cin + k);
+          if (row < csn && k < a.Cin) v[u] = *reinterpret_cast<const uint4*>(a.we + (size_t)(cs0 + row) * a.Cin + k);
         } else if (i < n_we + n_wp) {
           const int j = i - n_we, col = j / CS8, k = (j - col * CS8) * 8;
-          if (col < a.Cout && k < csn)
-            v[u] = *reinterpret_cast<const uint4*>(a.wp + (size_t)col * a.Cexp + cs0 + k);
+          if (col < a.Cout && k < csn) v[u] = *reinterpret_cast<const uint4*>(a.wp + (size_t)col * a.Cexp + cs0 + k);
         } else if (i < total) {
           const int j = i - n_we - n_wp, p = j / KX8, c = (j - p * KX8) * 8;
           if (p < pin && c < a.Cin) {
@@ -162,6 +135,39 @@ __global__ __launch_bounds__(NT) void mb_infer_kernel(MbInferArgs a) {
             if (a.res) r[u] = *reinterpret_cast<const uint4*>(a.res + pix * a.ldres + c);
           }
         }
+      }
+      if (base == 0) {
+        const int nx = g.KX, nes = g.CS, np = g.NTO * 16, nwd = 9 * g.CS;
+        for (int i = tid; i < nx + nes + np + nwd; i += NT) {
+          if (i < nx) {
+            float s = 0.f, f = 0.f;
+            if (i < a.Cin) bn_coeffs(a.xbn, i, s, f);
+            x_sc[i] = s;
+            x_sf[i] = f;
+          } else if (i < nx + nes) {
+            const int lc = i - nx, c = cs0 + lc;
+            float s = 0.f, f = 0.f, s2 = 0.f, f2 = 0.f;
+            if (lc < csn) {
+              if (expand) bn_coeffs(a.ebn, c, s, f);
+              bn_coeffs(a.dbn, c, s2, f2);
+            }
+            e_sc[lc] = s;
+            e_sf[lc] = f;
+            d_sc[lc] = s2;
+            d_sf[lc] = f2;
+          } else if (i < nx + nes + np) {
+            const int c = i - nx - nes;
+            float s = 0.f, f = 0.f;
+            if (c < a.Cout) bn_coeffs(a.pbn, c, s, f);
+            p_sc[c] = s;
+            p_sf[c] = f;
+          } else {
+            const int j = i - nx - nes - np, t = j / g.CS, lc = j - t * g.CS;
+            s_wd[j] = lc < csn ? a.wd[(size_t)t * a.Cexp + cs0 + lc] : 0.f;
+          }
+        }
+        __syncthreads();  // x_sc / x_sf feed the input transform below
+        IDC_MBI_STAMP(1);
       }
 #pragma unroll
       for (int u = 0; u < U; ++u) {
@@ -180,7 +186,7 @@ __global__ __launch_bounds__(NT) void mb_infer_kernel(MbInferArgs a) {
             unpack8(v[u], xv);
             unpack8(r[u], rv);
 #pragma unroll
-            for (int q = 0; q < 8; ++q) xv[q] = clampf(fmaf(xv[q], x_sc[c + q], x_sf[c + q]), lo, hi) + rv[q];
+            for (int q = 0; q < 8; ++q) xv[q] = clampf(fmaf(xv[q], x_sc[c + q], x_sf[c + q]), xlo, xhi) + rv[q];
             out = pack8(xv);
           }
           *reinterpret_cast<uint4*>(Xs + p * g.XS + c) = out;
@@ -189,6 +195,7 @@ __global__ __launch_bounds__(NT) void mb_infer_kernel(MbInferArgs a) {
     }
   }
   __syncthreads();
+  IDC_MBI_STAMP(2);
 
   // ---- 1. chunks of the slice
   const int ntile = g.MTO * g.NTO;
@@ -257,6 +264,7 @@ __global__ __launch_bounds__(NT) void mb_infer_kernel(MbInferArgs a) {
       }
     }
     __syncthreads();
+    if (ch == 0) IDC_MBI_STAMP(3);
     // (C) project partial: Y += D . Wp[:, chunk]^T
 #pragma unroll
     for (int j = 0; j < MBI_MAX_ACC; ++j) {
@@ -272,47 +280,61 @@ __global__ __launch_bounds__(NT) void mb_infer_kernel(MbInferArgs a) {
     //  which every wave reaches after finishing this step)
   }
 
+  IDC_MBI_STAMP(4);
   // ---- 2. several slices: publish the partial, the group's last arriver sums them in order
   if (g.NSPLIT > 1) {
     constexpr int PT = NW * MBI_MAX_ACC * 64;  // float4 slots of one slice's partial
     float4* gslab = reinterpret_cast<float4*>(a.slab) + (size_t)group * g.NSPLIT * PT;
     float4* mine = gslab + (size_t)split * PT;
+    // (persist.h memory model: agent-scope stores, drained before one lane's ticket increment;
+    //  the last arriver reads them with agent-scope loads -- no L2 write-back / invalidate fences)
 #pragma unroll
     for (int j = 0; j < MBI_MAX_ACC; ++j)
-      if (wid + NW * j < ntile) mine[(j * NW + wid) * 64 + lane] = make_float4(pacc[j][0], pacc[j][1], pacc[j][2], pacc[j][3]);
+      if (wid + NW * j < ntile)
+        persist::st_coh16(mine + (j * NW + wid) * 64 + lane,
+                          make_uint4(__float_as_uint(pacc[j][0]), __float_as_uint(pacc[j][1]),
+                                     __float_as_uint(pacc[j][2]), __float_as_uint(pacc[j][3])));
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     int* s_flag = reinterpret_cast<int*>(Ds);  // (D is free: every wave is past the chunk loop)
     if (tid == 0) {
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       const unsigned prev = __hip_atomic_fetch_add(&a.tickets[group], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      const int last = (prev % (unsigned)g.NSPLIT) == (unsigned)(g.NSPLIT - 1);
-      if (last) {
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      }
-      s_flag[0] = last;
+      s_flag[0] = (prev % (unsigned)g.NSPLIT) == (unsigned)(g.NSPLIT - 1);
     }
     __syncthreads();
     const int last = s_flag[0];
+    IDC_MBI_STAMP(5);
     if (!last) return;
 #pragma unroll
     for (int j = 0; j < MBI_MAX_ACC; ++j) pacc[j] = (v4f){0.f, 0.f, 0.f, 0.f};
-    for (int sl = 0; sl < g.NSPLIT; ++sl) {
-      const float4* o = gslab + (size_t)sl * PT;
+    // two slices' tiles in flight per round trip, summed in slice order
+    for (int sl = 0; sl < g.NSPLIT; sl += 2) {
+      uint4 q0[MBI_MAX_ACC], q1[MBI_MAX_ACC];
+      const float4* o0 = gslab + (size_t)sl * PT;
+      const float4* o1 = gslab + (size_t)(sl + 1) * PT;
+      const bool two = sl + 1 < g.NSPLIT;
 #pragma unroll
       for (int j = 0; j < MBI_MAX_ACC; ++j)
         if (wid + NW * j < ntile) {
-          const float4 q = o[(j * NW + wid) * 64 + lane];
-          pacc[j][0] += q.x;
-          pacc[j][1] += q.y;
-          pacc[j][2] += q.z;
-          pacc[j][3] += q.w;
+          q0[j] = persist::ld_coh16(o0 + (j * NW + wid) * 64 + lane);
+          q1[j] = two ? persist::ld_coh16(o1 + (j * NW + wid) * 64 + lane) : make_uint4(0, 0, 0, 0);
+        }
+#pragma unroll
+      for (int j = 0; j < MBI_MAX_ACC; ++j)
+        if (wid + NW * j < ntile) {
+          pacc[j][0] += __uint_as_float(q0[j].x);
+          pacc[j][1] += __uint_as_float(q0[j].y);
+          pacc[j][2] += __uint_as_float(q0[j].z);
+          pacc[j][3] += __uint_as_float(q0[j].w);
+          pacc[j][0] += __uint_as_float(q1[j].x);
+          pacc[j][1] += __uint_as_float(q1[j].y);
+          pacc[j][2] += __uint_as_float(q1[j].z);
+          pacc[j][3] += __uint_as_float(q1[j].w);
         }
     }
   }
 
+  IDC_MBI_STAMP(6);
   // ---- 3. y = pbn(Y) (+ x_eff)
 #pragma unroll
   for (int j = 0; j < MBI_MAX_ACC; ++j) {
@@ -334,6 +356,7 @@ __global__ __launch_bounds__(NT) void mb_infer_kernel(MbInferArgs a) {
       }
     }
   }
+  IDC_MBI_STAMP(7);
 }
 
 long long mb_infer_smem(const MbInferArgs& a) {

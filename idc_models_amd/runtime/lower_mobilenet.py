@@ -101,14 +101,15 @@ def lower_mobilenet(b: Builder, net, U: int, input_dtype):
         # a block no gradient reaches, whose BatchNorms all run on moving statistics (evaluate(),
         # the frozen base of phase 1, the frozen prefix of the fine-tune phase): ONE launch for
         # expand -> depthwise -> project (builder.mb_infer, csrc/kernels/mb_infer.hip)
-        # Only the blocks with <= IDC_MB_INFER_MAX_CEXP expanded channels (default 192: blocks 0-6,
-        # the 25x25 / 13x13 / 7x7 maps): there one launch beats the three per-layer ones (block 1,
-        # 25x25 -> 13x13, 96 channels: 33 vs 92 us); on the wide 4x4 / 2x2 blocks (384-960 channels)
-        # the per-layer launches are faster (block 16: 77 vs 37 us), see BASELINE.md round 6
+        # Only the blocks with <= IDC_MB_INFER_MAX_CEXP expanded channels (default 576: blocks 0-13):
+        # there one launch beats the three per-layer ones (block 1, 25x25 -> 13x13, 96 channels: 33
+        # vs 92 us); on the 2x2 blocks with 960 channels the per-layer launches are still faster
+        # (frozen-base step 0.687-0.688 ms at 576, 0.703-0.708 at 192, 0.712-0.726 with every block
+        # fused, 0.833-0.847 per-layer: profiles/mobilenetv2_mb_infer_blocks.md)
         prjbn_l = L[pre + "project_BN"]
         cexp_b = L[pre + "expand"].filters if bid else cin
         if not ch_on and not fz.at_or_before(prjbn_l) and \
-                cexp_b <= int(os.environ.get("IDC_MB_INFER_MAX_CEXP", "192")):
+                cexp_b <= int(os.environ.get("IDC_MB_INFER_MAX_CEXP", "576")):
             ex = L[pre + "expand"] if bid else None
             bn_e = BNRef(L[pre + "expand_BN"], b, None, RELU6) if bid else None
             dwl = L[pre + "depthwise"]

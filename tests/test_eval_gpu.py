@@ -36,7 +36,7 @@ def _randomise_bn(net, seed):
                                                    ("densenet201", 256, (32, 32, 3), False)])
 def test_fused_eval_matches_eager_inference(monkeypatch, arch, B, shape, fuse_all):
     """``fuse_all``: every MobileNetV2 block as one mb_infer launch (IDC_MB_INFER_MAX_CEXP lifted;
-    the default fuses blocks 0-6 only)."""
+    the default fuses blocks 0-13 only)."""
     if fuse_all:
         monkeypatch.setenv("IDC_MB_INFER_MAX_CEXP", "4096")
     from idc_models_amd.engine import Model, RMSprop
