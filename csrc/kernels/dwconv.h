@@ -41,5 +41,10 @@ long long dwconv_wgrad_ws_floats(long long M, int C, int taps);
 hipError_t dwconv_fwd(const DwArgs& a, hipStream_t st);
 hipError_t dwconv_bwd_data(const DwArgs& a, hipStream_t st);
 hipError_t dwconv_wgrad(const DwArgs& a, hipStream_t st);
+// stride-1 3x3: data + weight gradients in one pass (dx, gsum/gsumx as dwconv_bwd_data; the weight
+// gradient's per-block partials into ws), then dwconv_wgrad_sum folds ws into dw
+bool dwconv_bwd_fused_ok(const DwArgs& a);
+hipError_t dwconv_bwd_fused(const DwArgs& a, hipStream_t st);
+hipError_t dwconv_wgrad_sum(const DwArgs& a, hipStream_t st);
 
 }  // namespace idc

@@ -520,6 +520,179 @@ __global__ __launch_bounds__(256) void dw_bwd3_kernel(DwArgs a, GroupArg ga) {
 }
 
 
+// Stride-1 depthwise 3x3 backward, data AND weight gradients in one pass over the same operands
+// (VERDICT r5 item 5a).  A thread's strip of P pixels x 8 channels loads the 3 x (P+2) window of
+// dY (the data gradient's gather, as dw_bwd3_kernel) and the 3 x (P+2) window of the raw input x
+// (the weight gradient's taps, as dw_wgrad3_part_kernel): 36 loads per strip where the two kernels
+// issue 22 + 22, the strip's own dY row and x row are shared, and one launch replaces two.  The
+// data gradient's epilogue (act' mask of the pending BN + activation, the BN-backward sums) is
+// dw_bwd3_kernel's; the weight-gradient partials are reduced per block into ws[block][9][C] like
+// dw_wgrad3_part_kernel's and summed by dwconv_wgrad_sum (a separate, side-lane launch).
+__global__ __launch_bounds__(256) void dw_bwd3_fused_kernel(DwArgs a, GroupArg ga) {
+  gshift(a, goff(ga));
+  constexpr int P = kDwStrip, NCOL = P + 2;
+  extern __shared__ float sh[];
+  const DwChunks dc = dw_chunks(a.C);
+  const int CB = dc.c8b * 8, cb = blockIdx.y * CB;
+  float* s_sc = sh;
+  float* s_sf = sh + CB;
+  float* s_mu = sh + 2 * CB;
+  float* s_rs = sh + 3 * CB;
+  float* s_a = sh + 4 * CB;
+  float* s_b = sh + 5 * CB;
+  float* s_tmp = sh + 6 * CB;  // chunk_sums scratch (2 x 256 x 8) / weight-gradient rows (256 x 24)
+  const bool epi = !(a.pro.mode == 0 && a.pro.act == ACT_NONE);
+  for (int i = threadIdx.x; i < CB; i += blockDim.x) {
+    const int c = cb + i;
+    bn_coeffs(a.pro, c, s_sc[i], s_sf[i]);
+    float mean = 0.f, rstd = 1.f;
+    if (a.pro.mode) bn_mean_rstd(a.pro, c, mean, rstd);
+    s_mu[i] = mean; s_rs[i] = rstd; s_a[i] = 0.f; s_b[i] = 0.f;
+  }
+  __syncthreads();
+  const int tx = threadIdx.x % dc.c8b, ty = threadIdx.x / dc.c8b;
+  const int WS = (a.W + P - 1) / P;
+  const int strips = a.N * a.H * WS;
+  float ps[8] = {0}, px[8] = {0};
+  float acc[9][8];
+#pragma unroll
+  for (int t = 0; t < 9; ++t)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc[t][j] = 0.f;
+  if (ty < dc.R) {
+    const int cl = tx * 8, c = cb + cl;
+    float wk[9][8], sc[8], sf[8], mu[8], rs[8];
+#pragma unroll
+    for (int t = 0; t < 9; ++t) {
+      const float4 w0 = *reinterpret_cast<const float4*>(a.w + (size_t)t * a.C + c);
+      const float4 w1 = *reinterpret_cast<const float4*>(a.w + (size_t)t * a.C + c + 4);
+      wk[t][0] = w0.x; wk[t][1] = w0.y; wk[t][2] = w0.z; wk[t][3] = w0.w;
+      wk[t][4] = w1.x; wk[t][5] = w1.y; wk[t][6] = w1.z; wk[t][7] = w1.w;
+    }
+#pragma unroll
+    for (int j = 0; j < 8; ++j) { sc[j] = s_sc[cl + j]; sf[j] = s_sf[cl + j]; mu[j] = s_mu[cl + j]; rs[j] = s_rs[cl + j]; }
+    const float lo = act_lo(a.pro.act), hi = act_hi(a.pro.act);
+    for (int st = blockIdx.x * dc.R + ty; st < strips; st += gridDim.x * dc.R) {
+      const int ws = st % WS, t = st / WS, h = t % a.H, n = t / a.H;
+      const int w0 = ws * P;
+      float g[P][8], dcen[P][8], xcen[P][8];
+#pragma unroll
+      for (int p = 0; p < P; ++p)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) { g[p][j] = 0.f; dcen[p][j] = 0.f; xcen[p][j] = 0.f; }
+      // the centre rows first: the strip's own dY (weight gradient) and x (data-gradient mask)
+      constexpr int RORD[3] = {1, 0, 2};
+#pragma unroll
+      for (int ri = 0; ri < 3; ++ri) {
+        const int r = RORD[ri];
+        const int ho = h + a.PT - r;                  // dY row feeding this strip through tap row r
+        const bool hv = (unsigned)ho < (unsigned)a.Ho;
+        const int hx = h - a.PT + r;                  // x row under tap row r of the strip's outputs
+        const bool xv_ok = (unsigned)hx < (unsigned)a.H;
+        uint4 dv[NCOL], xv[NCOL];
+        float md[NCOL], mx[NCOL];
+#pragma unroll
+        for (int q = 0; q < NCOL; ++q) {
+          const int wo = w0 + a.PL - 2 + q;  // column q feeds pixel p through tap s = p + 2 - q
+          const bool v = hv && (unsigned)wo < (unsigned)a.Wo;
+          md[q] = v ? 1.f : 0.f;
+          const size_t o = v ? ((size_t)(n * a.Ho + ho) * a.Wo + wo) : 0;
+          dv[q] = *reinterpret_cast<const uint4*>(a.dy + o * a.lddy + c);
+          const int wx = w0 - a.PL + q;      // input column q: tap s = q - p of output pixel p
+          const bool vx = xv_ok && (unsigned)wx < (unsigned)a.W;
+          mx[q] = vx ? 1.f : 0.f;
+          const size_t pix = vx ? ((size_t)(n * a.H + hx) * a.W + wx) : 0;
+          xv[q] = *reinterpret_cast<const uint4*>(a.x + pix * a.ldx + c);
+        }
+        if (r == 1) {  // stride 1, PT = PL = 1: dY column q = p + 1 is output pixel p; x column q = p + 1 is pixel p
+#pragma unroll
+          for (int p = 0; p < P; ++p) {
+            float d[8], xx[8];
+            unpack8(dv[p + 1], d);
+            unpack8(xv[p + 1], xx);
+            const float vo = (w0 + p < a.W) ? md[p + 1] : 0.f;
+#pragma unroll
+            for (int j = 0; j < 8; ++j) { dcen[p][j] = d[j] * vo; xcen[p][j] = xx[j]; }
+          }
+        }
+#pragma unroll
+        for (int q = 0; q < NCOL; ++q) {
+          float d[8], u[8];
+          unpack8(dv[q], d);
+          unpack8(xv[q], u);
+#pragma unroll
+          for (int j = 0; j < 8; ++j) u[j] = clampf(fmaf(u[j], sc[j], sf[j]), lo, hi) * mx[q];
+#pragma unroll
+          for (int p = 0; p < P; ++p) {
+            const int sd = p + 2 - q;  // data gradient: dY column q through tap (r, sd) into pixel p
+            if (sd >= 0 && sd < 3) {
+#pragma unroll
+              for (int j = 0; j < 8; ++j) g[p][j] = fmaf(d[j] * md[q], wk[r * 3 + sd][j], g[p][j]);
+            }
+            const int sw = q - p;      // weight gradient: x column q under tap (r, sw) of pixel p
+            if (sw >= 0 && sw < 3) {
+#pragma unroll
+              for (int j = 0; j < 8; ++j) acc[r * 3 + sw][j] = fmaf(u[j], dcen[p][j], acc[r * 3 + sw][j]);
+            }
+          }
+        }
+      }
+      const size_t ib = (size_t)(n * a.H + h) * a.W;
+#pragma unroll
+      for (int p = 0; p < P; ++p) {
+        if (w0 + p >= a.W) break;
+        const size_t i = ib + w0 + p;
+        if (epi) {
+#pragma unroll
+          for (int j = 0; j < 8; ++j) {
+            const float z = fmaf(xcen[p][j], sc[j], sf[j]);
+            g[p][j] = (z > lo && z < hi) ? g[p][j] : 0.f;
+          }
+          const uint4 pk = pack8(g[p]);
+          *reinterpret_cast<uint4*>(a.dx + i * a.lddx + c) = pk;
+          float r8[8];
+          unpack8(pk, r8);
+#pragma unroll
+          for (int j = 0; j < 8; ++j) { ps[j] += r8[j]; px[j] += r8[j] * (xcen[p][j] - mu[j]) * rs[j]; }
+        } else {
+          *reinterpret_cast<uint4*>(a.dx + i * a.lddx + c) = pack8(g[p]);
+        }
+      }
+    }
+  }
+  if (epi) {
+    chunk_sums(CB, dc.R, tx, ty, ps, px, s_tmp, s_a, s_b);
+    __syncthreads();
+    const size_t so = (size_t)(blockIdx.x % stat_slots(a.gsum_slots)) * a.gsum_ld;
+    for (int i = threadIdx.x; i < CB; i += blockDim.x) {
+      if (a.gsum) atomicAdd(&a.gsum[so + cb + i], s_a[i]);
+      if (a.gsumx) atomicAdd(&a.gsumx[so + cb + i], s_b[i]);
+    }
+  }
+  // weight-gradient partials of this block: one tap row per round through LDS, summed in order
+  float* out = a.ws + (size_t)blockIdx.x * 9 * a.C + cb;
+  const int C8 = dc.c8b;
+  const bool act = ty < dc.R;
+#pragma unroll
+  for (int r = 0; r < 3; ++r) {
+    __syncthreads();
+    float4* d = reinterpret_cast<float4*>(s_tmp + threadIdx.x * 24);
+#pragma unroll
+    for (int s = 0; s < 3; ++s) {
+      const float* v = acc[r * 3 + s];
+      d[2 * s] = act ? make_float4(v[0], v[1], v[2], v[3]) : make_float4(0.f, 0.f, 0.f, 0.f);
+      d[2 * s + 1] = act ? make_float4(v[4], v[5], v[6], v[7]) : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+    __syncthreads();
+    for (int o = threadIdx.x; o < 3 * CB; o += blockDim.x) {
+      const int s = o / CB, c = o - s * CB, cx = c >> 3, j = c & 7;
+      float sum = 0.f;
+      for (int y = 0; y < dc.R; ++y) sum += s_tmp[(y * C8 + cx) * 24 + s * 8 + j];
+      out[(r * 3 + s) * a.C + c] = sum;
+    }
+  }
+}
+
 hipError_t dwconv_fwd(const DwArgs& a, hipStream_t st) {
   if (a.KH == 3 && a.KW == 3 && (a.S == 1 || a.S == 2) && a.C % 8 == 0 && a.C <= 2048) {
     const long long strips = (long long)a.N * a.Ho * ((a.Wo + kDwStrip - 1) / kDwStrip);
@@ -562,6 +735,28 @@ hipError_t dwconv_bwd_data(const DwArgs& a, hipStream_t st) {
   if (aff) return hipErrorInvalidValue;  // the backward affine prologue is 3x3-only
   hipLaunchKernelGGL(dw_bwd_data_kernel, ggrid(dim3(nblocks((long long)a.N * a.H * a.W, a.C, 4))), dim3(256),
                      6 * a.C * 4, st, a, garg());
+  return hipGetLastError();
+}
+
+namespace {
+inline bool dw_fused_ok(const DwArgs& a) {
+  return a.KH == 3 && a.KW == 3 && a.S == 1 && a.PT == 1 && a.PL == 1 && a.H == a.Ho && a.W == a.Wo &&
+         a.C % 8 == 0 && a.C <= 2048 && a.dyaff.mode == 0 && a.ws != nullptr && a.dw != nullptr;
+}
+inline int dw_fused_blocks(const DwArgs& a) {
+  const long long strips = (long long)a.N * a.H * ((a.W + kDwStrip - 1) / kDwStrip);
+  return dw_pblocks(strips, dw_chunks(a.C));
+}
+}  // namespace
+
+bool dwconv_bwd_fused_ok(const DwArgs& a) { return dw_fused_ok(a); }
+
+hipError_t dwconv_bwd_fused(const DwArgs& a, hipStream_t st) {
+  if (!dw_fused_ok(a)) return hipErrorInvalidValue;
+  const DwChunks dc = dw_chunks(a.C);
+  const size_t shm = (6 * dc.c8b * 8 + (2 * 256 * 8 > 256 * 24 ? 2 * 256 * 8 : 256 * 24)) * 4;
+  const dim3 g(dw_fused_blocks(a), dc.nchunk);
+  hipLaunchKernelGGL(dw_bwd3_fused_kernel, ggrid(g), dim3(256), shm, st, a, garg());
   return hipGetLastError();
 }
 
@@ -831,6 +1026,19 @@ hipError_t dwconv_wgrad(const DwArgs& a, hipStream_t st) {
     return hipGetLastError();
   }
   hipLaunchKernelGGL(dw_wgrad_kernel, ggrid(dim3(nblocks(Mo, a.C, 32))), dim3(256), (2 + T) * a.C * 4, st, a, garg());
+  return hipGetLastError();
+}
+
+// column sums of dw_bwd3_fused_kernel's per-block weight-gradient partials (side lane)
+hipError_t dwconv_wgrad_sum(const DwArgs& a, hipStream_t st) {
+  if (!dw_fused_ok(a)) return hipErrorInvalidValue;
+  const int nblk = dw_fused_blocks(a);
+  const int n = 9 * a.C;
+  const int cols = (n + 255) / 256;
+  int split = (nblk + 31) / 32;
+  if (split > 64) split = 64;
+  if (split < 1) split = 1;
+  hipLaunchKernelGGL(dw_wgrad_sum_kernel, ggrid(dim3(cols, split)), dim3(256), 0, st, a.ws, nblk, n, a.dw, garg());
   return hipGetLastError();
 }
 

@@ -661,8 +661,15 @@ class Plan {
         break;
       }
       case OP_DW_FWD: check(dwconv_fwd(as<DwArgs>(op), st), "dwconv_fwd"); break;
-      case OP_DW_BWD_DATA: check(dwconv_bwd_data(as<DwArgs>(op), st), "dwconv_bwd_data"); break;
-      case OP_DW_WGRAD: check(dwconv_wgrad(as<DwArgs>(op), st), "dwconv_wgrad"); break;
+      // i[0] 1: data + weight-gradient partials in one pass (dwconv_bwd_fused)
+      case OP_DW_BWD_DATA:
+        check(op.i[0] == 1 ? dwconv_bwd_fused(as<DwArgs>(op), st) : dwconv_bwd_data(as<DwArgs>(op), st),
+              "dwconv_bwd_data");
+        break;
+      // i[0] 2: only the column sums of a fused backward's partials (dwconv_wgrad_sum)
+      case OP_DW_WGRAD:
+        check(op.i[0] == 2 ? dwconv_wgrad_sum(as<DwArgs>(op), st) : dwconv_wgrad(as<DwArgs>(op), st), "dwconv_wgrad");
+        break;
       case OP_FINITE_CHECK:
         if (op.i[0] == 0)
           check(finite_check(reinterpret_cast<const float*>(op.p[0]), op.l[0], reinterpret_cast<int*>(op.p[1]), st),
@@ -1141,6 +1148,11 @@ PYBIND11_MODULE(_idc_native, m) {
   m.attr("DS_MAX_CIN") = DS_MAX_CIN;
   m.attr("OP_MB_CHAIN") = (int)OP_MB_CHAIN;
   m.attr("OP_MB_INFER") = (int)OP_MB_INFER;
+  m.def("dw_bwd_fused_ok", [](py::bytes payload) {
+    std::string s = payload;
+    if (s.size() != sizeof(DwArgs)) throw std::runtime_error("dw_bwd_fused_ok: bad payload");
+    return dwconv_bwd_fused_ok(*reinterpret_cast<const DwArgs*>(s.data()));
+  });
   m.def("mb_infer_smem", [](py::bytes payload) {
     std::string s = payload;
     if (s.size() != sizeof(MbInferArgs)) throw std::runtime_error("mb_infer_smem: bad payload");

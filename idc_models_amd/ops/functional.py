@@ -458,6 +458,27 @@ def dwconv_bwd(x, kernel, dy, stride=1, pads=(1, 1), pro: Optional[BN] = None, g
     return dx, dw
 
 
+def dwconv_bwd_fused(x, kernel, dy, pads=(1, 1), pro: Optional[BN] = None, gsum=None, gsumx=None):
+    """Stride-1 3x3 depthwise backward, data and weight gradients in one pass
+    (dwconv.hip dw_bwd3_fused_kernel) plus the partials' column sums: returns (dx, dw)."""
+    N, H, W, C = x.shape
+    a = _dw_args(x, kernel, 1, pads, H, W, pro)
+    dx = torch.empty_like(x)
+    dw = torch.zeros(kernel.shape, dtype=torch.float32, device=x.device)
+    a.dy, a.lddy = dy.data_ptr(), C
+    a.dx, a.lddx = dx.data_ptr(), C
+    a.gsum, a.gsumx = nat.ptr(gsum), nat.ptr(gsumx)
+    a.dw = dw.data_ptr()
+    ws = torch.empty(int(nat.require().dw_wgrad_ws_floats(N * H * W, C, 9)), dtype=torch.float32, device=x.device)
+    a.ws = ws.data_ptr()
+    if not nat.require().dw_bwd_fused_ok(nat.raw(a)):
+        raise ValueError("dwconv_bwd_fused: stride-1 3x3 'same' only")
+    _plan1(nat.OP_DW_BWD_DATA, a, ints=(1,))
+    _plan1(nat.OP_DW_WGRAD, a, ints=(2,))
+    torch.cuda.current_stream(x.device).synchronize()  # ws dies with this frame
+    return dx, dw
+
+
 def bn_moments(stats: torch.Tensor, count: int, shift: Optional[torch.Tensor] = None):
     """(mean, unbiased variance) per channel as the BatchNorm consumers compute them from
     [sum|sumsq] statistics (with ``shift``: sums of y - K), read out through the moving-statistics

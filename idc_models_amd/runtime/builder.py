@@ -1233,6 +1233,29 @@ class Builder:
         self.emit(nat.OP_DW_BWD_DATA, a)
         self.finish_grad_sums(bn)
 
+    def dw_bwd_fused(self, x: Tensor4, layer, dy: Tensor4, dz: Tensor4, dw: torch.Tensor, *, pads=(1, 1),
+                     bn: Optional["BNRef"] = None) -> bool:
+        """Stride-1 3x3 depthwise backward with the data and weight gradients in ONE pass
+        (dwconv.hip dw_bwd3_fused_kernel): dz as dw_bwd_data, the weight gradient's per-block
+        partials into a workspace whose column sums run as a side-lane op.  Returns False (nothing
+        emitted) outside the kernel's shapes."""
+        kh, kw = layer.kernel_size
+        a = self._dw_args(x, layer, dy.H, dy.W, 1, pads, bn.args() if bn is not None else None)
+        a.dy, a.lddy = dy.ptr, dy.ld
+        a.dx, a.lddx = dz.ptr, dz.ld
+        a.dw = dw.data_ptr()
+        ws = self.alloc((int(nat.load().dw_wgrad_ws_floats(dy.M, dy.C, kh * kw)),), F32)
+        a.ws = ws.data_ptr()
+        if not nat.load().dw_bwd_fused_ok(nat.raw(a)):
+            return False
+        if bn is not None:
+            a.gsum, a.gsumx, a.gsum_slots, a.gsum_ld = self.grad_sums(
+                bn, dz.M, slotted=os.environ.get("IDC_DW_STAT_SLOTS", "1") != "0")
+        self.emit(nat.OP_DW_BWD_DATA, a, ints=(1,))
+        self.finish_grad_sums(bn)
+        self.emit(nat.OP_DW_WGRAD, a, ints=(2,), lane=1)  # column sums of the partials
+        return True
+
     def dw_wgrad(self, x: Tensor4, layer, dy: Tensor4, dw: torch.Tensor, *, stride=1, pads=(1, 1),
                  pro=None, lane=0, dyaff: Optional[nat.BwdAff] = None):
         a = self._dw_args(x, layer, dy.H, dy.W, stride, pads, pro)

@@ -298,13 +298,21 @@ def lower_mobilenet(b: Builder, net, U: int, input_dtype):
             dd, aff_d = b.nhwc(d.N, d.H, d.W, d.C), None
             b.bn_bwd_apply(zd, d, bn_d, dd, accumulate=False)
             b.mark_grads_ready([bn_d.gamma, bn_d.beta])
+        # IDC_DW_FUSED_BWD=1: stride-1 blocks run the depthwise data and weight gradients as one
+        # pass over dd and e (dwconv.hip dw_bwd3_fused_kernel)
+        fused_dw = False
         if fz.before(dwl) or aff_d is not None:
             ze = b.nhwc(e.N, e.H, e.W, e.C)
             if fz.before(dwl):
-                b.dw_bwd_data(e, dwl, dd, ze, stride=blk["stride"], pads=blk["pads"], bn=bn_in, dyaff=aff_d)
+                if os.environ.get("IDC_DW_FUSED_BWD", "0") == "1" and blk["stride"] == 1 and aff_d is None \
+                        and fz.trainable(dwl):
+                    fused_dw = b.dw_bwd_fused(e, dwl, dd, ze, b.arena.grad_of(dwl.depthwise_kernel),
+                                              pads=blk["pads"], bn=bn_in)
+                if not fused_dw:
+                    b.dw_bwd_data(e, dwl, dd, ze, stride=blk["stride"], pads=blk["pads"], bn=bn_in, dyaff=aff_d)
         if aff_d is not None:
             b.mark_grads_ready([bn_d.gamma, bn_d.beta])
-        if fz.trainable(dwl):
+        if fz.trainable(dwl) and not fused_dw:
             b.dw_wgrad(e, dwl, dd, b.arena.grad_of(dwl.depthwise_kernel), stride=blk["stride"],
                        pads=blk["pads"], pro=bn_in.args(), lane=1,
                        dyaff=b.bwd_aff(bn_d, d) if aff_d is not None else None)

@@ -397,6 +397,43 @@ def test_dwconv(fn, s, H, pads, ho, C):
     assert relerr(dw.cpu(), kr.grad) < 1e-2
 
 
+@pytest.mark.parametrize("H,C,pro", [(13, 144, False), (13, 144, True), (25, 32, True), (7, 192, True),
+                                     (4, 384, True), (2, 960, True), (5, 24, True)])
+def test_dwconv_bwd_fused_matches_separate_kernels(fn, H, C, pro):
+    """The one-pass stride-1 depthwise backward (dw_bwd3_fused_kernel: data gradient through the
+    pending BN + ReLU6 and its BatchNorm-backward sums, weight-gradient partials + column sums) vs
+    the data-gradient and weight-gradient kernels it replaces (themselves checked against fp32
+    autograd in test_dwconv), and without a prologue vs fp32 autograd on the CPU directly."""
+    N = 3
+    torch.manual_seed(H * 10 + C)
+    x = bf(torch.randn(N, H, H, C, device=DEV) * 2 + 0.3)
+    k = torch.randn(3, 3, C, 1, device=DEV) * 0.3
+    dy = bf(torch.randn(N, H, H, C, device=DEV))
+    bn = None
+    if pro:
+        st = torch.cat([x.sum((0, 1, 2)), (x * x).sum((0, 1, 2))])
+        bn = fn.BN(stats=st, gamma=torch.rand(C, device=DEV) + 0.5, beta=torch.randn(C, device=DEV) * 0.1,
+                   count=N * H * H, eps=1e-3, act=2)
+    xb, dyb = x.to(torch.bfloat16), dy.to(torch.bfloat16)
+    sums = [torch.zeros(C, device=DEV) for _ in range(4)]
+    dx0, dw0 = fn.dwconv_bwd(xb, k, dyb, stride=1, pads=(1, 1), pro=bn, gsum=sums[0] if pro else None,
+                             gsumx=sums[1] if pro else None)
+    dx1, dw1 = fn.dwconv_bwd_fused(xb, k, dyb, pads=(1, 1), pro=bn, gsum=sums[2] if pro else None,
+                                   gsumx=sums[3] if pro else None)
+    assert relerr(dx1, dx0) < 4e-3, relerr(dx1, dx0)
+    assert relerr(dw1, dw0) < 1e-4, relerr(dw1, dw0)
+    if pro:
+        assert relerr(sums[2], sums[0]) < 4e-3 and relerr(sums[3], sums[1]) < 4e-3
+    else:
+        xr = x.cpu().clone()
+        kr = k.cpu().clone().requires_grad_(True)
+        xr.requires_grad_(True)
+        ref = F.conv2d(F.pad(xr.permute(0, 3, 1, 2), (1, 1, 1, 1)), kr.permute(2, 3, 0, 1), groups=C)
+        ref.backward(dy.cpu().permute(0, 3, 1, 2))
+        assert relerr(dx1.cpu(), xr.grad) < 1e-2
+        assert relerr(dw1.cpu(), kr.grad) < 1e-2
+
+
 def test_rmsprop_kernel_matches_keras_formula():
     from idc_models_amd.ops.optim import rmsprop_
     n = 4096

@@ -149,6 +149,25 @@ def test_mb_infer_lowering(monkeypatch, ft, training, fused):
     assert nat.OP_MB_INFER not in [op[1] for op in b0.ops]
 
 
+def test_dw_fused_backward_lowering(monkeypatch):
+    """IDC_DW_FUSED_BWD=1: every stride-1 depthwise layer's data and weight gradients lower to ONE
+    main-lane op (OP_DW_BWD_DATA, ints[0] 1) plus the partials' column sums on the side lane
+    (OP_DW_WGRAD, ints[0] 2); the stride-2 layers keep their two kernels."""
+    _, _, b0 = _lower("mobilenetv2", None, True)
+    monkeypatch.setenv("IDC_DW_FUSED_BWD", "1")
+    _, _, b1 = _lower("mobilenetv2", None, True)
+
+    def ops(b, kind):
+        return [op[3][0] if op[3] else 0 for op in b.ops if op[1] == kind]
+    fused = [i for i in ops(b1, nat.OP_DW_BWD_DATA) if i == 1]
+    sums = [(op[3][0] if op[3] else 0, op[7]) for op in b1.ops if op[1] == nat.OP_DW_WGRAD]
+    assert len(fused) == 13
+    assert sum(1 for i, lane in sums if i == 2 and lane == 1) == 13
+    assert sum(1 for i, lane in sums if i != 2) == 4  # the stride-2 layers' own weight gradients
+    assert len(ops(b0, nat.OP_DW_BWD_DATA)) == len(ops(b1, nat.OP_DW_BWD_DATA)) == 17
+    assert not [i for i in ops(b0, nat.OP_DW_BWD_DATA) if i == 1]
+
+
 def test_fine_tune_backward_stops_at_first_trainable_layer():
     m, net, b = _lower("mobilenetv2", 100, True)
     n_wgrad = sum(1 for op in b.ops if op[1] in (nat.OP_WGRAD, nat.OP_DW_WGRAD))
