@@ -526,6 +526,9 @@ def test_mb_chain_matches_per_layer(monkeypatch, B, frozen):
     agree to a bf16-level bound, the give-up counter stays zero, and the chain program's loss and
     gradients pass the fp32 check (_check).  ``frozen``: inference-mode BatchNorms (phase 1)."""
     from idc_models_amd.ops import _native as nat
+    # (the per-layer side: the frozen blocks would otherwise be single mb_infer launches, whose
+    #  expanded / depthwise tensors never exist in global memory to compare)
+    monkeypatch.setenv("IDC_MB_INFER", "0")
     outs = []
     for on in ("0", "1"):
         monkeypatch.setenv("IDC_MB_CHAIN", on)
