@@ -167,4 +167,18 @@ bool dense_rows_bwd_geometry(int N, int H, int W, int ld, int nlayers, int& ipg,
 hipError_t dense_rows_bwd(const DenseBwdArgs& a, hipStream_t st);
 long long dense_rows_bwd_part_floats(int c0, int nlayers, int grid);
 
+// A whole dense block in INFERENCE mode (every BatchNorm on its moving statistics: evaluation, a
+// frozen base, the frozen prefix of a fine-tuned net) as ONE launch with no cross-workgroup
+// traffic at all (dense_infer.hip): a workgroup owns `ipg` whole images, keeps their concat buffer
+// in LDS and runs every layer's BN1+ReLU -> 1x1 -> BN2+ReLU -> 3x3 on it.  For the large maps
+// (stages 1-2: 13x13 / 6x6 at 50x50) that the per-image row kernel (dense_rows.hip) cannot hold.
+struct DenseInferArgs {
+  bf16_t* buf;                    // stage buffer [N][H][W][ld]: channels [0, c0) in, [c0, c0 + 32 L) out
+  int ld;
+  int N, H, W, c0, L, ipg, act;   // act: the BatchNorms' activation (ReLU)
+  const DenseLayerDesc* layers;   // L descriptors (w1, w2, g1/b1/mm1/mv1, g2/b2/mm2/mv2, eps, cin)
+};
+long long dense_infer_smem(const DenseInferArgs& a);  // dynamic LDS bytes, -1: shape not supported
+hipError_t dense_infer(const DenseInferArgs& a, hipStream_t st);
+
 }  // namespace idc

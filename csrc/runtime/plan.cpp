@@ -93,6 +93,8 @@ enum OpKind : int {
   OP_MB_CHAIN = 30,
   // one MobileNetV2 block in inference mode (mb_infer.hip): payload MbInferArgs
   OP_MB_INFER = 31,
+  // a whole DenseNet dense block in inference mode (dense_infer.hip): payload DenseInferArgs
+  OP_DENSE_INFER = 32,
 };
 
 struct Op {
@@ -451,7 +453,7 @@ class Plan {
                                   "input", "memset", "bn_stats", "bn_apply", "dw_fwd", "dw_bwd_data",
                                   "dw_wgrad", "copy", "finite_check", "mlp_fwd", "mlp_bwd", "mlp_step",
                                   "collapse", "stats_shift", "allreduce", "wgrad_batch", "dense_stage",
-                                  "dense_stage_bwd", "mb_chain", "mb_infer"};
+                                  "dense_stage_bwd", "mb_chain", "mb_infer", "dense_infer"};
     int k = ops_.at(idx).kind;
     return (k >= 0 && k < (int)(sizeof(names) / sizeof(names[0]))) ? names[k] : "?";
   }
@@ -696,6 +698,7 @@ class Plan {
       case OP_DENSE_STAGE_BWD: check(dense_stage_bwd(as<DenseBwdArgs>(op), op.i[0], st), "dense_stage_bwd"); break;
       case OP_MB_CHAIN: check(mb_chain(as<MbChainArgs>(op), op.i[0], op.i[1], st), "mb_chain"); break;
       case OP_MB_INFER: check(mb_infer(as<MbInferArgs>(op), st), "mb_infer"); break;
+      case OP_DENSE_INFER: check(dense_infer(as<DenseInferArgs>(op), st), "dense_infer"); break;
       case OP_STATS_SHIFT:
         check(stats_shift(reinterpret_cast<const ShiftDesc*>(op.p[0]), op.i[0], op.i[1], st), "stats_shift");
         break;
@@ -810,6 +813,7 @@ py::dict struct_sizes() {
   d["DenseBwdPhase"] = sizeof(DenseBwdPhase);
   d["MbPhaseDesc"] = sizeof(MbPhaseDesc);
   d["MbInferArgs"] = sizeof(MbInferArgs);
+  d["DenseInferArgs"] = sizeof(DenseInferArgs);
   d["MbChainArgs"] = sizeof(MbChainArgs);
   d["MbPhaseDesc.pre"] = offsetof(MbPhaseDesc, pre);
   d["BnArgs.shift"] = offsetof(BnArgs, shift);
@@ -1148,6 +1152,12 @@ PYBIND11_MODULE(_idc_native, m) {
   m.attr("DS_MAX_CIN") = DS_MAX_CIN;
   m.attr("OP_MB_CHAIN") = (int)OP_MB_CHAIN;
   m.attr("OP_MB_INFER") = (int)OP_MB_INFER;
+  m.attr("OP_DENSE_INFER") = (int)OP_DENSE_INFER;
+  m.def("dense_infer_smem", [](py::bytes payload) {
+    std::string s = payload;
+    if (s.size() != sizeof(DenseInferArgs)) throw std::runtime_error("dense_infer_smem: bad payload");
+    return dense_infer_smem(*reinterpret_cast<const DenseInferArgs*>(s.data()));
+  });
   m.def("dw_bwd_fused_ok", [](py::bytes payload) {
     std::string s = payload;
     if (s.size() != sizeof(DwArgs)) throw std::runtime_error("dw_bwd_fused_ok: bad payload");

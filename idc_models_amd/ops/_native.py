@@ -197,6 +197,12 @@ class MbInferArgs(C.Structure):
                [("slab", vp), ("tickets", vp)]
 
 
+class DenseInferArgs(C.Structure):
+    """A whole dense block in inference mode, one launch (csrc/kernels/dense_stage.h)."""
+    _fields_ = [("buf", vp), ("ld", ci)] + [(n, ci) for n in ("N", "H", "W", "c0", "L", "ipg", "act")] + \
+               [("layers", vp)]
+
+
 def mb_infer_default_cs(cexp: int, groups: int, expand: bool = True) -> int:
     """Expanded channels per workgroup of an mb_infer launch (csrc/kernels/mb_infer.h): enough
     slices per image group that the launch has >= 256 workgroups, in multiples of 32."""
@@ -214,7 +220,8 @@ _STRUCTS = {"BnArgs": BnArgs, "BwdAff": BwdAff, "ConvArgs": ConvArgs, "WgradArgs
             "DwArgs": DwArgs, "Mlp2Args": Mlp2Args, "ShiftDesc": ShiftDesc,
             "DenseStageArgs": DenseStageArgs, "DenseLayerDesc": DenseLayerDesc,
             "DenseBwdArgs": DenseBwdArgs, "DenseBwdLayerDesc": DenseBwdLayerDesc, "DenseBwdPhase": DenseBwdPhase,
-            "MbPhaseDesc": MbPhaseDesc, "MbChainArgs": MbChainArgs, "MbInferArgs": MbInferArgs}
+            "MbPhaseDesc": MbPhaseDesc, "MbChainArgs": MbChainArgs, "MbInferArgs": MbInferArgs,
+            "DenseInferArgs": DenseInferArgs}
 
 # op kinds (csrc/runtime/plan.cpp)
 OP_CONV, OP_WGRAD, OP_BN_BWD_APPLY, OP_BN_BWD_REDUCE, OP_MAXPOOL, OP_AVGPOOL, OP_POOL_BWD = range(7)
@@ -225,6 +232,7 @@ OP_DENSE_STAGE = 28
 OP_DENSE_STAGE_BWD = 29
 OP_MB_CHAIN = 30
 OP_MB_INFER = 31
+OP_DENSE_INFER = 32
 
 ACT = {None: 0, "none": 0, "linear": 0, "relu": 1, "relu6": 2}
 OUT_BF16, OUT_F32, OUT_F32_ACC = 0, 1, 2
@@ -233,7 +241,8 @@ OUT_BF16, OUT_F32, OUT_F32_ACC = 0, 1, 2
 def _verify(ext):
     if ext.OP_ALLREDUCE != OP_ALLREDUCE:
         raise RuntimeError("native op-kind table drifted (OP_ALLREDUCE)")
-    if ext.OP_DENSE_STAGE != OP_DENSE_STAGE or ext.OP_MB_CHAIN != OP_MB_CHAIN or ext.OP_MB_INFER != OP_MB_INFER:
+    if ext.OP_DENSE_STAGE != OP_DENSE_STAGE or ext.OP_MB_CHAIN != OP_MB_CHAIN or ext.OP_MB_INFER != OP_MB_INFER \
+            or ext.OP_DENSE_INFER != OP_DENSE_INFER:
         raise RuntimeError("native op-kind table drifted (OP_DENSE_STAGE / OP_MB_CHAIN)")
     sizes = ext.struct_sizes()
     for name, cls in _STRUCTS.items():

@@ -556,6 +556,31 @@ def dense_stage(buf: torch.Tensor, sstats: torch.Tensor, layers, sshift: Optiona
     return sync[:3 + 16 * len(layers)], err, st
 
 
+def dense_infer(buf: torch.Tensor, layers, act: int = RELU, ipg: int = 1):
+    """A whole dense block in inference mode as one launch (csrc/kernels/dense_infer.hip).
+    ``buf``: NHWC bf16 stage buffer [N, H, W, ld] with channels [0, c0) filled; ``layers``: dicts
+    with w1 ([128][cin] bf16), w2 ([32][3][3][128] bf16), g1, b1, mm1, mv1 ([cin]), g2, b2, mm2, mv2
+    ([128]), eps1, eps2, cin (= c0 + 32 i).  Writes channels [c0, c0 + 32 L) of ``buf``."""
+    N, H, W, ld = buf.shape
+    arr = (nat.DenseLayerDesc * len(layers))()
+    for d, L in zip(arr, layers):
+        d.w1, d.w2 = L["w1"].data_ptr(), L["w2"].data_ptr()
+        d.g1, d.b1, d.g2, d.b2 = (L[k].data_ptr() for k in ("g1", "b1", "g2", "b2"))
+        d.mm1, d.mv1, d.mm2, d.mv2 = (L[k].data_ptr() for k in ("mm1", "mv1", "mm2", "mv2"))
+        d.eps1, d.eps2, d.cin = L["eps1"], L["eps2"], L["cin"]
+    import ctypes
+    tab = torch.frombuffer(bytearray(ctypes.string_at(ctypes.addressof(arr), ctypes.sizeof(arr))),
+                           dtype=torch.uint8).to(buf.device)
+    a = nat.DenseInferArgs()
+    a.buf, a.ld = buf.data_ptr(), ld
+    a.N, a.H, a.W, a.c0, a.L, a.ipg, a.act = N, H, W, layers[0]["cin"], len(layers), ipg, act
+    a.layers = tab.data_ptr()
+    if nat.require().dense_infer_smem(nat.raw(a)) < 0:
+        raise ValueError("dense_infer: shape outside the kernel's limits")
+    _plan1(nat.OP_DENSE_INFER, a)
+    torch.cuda.current_stream(buf.device).synchronize()  # the layer table dies with this frame
+
+
 def dense_bwd_queue(L: int, nmt: int, c0: int, kg: int):
     """Work queue of a persistent dense-stage backward launch (dense_stage_bwd.hip), in ticket
     order: (first ticket, kind, layer, tiles).  Kinds: 1 P, 2 QN, 3 G, 4 GIN, 5 FIN1, 6 FIN2."""

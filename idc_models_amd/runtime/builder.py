@@ -840,13 +840,8 @@ class Builder:
                 return False
         return bool(ext.dense_stage_shape_ok(self.B, H, W, max(lay["cin"] for lay in layers)))
 
-    def dense_stage(self, buf: Tensor4, sbuf: Stats, layers, act: int):
-        """Emit ONE persistent launch for the dense layers ``layers`` of a stage (dicts with cin,
-        bn1, cv1, bn2, cv2, t, stt as in lower_densenet): same buffers, statistics and weights as
-        the per-layer convs, so everything downstream (backward included) is unchanged."""
-        H, W = buf.H, buf.W
-        center = self.is_center_only(layers[0]["cv2"], H, W, (1, 1), (1, 1))
-        infer = all(lay["bn1"].mode == 2 and lay["bn2"].mode == 2 for lay in layers)
+    def _dense_layer_table(self, layers, center: bool, infer: bool) -> torch.Tensor:
+        """Device table of DenseLayerDesc (dense_stage.h) for a stage's dense layers."""
         arr = (nat.DenseLayerDesc * len(layers))()
         for d, lay in zip(arr, layers):
             cin, bn1, bn2 = lay["cin"], lay["bn1"], lay["bn2"]
@@ -854,9 +849,9 @@ class Builder:
             d.w2 = self.conv_weight(lay["cv2"], cin_pad=128, center=center)["fwd"].data_ptr()
             d.g1, d.b1 = bn1.gamma.data_ptr(), bn1.beta.data_ptr()
             d.g2, d.b2 = bn2.gamma.data_ptr(), bn2.beta.data_ptr()
-            if lay["stt"] is not None:
+            if lay.get("stt") is not None:
                 d.tstats, d.tshift = lay["stt"].ptr, lay["stt"].shift_ptr()
-            d.t = lay["t"].ptr
+            d.t = lay["t"].ptr if lay.get("t") is not None else 0
             d.eps1, d.eps2 = bn1.layer.epsilon, bn2.layer.epsilon
             d.cin = cin
             d.mm1, d.mv1 = bn1.layer.moving_mean.data_ptr(), bn1.layer.moving_variance.data_ptr()
@@ -865,6 +860,48 @@ class Builder:
         host = torch.frombuffer(bytearray(C.string_at(C.addressof(arr), C.sizeof(arr))), dtype=torch.uint8)
         tab = host.to(self.device)
         self.keep.append(tab)
+        return tab
+
+    def dense_infer(self, buf: Tensor4, layers, act: int) -> bool:
+        """A whole dense block in inference mode as ONE launch (dense_infer.hip): every layer's
+        BatchNorms on moving statistics, nothing downstream needing the stage's statistics.  Writes
+        the new channels into ``buf``; no t buffers, no statistics.  False (nothing emitted) outside
+        the kernel's shapes, in grouped programs or with IDC_DENSE_INFER=0."""
+        if os.environ.get("IDC_DENSE_INFER", "1") != "1" or getattr(self, "grouped", False):
+            return False
+        if any(lay["bn1"].mode != 2 or lay["bn2"].mode != 2 for lay in layers):
+            return False
+        if any(tuple(lay["cv2"].kernel_size) != (3, 3) or tuple(lay["cv1"].kernel_size) != (1, 1)
+               or lay["cv1"].filters != 128 or lay["cv2"].filters != 32 for lay in layers):
+            return False
+        if self.is_center_only(layers[0]["cv2"], buf.H, buf.W, (1, 1), (1, 1)):
+            return False
+        ext = nat.load()
+        a = nat.DenseInferArgs()
+        a.buf, a.ld = buf.ptr, buf.ld
+        a.N, a.H, a.W, a.c0, a.L, a.act = buf.N, buf.H, buf.W, layers[0]["cin"], len(layers), layers[0]["bn1"].act
+        if any(lay["cin"] != a.c0 + 32 * i for i, lay in enumerate(layers)):
+            return False
+        # whole images per workgroup: two on the small maps (weights re-read per workgroup), one
+        # on the large ones (the LDS holds one 13x13 image's concat buffer and z2 grid)
+        want = int(os.environ.get("IDC_DENSE_INFER_IPG", "0")) or (2 if buf.H * buf.W <= 64 else 1)
+        for ipg in sorted({want, 1}, reverse=True):
+            a.ipg = ipg
+            a.layers = 1  # (placeholder: the size query checks shapes only)
+            if int(ext.dense_infer_smem(nat.raw(a))) >= 0:
+                a.layers = self._dense_layer_table(layers, False, True).data_ptr()
+                self.emit(nat.OP_DENSE_INFER, a)
+                return True
+        return False
+
+    def dense_stage(self, buf: Tensor4, sbuf: Stats, layers, act: int):
+        """Emit ONE persistent launch for the dense layers ``layers`` of a stage (dicts with cin,
+        bn1, cv1, bn2, cv2, t, stt as in lower_densenet): same buffers, statistics and weights as
+        the per-layer convs, so everything downstream (backward included) is unchanged."""
+        H, W = buf.H, buf.W
+        center = self.is_center_only(layers[0]["cv2"], H, W, (1, 1), (1, 1))
+        infer = all(lay["bn1"].mode == 2 and lay["bn2"].mode == 2 for lay in layers)
+        tab = self._dense_layer_table(layers, center, infer)
         if getattr(self, "dense_err", None) is None:
             # count of dense-stage launches of this program that gave up on a wait (FusedProgram
             # checks it under IDC_VALIDATE; tests read it)

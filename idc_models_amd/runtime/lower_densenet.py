@@ -91,7 +91,14 @@ def lower_densenet(b: Builder, net, U: int, input_dtype):
             stt = b.stats(128, M) if training else None
             bn2 = BNRef(bn2l, b, stt, RELU)
             st["layers"].append({"cin": cin, "bn1": bn1, "cv1": cv1, "bn2": bn2, "cv2": cv2, "t": t, "stt": stt})
-        if M <= stage_maxm and b.dense_stage_ok(sbuf, st["layers"], Hs, Ws):
+        # a stage no statistics are needed from (every BatchNorm reading it on moving statistics:
+        # evaluation, a frozen base, the frozen stages of the fine-tune phase) and too large for
+        # the per-image row kernel: ONE dense_infer launch for the whole block (dense_infer.hip)
+        consumer = L[f"pool{si + 2}_bn"] if si < len(nblocks) - 1 else L["bn"]
+        consumer_infer = not (b.training and consumer.trainable)
+        if M > stage_maxm and consumer_infer and b.dense_infer(buf, st["layers"], RELU):
+            st["infer"] = True
+        elif M <= stage_maxm and b.dense_stage_ok(sbuf, st["layers"], Hs, Ws):
             b.dense_stage(buf, sbuf, st["layers"], RELU)
         else:
             for lay in st["layers"]:

@@ -1183,6 +1183,49 @@ def test_dense_stage_inference_mode_matches_reference(fn, N, H, c0, L, grid, ks,
     assert all(float(d["tstats"].abs().sum()) == 0.0 for d in lays)  # no statistics produced
 
 
+@pytest.mark.parametrize("N,H,c0,L,ipg", [(3, 13, 64, 6, 1), (5, 6, 128, 12, 2), (4, 6, 128, 12, 1),
+                                          (2, 13, 64, 3, 1), (3, 5, 96, 4, 3)])
+def test_dense_infer_matches_reference(fn, N, H, c0, L, ipg):
+    """A whole dense block in inference mode as ONE launch (dense_infer.hip: whole images per
+    workgroup, the concat buffer and the zero-bordered z2 grid in LDS) vs a PyTorch reference of
+    the same layers on moving statistics, intermediates rounded to bf16 where the kernel stores
+    them.  DenseNet-121 stage 1 (13x13, c0 64, 6 layers) and stage 2 (6x6, c0 128, 12 layers) with
+    one and two images per workgroup (5 images: a short last group), and an odd map."""
+    W = H
+    ld = c0 + 32 * L
+    g = torch.Generator(device="cpu").manual_seed(N * 11 + H + L)
+    buf = torch.zeros(N, H, W, ld)
+    buf[..., :c0] = torch.randn(N, H, W, c0, generator=g) * 1.5 + 0.3
+    buf = buf.to(torch.bfloat16).to(DEV)
+    lays, refs = [], []
+    for i in range(L):
+        cin = c0 + 32 * i
+        w1 = bf(torch.randn(1, 1, cin, 128, generator=g) * (2.0 / cin) ** 0.5).to(DEV)
+        w2 = bf(torch.randn(3, 3, 128, 32, generator=g) * (2.0 / 1152) ** 0.5).to(DEV)
+        d = dict(w1=fn.weight_fwd_layout(w1, cin), w2=fn.weight_fwd_layout(w2, 128),
+                 g1=(torch.rand(cin, generator=g) + 0.5).to(DEV), b1=(torch.randn(cin, generator=g) * 0.1).to(DEV),
+                 g2=(torch.rand(128, generator=g) + 0.5).to(DEV), b2=(torch.randn(128, generator=g) * 0.1).to(DEV),
+                 mm1=(torch.randn(cin, generator=g) * 0.3).to(DEV), mv1=(torch.rand(cin, generator=g) * 2 + 0.2).to(DEV),
+                 mm2=(torch.randn(128, generator=g) * 0.3).to(DEV), mv2=(torch.rand(128, generator=g) * 2 + 0.2).to(DEV),
+                 eps1=1e-3, eps2=1.001e-5, cin=cin)
+        lays.append(d)
+        refs.append((w1, w2))
+    rbuf = buf.float().clone()
+    for i, d in enumerate(lays):
+        cin = d["cin"]
+        w1, w2 = refs[i]
+        a1 = bf(torch.relu((rbuf[..., :cin] - d["mm1"]) * torch.rsqrt(d["mv1"] + d["eps1"]) * d["g1"] + d["b1"]))
+        t = ref_conv(a1, w1, 1, (0, 0, 0, 0))
+        a2 = bf(torch.relu((t - d["mm2"]) * torch.rsqrt(d["mv2"] + d["eps2"]) * d["g2"] + d["b2"]))
+        rbuf[..., cin:cin + 32] = bf(ref_conv(a2, w2, 1, (1, 1, 1, 1)))
+    fn.dense_infer(buf, lays, ipg=ipg)
+    assert torch.equal(buf[..., :c0].float(), rbuf[..., :c0])  # the block input is left alone
+    errs = [relerr(buf[..., c0 + 32 * i:c0 + 32 * (i + 1)].float(), rbuf[..., c0 + 32 * i:c0 + 32 * (i + 1)])
+            for i in range(L)]
+    assert max(errs) < 2e-2, errs
+    assert torch.isfinite(buf.float()).all()
+
+
 @pytest.mark.parametrize("N,H", [(5, 13), (7, 6), (9, 3), (3, 8), (64, 6)])
 def test_conv_img_forward_matches_reference(fn, N, H):
     """Image-resident 3x3 kernel (conv_img.hip, tile TILE_IMG), DenseNet growth conv 128 -> 32:

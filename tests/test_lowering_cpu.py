@@ -44,7 +44,7 @@ STRUCTS = {nat.OP_CONV: nat.ConvArgs, nat.OP_WGRAD: nat.WgradArgs, nat.OP_BN_BWD
            nat.OP_DW_WGRAD: nat.DwArgs, nat.OP_BN_APPLY: nat.BnArgs, nat.OP_MLP_FWD: nat.Mlp2Args,
            nat.OP_MLP_BWD: nat.Mlp2Args, nat.OP_DENSE_STAGE: nat.DenseStageArgs,
            nat.OP_DENSE_STAGE_BWD: nat.DenseBwdArgs, nat.OP_MB_CHAIN: nat.MbChainArgs,
-           nat.OP_MB_INFER: nat.MbInferArgs}
+           nat.OP_MB_INFER: nat.MbInferArgs, nat.OP_DENSE_INFER: nat.DenseInferArgs}
 
 
 def _pointers(obj, out):
@@ -147,6 +147,25 @@ def test_mb_infer_lowering(monkeypatch, ft, training, fused):
     monkeypatch.setenv("IDC_MB_INFER", "0")
     _, _, b0 = _lower("mobilenetv2", ft, training)
     assert nat.OP_MB_INFER not in [op[1] for op in b0.ops]
+
+
+@pytest.mark.parametrize("ft,training,n", [("frozen", True, 2), (None, False, 2), (150, True, 2), (None, True, 0)])
+def test_dense_infer_lowering(monkeypatch, ft, training, n):
+    """DenseNet stages whose BatchNorms (and the stage's consumer BatchNorm) all run on moving
+    statistics and which are larger than the persistent launches take (stages 1-2 at 50x50, batch
+    128 here; 256 in the bench) lower to ONE OP_DENSE_INFER each (dense_infer.hip): in evaluation, the frozen
+    base and the frozen stages of the fine-tune phase; never in full training.  IDC_DENSE_INFER=0
+    restores the per-layer convs."""
+    _, _, b = _lower("densenet121", ft, training, B=128)
+    kinds = [op[1] for op in b.ops if op[0] == "fwd"]
+    assert kinds.count(nat.OP_DENSE_INFER) == n
+    for op in b.ops:
+        if op[1] == nat.OP_DENSE_INFER:
+            a = nat.DenseInferArgs.from_buffer_copy(op[2])
+            assert (a.H, a.L) in ((13, 6), (6, 12)) and nat.load().dense_infer_smem(op[2]) > 0
+    monkeypatch.setenv("IDC_DENSE_INFER", "0")
+    _, _, b0 = _lower("densenet121", ft, training, B=128)
+    assert nat.OP_DENSE_INFER not in [op[1] for op in b0.ops]
 
 
 def test_dw_fused_backward_lowering(monkeypatch):

@@ -42,6 +42,7 @@ SOURCES = [
     "kernels/dwconv.hip",
     "kernels/dense_stage.hip",
     "kernels/dense_rows.hip",
+    "kernels/dense_infer.hip",
     "kernels/mb_chain.hip",
     "kernels/mb_infer.hip",
     "kernels/dense_stage_bwd.hip",
