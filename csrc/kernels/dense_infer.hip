@@ -24,9 +24,9 @@ namespace {
 
 constexpr int NT = 512, NW = NT / 64;
 constexpr int ZS = 128 + 8;    // z2 grid row stride (elements)
-constexpr int MAXMI = 2;       // GEMM1 M tiles per wave (MT <= 16)
-constexpr int MAXG2 = 4;       // GEMM2 tiles per wave (MT * 2 <= 32)
-constexpr int BDEPTH = 4;      // GEMM2 B-fragment prefetch depth (K steps)
+constexpr int MAXMT = 12;      // M tiles of a workgroup (rows <= 192)
+constexpr int MAXKS = 16;      // GEMM1 K steps (cin <= 512)
+constexpr int MAXG2 = 3;       // GEMM2 tiles per wave (MT * 2 <= 24)
 
 struct DiGeo {
   int HW, P, RP, MT, CT, CS, GW, GP;
@@ -44,7 +44,7 @@ __host__ __device__ inline DiGeo di_geo(const DenseInferArgs& a) {
   return g;
 }
 __host__ __device__ inline long long di_bytes(const DenseInferArgs& a, const DiGeo& g) {
-  return (long long)g.RP * g.CS * 2 + (long long)a.ipg * g.GP * ZS * 2 + (2LL * g.CT + 256) * 4;
+  return (long long)g.RP * g.CS * 2 + (long long)a.ipg * g.GP * ZS * 2 + (2LL * g.CT + 256 + g.RP) * 4;
 }
 
 __device__ __forceinline__ v8bf ld_frag(const bf16_t* p) { return *reinterpret_cast<const v8bf*>(p); }
@@ -58,38 +58,6 @@ __device__ __forceinline__ void inf_coeff(const float* g, const float* b, const 
   sf = bb - mm[c] * sc;
 }
 
-// one K step of GEMM1: prefetch the next step's B fragments into `nxt`, transform this step's A
-// fragments (BN1 affine + activation of the raw concat channels) and issue the MFMAs with `cur`
-__device__ __forceinline__ void gemm1_step(int ks, int KS, int cin, const bf16_t* __restrict__ w1, int frow, int fk,
-                                           int wid, int MT, int CS, const bf16_t* Cat, const float* sc1,
-                                           const float* sf1, float lo, float hi, const v8bf (&cur)[8],
-                                           v8bf (&nxt)[8], v4f (&acc)[MAXMI][8]) {
-  if (ks + 1 < KS) {
-#pragma unroll
-    for (int n = 0; n < 8; ++n) nxt[n] = ld_frag(w1 + (size_t)(n * 16 + frow) * cin + (ks + 1) * 32 + fk);
-  }
-  const int k0 = ks * 32 + fk;
-  const float4 s0 = *reinterpret_cast<const float4*>(sc1 + k0);
-  const float4 s1 = *reinterpret_cast<const float4*>(sc1 + k0 + 4);
-  const float4 f0 = *reinterpret_cast<const float4*>(sf1 + k0);
-  const float4 f1 = *reinterpret_cast<const float4*>(sf1 + k0 + 4);
-  const float scv[8] = {s0.x, s0.y, s0.z, s0.w, s1.x, s1.y, s1.z, s1.w};
-  const float sfv[8] = {f0.x, f0.y, f0.z, f0.w, f1.x, f1.y, f1.z, f1.w};
-#pragma unroll
-  for (int mi = 0; mi < MAXMI; ++mi) {
-    const int mt = wid + NW * mi;
-    if (mt < MT) {
-      float x[8];
-      unpack8(*reinterpret_cast<const uint4*>(Cat + (mt * 16 + frow) * CS + k0), x);
-#pragma unroll
-      for (int j = 0; j < 8; ++j) x[j] = clampf(fmaf(x[j], scv[j], sfv[j]), lo, hi);
-      const v8bf af = __builtin_bit_cast(v8bf, pack8(x));
-#pragma unroll
-      for (int n = 0; n < 8; ++n) acc[mi][n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, cur[n], acc[mi][n], 0, 0, 0);
-    }
-  }
-}
-
 }  // namespace
 
 __global__ __launch_bounds__(NT) void dense_infer_kernel(DenseInferArgs a) {
@@ -101,6 +69,9 @@ __global__ __launch_bounds__(NT) void dense_infer_kernel(DenseInferArgs a) {
   float* sf1 = sc1 + g.CT;
   float* sc2 = sf1 + g.CT;
   float* sf2 = sc2 + 128;
+  // per row: the top-left cell of its 3x3 window in the padded z2 grid (its own cell is + GW + 1);
+  // read from LDS where needed rather than kept in registers across the layer loop
+  int* gtl = reinterpret_cast<int*>(sf2 + 128);
   const int tid = threadIdx.x, lane = tid & 63;
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int img0 = blockIdx.x * a.ipg;
@@ -134,6 +105,11 @@ __global__ __launch_bounds__(NT) void dense_infer_kernel(DenseInferArgs a) {
     }
     const int nz = a.ipg * g.GP * ZS / 8;
     for (int i = tid; i < nz; i += NT) reinterpret_cast<uint4*>(Z2)[i] = make_uint4(0, 0, 0, 0);
+    for (int row = tid; row < g.RP; row += NT) {
+      const int rr = row < pv ? row : 0;
+      const int im = rr / g.HW, rem = rr - im * g.HW, h = rem / a.W, w = rem - h * a.W;
+      gtl[row] = im * g.GP + h * g.GW + w;
+    }
   }
 
   for (int l = 0; l < a.L; ++l) {
@@ -148,39 +124,53 @@ __global__ __launch_bounds__(NT) void dense_infer_kernel(DenseInferArgs a) {
     }
     __syncthreads();
 
-    // ---- GEMM1: t = z1 . W1^T (M tiles wid, wid + 8; all 8 N tiles), epilogue into the z2 grid
+    // ---- GEMM1: t = z1 . W1^T.  Wave w owns N tile w (16 of the 128 bottleneck channels) over
+    // every M tile, so its B fragments -- all K steps of one 16-row slice of W1 -- are loaded ONCE
+    // per layer (one memory latency, issued with the tables) instead of streamed per K step
     {
       const int KS = cin / 32;
-      v4f acc[MAXMI][8];
+      v8bf bw[MAXKS];
 #pragma unroll
-      for (int mi = 0; mi < MAXMI; ++mi)
+      for (int ks = 0; ks < MAXKS; ++ks)
+        if (ks < KS) bw[ks] = ld_frag(w1 + (size_t)(wid * 16 + frow) * cin + ks * 32 + fk);
+      v4f acc[MAXMT];
 #pragma unroll
-        for (int n = 0; n < 8; ++n) acc[mi][n] = (v4f){0.f, 0.f, 0.f, 0.f};
-      v8bf bqa[8], bqb[8];
+      for (int mt = 0; mt < MAXMT; ++mt) acc[mt] = (v4f){0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-      for (int n = 0; n < 8; ++n) bqa[n] = ld_frag(w1 + (size_t)(n * 16 + frow) * cin + fk);
-      // two K steps per trip, so the double buffer's halves are named registers (a dynamic index
-      // into bq[2][8] put the fragments on the scratch stack)
-      for (int ks = 0; ks < KS; ks += 2) {
-        gemm1_step(ks, KS, cin, w1, frow, fk, wid, g.MT, g.CS, Cat, sc1, sf1, lo, hi, bqa, bqb, acc);
-        if (ks + 1 < KS)
-          gemm1_step(ks + 1, KS, cin, w1, frow, fk, wid, g.MT, g.CS, Cat, sc1, sf1, lo, hi, bqb, bqa, acc);
+      for (int ks = 0; ks < MAXKS; ++ks) {
+        if (ks < KS) {
+          const int k0 = ks * 32 + fk;
+          const float4 s0 = *reinterpret_cast<const float4*>(sc1 + k0);
+          const float4 s1 = *reinterpret_cast<const float4*>(sc1 + k0 + 4);
+          const float4 f0 = *reinterpret_cast<const float4*>(sf1 + k0);
+          const float4 f1 = *reinterpret_cast<const float4*>(sf1 + k0 + 4);
+          const float scv[8] = {s0.x, s0.y, s0.z, s0.w, s1.x, s1.y, s1.z, s1.w};
+          const float sfv[8] = {f0.x, f0.y, f0.z, f0.w, f1.x, f1.y, f1.z, f1.w};
+#pragma unroll
+          for (int mt = 0; mt < MAXMT; ++mt) {
+            if (mt < g.MT) {
+              float x[8];
+              unpack8(*reinterpret_cast<const uint4*>(Cat + (mt * 16 + frow) * g.CS + k0), x);
+#pragma unroll
+              for (int q = 0; q < 8; ++q) x[q] = clampf(fmaf(x[q], scv[q], sfv[q]), lo, hi);
+              const v8bf af = __builtin_bit_cast(v8bf, pack8(x));
+              acc[mt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, bw[ks], acc[mt], 0, 0, 0);
+            }
+          }
+          // (keeps the scheduler from hoisting every step's A fragments into registers at once)
+          __builtin_amdgcn_sched_barrier(0);
+        }
       }
+      const int col = wid * 16 + frow;
+      const float s2 = sc2[col], f2 = sf2[col];
 #pragma unroll
-      for (int mi = 0; mi < MAXMI; ++mi) {
-        const int mt = wid + NW * mi;
+      for (int mt = 0; mt < MAXMT; ++mt) {
         if (mt >= g.MT) continue;
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
           const int row = mt * 16 + (lane >> 4) * 4 + q;
           if (row >= pv) continue;
-          const int im = row / g.HW, rem = row - im * g.HW, h = rem / a.W, w = rem - h * a.W;
-          bf16_t* zrow = Z2 + (size_t)(im * g.GP + (h + 1) * g.GW + (w + 1)) * ZS;
-#pragma unroll
-          for (int n = 0; n < 8; ++n) {
-            const int col = n * 16 + frow;
-            zrow[col] = f2bf(clampf(fmaf(acc[mi][n][q], sc2[col], sf2[col]), lo, hi));
-          }
+          Z2[(size_t)(gtl[row] + g.GW + 1) * ZS + col] = f2bf(clampf(fmaf(acc[mt][q], s2, f2), lo, hi));
         }
       }
     }
@@ -189,37 +179,36 @@ __global__ __launch_bounds__(NT) void dense_infer_kernel(DenseInferArgs a) {
     // ---- GEMM2: n = conv3x3(z2) . W2^T (tiles wid + 8 j, all of one N tile), epilogue into cat
     {
       const int nt = wid & 1;
-      const bf16_t* __restrict__ wb = w2 + (size_t)(nt * 16 + frow) * 1152 + fk;
+      // the 3x3's B fragments of this wave's N tile, in two halves of 18 K steps: the second half
+      // is issued once the first 9 steps have consumed their fragments (27 in registers at most)
+      const bf16_t* __restrict__ wrow = w2 + (size_t)(nt * 16 + frow) * 1152 + fk;
+      v8bf w2f[36];
+#pragma unroll
+      for (int kk = 0; kk < 18; ++kk) w2f[kk] = ld_frag(wrow + kk * 32);
       v4f acc[MAXG2];
       int gb[MAXG2];
 #pragma unroll
       for (int j = 0; j < MAXG2; ++j) {
         acc[j] = (v4f){0.f, 0.f, 0.f, 0.f};
         const int mt = (wid + NW * j) >> 1;
-        int row = mt * 16 + frow;
-        if (row >= pv) row = 0;
-        const int im = row / g.HW, rem = row - im * g.HW, h = rem / a.W, w = rem - h * a.W;
-        gb[j] = im * g.GP + h * g.GW + w;  // top-left of the 3x3 window in the padded grid
+        gb[j] = mt < g.MT ? gtl[mt * 16 + frow] : 0;  // top-left of the 3x3 window
       }
-      v8bf bq[BDEPTH];
 #pragma unroll
-      for (int k = 0; k < BDEPTH; ++k) bq[k] = ld_frag(wb + k * 32);
-      for (int ks = 0; ks < 36; ks += BDEPTH) {
+      for (int kk = 0; kk < 36; ++kk) {
+        if (kk == 9) {
 #pragma unroll
-        for (int k = 0; k < BDEPTH; ++k) {
-          const int kk = ks + k;
-          const v8bf bf = bq[k];
-          if (kk + BDEPTH < 36) bq[k] = ld_frag(wb + (kk + BDEPTH) * 32);
-          const int tap = kk >> 2, cc = (kk & 3) * 32;
-          const int r = tap / 3, s = tap - r * 3;
+          for (int k2 = 18; k2 < 36; ++k2) w2f[k2] = ld_frag(wrow + k2 * 32);
+        }
+        const int tap = kk >> 2, cc = (kk & 3) * 32;
+        const int r = tap / 3, s = tap - r * 3;
 #pragma unroll
-          for (int j = 0; j < MAXG2; ++j) {
-            if (((wid + NW * j) >> 1) < g.MT) {
-              const v8bf af = ld_frag(Z2 + (size_t)(gb[j] + r * g.GW + s) * ZS + cc + fk);
-              acc[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, bf, acc[j], 0, 0, 0);
-            }
+        for (int j = 0; j < MAXG2; ++j) {
+          if (((wid + NW * j) >> 1) < g.MT) {
+            const v8bf af = ld_frag(Z2 + (size_t)(gb[j] + r * g.GW + s) * ZS + cc + fk);
+            acc[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, w2f[kk], acc[j], 0, 0, 0);
           }
         }
+        __builtin_amdgcn_sched_barrier(0);
       }
 #pragma unroll
       for (int j = 0; j < MAXG2; ++j) {
@@ -251,7 +240,9 @@ long long dense_infer_smem(const DenseInferArgs& a) {
   if (a.c0 % 32 || a.ld % 8 || a.c0 + 32 * a.L > a.ld) return -1;
   if ((uintptr_t)a.buf % 16) return -1;
   const DiGeo g = di_geo(a);
-  if (g.MT > NW * MAXMI || 2 * g.MT > NW * MAXG2) return -1;
+  if (g.MT > MAXMT || 2 * g.MT > NW * MAXG2) return -1;
+  for (int l = 0; l < a.L; ++l)
+    if ((a.c0 + 32 * l) / 32 > MAXKS) return -1;
   const long long b = di_bytes(a, g);
   return b <= 160 * 1024 ? b : -1;
 }

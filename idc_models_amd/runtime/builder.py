@@ -882,9 +882,10 @@ class Builder:
         a.N, a.H, a.W, a.c0, a.L, a.act = buf.N, buf.H, buf.W, layers[0]["cin"], len(layers), layers[0]["bn1"].act
         if any(lay["cin"] != a.c0 + 32 * i for i, lay in enumerate(layers)):
             return False
-        # whole images per workgroup: two on the small maps (weights re-read per workgroup), one
-        # on the large ones (the LDS holds one 13x13 image's concat buffer and z2 grid)
-        want = int(os.environ.get("IDC_DENSE_INFER_IPG", "0")) or (2 if buf.H * buf.W <= 64 else 1)
+        # one image per workgroup: with the layer's weight fragments held in registers the
+        # re-read is cheap and twice the workgroups wins (measured 0.973-0.980 ms frozen step
+        # at ipg 1 vs 1.012-1.014 at ipg 2 on the 7x7 stage); IDC_DENSE_INFER_IPG overrides
+        want = int(os.environ.get("IDC_DENSE_INFER_IPG", "0")) or 1
         for ipg in sorted({want, 1}, reverse=True):
             a.ipg = ipg
             a.layers = 1  # (placeholder: the size query checks shapes only)
