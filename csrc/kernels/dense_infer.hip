@@ -24,9 +24,11 @@ namespace {
 
 constexpr int NT = 512, NW = NT / 64;
 constexpr int ZS = 128 + 8;    // z2 grid row stride (elements)
-constexpr int MAXMT = 12;      // M tiles of a workgroup (rows <= 192)
-constexpr int MAXKS = 16;      // GEMM1 K steps (cin <= 512)
-constexpr int MAXG2 = 3;       // GEMM2 tiles per wave (MT * 2 <= 24)
+// two instantiations: <12, 16> (up to 12 M tiles = 192 rows; GEMM1 B fragments in chunks of 16 K
+// steps = 512 channels) for the large maps, <2, 24> (32 rows; 768 channels of B fragments in one
+// memory latency; 32 steps spill) for the small ones
+constexpr int BIG_MT = 12, BIG_KS = 16, SMALL_MT = 2, SMALL_KS = 24;
+constexpr int MAXCT = 2048;    // widest stage (concat channels)
 
 struct DiGeo {
   int HW, P, RP, MT, CT, CS, GW, GP;
@@ -49,18 +51,45 @@ __host__ __device__ inline long long di_bytes(const DenseInferArgs& a, const DiG
 
 __device__ __forceinline__ v8bf ld_frag(const bf16_t* p) { return *reinterpret_cast<const v8bf*>(p); }
 
-// BatchNorm (moving statistics) scale / shift of channel c
-__device__ __forceinline__ void inf_coeff(const float* g, const float* b, const float* mm, const float* mv,
-                                          float eps, int c, float& sc, float& sf) {
-  const float r = rsqrtf(mv[c] + eps);
-  const float gg = g ? g[c] : 1.f, bb = b ? b[c] : 0.f;
-  sc = gg * r;
-  sf = bb - mm[c] * sc;
+// BN tables of layer e: sc1/sf1 over its cin input channels, sc2/sf2 over the 128 bottleneck
+// channels.  Every load of the thread's (up to TU) channels is issued before any is used, so the
+// tables cost one memory latency at every width (a plain strided loop pays one per 512 channels).
+__device__ __forceinline__ void layer_tables(const DenseLayerDesc& e, float* sc1, float* sf1, float* sc2,
+                                             float* sf2, int tid) {
+  constexpr int TU = (MAXCT + 128 + NT - 1) / NT;
+  const int n = e.cin + 128;
+  float gg[TU], bb[TU], mm[TU], vv[TU];
+#pragma unroll
+  for (int u = 0; u < TU; ++u) {
+    const int c = tid + u * NT;
+    gg[u] = 1.f; bb[u] = 0.f; mm[u] = 0.f; vv[u] = 1.f;
+    if (c < e.cin) {
+      if (e.g1) gg[u] = e.g1[c];
+      if (e.b1) bb[u] = e.b1[c];
+      mm[u] = e.mm1[c]; vv[u] = e.mv1[c];
+    } else if (c < n) {
+      const int k = c - e.cin;
+      if (e.g2) gg[u] = e.g2[k];
+      if (e.b2) bb[u] = e.b2[k];
+      mm[u] = e.mm2[k]; vv[u] = e.mv2[k];
+    }
+  }
+#pragma unroll
+  for (int u = 0; u < TU; ++u) {
+    const int c = tid + u * NT;
+    if (c >= n) continue;
+    const float sc = gg[u] * rsqrtf(vv[u] + (c < e.cin ? e.eps1 : e.eps2));
+    const float sf = bb[u] - mm[u] * sc;
+    if (c < e.cin) { sc1[c] = sc; sf1[c] = sf; }
+    else { sc2[c - e.cin] = sc; sf2[c - e.cin] = sf; }
+  }
 }
 
 }  // namespace
 
+template <int MAXMT, int MAXKS>
 __global__ __launch_bounds__(NT) void dense_infer_kernel(DenseInferArgs a) {
+  constexpr int MAXG2 = (2 * MAXMT + NW - 1) / NW;  // GEMM2 tiles per wave
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const DiGeo g = di_geo(a);
   bf16_t* Cat = reinterpret_cast<bf16_t*>(smem);
@@ -112,34 +141,38 @@ __global__ __launch_bounds__(NT) void dense_infer_kernel(DenseInferArgs a) {
     }
   }
 
+  // 3x3 on 1x1 maps (stage 4 at 50x50): only the centre tap sees data, and w2 is the centre
+  // slice [32][128] (dense_stage.h DenseLayerDesc::w2, k2 = 1)
+  const bool c1 = a.H == 1 && a.W == 1;
+  // BN tables of layer 0; those of layer l + 1 are written during layer l's GEMM2 (the tables are
+  // last read by GEMM1 and its epilogue), so a layer costs two barriers
+  layer_tables(a.layers[0], sc1, sf1, sc2, sf2, tid);
+  __syncthreads();
+
   for (int l = 0; l < a.L; ++l) {
     const DenseLayerDesc& d = a.layers[l];
     const int cin = d.cin;
     const bf16_t* __restrict__ w1 = d.w1;
     const bf16_t* __restrict__ w2 = d.w2;
-    // ---- BN tables of the layer (one memory latency; the previous layer's barrier orders reuse)
-    for (int c = tid; c < cin + 128; c += NT) {
-      if (c < cin) inf_coeff(d.g1, d.b1, d.mm1, d.mv1, d.eps1, c, sc1[c], sf1[c]);
-      else inf_coeff(d.g2, d.b2, d.mm2, d.mv2, d.eps2, c - cin, sc2[c - cin], sf2[c - cin]);
-    }
-    __syncthreads();
 
     // ---- GEMM1: t = z1 . W1^T.  Wave w owns N tile w (16 of the 128 bottleneck channels) over
     // every M tile, so its B fragments -- all K steps of one 16-row slice of W1 -- are loaded ONCE
     // per layer (one memory latency, issued with the tables) instead of streamed per K step
     {
       const int KS = cin / 32;
-      v8bf bw[MAXKS];
-#pragma unroll
-      for (int ks = 0; ks < MAXKS; ++ks)
-        if (ks < KS) bw[ks] = ld_frag(w1 + (size_t)(wid * 16 + frow) * cin + ks * 32 + fk);
       v4f acc[MAXMT];
 #pragma unroll
       for (int mt = 0; mt < MAXMT; ++mt) acc[mt] = (v4f){0.f, 0.f, 0.f, 0.f};
+      // chunks of MAXKS K steps (one chunk up to cin 512; stages 3-4 take two)
+      for (int kc = 0; kc < KS; kc += MAXKS) {
+      v8bf bw[MAXKS];
+#pragma unroll
+      for (int ks = 0; ks < MAXKS; ++ks)
+        if (kc + ks < KS) bw[ks] = ld_frag(w1 + (size_t)(wid * 16 + frow) * cin + (kc + ks) * 32 + fk);
 #pragma unroll
       for (int ks = 0; ks < MAXKS; ++ks) {
-        if (ks < KS) {
-          const int k0 = ks * 32 + fk;
+        if (kc + ks < KS) {
+          const int k0 = (kc + ks) * 32 + fk;
           const float4 s0 = *reinterpret_cast<const float4*>(sc1 + k0);
           const float4 s1 = *reinterpret_cast<const float4*>(sc1 + k0 + 4);
           const float4 f0 = *reinterpret_cast<const float4*>(sf1 + k0);
@@ -161,6 +194,7 @@ __global__ __launch_bounds__(NT) void dense_infer_kernel(DenseInferArgs a) {
           __builtin_amdgcn_sched_barrier(0);
         }
       }
+      }
       const int col = wid * 16 + frow;
       const float s2 = sc2[col], f2 = sf2[col];
 #pragma unroll
@@ -177,7 +211,29 @@ __global__ __launch_bounds__(NT) void dense_infer_kernel(DenseInferArgs a) {
     __syncthreads();
 
     // ---- GEMM2: n = conv3x3(z2) . W2^T (tiles wid + 8 j, all of one N tile), epilogue into cat
-    {
+    if (c1) {
+      const int nt = wid & 1;
+      const bf16_t* __restrict__ wrow = w2 + (size_t)(nt * 16 + frow) * 128 + fk;
+      v8bf wc[4];
+#pragma unroll
+      for (int kk = 0; kk < 4; ++kk) wc[kk] = ld_frag(wrow + kk * 32);
+      if (l + 1 < a.L) layer_tables(a.layers[l + 1], sc1, sf1, sc2, sf2, tid);
+#pragma unroll
+      for (int j = 0; j < MAXG2; ++j) {
+        const int mt = (wid + NW * j) >> 1;
+        if (mt >= g.MT) continue;
+        const int zc = gtl[mt * 16 + frow] + g.GW + 1;
+        v4f acc = (v4f){0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int kk = 0; kk < 4; ++kk)
+          acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ld_frag(Z2 + (size_t)zc * ZS + kk * 32 + fk), wc[kk], acc, 0, 0, 0);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const int row = mt * 16 + (lane >> 4) * 4 + q;
+          if (row < pv) Cat[row * g.CS + cin + nt * 16 + frow] = f2bf(acc[q]);
+        }
+      }
+    } else {
       const int nt = wid & 1;
       // the 3x3's B fragments of this wave's N tile, in two halves of 18 K steps: the second half
       // is issued once the first 9 steps have consumed their fragments (27 in registers at most)
@@ -185,6 +241,7 @@ __global__ __launch_bounds__(NT) void dense_infer_kernel(DenseInferArgs a) {
       v8bf w2f[36];
 #pragma unroll
       for (int kk = 0; kk < 18; ++kk) w2f[kk] = ld_frag(wrow + kk * 32);
+      if (l + 1 < a.L) layer_tables(a.layers[l + 1], sc1, sf1, sc2, sf2, tid);
       v4f acc[MAXG2];
       int gb[MAXG2];
 #pragma unroll
@@ -240,9 +297,8 @@ long long dense_infer_smem(const DenseInferArgs& a) {
   if (a.c0 % 32 || a.ld % 8 || a.c0 + 32 * a.L > a.ld) return -1;
   if ((uintptr_t)a.buf % 16) return -1;
   const DiGeo g = di_geo(a);
-  if (g.MT > MAXMT || 2 * g.MT > NW * MAXG2) return -1;
-  for (int l = 0; l < a.L; ++l)
-    if ((a.c0 + 32 * l) / 32 > MAXKS) return -1;
+  if (g.MT > BIG_MT) return -1;
+  if (g.CT > MAXCT) return -1;
   const long long b = di_bytes(a, g);
   return b <= 160 * 1024 ? b : -1;
 }
@@ -250,7 +306,12 @@ long long dense_infer_smem(const DenseInferArgs& a) {
 hipError_t dense_infer(const DenseInferArgs& a, hipStream_t st) {
   const long long smem = dense_infer_smem(a);
   if (smem < 0) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(dense_infer_kernel, dim3((a.N + a.ipg - 1) / a.ipg), dim3(NT), (size_t)smem, st, a);
+  const DiGeo g = di_geo(a);
+  const dim3 grid((a.N + a.ipg - 1) / a.ipg);
+  if (g.MT <= SMALL_MT)
+    hipLaunchKernelGGL((dense_infer_kernel<SMALL_MT, SMALL_KS>), grid, dim3(NT), (size_t)smem, st, a);
+  else
+    hipLaunchKernelGGL((dense_infer_kernel<BIG_MT, BIG_KS>), grid, dim3(NT), (size_t)smem, st, a);
   return hipGetLastError();
 }
 

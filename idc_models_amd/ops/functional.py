@@ -559,7 +559,8 @@ def dense_stage(buf: torch.Tensor, sstats: torch.Tensor, layers, sshift: Optiona
 def dense_infer(buf: torch.Tensor, layers, act: int = RELU, ipg: int = 1):
     """A whole dense block in inference mode as one launch (csrc/kernels/dense_infer.hip).
     ``buf``: NHWC bf16 stage buffer [N, H, W, ld] with channels [0, c0) filled; ``layers``: dicts
-    with w1 ([128][cin] bf16), w2 ([32][3][3][128] bf16), g1, b1, mm1, mv1 ([cin]), g2, b2, mm2, mv2
+    with w1 ([128][cin] bf16), w2 ([32][3][3][128] bf16; on 1x1 maps the centre slice [32][128]),
+    g1, b1, mm1, mv1 ([cin]), g2, b2, mm2, mv2
     ([128]), eps1, eps2, cin (= c0 + 32 i).  Writes channels [c0, c0 + 32 L) of ``buf``."""
     N, H, W, ld = buf.shape
     arr = (nat.DenseLayerDesc * len(layers))()

@@ -874,7 +874,8 @@ class Builder:
         if any(tuple(lay["cv2"].kernel_size) != (3, 3) or tuple(lay["cv1"].kernel_size) != (1, 1)
                or lay["cv1"].filters != 128 or lay["cv2"].filters != 32 for lay in layers):
             return False
-        if self.is_center_only(layers[0]["cv2"], buf.H, buf.W, (1, 1), (1, 1)):
+        center = self.is_center_only(layers[0]["cv2"], buf.H, buf.W, (1, 1), (1, 1))
+        if center != (buf.H == 1 and buf.W == 1):  # (the kernel takes the centre slice on 1x1 maps)
             return False
         ext = nat.load()
         a = nat.DenseInferArgs()
@@ -884,13 +885,16 @@ class Builder:
             return False
         # one image per workgroup: with the layer's weight fragments held in registers the
         # re-read is cheap and twice the workgroups wins (measured 0.973-0.980 ms frozen step
-        # at ipg 1 vs 1.012-1.014 at ipg 2 on the 7x7 stage); IDC_DENSE_INFER_IPG overrides
-        want = int(os.environ.get("IDC_DENSE_INFER_IPG", "0")) or 1
+        # at ipg 1 vs 1.012-1.014 at ipg 2 on the 6x6 stage); maps of fewer than
+        # IDC_DENSE_INFER_ROWS pixels group images up to that many rows (1x1 maps: 16 images);
+        # IDC_DENSE_INFER_IPG overrides
+        rows = int(os.environ.get("IDC_DENSE_INFER_ROWS", "16"))
+        want = int(os.environ.get("IDC_DENSE_INFER_IPG", "0")) or max(1, rows // (buf.H * buf.W))
         for ipg in sorted({want, 1}, reverse=True):
             a.ipg = ipg
             a.layers = 1  # (placeholder: the size query checks shapes only)
             if int(ext.dense_infer_smem(nat.raw(a))) >= 0:
-                a.layers = self._dense_layer_table(layers, False, True).data_ptr()
+                a.layers = self._dense_layer_table(layers, center, True).data_ptr()
                 self.emit(nat.OP_DENSE_INFER, a)
                 return True
         return False

@@ -92,11 +92,15 @@ def lower_densenet(b: Builder, net, U: int, input_dtype):
             bn2 = BNRef(bn2l, b, stt, RELU)
             st["layers"].append({"cin": cin, "bn1": bn1, "cv1": cv1, "bn2": bn2, "cv2": cv2, "t": t, "stt": stt})
         # a stage no statistics are needed from (every BatchNorm reading it on moving statistics:
-        # evaluation, a frozen base, the frozen stages of the fine-tune phase) and too large for
-        # the per-image row kernel: ONE dense_infer launch for the whole block (dense_infer.hip)
+        # evaluation, a frozen base, the frozen stages of the fine-tune phase): ONE dense_infer
+        # launch for the whole block (dense_infer.hip).  The stages the persistent launches take
+        # (M <= IDC_DENSE_STAGE_MAXM: stages 3-4 at 50x50) stay on them unless IDC_DENSE_INFER_LATE=1:
+        # measured 435 us (stage 3) and 208 us (stage 4) as dense_infer against 260 / 136 us for the
+        # row-resident / work-queue launches (frozen phase 1.23 vs 0.98-1.02 ms/step)
         consumer = L[f"pool{si + 2}_bn"] if si < len(nblocks) - 1 else L["bn"]
         consumer_infer = not (b.training and consumer.trainable)
-        if M > stage_maxm and consumer_infer and b.dense_infer(buf, st["layers"], RELU):
+        late_ok = M > stage_maxm or os.environ.get("IDC_DENSE_INFER_LATE", "0") == "1"
+        if late_ok and consumer_infer and b.dense_infer(buf, st["layers"], RELU):
             st["infer"] = True
         elif M <= stage_maxm and b.dense_stage_ok(sbuf, st["layers"], Hs, Ws):
             b.dense_stage(buf, sbuf, st["layers"], RELU)

@@ -1184,13 +1184,16 @@ def test_dense_stage_inference_mode_matches_reference(fn, N, H, c0, L, grid, ks,
 
 
 @pytest.mark.parametrize("N,H,c0,L,ipg", [(3, 13, 64, 6, 1), (5, 6, 128, 12, 2), (4, 6, 128, 12, 1),
-                                          (2, 13, 64, 3, 1), (3, 5, 96, 4, 3)])
+                                          (2, 13, 64, 3, 1), (3, 5, 96, 4, 3), (5, 3, 256, 24, 1),
+                                          (3, 3, 256, 24, 2), (37, 1, 512, 16, 16), (5, 1, 512, 16, 1)])
 def test_dense_infer_matches_reference(fn, N, H, c0, L, ipg):
     """A whole dense block in inference mode as ONE launch (dense_infer.hip: whole images per
     workgroup, the concat buffer and the zero-bordered z2 grid in LDS) vs a PyTorch reference of
     the same layers on moving statistics, intermediates rounded to bf16 where the kernel stores
-    them.  DenseNet-121 stage 1 (13x13, c0 64, 6 layers) and stage 2 (6x6, c0 128, 12 layers) with
-    one and two images per workgroup (5 images: a short last group), and an odd map."""
+    them.  DenseNet-121 stage 1 (13x13, c0 64, 6 layers), stage 2 (6x6, c0 128, 12 layers), stage 3
+    (3x3, c0 256, 24 layers: the 1x1 K in two register chunks) and stage 4 (1x1, c0 512, 16 layers:
+    the 3x3's centre slice only; 37 images = a short last group of 16) with one and several images
+    per workgroup, and an odd map."""
     W = H
     ld = c0 + 32 * L
     g = torch.Generator(device="cpu").manual_seed(N * 11 + H + L)
@@ -1202,7 +1205,8 @@ def test_dense_infer_matches_reference(fn, N, H, c0, L, ipg):
         cin = c0 + 32 * i
         w1 = bf(torch.randn(1, 1, cin, 128, generator=g) * (2.0 / cin) ** 0.5).to(DEV)
         w2 = bf(torch.randn(3, 3, 128, 32, generator=g) * (2.0 / 1152) ** 0.5).to(DEV)
-        d = dict(w1=fn.weight_fwd_layout(w1, cin), w2=fn.weight_fwd_layout(w2, 128),
+        w2k = w2[1:2, 1:2] if H == 1 else w2  # 1x1 maps: the kernel reads the centre slice
+        d = dict(w1=fn.weight_fwd_layout(w1, cin), w2=fn.weight_fwd_layout(w2k, 128),
                  g1=(torch.rand(cin, generator=g) + 0.5).to(DEV), b1=(torch.randn(cin, generator=g) * 0.1).to(DEV),
                  g2=(torch.rand(128, generator=g) + 0.5).to(DEV), b2=(torch.randn(128, generator=g) * 0.1).to(DEV),
                  mm1=(torch.randn(cin, generator=g) * 0.3).to(DEV), mv1=(torch.rand(cin, generator=g) * 2 + 0.2).to(DEV),

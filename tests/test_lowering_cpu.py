@@ -149,20 +149,27 @@ def test_mb_infer_lowering(monkeypatch, ft, training, fused):
     assert nat.OP_MB_INFER not in [op[1] for op in b0.ops]
 
 
-@pytest.mark.parametrize("ft,training,n", [("frozen", True, 2), (None, False, 2), (150, True, 2), (None, True, 0)])
+@pytest.mark.parametrize("ft,training,n", [("frozen", True, 4), (None, False, 4), (150, True, 2), (None, True, 0)])
 def test_dense_infer_lowering(monkeypatch, ft, training, n):
     """DenseNet stages whose BatchNorms (and the stage's consumer BatchNorm) all run on moving
-    statistics and which are larger than the persistent launches take (stages 1-2 at 50x50, batch
-    128 here; 256 in the bench) lower to ONE OP_DENSE_INFER each (dense_infer.hip): in evaluation, the frozen
-    base and the frozen stages of the fine-tune phase; never in full training.  IDC_DENSE_INFER=0
-    restores the per-layer convs."""
+    statistics lower to ONE OP_DENSE_INFER each (dense_infer.hip): with IDC_DENSE_INFER_LATE=1 all
+    four stages in evaluation and the frozen base, stages 1-2 in the fine-tune phase (its cut falls
+    in stage 3); never in full training.  By default stages 3-4 (M <= 2304 rows, batch 128 here)
+    stay on the persistent launches; IDC_DENSE_INFER=0 restores the per-layer convs."""
+    monkeypatch.setenv("IDC_DENSE_INFER_LATE", "1")
     _, _, b = _lower("densenet121", ft, training, B=128)
     kinds = [op[1] for op in b.ops if op[0] == "fwd"]
     assert kinds.count(nat.OP_DENSE_INFER) == n
+    shapes = []
     for op in b.ops:
         if op[1] == nat.OP_DENSE_INFER:
             a = nat.DenseInferArgs.from_buffer_copy(op[2])
-            assert (a.H, a.L) in ((13, 6), (6, 12)) and nat.load().dense_infer_smem(op[2]) > 0
+            shapes.append((a.H, a.L, a.ipg))
+            assert nat.load().dense_infer_smem(op[2]) > 0
+    assert shapes == [(13, 6, 1), (6, 12, 1), (3, 24, 1), (1, 16, 16)][:n]
+    monkeypatch.delenv("IDC_DENSE_INFER_LATE")
+    _, _, bl = _lower("densenet121", ft, training, B=128)
+    assert [op[1] for op in bl.ops].count(nat.OP_DENSE_INFER) == min(n, 2)
     monkeypatch.setenv("IDC_DENSE_INFER", "0")
     _, _, b0 = _lower("densenet121", ft, training, B=128)
     assert nat.OP_DENSE_INFER not in [op[1] for op in b0.ops]
