@@ -16,6 +16,8 @@ from __future__ import annotations
 import copy
 from typing import Dict, List, Sequence
 
+import os
+
 import torch
 import torch.nn.functional as F
 
@@ -97,12 +99,14 @@ def param_report(arena, grad: torch.Tensor, g32: Sequence[torch.Tensor],
 
 
 FACTOR = 1.5
-FLOOR = 0.05
+FLOOR = 0.02
 # every parameter must stay within HARD_FACTOR x autocast's error; at most SOFT_FRACTION of them
 # (at least one) may exceed FACTOR x: each parameter's error is one random draw of the rounding
 # noise, and a network with ~600 parameter tensors occasionally draws one past 1.5x (DenseNet-201
 # at batch 32: 1.16 vs a 1.14 bound), while a systematic error moves many, or one by far more
-HARD_FACTOR = 3.0
+# (round 6: 3.0 -> 2.0 and the floor 0.05 -> 0.02; the worst non-invariant draw measured is 1.19x,
+# profiles/densenet121_gradient_fidelity.md)
+HARD_FACTOR = 2.0
 SOFT_FRACTION = 0.01
 # Parameters whose fp32 per-element RMS gradient is below 1e-2 x the network's median are
 # directions the loss is invariant to.  Measured (fp32, CPU): DenseNet-121/201 stem BN gamma at
@@ -147,6 +151,12 @@ def grad_failures(arena, grad: torch.Tensor, g32: Sequence[torch.Tensor], g16: S
             soft.append(row)
     if len(soft) > max(1, int(SOFT_FRACTION * len(rows))):
         bad += soft
+    if os.environ.get("IDC_FIDELITY_LOG") == "1":  # margin report: the worst ratio and its bound
+        ratios = sorted(r["rel"] / max(r["rel_autocast"], 1e-300) for r in rows if rms[r["param"]] >= INVARIANT * med)
+        if ratios:
+            print(f"[fidelity] {len(ratios)} params: ratio p50 {ratios[len(ratios) // 2]:.3f} "
+                  f"p99 {ratios[int(0.99 * (len(ratios) - 1))]:.3f} max {ratios[-1]:.3f} "
+                  f"(soft {factor}x + {floor}, hard {HARD_FACTOR}x)", flush=True)
     return bad
 
 
