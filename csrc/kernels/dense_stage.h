@@ -180,5 +180,10 @@ struct DenseInferArgs {
 };
 long long dense_infer_smem(const DenseInferArgs& a);  // dynamic LDS bytes, -1: shape not supported
 hipError_t dense_infer(const DenseInferArgs& a, hipStream_t st);
+// the same per-image block in TRAINING mode (dense_infer.hip; DenseStageArgs::rows == 2): BatchNorm
+// batch statistics through slot copies and two sharded barriers per layer, outputs as the per-layer
+// convs.  For stages whose images the row-resident launch cannot hold (13x13 / 6x6 at 50x50)
+bool dense_img_ok(const DenseStageArgs& a);
+hipError_t dense_img_fwd(const DenseStageArgs& a, hipStream_t st);
 
 }  // namespace idc

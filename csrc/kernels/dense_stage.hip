@@ -678,6 +678,7 @@ bool dense_stage_shape_ok(int N, int H, int W, int max_cin) {
 }
 
 hipError_t dense_stage_fwd(const DenseStageArgs& a, int grid, hipStream_t st) {
+  if (a.rows == 2) return dense_img_fwd(a, st);  // per-image training launch (dense_infer.hip)
   if (a.nlayers < 1 || (a.k2 != 1 && a.k2 != 3) || a.ld % 8 != 0 || a.N < 1 || a.H < 1 || a.W < 1 ||
       a.buf == nullptr || a.layers == nullptr || a.sync == nullptr ||
       (!a.infer && (a.sstats == nullptr || a.scratch == nullptr)) || !dense_stage_shape_ok(a.N, a.H, a.W, 0) ||

@@ -1158,6 +1158,11 @@ PYBIND11_MODULE(_idc_native, m) {
     if (s.size() != sizeof(DenseInferArgs)) throw std::runtime_error("dense_infer_smem: bad payload");
     return dense_infer_smem(*reinterpret_cast<const DenseInferArgs*>(s.data()));
   });
+  m.def("dense_img_ok", [](py::bytes payload) {
+    std::string s = payload;
+    if (s.size() != sizeof(DenseStageArgs)) throw std::runtime_error("dense_img_ok: bad payload");
+    return dense_img_ok(*reinterpret_cast<const DenseStageArgs*>(s.data()));
+  });
   m.def("dw_bwd_fused_ok", [](py::bytes payload) {
     std::string s = payload;
     if (s.size() != sizeof(DwArgs)) throw std::runtime_error("dw_bwd_fused_ok: bad payload");

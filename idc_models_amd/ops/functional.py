@@ -511,12 +511,14 @@ def dense_stage(buf: torch.Tensor, sstats: torch.Tensor, layers, sshift: Optiona
     ``infer``: inference-mode BatchNorms from each layer's mm1 / mv1 ([cin]) and mm2 / mv2 ([128])
     moving statistics; no statistics are produced (``sstats`` may be None).
     ``ksplit``: work items per 1x1 tile (split K of the older channels, <= DS_MAX_KSPLIT).
-    ``rows``: 1 runs the row-resident launch (dense_rows.hip) where its geometry fits.
+    ``rows``: 1 runs the row-resident launch (dense_rows.hip) where its geometry fits; 2 the
+    per-image launch of large maps (dense_infer.hip dense_img_fwd; the buffer exactly c0 + 32 L).
     Returns (sync counters [ticket, 16 per layer, last-slice count, fail], err counter, stamps or
     None) for inspection."""
     N, H, W, ld = buf.shape
     ext = nat.require()
-    if max(L["cin"] for L in layers) > int(ext.DS_MAX_CIN) or not ext.dense_stage_shape_ok(N, H, W, 0):
+    if max(L["cin"] for L in layers) > int(ext.DS_MAX_CIN) or \
+            (rows != 2 and not ext.dense_stage_shape_ok(N, H, W, 0)):
         raise ValueError("dense_stage: shape outside the persistent launch's limits")
     arr = (nat.DenseLayerDesc * len(layers))()
     for d, L in zip(arr, layers):
@@ -548,8 +550,9 @@ def dense_stage(buf: torch.Tensor, sstats: torch.Tensor, layers, sshift: Optiona
     a.partials = partials.data_ptr() if pfl else 0
     a.rows = rows
     st = None
-    if stamps:
-        st = torch.zeros(8 * int(ext.dense_stage_tasks(nat.raw(a))), dtype=torch.int64, device=buf.device)
+    if stamps:  # (the per-image launch: one row per layer and workgroup, at most 256 workgroups)
+        n = len(layers) * 256 if rows == 2 else int(ext.dense_stage_tasks(nat.raw(a)))
+        st = torch.zeros(8 * n, dtype=torch.int64, device=buf.device)
         a.stamps = st.data_ptr()
     _plan1(nat.OP_DENSE_STAGE, a, ints=(grid, len(layers)), ptrs=(tab.data_ptr(),))
     torch.cuda.current_stream().synchronize()

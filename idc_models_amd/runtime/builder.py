@@ -275,10 +275,11 @@ class Builder:
         self._stats_size += n
         return v
 
-    def stats(self, ld: int, count: int, slotted: bool = False) -> Stats:
+    def stats(self, ld: int, count: int, slotted: bool = False, single: bool = False) -> Stats:
         """``slotted``: this producer spreads its adds over slot copies even when IDC_STAT_SLOTS
-        is off (producers with ~1k workgroups per channel, e.g. the depthwise convs)."""
-        slots = stat_slots_for(count) if ((self.stat_slots_on or slotted) and not self.det) else 1
+        is off (producers with ~1k workgroups per channel, e.g. the depthwise convs).  ``single``:
+        one copy regardless (read by a persistent launch)."""
+        slots = stat_slots_for(count) if ((self.stat_slots_on or slotted) and not self.det and not single) else 1
         st = Stats(self._stats_floats(2 * ld * slots), ld, count, slots,
                    self.alloc((ld,), F32) if self.shift_stats else None)
         self.all_stats.append(st)
@@ -899,10 +900,37 @@ class Builder:
                 return True
         return False
 
-    def dense_stage(self, buf: Tensor4, sbuf: Stats, layers, act: int):
+    def dense_img_candidate(self, rows: int, H: int, W: int) -> bool:
+        """Before a stage's statistics are allocated: whether it may take the per-image training
+        launch (dense_img_ok), so its statistics get the single copy that launch reads."""
+        return (self.training and os.environ.get("IDC_DENSE_IMG", "0") == "1" and H * W > 1
+                and rows > int(os.environ.get("IDC_DENSE_STAGE_MAXM", "2304"))
+                and not getattr(self, "grouped", False) and not self.shared_device and not self.det)
+
+    def dense_img_ok(self, buf: Tensor4, sbuf: Optional[Stats], layers) -> bool:
+        """Whether a TRAINING stage whose images the row-resident launch cannot hold (13x13 / 6x6
+        at 50x50) can run as ONE per-image launch (dense_infer.hip dense_img_fwd, DenseStageArgs
+        rows 2): the persistent-launch conditions of dense_stage_ok, 3x3 maps of more than one
+        pixel, a stage buffer exactly c0 + 32 L wide, the grid co-resident (no grouped / shared-
+        device programs) and the LDS fit.  IDC_DENSE_IMG=0: per-layer convs."""
+        if os.environ.get("IDC_DENSE_IMG", "0") != "1" or getattr(self, "grouped", False) or self.shared_device:
+            return False
+        if any(lay["bn1"].mode == 2 and lay["bn2"].mode == 2 for lay in layers) or not self.training:
+            return False
+        if buf.H * buf.W <= 1 or buf.ld != layers[0]["cin"] + 32 * len(layers):
+            return False
+        if not self.dense_stage_ok(sbuf, layers, 1, 1):  # (1 x 1: skip the work-queue staging check)
+            return False
+        a = nat.DenseStageArgs()
+        a.buf, a.ld, a.N, a.H, a.W, a.nlayers, a.k2 = buf.ptr, buf.ld, buf.N, buf.H, buf.W, len(layers), 3
+        a.act1 = a.act2 = layers[0]["bn1"].act
+        return bool(nat.load().dense_img_ok(nat.raw(a)))
+
+    def dense_stage(self, buf: Tensor4, sbuf: Stats, layers, act: int, img: bool = False):
         """Emit ONE persistent launch for the dense layers ``layers`` of a stage (dicts with cin,
         bn1, cv1, bn2, cv2, t, stt as in lower_densenet): same buffers, statistics and weights as
-        the per-layer convs, so everything downstream (backward included) is unchanged."""
+        the per-layer convs, so everything downstream (backward included) is unchanged.  ``img``:
+        the per-image training launch (dense_img_ok)."""
         H, W = buf.H, buf.W
         center = self.is_center_only(layers[0]["cv2"], H, W, (1, 1), (1, 1))
         infer = all(lay["bn1"].mode == 2 and lay["bn2"].mode == 2 for lay in layers)
@@ -950,8 +978,10 @@ class Builder:
         a.rows = 1 if (os.environ.get("IDC_DS_ROWS", "1") == "1" and not getattr(self, "grouped", False)
                        and not self.shared_device
                        and M >= int(os.environ.get("IDC_DS_ROWS_MINM", "1024"))) else 0
+        if img:
+            a.rows = 2
         self._fail_words(a)
-        if os.environ.get("IDC_DS_STAMPS", "0") == "1":
+        if not img and os.environ.get("IDC_DS_STAMPS", "0") == "1":
             # per-work-item s_memrealtime stamps (tools/dense_stamps.py reads them after a step);
             # row-resident launches: one row per (layer, workgroup)
             rows_geo = tuple(ext.dense_rows_geometry(buf.N, H, W, buf.ld, max(lay["cin"] for lay in layers))) \

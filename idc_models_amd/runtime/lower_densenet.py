@@ -74,7 +74,8 @@ def lower_densenet(b: Builder, net, U: int, input_dtype):
     nblocks = base.blocks
     ctot = c0 + 32 * nblocks[0]
     buf = b.nhwc(B, Hs, Ws, ctot)
-    sbuf = b.stats(ctot, B * Hs * Ws, slotted=slotted_stage(B * Hs * Ws)) if training else None
+    sbuf = b.stats(ctot, B * Hs * Ws, slotted=slotted_stage(B * Hs * Ws),
+                   single=b.dense_img_candidate(B * Hs * Ws, Hs, Ws)) if training else None
     argmax = b.alloc((B * Hs * Ws * 64,), torch.uint8)
     b.pool(ys, buf.slice(0, 64), k=3, s=2, pt=1, pl=1, pro=bn_stem.args(), is_max=True,
            argmax=argmax, stats=sbuf, stats_off=0)
@@ -88,7 +89,7 @@ def lower_densenet(b: Builder, net, U: int, input_dtype):
             bn1 = BNRef(L[name + "_0_bn"], b, sbuf, RELU)
             cv1, bn2l, cv2 = L[name + "_1_conv"], L[name + "_1_bn"], L[name + "_2_conv"]
             t = b.nhwc(B, Hs, Ws, 128)
-            stt = b.stats(128, M) if training else None
+            stt = b.stats(128, M, single=b.dense_img_candidate(M, Hs, Ws)) if training else None
             bn2 = BNRef(bn2l, b, stt, RELU)
             st["layers"].append({"cin": cin, "bn1": bn1, "cv1": cv1, "bn2": bn2, "cv2": cv2, "t": t, "stt": stt})
         # a stage no statistics are needed from (every BatchNorm reading it on moving statistics:
@@ -104,6 +105,10 @@ def lower_densenet(b: Builder, net, U: int, input_dtype):
             st["infer"] = True
         elif M <= stage_maxm and b.dense_stage_ok(sbuf, st["layers"], Hs, Ws):
             b.dense_stage(buf, sbuf, st["layers"], RELU)
+        elif M > stage_maxm and b.dense_img_ok(buf, sbuf, st["layers"]):
+            # training stages of large maps (1-2 at 50x50): one per-image launch, BatchNorm
+            # statistics through two barriers per layer (dense_infer.hip dense_img_fwd)
+            b.dense_stage(buf, sbuf, st["layers"], RELU, img=True)
         else:
             for lay in st["layers"]:
                 cin, t = lay["cin"], lay["t"]
@@ -122,7 +127,8 @@ def lower_densenet(b: Builder, net, U: int, input_dtype):
             c0n = ctot // 2
             ctotn = c0n + 32 * nblocks[si + 1]
             bufn = b.nhwc(B, Hn, Wn, ctotn)
-            sbufn = b.stats(ctotn, B * Hn * Wn, slotted=slotted_stage(B * Hn * Wn)) if training else None
+            sbufn = b.stats(ctotn, B * Hn * Wn, slotted=slotted_stage(B * Hn * Wn),
+                            single=b.dense_img_candidate(B * Hn * Wn, Hn, Wn)) if training else None
             b.conv(p, cvt, bufn.slice(0, c0n), stats=sbufn, stats_off=0)
             b.add_moving(bnt)
             st["trans"] = {"bn": bnt, "conv": cvt, "p": p}

@@ -892,7 +892,10 @@ def test_wgrad_batch_matches_single_launches(fn, kind, N, H):
                                              (3, 5, 32, 2, 1, -2), (5, 2, 256, 4, 256, -2),
                                              (2, 1, 1120, 3, 256, -1), (256, 3, 256, 24, 256, -2),
                                              (256, 3, 256, 24, 256, -1), (256, 1, 512, 16, 256, -2),
-                                             (256, 1, 512, 16, 256, -1)])
+                                             (256, 1, 512, 16, 256, -1),
+                                             # ks 0: the per-image training launch of large maps
+                                             (256, 13, 64, 6, 256, 0), (256, 6, 128, 12, 256, 0),
+                                             (5, 13, 64, 6, 256, 0), (301, 6, 128, 4, 256, 0)])
 def test_dense_stage_persistent_matches_reference(fn, N, H, c0, L, grid, ks, monkeypatch):
     """The persistent dense-stage launch (work queue + per-phase completion counters, 1x1 partial
     sums over the finished channels accumulated before the newest slice is waited for, slotted
@@ -906,7 +909,11 @@ def test_dense_stage_persistent_matches_reference(fn, N, H, c0, L, grid, ks, mon
     (256, 1, 512, 16): its stage 4.  ks > 1: each 1x1 tile's older channels split over ks work
     items whose fp32 partials the tile's finalizer adds (grid 1 / 7: helpers queued before their
     finalizer, so the queue drains with any number of workgroups).  ks < 0: the row-resident
-    launch with -ks row blocks (16 rows each) of whole images per workgroup."""
+    launch with -ks row blocks (16 rows each) of whole images per workgroup.  ks 0: the per-image
+    training launch (dense_infer.hip dense_img_fwd, rows 2) at DenseNet-121's stage-1 / stage-2
+    bench shapes (13x13 / 6x6, 256 images: 256 workgroups), a small batch, and 301 images (two per
+    workgroup, a short last group)."""
+    ipg = -(-N // 256)
     if ks < 0:
         monkeypatch.setenv("IDC_DS_ROWS_RB", str(-ks))
         ext = fn.nat.require()
@@ -962,12 +969,13 @@ def test_dense_stage_persistent_matches_reference(fn, N, H, c0, L, grid, ks, mon
         rst[ld + cin:ld + cin + 32] = (yk * yk).sum(0)
         rts.append(t)
         rtst.append(tst)
-    sync, err, _ = fn.dense_stage(buf, sst, lays, sshift=K, grid=grid, k2=k2, ksplit=max(ks, 1), rows=int(ks < 0))
+    sync, err, _ = fn.dense_stage(buf, sst, lays, sshift=K, grid=grid, k2=k2, ksplit=max(ks, 1),
+                                  rows=2 if ks == 0 else int(ks < 0))
     M = N * H * W
     nA, nB = -(-M // 32) * 2, -(-M // 32)
     assert int(err[0].item()) == 0 and int(sync[-1].item()) == 0
     cnt = sync[1:1 + 16 * L].reshape(L, 2, 8).sum(-1)  # per layer: A_l, B_l sharded counters
-    if ks < 0:  # barrier arrivals: every workgroup at both barriers of every layer but the last
+    if ks <= 0:  # barrier arrivals: every workgroup at both barriers of every layer but the last
         G = -(-N // ipg)
         assert cnt[:-1, 0].tolist() == [G] * (L - 1) and cnt[:-1, 1].tolist() == [G] * (L - 1), sync.tolist()
     else:

@@ -175,6 +175,31 @@ def test_dense_infer_lowering(monkeypatch, ft, training, n):
     assert nat.OP_DENSE_INFER not in [op[1] for op in b0.ops]
 
 
+def test_dense_img_lowering(monkeypatch):
+    """Training DenseNet-121 at 50x50: stages 1-2 (13x13 / 6x6, more rows than the persistent
+    launches take) lower to ONE per-image launch each (OP_DENSE_STAGE with rows 2: dense_infer.hip
+    dense_img_fwd) whose statistics (stage buffers, every t) have the single copy it reads; stage 3
+    keeps the row-resident launch, stage 4 the work queue.  Opt-in (IDC_DENSE_IMG=1: measured slower
+    than the per-layer convs); off, per-layer convs on slotted statistics.  Never in the fine-tune
+    phase's frozen stages (dense_infer there)."""
+    monkeypatch.setenv("IDC_DENSE_IMG", "1")
+
+    def stages(b):
+        return [(a.H, a.rows) for a in (nat.DenseStageArgs.from_buffer_copy(op[2]) for op in b.ops
+                                        if op[1] == nat.OP_DENSE_STAGE)]
+    _, _, b = _lower("densenet121", None, True, B=256)
+    assert stages(b) == [(13, 2), (6, 2), (3, 1), (1, 0)]
+    for op in b.ops:
+        if op[1] == nat.OP_DENSE_STAGE and nat.DenseStageArgs.from_buffer_copy(op[2]).rows == 2:
+            assert nat.load().dense_img_ok(op[2])
+    _, _, bf = _lower("densenet121", 150, True, B=256)
+    assert stages(bf) == [(3, 1), (1, 0)]
+    monkeypatch.setenv("IDC_DENSE_IMG", "0")
+    _, _, b0 = _lower("densenet121", None, True, B=256)
+    assert stages(b0) == [(3, 1), (1, 0)]
+    assert sum(1 for op in b0.ops if op[0] == "fwd") == sum(1 for op in b.ops if op[0] == "fwd") + 34
+
+
 def test_dw_fused_backward_lowering(monkeypatch):
     """IDC_DW_FUSED_BWD=1: every stride-1 depthwise layer's data and weight gradients lower to ONE
     main-lane op (OP_DW_BWD_DATA, ints[0] 1) plus the partials' column sums on the side lane
@@ -232,7 +257,10 @@ def test_struct_layouts_match_native():
 
 def test_dense_stage_lowering(monkeypatch):
     """Late DenseNet stages lower to one OP_DENSE_STAGE each (per-layer convs otherwise); the
-    deterministic mode and slotted statistics keep the per-layer convs."""
+    deterministic mode and slotted statistics keep the per-layer convs.  (Stages 1-2's per-image
+    launch is off here: test_dense_img_lowering.)"""
+    monkeypatch.setenv("IDC_DENSE_IMG", "0")
+
     def count(env):
         for k, v in env.items():
             monkeypatch.setenv(k, v)
@@ -328,8 +356,10 @@ def test_mb_chain_lowering(monkeypatch):
 def test_stat_slot_copies_default_and_cap(monkeypatch):
     """Large-map reductions keep statistics slot copies by default, at most 4 (the consumers'
     batched table loads take <= 4: builder.stat_slots_for); IDC_STAT_SLOTS_CAP moves the cap and
-    IDC_STAT_SLOTS=0 keeps one copy everywhere."""
+    IDC_STAT_SLOTS=0 keeps one copy everywhere.  (With stages 1-2 as per-image launches their
+    statistics have the one copy those read: test_dense_img_lowering; off here.)"""
     from idc_models_amd.runtime.builder import stat_slots_for
+    monkeypatch.setenv("IDC_DENSE_IMG", "0")
     monkeypatch.delenv("IDC_STAT_SLOTS_CAP", raising=False)
     assert [stat_slots_for(r) for r in (256, 2304, 4096, 9216, 43264, 160000)] == [1, 1, 1, 4, 4, 4]
     monkeypatch.setenv("IDC_STAT_SLOTS_CAP", "16")
