@@ -50,7 +50,7 @@ def _cos(a, b):
 def _check(m, ref, x, y, slack=0.03, loss_slack=None):
     """Fused (bf16) vs eager fp32, judged against the eager bf16-autocast drift from fp32 (the
     precision floor of bf16 training) on the same net and batch: per parameter, the relative L2
-    error vs fp32 must stay within 1.5x autocast's + 0.02 (idc_models_amd/utils/fidelity.py;
+    error vs fp32 must stay within 1.5x autocast's + 0.05, every one within 2x (utils/fidelity.py;
     direction and magnitude); logits within 2x the autocast deviation + 0.05."""
     from idc_models_amd.utils.fidelity import grad_failures
     ref16 = copy.deepcopy(ref)
@@ -301,7 +301,7 @@ def test_batched_weight_gradients_match_per_layer(monkeypatch, maxm):
     """DenseNet-121 at the bench batch: the late stages' weight gradients launched as one batched
     kernel per shape (OP_WGRAD_BATCH, the default for M <= 2304 pixels; here also stage 2) and the
     per-layer launches, EACH against the fp32 eager gradient of the same weights and batch: every
-    parameter within 1.5x bf16 autocast's relative error + 0.02 (utils/fidelity.py).  The kernel
+    parameter within 1.5x bf16 autocast's relative error + 0.05 (utils/fidelity.py).  The kernel
     itself is checked exactly in test_kernels_gpu.py::test_wgrad_batch_matches_single_launches."""
     from idc_models_amd.engine import Model, RMSprop
     from idc_models_amd.models import build_model
@@ -335,7 +335,7 @@ def test_dense_stage_matches_per_layer(monkeypatch, B, maxm):
     against the per-layer convs on the same weights and input.  Forward stage buffers and every
     statistics array agree with the per-layer program to a FIXED bf16-level bound, the timeout
     counter stays zero, and both programs' training-step gradients pass the fp32 check
-    (utils/fidelity.py: per parameter within 1.5x bf16 autocast's relative error + 0.02).  The
+    (utils/fidelity.py: per parameter within 1.5x bf16 autocast's relative error + 0.05).  The
     bench default (256, 2304) also runs stages 1-2 as the per-image training launch
     (dense_infer.hip dense_img_fwd); the other cuts test the work-queue launch with it off."""
     from idc_models_amd.engine import Model, RMSprop
