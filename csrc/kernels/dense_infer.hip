@@ -12,9 +12,13 @@
 //                                                       grid (no bounds checks), K = 9 taps x 128
 //          cat[:, cin:cin+32] = n (raw: later layers' BN1 normalise it)
 // and finally writes the new 32 L channels of its images to the stage buffer once.  No statistics,
-// no grid barriers, no global round trips between layers; weights stream from L2 into MFMA B
-// fragments.  The per-layer path it replaces runs 2 launches per layer (12 + 24 for stages 1-2 of
-// DenseNet-121 at 50x50, ~390 us of the frozen-base step, profiles/densenet121_frozen_*).
+// no grid barriers, no global round trips between layers.  Each wave holds its N tile's W1
+// fragments (16 K steps at a time) and its W2 fragments (two halves of 18) in registers, loaded
+// once per layer; the next layer's BN tables are written while the 3x3 runs.  The per-layer path it
+// replaces runs 2 launches per layer (36 for stages 1-2 of DenseNet-121 at 50x50: ~390 us of the
+// frozen-base step against 143 + 215 us here, profiles/densenet121_frozen_dense_infer_*).  On the
+// 3x3 / 1x1 maps of stages 3-4 (a <2, 24> instantiation, centre tap only on 1x1) it is correct but
+// slower than the row-resident / work-queue launches, so those stay the default there.
 //
 // TRAINING mode (dense_img_fwd, DenseStageArgs::rows == 2: stages 1-2 of DenseNet-121 at 50x50,
 // 13x13 / 6x6 images that the row-resident launch of dense_rows.hip cannot hold): the same
